@@ -1,0 +1,266 @@
+#!/usr/bin/env python3
+"""Benchmark: frame pairs/s for one CorrBlock build + 12 lookups (BASELINE.json metric).
+
+One "step" = for each of this rank's pairs, ``CorrBlock(fmap1, fmap2, radius=4)``
+(the fused MFMA build of the 4-level pyramid) followed by 12 ``__call__(coords)``
+lookups with 12 different coordinate sets, exactly the reference's per-forward
+usage (core/raft.py:147, :169-173).  Inputs (fmaps [B,256,H/8,W/8] float32,
+coords = grid + N(0, 4^2) px) are synthetic and resident in HBM before timing.
+
+Launch: ``python bench.py [--gpus N --steps K --warmup W]``; for N > 1 the driver
+runs it under torch.distributed.run, one rank per GPU.  Pairs are independent,
+so each rank processes its own pairs (weak scaling, no collective on the data
+path); ranks are bracketed by barriers and the max elapsed time over ranks is
+used.  Rank 0 prints ONE JSON line.
+
+Execution: the step is captured into two HIP graphs (build, lookups) and
+replayed — the launch-bound lookups would otherwise be host-bound in Python.
+HIP events between the two replays give the build kernel's duration inside the
+timed region (the roofline's ``achieved``).  ``--mode eager`` times plain
+Python calls instead.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO))
+
+METRIC = "frame pairs/sec (corr build + 12 lookups) @436x1024, 1–8 GPU; % MFMA/HBM peak"
+PEAK_F32_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+PEAK_BF16_TFLOPS = 2500.0    # dense BF16 MFMA
+PEAK_HBM_GBS = 8000.0        # HBM3E spec
+
+# name -> (image H, W after InputPadder, fmap H, W, default pairs per GPU, dtype)
+WORKLOADS = {
+    "sintel": ((440, 1024), (55, 128), 1, "f32"),
+    "chairs": ((368, 496), (46, 62), 1, "f32"),
+    "kitti": ((376, 1248), (47, 156), 8, "bf16"),
+    "1080p": ((1088, 1920), (136, 240), 1, "f32"),
+}
+D, RADIUS, LEVELS, ITERS = 256, 4, 4, 12
+
+
+def level_sizes(H, W, L=LEVELS):
+    s = [(H, W)]
+    for _ in range(L - 1):
+        s.append((s[-1][0] // 2, s[-1][1] // 2))
+    return s
+
+
+def build_flops(B, H, W):
+    n = H * W
+    return 2.0 * B * n * n * D
+
+
+def build_bytes(B, H, W, s_in=4, s_out=4):
+    n = H * W
+    cells = sum(h * w for h, w in level_sizes(H, W))
+    return B * 2 * D * n * s_in + B * n * cells * s_out
+
+
+def lookup_bytes(B, H, W, s_pyr=4):
+    """Compulsory bytes of one lookup: window cells clipped to
+    the level, the coords and the float32 output."""
+    rd = 2 * RADIUS + 1
+    win = sum(min(rd + 1, h) * min(rd + 1, w) for h, w in level_sizes(H, W))
+    return B * H * W * (win * s_pyr + 8 + LEVELS * rd * rd * 4)
+
+
+def init_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def make_inputs(B, H, W, dtype, seed, dev):
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    f1 = torch.randn((B, D, H, W), generator=g, device=dev)
+    f2 = torch.randn((B, D, H, W), generator=g, device=dev)
+    if dtype == "bf16":
+        f1, f2 = f1.bfloat16(), f2.bfloat16()
+    ys, xs = torch.meshgrid(torch.arange(H, device=dev, dtype=torch.float32),
+                            torch.arange(W, device=dev, dtype=torch.float32), indexing="ij")
+    grid = torch.stack((xs, ys))[None].expand(B, 2, H, W)
+    coords = [(grid + 4.0 * torch.randn((B, 2, H, W), generator=g, device=dev)).contiguous()
+              for _ in range(ITERS)]
+    return f1, f2, coords
+
+
+def cpu_baseline(H, W, budget_s):
+    """Time the numpy oracle (oracle/, float32: the reference's op sequence —
+    matmul, /sqrt(D), 3x 2x2 avg-pool, 12 x 4-level bilinear lookups) on host cores."""
+    sys.path.insert(0, str(REPO / "tests"))
+    import datagen as dg
+    import oracle
+    from threadpoolctl import threadpool_info
+    f1 = dg.fmap(0, 1, D, H, W)
+    f2 = dg.fmap(1, 1, D, H, W)
+    cs = [dg.coords(100 + k, 1, H, W, "normal", 4.0) for k in range(ITERS)]
+    pairs, t0 = 0, time.perf_counter()
+    while True:
+        pyr = oracle.corr_pyramid(f1, f2, LEVELS, np.float32)
+        for c in cs:
+            oracle.corr_lookup(pyr, c, RADIUS)
+        pairs += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or pairs >= 50:
+            break
+    threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    return {"value": pairs / el, "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{pairs} pair(s) of fmap {H}x{W}, D={D}: build + {ITERS} lookups, "
+                      f"numpy float32 oracle, {el:.1f} s; matmul on {threads} BLAS threads, "
+                      f"lookups single-threaded"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="sintel", choices=sorted(WORKLOADS))
+    ap.add_argument("--batch", type=int, default=None, help="pairs per GPU per step")
+    ap.add_argument("--dtype", default=None, choices=["f32", "bf16"])
+    ap.add_argument("--mode", default="graph", choices=["graph", "eager"])
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world, rank, local = init_dist()
+    dev = torch.device("cuda", local if world > 1 else 0)
+    import dexiraft_amd
+    dexiraft_amd.load_native()
+
+    (img_h, img_w), (H, W), b_default, dt_default = WORKLOADS[args.workload]
+    B = args.batch or b_default
+    dtype = args.dtype or dt_default
+    f1, f2, coords = make_inputs(B, H, W, dtype, seed=1234 + rank, dev=dev)
+    stream = torch.cuda.Stream(device=dev)
+
+    state = {}
+
+    def build():
+        state["cb"] = dexiraft_amd.CorrBlock(f1, f2, radius=RADIUS)
+
+    def lookups():
+        state["outs"] = [state["cb"](c) for c in coords]
+
+    with torch.no_grad(), torch.cuda.stream(stream):
+        for _ in range(max(args.warmup, 1)):          # eager warmup (also JIT-free check)
+            build()
+            lookups()
+        torch.cuda.synchronize()
+        if args.mode == "graph":
+            g_build, g_look = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_build, stream=stream):
+                build()
+            with torch.cuda.graph(g_look, stream=stream, pool=g_build.pool()):
+                lookups()
+            run_build, run_look = g_build.replay, g_look.replay
+            for _ in range(max(args.warmup, 1)):
+                run_build()
+                run_look()
+        else:
+            run_build, run_look = build, lookups
+        torch.cuda.synchronize()
+
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+                torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        barrier(world)
+        t0 = time.perf_counter()
+        for e0, e1, e2 in evs:
+            e0.record(stream)
+            run_build()
+            e1.record(stream)
+            run_look()
+            e2.record(stream)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        barrier(world)
+
+    build_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in evs]))
+    look_ms = float(np.mean([b.elapsed_time(c) for _, b, c in evs])) / ITERS
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        # Correctness sanity outside the timed region: every rank's last lookup is finite.
+        ok = torch.tensor([float(torch.isfinite(state["outs"][-1]).all())], device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        assert ok.item() == 1.0
+    elapsed = t.item()
+
+    if rank == 0:
+        pairs = world * B * args.steps
+        value = pairs / elapsed
+        s_in = 2 if dtype == "bf16" else 4
+        flops = build_flops(B, H, W)
+        peak = PEAK_BF16_TFLOPS if dtype == "bf16" else PEAK_F32_TFLOPS
+        achieved = flops / (build_ms * 1e-3) / 1e12
+        lb = lookup_bytes(B, H, W, s_pyr=s_in)
+        res = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": dtype,
+            "data": "synthetic (torch.randn fmaps, coords = grid + N(0,4^2) px)",
+            "config": {
+                "workload": f"CorrBlock build + {ITERS} lookups, {args.workload} "
+                            f"{img_h}x{img_w} (fmap {H}x{W}), D={D}, r={RADIUS}, L={LEVELS}",
+                "pairs_per_gpu": B, "mode": args.mode, "parallelism": f"pairs sharded x{world}",
+            },
+            "roofline": {
+                "kernel": "corr_build_f32_kernel (stage a+b)",
+                "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
+                "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                "traffic": None,
+                "algorithmic_flops_per_launch": flops,
+                "avg_launch_us": round(build_ms * 1e3, 2),
+            },
+            "lookup_roofline": {
+                "kernel": "corr_lookup_kernel (stage c)",
+                "bound": "hbm", "achieved": round(lb / (look_ms * 1e-3) / 1e9, 1),
+                "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(lb / (look_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                "algorithmic_bytes_per_launch": lb,
+                "avg_launch_us": round(look_ms * 1e3, 2),
+            },
+            "build_bytes_per_launch": build_bytes(B, H, W, s_in, s_in),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(H, W, args.cpu_seconds)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,147 @@
+/*
+ * dexiraft_corr.h — C-ABI of the MI355X-native RAFT correlation subsystem.
+ *
+ * This is the drop-in boundary for the hot path named in BASELINE.json
+ * (`north_star`): RAFT's correlation block as used by Dexi+RAFT.  Every entry
+ * point takes plain device pointers, int64 sizes and a hipStream_t; none
+ * allocates, none throws, and each returns a status code (0 = ok, >0 = invalid
+ * argument / unsupported, <0 = HIP launch error).  Outputs and workspaces are
+ * allocated by the caller (the Python shell allocates them from torch's caching
+ * allocator).  Functions are reentrant and thread-safe per stream.
+ *
+ * Reference interfaces replaced (paths relative to the reference repository):
+ *   dxr_corr_pyramid_build   core/corr.py:13-27  CorrBlock.__init__ (matmul,
+ *                            / sqrt(D), 3x F.avg_pool2d) and core/corr.py:52-60
+ *                            CorrBlock.corr (num_levels = 1)
+ *   dxr_corr_lookup          core/corr.py:29-50  CorrBlock.__call__ together with
+ *                            core/utils/utils.py:57-71 bilinear_sampler
+ *                            (F.grid_sample, align_corners=True, zero padding)
+ *   dxr_avg_pool2x2          core/corr.py:69-71  F.avg_pool2d(fmap, 2, stride=2)
+ *                            in AlternateCorrBlock.__init__
+ *   dxr_alt_corr_forward     alt_cuda_corr/correlation.cpp:23-33 `forward`
+ *                            (alt_cuda_corr/correlation_kernel.cu:260-286)
+ *   dxr_alt_corr_lookup      core/corr.py:74-91  AlternateCorrBlock.__call__
+ *                            (all levels in one launch, / sqrt(D) fused)
+ *
+ * Layouts (all row-major, C-contiguous):
+ *   fmap (CorrBlock)        [B, D, H, W]               (NCHW, as core/raft.py:139-142)
+ *   pyramid level l         [B*H*W, H_l, W_l]          H_0 = H, H_l = floor(H_{l-1}/2)
+ *                           levels stored back to back; element offset of level l
+ *                           is dxr_pyramid_level_offset(B,H,W,l).  This is exactly
+ *                           the reference's corr_pyramid[l] ([B*H*W,1,H_l,W_l]).
+ *   coords                  [B, 2, H, W] float32       channel 0 = x, 1 = y
+ *                           (core/utils/utils.py:74-77)
+ *   lookup output           [B, L*(2r+1)^2, H, W] float32, channel
+ *                           l*(2r+1)^2 + ix*(2r+1) + iy, x offset = ix - r
+ *                           (x-major, core/corr.py:37-46)
+ *   alt fmaps               [B, H, W, C]               (NHWC, core/corr.py:82-83)
+ *   alt coords              [B, Nc, H1, W1, 2]
+ *   alt output              [B, Nc, (2r+1)^2, H1, W1]  channel iy + (2r+1)*ix
+ *                           (alt_cuda_corr/correlation_kernel.cu:92-95)
+ */
+#ifndef DEXIRAFT_CORR_H
+#define DEXIRAFT_CORR_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* HIP's own definition; repeating an identical typedef is legal in C11/C++. */
+typedef struct ihipStream_t* hipStream_t;
+
+#define DXR_ABI_VERSION 1
+
+enum dxr_status {
+  DXR_OK = 0,
+  DXR_EINVAL = 1,        /* bad pointer / shape / radius / level count   */
+  DXR_EUNSUPPORTED = 2,  /* valid request this build does not implement  */
+  DXR_EHIP = -1          /* a HIP launch failed; see dxr_last_hip_error() */
+};
+
+enum dxr_dtype {
+  DXR_F32 = 0,
+  DXR_BF16 = 1          /* storage as IEEE bfloat16 bit patterns (uint16) */
+};
+
+/* ABI version of the loaded library (== DXR_ABI_VERSION it was built with). */
+int dxr_abi_version(void);
+
+/* Human-readable name of a dxr_status value. */
+const char* dxr_status_string(int status);
+
+/* hipError_t of the most recent failed launch on the calling thread. */
+int dxr_last_hip_error(void);
+
+/* Elements (not bytes) of a num_levels pyramid for B pairs of H x W fmaps. */
+int64_t dxr_pyramid_numel(int64_t B, int64_t H, int64_t W, int num_levels);
+
+/* Element offset of level `level` inside that pyramid buffer. */
+int64_t dxr_pyramid_level_offset(int64_t B, int64_t H, int64_t W, int level);
+
+/*
+ * Stage (a)+(b): all-pairs correlation fmap1^T . fmap2 / divisor and its
+ * avg-pool pyramid, written in one pass (pooling fused into the MFMA epilogue).
+ *   fmap1, fmap2 : [B, D, H, W], dtype in_dtype (DXR_F32 or DXR_BF16)
+ *   divisor      : the reference divides by sqrt(D) (core/corr.py:60)
+ *   pyramid      : dxr_pyramid_numel(B,H,W,num_levels) elements of pyr_dtype
+ *   num_levels   : >= 1; every level must be at least 1 x 1
+ * DXR_F32 inputs compute with exact-f32 MFMA (v_mfma_f32_32x32x2_f32); DXR_BF16
+ * inputs use bf16 MFMA with f32 accumulation.
+ */
+int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int in_dtype,
+                           int64_t B, int64_t D, int64_t H, int64_t W,
+                           int num_levels, float divisor,
+                           void* pyramid, int pyr_dtype, hipStream_t stream);
+
+/*
+ * Stage (c): radius-r bilinear lookup of every level around coords / 2^l.
+ *   pyramid : as produced by dxr_corr_pyramid_build
+ *   coords  : [B, 2, H, W] float32
+ *   out     : [B, num_levels*(2r+1)^2, H, W] float32
+ * A level with H_l == 1 or W_l == 1 yields NaN, as the reference does
+ * (bilinear_sampler divides by H_l-1 / W_l-1, core/utils/utils.py:61-62).
+ */
+int dxr_corr_lookup(const void* pyramid, int pyr_dtype,
+                    int64_t B, int64_t H, int64_t W, int num_levels, int radius,
+                    const float* coords, float* out, hipStream_t stream);
+
+/*
+ * 2x2 / stride-2 average pool, floor mode, of [planes, H, W] float32 into
+ * [planes, H/2, W/2] (F.avg_pool2d(x, 2, stride=2), core/corr.py:26,70-71).
+ */
+int dxr_avg_pool2x2(const float* in, float* out, int64_t planes,
+                    int64_t H, int64_t W, hipStream_t stream);
+
+/*
+ * Stage (d), reference-FFI form: alt_cuda_corr.forward(fmap1, fmap2, coords,
+ * radius) with the reference's layouts (see the header comment).  `corr` is
+ * fully overwritten (the reference zero-fills then accumulates).
+ */
+int dxr_alt_corr_forward(const float* fmap1, const float* fmap2,
+                         const float* coords, float* corr,
+                         int64_t B, int64_t H1, int64_t W1, int64_t H2,
+                         int64_t W2, int64_t C, int64_t Nc, int radius,
+                         hipStream_t stream);
+
+/*
+ * Stage (d), fused form used by AlternateCorrBlock.__call__: every level in one
+ * launch, output already divided by `divisor`, written in CorrBlock's layout.
+ *   fmap1        : [B, H, W, C] full resolution (NHWC)
+ *   fmap2_levels : num_levels pointers; level l is [B, H_l, W_l, C] (NHWC),
+ *                  H_l = floor(H_{l-1}/2)
+ *   coords       : [B, 2, H, W] float32 (CorrBlock convention)
+ *   out          : [B, num_levels*(2r+1)^2, H, W] float32
+ */
+int dxr_alt_corr_lookup(const float* fmap1, const float* const* fmap2_levels,
+                        const float* coords, float* out,
+                        int64_t B, int64_t H, int64_t W, int64_t C,
+                        int num_levels, int radius, float divisor,
+                        hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DEXIRAFT_CORR_H */

@@ -1,0 +1,90 @@
+"""ctypes binding of libdexiraft_corr.so (C-ABI: include/dexiraft_corr.h).
+
+The shared object is loaded only after ``import torch`` so that its
+``libamdhip64.so.7`` dependency resolves to the HIP runtime torch already
+loaded: device pointers and streams are then shared with torch's allocator.
+There is no fallback: if the library is missing or a call fails, an exception
+is raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+LIB_PATH = Path(__file__).resolve().with_name("libdexiraft_corr.so")
+ABI_VERSION = 1
+
+DXR_OK, DXR_EINVAL, DXR_EUNSUPPORTED, DXR_EHIP = 0, 1, 2, -1
+DXR_F32, DXR_BF16 = 0, 1
+
+# Every symbol include/dexiraft_corr.h declares, with its ctypes signature.
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+_vp = ctypes.c_void_p
+_f32 = ctypes.c_float
+SIGNATURES: dict[str, tuple[object, list[object]]] = {
+    "dxr_abi_version": (_int, []),
+    "dxr_status_string": (ctypes.c_char_p, [_int]),
+    "dxr_last_hip_error": (_int, []),
+    "dxr_pyramid_numel": (_i64, [_i64, _i64, _i64, _int]),
+    "dxr_pyramid_level_offset": (_i64, [_i64, _i64, _i64, _int]),
+    "dxr_corr_pyramid_build": (_int, [_vp, _vp, _int, _i64, _i64, _i64, _i64, _int, _f32,
+                                      _vp, _int, _vp]),
+    "dxr_corr_lookup": (_int, [_vp, _int, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp]),
+    "dxr_avg_pool2x2": (_int, [_vp, _vp, _i64, _i64, _i64, _vp]),
+    "dxr_alt_corr_forward": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64,
+                                    _i64, _int, _vp]),
+    "dxr_alt_corr_lookup": (_int, [_vp, ctypes.POINTER(_vp), _vp, _vp, _i64, _i64, _i64, _i64,
+                                   _int, _int, _f32, _vp]),
+}
+
+_lock = threading.Lock()
+_lib: ctypes.CDLL | None = None
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and return the native library; raise if it is unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not LIB_PATH.exists():
+                raise ImportError(
+                    f"{LIB_PATH.name} not found next to {Path(__file__).name}; build it with "
+                    "`python optical-flow_dexi-raft_amd/build.py` (hipcc, gfx950)")
+            lib = ctypes.CDLL(str(LIB_PATH))
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            ver = lib.dxr_abi_version()
+            if ver != ABI_VERSION:
+                raise ImportError(f"{LIB_PATH.name} ABI {ver} != expected {ABI_VERSION}; rebuild")
+            _lib = lib
+    return _lib
+
+
+def check(status: int, what: str) -> None:
+    """Raise the exception the reference would raise for a failed call."""
+    if status == DXR_OK:
+        return
+    lib = load()
+    msg = lib.dxr_status_string(status).decode()
+    if status == DXR_EHIP:
+        raise RuntimeError(f"{what}: HIP error {lib.dxr_last_hip_error()} ({msg})")
+    if status == DXR_EUNSUPPORTED:
+        raise NotImplementedError(f"{what}: {msg}")
+    raise RuntimeError(f"{what}: {msg}")
+
+
+def stream_of(t: torch.Tensor) -> int:
+    """hipStream_t (as int) of torch's current stream on t's device."""
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,94 @@
+"""Build libdexiraft_corr.so (HIP, gfx950) in-tree.
+
+Every ``csrc/*.hip`` file is compiled with ``hipcc --offload-arch=gfx950`` into
+``build/*.o`` and linked into ``libdexiraft_corr.so`` next to this file, so the
+shared object travels with the repository snapshot to the GPU box.  No torch
+headers are involved: the library is a plain C-ABI (include/dexiraft_corr.h).
+
+Usage: ``python optical-flow_dexi-raft_amd/build.py [--force] [--asm]``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+REPO_DIR = PKG_DIR.parent
+CSRC = PKG_DIR / "csrc"
+INCLUDE = REPO_DIR / "include"
+BUILD_DIR = PKG_DIR / "build"
+LIB_NAME = "libdexiraft_corr.so"
+LIB_PATH = PKG_DIR / LIB_NAME
+ARCH = "gfx950"
+
+CXXFLAGS = [
+    "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
+    "-Wall", "-Wno-unused-function",
+    f"-I{INCLUDE}", f"-I{CSRC}",
+]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found: the HIP toolchain (/opt/rocm) is required to build")
+
+
+def _sources() -> list[Path]:
+    return sorted(CSRC.glob("*.hip"))
+
+
+def _deps() -> list[Path]:
+    return _sources() + sorted(CSRC.glob("*.h")) + sorted(INCLUDE.glob("*.h")) + [Path(__file__)]
+
+
+def is_stale() -> bool:
+    if not LIB_PATH.exists():
+        return True
+    t = LIB_PATH.stat().st_mtime
+    return any(p.stat().st_mtime > t for p in _deps())
+
+
+def _compile(src: Path, extra: list[str]) -> Path:
+    obj = BUILD_DIR / (src.stem + ".o")
+    cmd = [hipcc(), *CXXFLAGS, *extra, "-c", str(src), "-o", str(obj)]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{' '.join(cmd)}\n{res.stderr}")
+    if res.stderr.strip():
+        sys.stderr.write(res.stderr)
+    return obj
+
+
+def build(force: bool = False, asm: bool = False, verbose: bool = False) -> Path:
+    """Compile and link the library if any source is newer than it."""
+    if not force and not asm and not is_stale():
+        return LIB_PATH
+    BUILD_DIR.mkdir(exist_ok=True)
+    extra = ["-save-temps=obj", "-Rpass-analysis=kernel-resource-usage"] if asm else []
+    srcs = _sources()
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(lambda s: _compile(s, extra), srcs))
+    tmp = LIB_PATH.with_suffix(".so.tmp")
+    cmd = [hipcc(), "-shared", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs)]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{res.stderr}")
+    os.replace(tmp, LIB_PATH)
+    if verbose:
+        print(f"built {LIB_PATH}")
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--asm", action="store_true", help="keep .s and print resource usage")
+    a = ap.parse_args()
+    build(force=a.force, asm=a.asm, verbose=True)

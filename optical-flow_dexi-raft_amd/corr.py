@@ -1,0 +1,248 @@
+"""MI355X-native drop-in for the reference ``core/corr.py``.
+
+``CorrBlock`` and ``AlternateCorrBlock`` keep the reference constructors and
+``__call__(coords)`` signatures (core/corr.py:12-91), so ``core/raft*.py`` and
+``core/update.py`` run unchanged on top of them.  All arithmetic happens in the
+HIP kernels of ``libdexiraft_corr.so``; the Python side only validates,
+allocates (from torch's caching allocator) and launches on torch's current
+stream.  There is no CPU path: host tensors raise.
+
+Differences from the reference, all loud:
+  * host (CPU) tensors raise ``RuntimeError`` instead of running on the CPU;
+  * inputs that would need autograd (``requires_grad`` under grad mode) raise
+    ``NotImplementedError`` — the reference trains through matmul / avg_pool /
+    grid_sample (train.py:175-178); the native backward is a listed next item.
+"""
+from __future__ import annotations
+
+import ctypes
+from functools import lru_cache
+
+import numpy as np
+import torch
+
+from . import _native as nat
+
+__all__ = ["CorrBlock", "AlternateCorrBlock"]
+
+
+@lru_cache(maxsize=None)
+def _sqrt_dim(dim: int) -> float:
+    # torch.sqrt(torch.tensor(dim).float()) (core/corr.py:60,91): f32 IEEE sqrt.
+    return float(np.sqrt(np.float32(dim), dtype=np.float32))
+
+
+def _require_device(t: torch.Tensor, name: str) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor, got {type(t).__name__}")
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            f"{name} is on {t.device}; dexiraft_amd runs only on HIP devices (no CPU path)")
+
+
+def _require_no_grad(*ts: torch.Tensor) -> None:
+    if torch.is_grad_enabled() and any(t.requires_grad for t in ts):
+        raise NotImplementedError(
+            "dexiraft_amd correlation is inference-only in this build: inputs require grad "
+            "(wrap the call in torch.no_grad() or detach the inputs)")
+
+
+def _fmap_geometry(fmap1: torch.Tensor, fmap2: torch.Tensor) -> tuple[int, int, int, int]:
+    _require_device(fmap1, "fmap1")
+    _require_device(fmap2, "fmap2")
+    if fmap1.dim() != 4 or fmap2.dim() != 4:
+        raise RuntimeError(f"fmaps must be [B, D, H, W]; got {tuple(fmap1.shape)} and "
+                           f"{tuple(fmap2.shape)}")
+    if fmap1.shape != fmap2.shape:
+        raise RuntimeError(f"fmap1 {tuple(fmap1.shape)} and fmap2 {tuple(fmap2.shape)} differ")
+    if fmap1.device != fmap2.device:
+        raise RuntimeError("fmap1 and fmap2 are on different devices")
+    if fmap1.dtype != fmap2.dtype:
+        raise RuntimeError(f"fmap dtypes differ: {fmap1.dtype} vs {fmap2.dtype}")
+    B, D, H, W = (int(s) for s in fmap1.shape)
+    return B, D, H, W
+
+
+def _level_sizes(H: int, W: int, num_levels: int) -> list[tuple[int, int]]:
+    sizes = [(H, W)]
+    for _ in range(num_levels - 1):
+        h, w = sizes[-1]
+        if h < 2 or w < 2:
+            # F.avg_pool2d raises here in the reference (core/corr.py:26).
+            raise RuntimeError(
+                f"pyramid level {len(sizes)} of a {H}x{W} fmap would be empty "
+                f"(avg_pool2d of {h}x{w}); num_levels={num_levels} is too many")
+        sizes.append((h // 2, w // 2))
+    return sizes
+
+
+class _Launch:
+    """Runs a native call with fmap's device current (multi-GPU processes)."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self._ctx = None
+
+    def __enter__(self):
+        if self.device.index is not None and self.device.index != torch.cuda.current_device():
+            self._ctx = torch.cuda.device(self.device)
+            self._ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self._ctx is not None:
+            self._ctx.__exit__(*exc)
+        return False
+
+
+def _check_coords(coords: torch.Tensor, B: int, H: int, W: int, device: torch.device) -> torch.Tensor:
+    _require_device(coords, "coords")
+    _require_no_grad(coords)
+    if coords.dim() != 4 or tuple(coords.shape) != (B, 2, H, W):
+        raise RuntimeError(f"coords must be [B, 2, H, W] = {(B, 2, H, W)}, got {tuple(coords.shape)}")
+    if coords.device != device:
+        raise RuntimeError(f"coords on {coords.device}, correlation block on {device}")
+    if coords.dtype != torch.float32:
+        coords = coords.float()
+    return coords.contiguous()
+
+
+class CorrBlock:
+    """All-pairs correlation pyramid + radius-r lookup (reference core/corr.py:12-60).
+
+    ``CorrBlock(fmap1, fmap2, num_levels=4, radius=4)`` builds the 4-level
+    pyramid of ``fmap1^T fmap2 / sqrt(D)`` in one fused MFMA launch
+    (``dxr_corr_pyramid_build``); each ``__call__(coords)`` is one lookup launch
+    (``dxr_corr_lookup``) returning a new contiguous float32
+    ``[B, num_levels*(2r+1)^2, H, W]`` tensor in the reference's channel order.
+
+    fp32 fmaps (the reference's dtype, core/raft.py:139-142) compute with exact
+    f32 MFMA and store an f32 pyramid; ``corr_pyramid`` then holds the
+    reference-layout ``[B*H*W, 1, H_l, W_l]`` levels as views of one buffer.
+    """
+
+    def __init__(self, fmap1, fmap2, num_levels=4, radius=4):
+        self.num_levels = num_levels
+        self.radius = radius
+        B, D, H, W = _fmap_geometry(fmap1, fmap2)
+        _require_no_grad(fmap1, fmap2)
+        if not isinstance(num_levels, int) or num_levels < 1:
+            raise ValueError(f"num_levels must be a positive int, got {num_levels!r}")
+        if not isinstance(radius, int) or radius < 0:
+            raise ValueError(f"radius must be a non-negative int, got {radius!r}")
+        sizes = _level_sizes(H, W, num_levels)
+        if fmap1.dtype == torch.float32:
+            in_dt, pyr_dt, pyr_torch = nat.DXR_F32, nat.DXR_F32, torch.float32
+        elif fmap1.dtype == torch.bfloat16:
+            in_dt, pyr_dt, pyr_torch = nat.DXR_BF16, nat.DXR_BF16, torch.bfloat16
+        else:
+            raise RuntimeError(f"fmaps must be float32 or bfloat16, got {fmap1.dtype}")
+        self._geom = (B, D, H, W)
+        self._pyr_dt = pyr_dt
+        self._device = fmap1.device
+        lib = nat.load()
+        numel = lib.dxr_pyramid_numel(B, H, W, num_levels)
+        self._buf = torch.empty(numel, dtype=pyr_torch, device=fmap1.device)
+        f1 = fmap1.contiguous()
+        f2 = fmap2.contiguous()
+        with _Launch(self._device):
+            st = lib.dxr_corr_pyramid_build(
+                f1.data_ptr(), f2.data_ptr(), in_dt, B, D, H, W, num_levels, _sqrt_dim(D),
+                self._buf.data_ptr(), pyr_dt, nat.stream_of(f1))
+        nat.check(st, "CorrBlock build (dxr_corr_pyramid_build)")
+        N = H * W
+        self.corr_pyramid = []
+        for lvl, (h, w) in enumerate(sizes):
+            off = lib.dxr_pyramid_level_offset(B, H, W, lvl)
+            self.corr_pyramid.append(self._buf[off:off + B * N * h * w].view(B * N, 1, h, w))
+
+    def __call__(self, coords):
+        B, D, H, W = self._geom
+        c = _check_coords(coords, B, H, W, self._device)
+        rd = 2 * self.radius + 1
+        out = torch.empty((B, self.num_levels * rd * rd, H, W), dtype=torch.float32,
+                          device=self._device)
+        lib = nat.load()
+        with _Launch(self._device):
+            st = lib.dxr_corr_lookup(self._buf.data_ptr(), self._pyr_dt, B, H, W,
+                                     self.num_levels, self.radius, c.data_ptr(),
+                                     out.data_ptr(), nat.stream_of(c))
+        nat.check(st, "CorrBlock lookup (dxr_corr_lookup)")
+        return out
+
+    @staticmethod
+    def corr(fmap1, fmap2):
+        """``[B, H, W, 1, H, W]`` volume ``fmap1^T fmap2 / sqrt(D)`` (core/corr.py:52-60)."""
+        B, D, H, W = _fmap_geometry(fmap1, fmap2)
+        _require_no_grad(fmap1, fmap2)
+        if fmap1.dtype != torch.float32:
+            raise RuntimeError(f"CorrBlock.corr expects float32 fmaps, got {fmap1.dtype}")
+        out = torch.empty((B, H, W, 1, H, W), dtype=torch.float32, device=fmap1.device)
+        f1, f2 = fmap1.contiguous(), fmap2.contiguous()
+        lib = nat.load()
+        with _Launch(fmap1.device):
+            st = lib.dxr_corr_pyramid_build(f1.data_ptr(), f2.data_ptr(), nat.DXR_F32, B, D, H,
+                                            W, 1, _sqrt_dim(D), out.data_ptr(), nat.DXR_F32,
+                                            nat.stream_of(f1))
+        nat.check(st, "CorrBlock.corr (dxr_corr_pyramid_build)")
+        return out
+
+
+class AlternateCorrBlock:
+    """On-the-fly correlation lookup (reference core/corr.py:63-91 + alt_cuda_corr).
+
+    Memory is O(H*W*D) instead of O((H*W)^2): only pooled fmaps are kept and each
+    ``__call__`` computes the (2r+2)^2 window dot products of every level in one
+    launch (``dxr_alt_corr_lookup``), already divided by sqrt(D).  As in the
+    reference, the constructor pools ``num_levels`` times, so fmaps smaller than
+    2^num_levels in either dimension raise (core/corr.py:69-71).
+    """
+
+    def __init__(self, fmap1, fmap2, num_levels=4, radius=4):
+        self.num_levels = num_levels
+        self.radius = radius
+        B, D, H, W = _fmap_geometry(fmap1, fmap2)
+        _require_no_grad(fmap1, fmap2)
+        if fmap1.dtype != torch.float32:
+            raise RuntimeError(f"AlternateCorrBlock expects float32 fmaps, got {fmap1.dtype}")
+        if not isinstance(num_levels, int) or num_levels < 1:
+            raise ValueError(f"num_levels must be a positive int, got {num_levels!r}")
+        if not isinstance(radius, int) or radius < 0:
+            raise ValueError(f"radius must be a non-negative int, got {radius!r}")
+        _level_sizes(H, W, num_levels + 1)  # the reference pools num_levels times
+        self._geom = (B, D, H, W)
+        self._device = fmap1.device
+        lib = nat.load()
+        f1, f2 = fmap1.contiguous(), fmap2.contiguous()
+        self.pyramid = [(f1, f2)]
+        with _Launch(self._device):
+            stream = nat.stream_of(f1)
+            for _ in range(num_levels):
+                p1, p2 = self.pyramid[-1]
+                h, w = p1.shape[-2:]
+                q1 = torch.empty((B, D, h // 2, w // 2), dtype=torch.float32, device=f1.device)
+                q2 = torch.empty_like(q1)
+                for src, dst in ((p1, q1), (p2, q2)):
+                    st = lib.dxr_avg_pool2x2(src.data_ptr(), dst.data_ptr(), B * D, h, w, stream)
+                    nat.check(st, "AlternateCorrBlock pooling (dxr_avg_pool2x2)")
+                self.pyramid.append((q1, q2))
+        # Channels-last copies once per block (the reference re-permutes on every
+        # call, core/corr.py:82-83): one coalesced 1 KiB vector per cell.
+        self._f1_nhwc = f1.permute(0, 2, 3, 1).contiguous()
+        self._f2_nhwc = [self.pyramid[i][1].permute(0, 2, 3, 1).contiguous()
+                         for i in range(num_levels)]
+        self._f2_ptrs = (ctypes.c_void_p * num_levels)(*[t.data_ptr() for t in self._f2_nhwc])
+
+    def __call__(self, coords):
+        B, D, H, W = self._geom
+        c = _check_coords(coords, B, H, W, self._device)
+        rd = 2 * self.radius + 1
+        out = torch.empty((B, self.num_levels * rd * rd, H, W), dtype=torch.float32,
+                          device=self._device)
+        lib = nat.load()
+        with _Launch(self._device):
+            st = lib.dxr_alt_corr_lookup(self._f1_nhwc.data_ptr(), self._f2_ptrs, c.data_ptr(),
+                                         out.data_ptr(), B, H, W, D, self.num_levels,
+                                         self.radius, _sqrt_dim(D), nat.stream_of(c))
+        nat.check(st, "AlternateCorrBlock lookup (dxr_alt_corr_lookup)")
+        return out

@@ -1,0 +1,15 @@
+"""CPU oracle for the RAFT correlation path — TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import this package, and only as the checker / the timed CPU baseline.
+The product (``dexiraft_amd``) never imports it and has no CPU fallback.
+
+Parity pinning: the restatement is checked against golden vectors produced by
+importing the reference ``core/corr.py`` in the build container
+(``tests/golden/make_golden.py``); see ``tests/test_oracle_golden.py``.
+"""
+from .corr_oracle import (alt_corr_block, alt_corr_forward, avg_pool2x2, bilinear_sample,
+                          corr_lookup, corr_pyramid, corr_volume, sample_coord)
+
+__all__ = ["alt_corr_block", "alt_corr_forward", "avg_pool2x2", "bilinear_sample",
+           "corr_lookup", "corr_pyramid", "corr_volume", "sample_coord"]

@@ -1,0 +1,338 @@
+"""GPU parity tests: HIP kernels (through the C-ABI) vs the reference's golden
+vectors and the oracle.  Tolerances (north star, BASELINE.json):
+  * fp32 pyramid: |ours - ref| <= 1e-4 * max|ref| per level;
+  * lookup on our own pyramid: same 1e-4-of-max bound;
+  * lookup on the reference's pyramid: bit-exact (same arithmetic as ATen's CPU
+    grid sampler, incl. its fused-multiply-add chain);
+  * integer/index properties (symmetry, batching, determinism, pooling of an
+    exactly representable volume): bit-exact.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import datagen as dg
+import oracle
+from conftest import large_cases, load_large, load_tiny, tiny_cases, tolerance_check
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-4
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def dx():
+    import dexiraft_amd
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    dexiraft_amd.load_native()
+    return dexiraft_amd
+
+
+def _t(a: np.ndarray) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+# --------------------------------------------------------------------------- tiny cases
+@pytest.mark.parametrize("name", tiny_cases())
+def test_pyramid_matches_reference(dx, name):
+    d = load_tiny(name)
+    cb = dx.CorrBlock(_t(d["fmap1"]), _t(d["fmap2"]), num_levels=d["num_levels"], radius=d["radius"])
+    rows = torch.from_numpy(d["pyr_rows"]).to(DEV)
+    assert len(cb.corr_pyramid) == d["num_levels"]
+    for lvl in range(d["num_levels"]):
+        ref = d[f"pyr{lvl}"]
+        got = cb.corr_pyramid[lvl][rows, 0].cpu().numpy()
+        tolerance_check(got, ref, RTOL)
+
+
+@pytest.mark.parametrize("name", tiny_cases())
+def test_lookup_matches_reference(dx, name):
+    d = load_tiny(name)
+    cb = dx.CorrBlock(_t(d["fmap1"]), _t(d["fmap2"]), num_levels=d["num_levels"], radius=d["radius"])
+    for k in range(d["n_coords"]):
+        out = cb(_t(d[f"coords{k}"]))
+        assert out.is_contiguous() and out.dtype == torch.float32
+        tolerance_check(out.cpu().numpy(), d[f"out{k}"], RTOL)
+
+
+@pytest.mark.parametrize("name", [n for n in tiny_cases()
+                                  if len(load_tiny(n)["pyr_rows"]) == load_tiny(n)["B"] *
+                                  load_tiny(n)["H"] * load_tiny(n)["W"]])
+def test_lookup_bitexact_on_reference_pyramid(dx, name):
+    """dxr_corr_lookup on the reference's own pyramid reproduces its bits."""
+    d = load_tiny(name)
+    from dexiraft_amd import _native as nat
+    lib = nat.load()
+    B, H, W, L, r = d["B"], d["H"], d["W"], d["num_levels"], d["radius"]
+    buf = torch.cat([_t(d[f"pyr{lvl}"]).reshape(-1) for lvl in range(L)])
+    assert buf.numel() == lib.dxr_pyramid_numel(B, H, W, L)
+    rd = 2 * r + 1
+    for k in range(d["n_coords"]):
+        c = _t(d[f"coords{k}"])
+        out = torch.empty((B, L * rd * rd, H, W), device=DEV)
+        st = lib.dxr_corr_lookup(buf.data_ptr(), nat.DXR_F32, B, H, W, L, r, c.data_ptr(),
+                                 out.data_ptr(), nat.stream_of(c))
+        assert st == 0
+        got, ref = out.cpu().numpy(), d[f"out{k}"]
+        assert np.array_equal(np.isnan(got), np.isnan(ref))
+        fin = ~np.isnan(ref)
+        assert np.array_equal(got[fin], ref[fin]), \
+            f"max diff {np.abs(got[fin] - ref[fin]).max():.3e}"
+
+
+@pytest.mark.parametrize("name", ["fnet", "ragged", "levels2_r1"])
+def test_corr_static_method(dx, name):
+    d = load_tiny(name)
+    vol = dx.CorrBlock.corr(_t(d["fmap1"]), _t(d["fmap2"]))
+    B, H, W = d["B"], d["H"], d["W"]
+    assert tuple(vol.shape) == (B, H, W, 1, H, W)
+    got = vol.reshape(B * H * W, H, W)[torch.from_numpy(d["pyr_rows"]).to(DEV)].cpu().numpy()
+    tolerance_check(got, d["pyr0"], RTOL)
+
+
+# --------------------------------------------------------------------------- benchmark shapes
+@pytest.mark.parametrize("name", large_cases())
+def test_large_shapes_against_reference_checksums(dx, name):
+    d = load_large(name)
+    B, D, H, W, r = d["B"], d["D"], d["H"], d["W"], d["radius"]
+    f1 = dg.fmap(d["fmap_seeds"][0], B, D, H, W, d["dist"])
+    f2 = dg.fmap(d["fmap_seeds"][1], B, D, H, W, d["dist"])
+    # generator drift would invalidate the comparison: pin the inputs first
+    np.testing.assert_allclose([f1.astype(np.float64).sum(), f2.astype(np.float64).sum()],
+                               d["fmap_checksum"], rtol=0, atol=1e-6)
+    cb = dx.CorrBlock(_t(f1), _t(f2), radius=r)
+    for lvl in range(4):
+        a = cb.corr_pyramid[lvl].reshape(-1)
+        maxabs = float(d[f"pyr{lvl}_maxabs"])
+        got = a[torch.from_numpy(d[f"pyr{lvl}_idx"]).to(DEV)].cpu().numpy()
+        assert np.abs(got - d[f"pyr{lvl}_val"]).max() <= RTOL * maxabs
+        s = a.double().sum().item()
+        s2 = (a.double() ** 2).sum().item()
+        ref_s, ref_s2 = d[f"pyr{lvl}_sum"]
+        assert abs(s - ref_s) <= 1e-6 * (abs(ref_s) + a.numel() * maxabs * 1e-3)
+        assert abs(s2 - ref_s2) <= 1e-5 * ref_s2
+        assert abs(a.abs().max().item() - maxabs) <= RTOL * maxabs
+    for k, (mode, scale, seed) in enumerate(d["coords"]):
+        c = dg.coords(int(seed), B, H, W, mode, float(scale))
+        assert abs(c.astype(np.float64).sum() - float(d[f"coords{k}_checksum"])) < 1e-3
+        out = cb(_t(c))
+        maxabs = float(d[f"out{k}_maxabs"])
+        got = out.reshape(-1)[torch.from_numpy(d[f"out{k}_idx"]).to(DEV)].cpu().numpy()
+        assert np.abs(got - d[f"out{k}_val"]).max() <= RTOL * maxabs
+        chsum = out.double().sum(dim=(0, 2, 3)).cpu().numpy()
+        np.testing.assert_allclose(chsum, d[f"out{k}_chsum"], rtol=0,
+                                   atol=1e-6 * B * H * W * maxabs)
+
+
+# --------------------------------------------------------------------------- properties
+def _pair(B=1, D=256, H=55, W=128, seed=0, dist="normal"):
+    return (_t(dg.fmap(seed, B, D, H, W, dist)), _t(dg.fmap(seed + 1, B, D, H, W, dist)))
+
+
+def test_symmetry_bitexact(dx):
+    """corr(f1, f2)[i, j] == corr(f2, f1)[j, i]: same k-ordered f32 chain."""
+    f1, f2 = _pair(H=23, W=40, seed=3)
+    a = dx.CorrBlock.corr(f1, f2).reshape(920, 920)
+    b = dx.CorrBlock.corr(f2, f1).reshape(920, 920)
+    assert torch.equal(a, b.t())
+
+
+def test_batch_independence_and_determinism(dx):
+    f1, f2 = _pair(B=3, H=30, W=44, seed=5, dist="fnet")
+    cbb = dx.CorrBlock(f1, f2)
+    cbb2 = dx.CorrBlock(f1, f2)
+    c = _t(dg.coords(9, 3, 30, 44, "normal", 4.0))
+    ob = cbb(c)
+    assert torch.equal(ob, cbb2(c))
+    for lvl in range(4):
+        assert torch.equal(cbb.corr_pyramid[lvl], cbb2.corr_pyramid[lvl])
+    n = 30 * 44
+    for b in range(3):
+        cb1 = dx.CorrBlock(f1[b:b + 1], f2[b:b + 1])
+        for lvl in range(4):
+            assert torch.equal(cb1.corr_pyramid[lvl], cbb.corr_pyramid[lvl][b * n:(b + 1) * n])
+        assert torch.equal(cb1(c[b:b + 1]), ob[b:b + 1])
+
+
+def test_linearity_bitexact(dx):
+    f1, f2 = _pair(H=21, W=36, seed=11)
+    a = dx.CorrBlock(f1, f2)
+    b = dx.CorrBlock(2.0 * f1, f2)
+    for lvl in range(4):
+        assert torch.equal(b.corr_pyramid[lvl], 2.0 * a.corr_pyramid[lvl])
+
+
+def test_fused_pooling_matches_torch_avg_pool(dx):
+    f1, f2 = _pair(H=55, W=128, seed=21)
+    cb = dx.CorrBlock(f1, f2)
+    for lvl in range(1, 4):
+        ref = torch.nn.functional.avg_pool2d(cb.corr_pyramid[lvl - 1], 2, stride=2)
+        assert ref.shape == cb.corr_pyramid[lvl].shape
+        err = (ref - cb.corr_pyramid[lvl]).abs().max().item()
+        assert err <= 1e-6 * ref.abs().max().item()
+
+
+def test_integer_coords_sample_cells(dx):
+    """At integer coordinates the centre tap is the pyramid cell itself, up to the
+    few-ulp shift of the reference's normalise/unnormalise round trip."""
+    H, W = 40, 52
+    f1, f2 = _pair(H=H, W=W, seed=31)
+    cb = dx.CorrBlock(f1, f2)
+    c = _t(dg.coords(33, 1, H, W, "integer", 5.0))
+    out = cb(c)
+    cx = c[0, 0].long().reshape(-1)
+    cy = c[0, 1].long().reshape(-1)
+    ok = (cx >= 0) & (cx < W) & (cy >= 0) & (cy < H)
+    q = torch.arange(H * W, device=DEV)
+    lvl0 = cb.corr_pyramid[0][:, 0]
+    centre = out[0, 4 * 9 + 4].reshape(-1)  # ix = iy = r at level 0
+    ref = lvl0[q[ok], cy[ok], cx[ok]]
+    assert (centre[ok] - ref).abs().max().item() <= 1e-5 * lvl0.abs().max().item()
+    assert ok.float().mean().item() > 0.5
+    assert (centre[~ok].abs() <= 1e-5 * lvl0.abs().max().item()).all()
+
+
+def test_far_coords_give_zero_and_nan_coords_give_nan(dx):
+    f1, f2 = _pair(H=20, W=24, seed=41)
+    cb = dx.CorrBlock(f1, f2)
+    c = _t(dg.coords(43, 1, 20, 24, "far"))
+    assert torch.all(cb(c) == 0)
+    c2 = c.clone()
+    c2[0, 0, 3, 5] = float("nan")
+    o = cb(c2)
+    assert torch.all(torch.isnan(o[0, :, 3, 5]))
+    assert not torch.isnan(o[0, :, 3, 6]).any()
+    c3 = c.clone()
+    c3[0, 1, 0, 0] = float("inf")
+    assert torch.all(torch.isnan(cb(c3)[0, :, 0, 0]))
+
+
+def test_full_size_against_oracle_float64(dx):
+    """Sintel shape, fnet-like data: whole pyramid + one lookup vs the float64 oracle."""
+    H, W = 55, 128
+    f1 = dg.fmap(51, 1, 256, H, W, "fnet")
+    f2 = dg.fmap(52, 1, 256, H, W, "fnet")
+    c = dg.coords(53, 1, H, W, "normal", 4.0)
+    pyr = oracle.corr_pyramid(f1, f2, 4, np.float64)
+    cb = dx.CorrBlock(_t(f1), _t(f2))
+    for lvl in range(4):
+        tolerance_check(cb.corr_pyramid[lvl][:, 0].cpu().numpy(), pyr[lvl], RTOL)
+    ref = oracle.corr_lookup(pyr, c, 4)
+    tolerance_check(cb(_t(c)).cpu().numpy(), ref, RTOL)
+
+
+# --------------------------------------------------------------------------- alternate path
+def test_alternate_block_matches_reference_corrblock(dx):
+    d = load_tiny("batch2_alt")
+    ab = dx.AlternateCorrBlock(_t(d["fmap1"]), _t(d["fmap2"]), radius=d["radius"])
+    assert len(ab.pyramid) == 5
+    for k in range(d["n_coords"]):
+        tolerance_check(ab(_t(d[f"coords{k}"])).cpu().numpy(), d[f"out{k}"], RTOL)
+
+
+@pytest.mark.parametrize("shape", [(1, 64, 24, 32, 4), (2, 37, 17, 19, 3)])
+def test_alternate_block_matches_oracle(dx, shape):
+    B, D, H, W, r = shape
+    f1 = dg.fmap(61, B, D, H, W)
+    f2 = dg.fmap(62, B, D, H, W)
+    c = dg.coords(63, B, H, W, "uniform", 9.0)
+    ref = oracle.alt_corr_block(f1, f2, c, 4, r, np.float64)
+    got = dx.AlternateCorrBlock(_t(f1), _t(f2), radius=r)(_t(c)).cpu().numpy()
+    tolerance_check(got, ref, RTOL)
+
+
+def test_alt_cuda_corr_forward_ffi(dx):
+    """Reference FFI form: NHWC fmaps, [B, N, H, W, 2] coords, H2 != H1."""
+    B, H1, W1, H2, W2, C, N, r = 2, 9, 13, 7, 11, 64, 2, 3
+    f1 = dg.normal(71, B * H1 * W1 * C).reshape(B, H1, W1, C).astype(np.float32)
+    f2 = dg.normal(72, B * H2 * W2 * C).reshape(B, H2, W2, C).astype(np.float32)
+    c = (dg.uniform(73, B * N * H1 * W1 * 2).reshape(B, N, H1, W1, 2) * 14 - 2).astype(np.float32)
+    ref = oracle.alt_corr_forward(f1, f2, c, r, np.float64)
+    (got,) = dx.alt_cuda_corr.forward(_t(f1), _t(f2), _t(c), r)
+    assert tuple(got.shape) == (B, N, (2 * r + 1) ** 2, H1, W1)
+    tolerance_check(got.cpu().numpy(), ref, RTOL)
+    with pytest.raises(RuntimeError):
+        dx.alt_cuda_corr.forward(_t(f1).transpose(1, 2), _t(f2), _t(c), r)
+
+
+def test_alternate_block_too_small_raises_like_reference(dx):
+    f1, f2 = _pair(H=15, W=40, seed=81)
+    with pytest.raises(RuntimeError):
+        dx.AlternateCorrBlock(f1, f2)
+
+
+# --------------------------------------------------------------------------- edge cases / API
+def test_empty_batch(dx):
+    f = torch.empty((0, 256, 20, 24), device=DEV)
+    cb = dx.CorrBlock(f, f)
+    out = cb(torch.empty((0, 2, 20, 24), device=DEV))
+    assert tuple(out.shape) == (0, 324, 20, 24)
+
+
+def test_too_small_fmap_raises(dx):
+    f1, f2 = _pair(H=7, W=30, seed=91)
+    with pytest.raises(RuntimeError):
+        dx.CorrBlock(f1, f2)          # level 3 of a 7-row map is empty
+    cb = dx.CorrBlock(f1, f2, num_levels=3)  # 7 -> 3 -> 1: fine
+    assert cb.corr_pyramid[2].shape[-2:] == (1, 7)
+
+
+def test_noncontiguous_inputs(dx):
+    f1, f2 = _pair(H=24, W=30, seed=93)
+    c = _t(dg.coords(94, 1, 24, 30, "normal", 3.0))
+    ref = dx.CorrBlock(f1, f2)(c)
+    g1 = f1.permute(0, 2, 3, 1).contiguous().permute(0, 3, 1, 2)
+    cnc = c.permute(0, 2, 3, 1).contiguous().permute(0, 3, 1, 2)
+    assert not g1.is_contiguous() and not cnc.is_contiguous()
+    assert torch.equal(dx.CorrBlock(g1, f2)(cnc), ref)
+
+
+def test_radius_and_levels_variants(dx):
+    H, W = 32, 40
+    f1 = dg.fmap(95, 1, 64, H, W)
+    f2 = dg.fmap(96, 1, 64, H, W)
+    c = dg.coords(97, 1, H, W, "normal", 3.0)
+    for L, r in ((1, 0), (2, 2), (4, 6), (6, 1)):
+        pyr = oracle.corr_pyramid(f1, f2, L, np.float64)
+        ref = oracle.corr_lookup(pyr, c, r)
+        got = dx.CorrBlock(_t(f1), _t(f2), num_levels=L, radius=r)(_t(c)).cpu().numpy()
+        tolerance_check(got, ref, RTOL)
+
+
+def test_grad_inputs_raise(dx):
+    f1, f2 = _pair(H=16, W=16, seed=98)
+    f1.requires_grad_(True)
+    with pytest.raises(NotImplementedError):
+        dx.CorrBlock(f1, f2)
+    with torch.no_grad():
+        dx.CorrBlock(f1, f2)
+
+
+def test_bad_coords_shape_raises(dx):
+    f1, f2 = _pair(H=16, W=16, seed=99)
+    cb = dx.CorrBlock(f1, f2)
+    with pytest.raises(RuntimeError):
+        cb(torch.zeros((1, 2, 16, 15), device=DEV))
+
+
+def test_side_stream(dx):
+    f1, f2 = _pair(H=30, W=40, seed=101)
+    c = _t(dg.coords(102, 1, 30, 40, "normal", 3.0))
+    ref = dx.CorrBlock(f1, f2)(c)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        out = dx.CorrBlock(f1, f2)(c)
+    torch.cuda.current_stream().wait_stream(s)
+    assert torch.equal(out, ref)
+
+
+def test_native_library_is_the_one_loaded(dx):
+    """The in-tree .so is mapped into this process (no silent fallback)."""
+    maps = open("/proc/self/maps").read()
+    assert str(dx.LIB_PATH) in maps
