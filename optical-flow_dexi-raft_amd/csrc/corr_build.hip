@@ -19,6 +19,9 @@
 // exchange between lane halves (lane ^ 32).  Floor-mode pooling falls out of the
 // per-level bounds checks (a pooled cell is written only if it exists at that
 // level).
+#include <cmath>
+#include <cstdlib>
+
 #include "dxr_common.h"
 
 namespace {
@@ -26,10 +29,6 @@ namespace {
 constexpr int TH = 8;            // target tile rows   (image-2 rows)
 constexpr int TW = 16;           // target tile cols
 constexpr int NTGT = TH * TW;    // 128 targets per workgroup
-constexpr int WAVES = 4;         // waves split the query dimension
-constexpr int BM = 32 * WAVES;   // 128 queries per workgroup
-constexpr int BK = 16;           // K (= D) step staged through LDS
-constexpr int NTHR = 64 * WAVES;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -38,86 +37,83 @@ struct BuildGeom {
   int levels;           // fused levels (1..4)
   int tiles_w;          // ceil(W / TW)
   float divisor;        // sqrt(D) in the reference
+  float recip;          // 1/divisor when that is exact (power of two), else 0
   int lh[4], lw[4];     // level sizes
   long long loff[4];    // element offset of each level
 };
 
-// Global -> register staging of one BK slice of the query panel (A) and the
-// target tile (B).  VEC: W % 4 == 0, so every float4 is fully in or fully out.
-template <bool VEC>
+// Global -> register staging of one BK slice of the query panel (A: [BK][BM])
+// and the target tile (B: [BK][TH][TW]).  VEC: W % 4 == 0, so every float4 is
+// fully inside or fully outside the map.
+template <bool VEC, int WAVES, int BK>
 struct Stage {
-  float a[8];
-  float b[8];
+  static constexpr int NT = 64 * WAVES;
+  static constexpr int BM = 32 * WAVES;
+  static constexpr int NA = VEC ? BK * BM / 4 / NT : BK * BM / NT;    // per-thread units
+  static constexpr int NB = VEC ? BK * NTGT / 4 / NT : BK * NTGT / NT;
+  static_assert(NA >= 1 && NB >= 1, "tile too small for the thread count");
+  float a[VEC ? 4 * NA : NA];
+  float b[VEC ? 4 * NB : NB];
 
   __device__ __forceinline__ void load(const float* __restrict__ f1b,
                                        const float* __restrict__ f2b, int k0,
                                        int q0, int th0, int tw0,
                                        const BuildGeom& g, int tid) {
-    if constexpr (VEC) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int idx = tid + NTHR * s;
-        // A: [BK][BM] as float4 -> k = idx / 32, col4 = idx % 32
-        {
-          const int k = idx >> 5, c = (idx & 31) * 4;
-          const int kk = k0 + k, q = q0 + c;
-          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (kk < g.D && q < g.N)
-            v = *reinterpret_cast<const float4*>(f1b + (long long)kk * g.N + q);
-          a[4 * s + 0] = v.x; a[4 * s + 1] = v.y; a[4 * s + 2] = v.z; a[4 * s + 3] = v.w;
-        }
-        // B: [BK][TH][TW] as float4 -> k = idx / 32, row = (idx/4) % 8, col4 = idx % 4
-        {
-          const int k = idx >> 5, r = (idx >> 2) & 7, c = (idx & 3) * 4;
-          const int kk = k0 + k, hh = th0 + r, ww = tw0 + c;
-          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (kk < g.D && hh < g.H && ww < g.W)
-            v = *reinterpret_cast<const float4*>(f2b + (long long)kk * g.N + hh * g.W + ww);
-          b[4 * s + 0] = v.x; b[4 * s + 1] = v.y; b[4 * s + 2] = v.z; b[4 * s + 3] = v.w;
-        }
+    for (int s = 0; s < NA; ++s) {
+      const int idx = tid + NT * s;
+      if constexpr (VEC) {
+        const int k = idx / (BM / 4), c = (idx % (BM / 4)) * 4;
+        const int kk = k0 + k, q = q0 + c;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (kk < g.D && q < g.N)
+          v = *reinterpret_cast<const float4*>(f1b + (long long)kk * g.N + q);
+        a[4 * s + 0] = v.x; a[4 * s + 1] = v.y; a[4 * s + 2] = v.z; a[4 * s + 3] = v.w;
+      } else {
+        const int k = idx / BM, c = idx % BM;
+        const int kk = k0 + k, q = q0 + c;
+        a[s] = (kk < g.D && q < g.N) ? f1b[(long long)kk * g.N + q] : 0.f;
       }
-    } else {
+    }
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const int idx = tid + NTHR * s;
-        {
-          const int k = idx >> 7, c = idx & 127;
-          const int kk = k0 + k, q = q0 + c;
-          a[s] = (kk < g.D && q < g.N) ? f1b[(long long)kk * g.N + q] : 0.f;
-        }
-        {
-          const int k = idx >> 7, r = (idx >> 4) & 7, c = idx & 15;
-          const int kk = k0 + k, hh = th0 + r, ww = tw0 + c;
-          b[s] = (kk < g.D && hh < g.H && ww < g.W)
-                     ? f2b[(long long)kk * g.N + hh * g.W + ww] : 0.f;
-        }
+    for (int s = 0; s < NB; ++s) {
+      const int idx = tid + NT * s;
+      if constexpr (VEC) {
+        const int k = idx >> 5, r = (idx >> 2) & 7, c = (idx & 3) * 4;
+        const int kk = k0 + k, hh = th0 + r, ww = tw0 + c;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (kk < g.D && hh < g.H && ww < g.W)
+          v = *reinterpret_cast<const float4*>(f2b + (long long)kk * g.N + hh * g.W + ww);
+        b[4 * s + 0] = v.x; b[4 * s + 1] = v.y; b[4 * s + 2] = v.z; b[4 * s + 3] = v.w;
+      } else {
+        const int k = idx >> 7, r = (idx >> 4) & 7, c = idx & 15;
+        const int kk = k0 + k, hh = th0 + r, ww = tw0 + c;
+        b[s] = (kk < g.D && hh < g.H && ww < g.W) ? f2b[(long long)kk * g.N + hh * g.W + ww]
+                                                  : 0.f;
       }
     }
   }
 
-  __device__ __forceinline__ void store(float (*As)[BM], float (*Bs)[NTGT], int tid) {
-    if constexpr (VEC) {
+  __device__ __forceinline__ void store(float* As, float* Bs, int tid) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int idx = tid + NTHR * s;
-        {
-          const int k = idx >> 5, c = (idx & 31) * 4;
-          *reinterpret_cast<float4*>(&As[k][c]) =
-              make_float4(a[4 * s], a[4 * s + 1], a[4 * s + 2], a[4 * s + 3]);
-        }
-        {
-          const int k = idx >> 5, r = (idx >> 2) & 7, c = (idx & 3) * 4;
-          *reinterpret_cast<float4*>(&Bs[k][r * TW + c]) =
-              make_float4(b[4 * s], b[4 * s + 1], b[4 * s + 2], b[4 * s + 3]);
-        }
+    for (int s = 0; s < NA; ++s) {
+      const int idx = tid + NT * s;
+      if constexpr (VEC) {
+        const int k = idx / (BM / 4), c = (idx % (BM / 4)) * 4;
+        *reinterpret_cast<float4*>(As + k * BM + c) =
+            make_float4(a[4 * s], a[4 * s + 1], a[4 * s + 2], a[4 * s + 3]);
+      } else {
+        As[idx] = a[s];
       }
-    } else {
+    }
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const int idx = tid + NTHR * s;
-        As[idx >> 7][idx & 127] = a[s];
-        const int k = idx >> 7, r = (idx >> 4) & 7, c = idx & 15;
-        Bs[k][r * TW + c] = b[s];
+    for (int s = 0; s < NB; ++s) {
+      const int idx = tid + NT * s;
+      if constexpr (VEC) {
+        *reinterpret_cast<float4*>(Bs + idx * 4) =
+            make_float4(b[4 * s], b[4 * s + 1], b[4 * s + 2], b[4 * s + 3]);
+      } else {
+        Bs[idx] = b[s];
       }
     }
   }
@@ -134,12 +130,13 @@ __device__ __forceinline__ void store4(float* dst, const float* v, int nvalid, b
   }
 }
 
-template <bool VEC>
-__global__ __launch_bounds__(NTHR, 2) void corr_build_f32_kernel(
+template <bool VEC, int WAVES, int BK>
+__global__ __launch_bounds__(64 * WAVES) void corr_build_f32_kernel(
     const float* __restrict__ f1, const float* __restrict__ f2,
     float* __restrict__ pyr, BuildGeom g) {
-  __shared__ float As[2][BK][BM];
-  __shared__ float Bs[2][BK][NTGT];
+  constexpr int BM = 32 * WAVES;
+  constexpr int KP = BK / 2;                        // MFMA k-pairs per stage
+  __shared__ float lds[2 * BK * (BM + NTGT)];       // [buf][A: BK*BM | B: BK*NTGT]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -164,26 +161,40 @@ __global__ __launch_bounds__(NTHR, 2) void corr_build_f32_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
-  Stage<VEC> st;
+  auto As = [&](int buf) { return lds + buf * BK * (BM + NTGT); };
+  auto Bs = [&](int buf) { return lds + buf * BK * (BM + NTGT) + BK * BM; };
+
+  Stage<VEC, WAVES, BK> st;
   const int nk = (g.D + BK - 1) / BK;
   st.load(f1b, f2b, 0, q0, th0, tw0, g, tid);
-  st.store(As[0], Bs[0], tid);
+  st.store(As(0), Bs(0), tid);
   __syncthreads();
 
   for (int ks = 0; ks < nk; ++ks) {
     const int buf = ks & 1;
     if (ks + 1 < nk) st.load(f1b, f2b, (ks + 1) * BK, q0, th0, tw0, g, tid);
+    const float* a_s = As(buf);
+    const float* b_s = Bs(buf);
+    // Operand fragments are read one k-pair ahead of the MFMAs that use them,
+    // so the LDS latency hides under four 64-cycle MFMAs.
+    float bq[2], at[2][4];
+    bq[0] = a_s[khalf * BM + qry_off];
 #pragma unroll
-    for (int kp = 0; kp < BK / 2; ++kp) {
-      const int k = 2 * kp + khalf;
-      const float bq = As[buf][k][qry_off];
+    for (int t = 0; t < 4; ++t) at[0][t] = b_s[khalf * NTGT + 2 * t * TW + tgt_off];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const float at = Bs[buf][k][2 * t * TW + tgt_off];
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(at, bq, acc[t], 0, 0, 0);
+    for (int kp = 0; kp < KP; ++kp) {
+      const int cur = kp & 1, nxt = cur ^ 1;
+      if (kp + 1 < KP) {
+        const int k = 2 * (kp + 1) + khalf;
+        bq[nxt] = a_s[k * BM + qry_off];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) at[nxt][t] = b_s[k * NTGT + 2 * t * TW + tgt_off];
       }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(at[cur][t], bq[cur], acc[t], 0, 0, 0);
     }
-    if (ks + 1 < nk) st.store(As[buf ^ 1], Bs[buf ^ 1], tid);
+    if (ks + 1 < nk) st.store(As(buf ^ 1), Bs(buf ^ 1), tid);
     __syncthreads();
   }
 
@@ -195,10 +206,18 @@ __global__ __launch_bounds__(NTHR, 2) void corr_build_f32_kernel(
   if (qi >= g.N) return;
   const long long qimg = (long long)b * g.N + qi;
 
+  // x / sqrt(D): a multiply is bit-identical when 1/sqrt(D) is exact (D = 4^k).
+  if (g.recip != 0.f) {
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = acc[t][r] / g.divisor;
+      for (int r = 0; r < 16; ++r) acc[t][r] *= g.recip;
+  } else {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = acc[t][r] / g.divisor;
+  }
 
   // Level 0: lane writes 16 contiguous columns of row th0 + 2t + h.
   {
@@ -311,6 +330,35 @@ int launch_avg_pool(const float* in, float* out, long long planes, int H, int W,
   return dxr::launch_status();
 }
 
+// Tile variants (queries per workgroup = 32 * WAVES, K step BK).  Selected by
+// DXR_BUILD_VARIANT for same-process A/B timing; 0 is the tuned default.
+template <bool VEC, int WAVES, int BK>
+int launch_build_cfg(const float* f1, const float* f2, float* pyr, const BuildGeom& g,
+                     int tiles_t, int B, hipStream_t stream) {
+  constexpr int BM = 32 * WAVES;
+  const dim3 grid((unsigned)tiles_t, (unsigned)((g.N + BM - 1) / BM), (unsigned)B);
+  if (grid.y > 65535) return DXR_EINVAL;
+  hipLaunchKernelGGL((corr_build_f32_kernel<VEC, WAVES, BK>), grid, dim3(64 * WAVES), 0, stream,
+                     f1, f2, pyr, g);
+  return dxr::launch_status();
+}
+
+int build_variant() {
+  const char* v = std::getenv("DXR_BUILD_VARIANT");
+  return v ? std::atoi(v) : 0;
+}
+
+int launch_build_f32(bool vec, int variant, const float* f1, const float* f2, float* pyr,
+                     const BuildGeom& g, int tiles_t, int B, hipStream_t stream) {
+  if (!vec) return launch_build_cfg<false, 4, 16>(f1, f2, pyr, g, tiles_t, B, stream);
+  switch (variant) {
+    case 1: return launch_build_cfg<true, 4, 32>(f1, f2, pyr, g, tiles_t, B, stream);
+    case 2: return launch_build_cfg<true, 8, 16>(f1, f2, pyr, g, tiles_t, B, stream);
+    case 3: return launch_build_cfg<true, 8, 32>(f1, f2, pyr, g, tiles_t, B, stream);
+    default: return launch_build_cfg<true, 4, 16>(f1, f2, pyr, g, tiles_t, B, stream);
+  }
+}
+
 }  // namespace
 
 extern "C" int dxr_avg_pool2x2(const float* in, float* out, int64_t planes, int64_t H,
@@ -339,23 +387,20 @@ extern "C" int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int 
   g.levels = num_levels < 4 ? num_levels : 4;
   g.tiles_w = (int)((W + TW - 1) / TW);
   g.divisor = divisor;
+  int e2 = 0;
+  g.recip = (std::frexp(divisor, &e2) == 0.5f) ? 1.f / divisor : 0.f;  // exact iff 2^k
   for (int l = 0; l < 4; ++l) {
     g.lh[l] = l < L.n ? L.h[l] : 1;
     g.lw[l] = l < L.n ? L.w[l] : 1;
     g.loff[l] = l < L.n ? L.off[l] : 0;
   }
-  const int tiles_h = (int)((H + TH - 1) / TH);
-  const dim3 grid((unsigned)(tiles_h * g.tiles_w), (unsigned)((g.N + BM - 1) / BM), (unsigned)B);
-  if (grid.y > 65535) return DXR_EINVAL;
   float* pyr = static_cast<float*>(pyramid);
   const float* f1 = static_cast<const float*>(fmap1);
   const float* f2 = static_cast<const float*>(fmap2);
-  if ((W % 4) == 0 && ((uintptr_t)f1 % 16) == 0 && ((uintptr_t)f2 % 16) == 0 &&
-      ((uintptr_t)pyr % 16) == 0)
-    hipLaunchKernelGGL(corr_build_f32_kernel<true>, grid, dim3(NTHR), 0, stream, f1, f2, pyr, g);
-  else
-    hipLaunchKernelGGL(corr_build_f32_kernel<false>, grid, dim3(NTHR), 0, stream, f1, f2, pyr, g);
-  int st = dxr::launch_status();
+  const bool vec = (W % 4) == 0 && ((uintptr_t)f1 % 16) == 0 && ((uintptr_t)f2 % 16) == 0 &&
+                   ((uintptr_t)pyr % 16) == 0;
+  const int tiles_t = (int)((H + TH - 1) / TH) * g.tiles_w;
+  int st = launch_build_f32(vec, build_variant(), f1, f2, pyr, g, tiles_t, (int)B, stream);
   if (st != DXR_OK) return st;
 
   // Levels beyond the fused four: plain pooling passes, level l from level l-1.

@@ -1,36 +1,43 @@
-// Stage (c): radius-r bilinear lookup into every pyramid level, one launch.
+// Stage (c): radius-r bilinear lookup into every pyramid level.
 //
 // Replaces core/corr.py:29-50 (CorrBlock.__call__) and the helper it calls,
 // core/utils/utils.py:57-71 (bilinear_sampler -> F.grid_sample with
 // align_corners=True, bilinear, zero padding).  The reference builds a
 // (2r+1)^2 delta grid on the host and copies it to the device per level per
 // call (core/corr.py:37-39), runs one grid_sample per level, then cat + permute
-// + contiguous.  Here one kernel writes the final [B, L*(2r+1)^2, H, W] tensor.
+// + contiguous.  Here one launch writes the final [B, L*(2r+1)^2, H, W] tensor.
 //
-// Arithmetic follows the reference sample by sample:
+// Arithmetic is the reference's, sample by sample (bit-exact on its golden vectors):
 //   c   = coords / 2^l + (o - r)                            (core/corr.py:41-43)
 //   g   = 2*c / (S_l - 1) - 1                               (utils.py:61-62)
 //   u   = (g + 1) * ((S_l - 1) / 2)                         (grid_sample unnormalise)
-//   taps at floor(u), floor(u)+1, weights (1-f, f), f = u - floor(u), out-of-range
-//   taps contribute 0, and the four products are summed as the fused chain
-//   fma(se, v_se, fma(sw, v_sw, fma(ne, v_ne, nw*v_nw))) — the exact arithmetic of
-//   the reference's compiled CPU grid sampler (bit-exact on the golden vectors).
-// Consecutive samples of one query share taps, so a thread loads a
-// (2r+2) x (OXG+1) window once and produces OXG x (2r+1) outputs.  A sample whose
-// normalise/unnormalise round trip lands a few ulps across an integer keeps the
-// window's cell and gets a fraction of -eps or 1+eps: the value equals the
-// reference's up to eps * |cell difference|.
+//   taps at floor(u), floor(u)+1 with weights 1-f, f (f = u - floor(u)); taps off
+//   the level contribute 0; the four products are summed as the fused chain
+//   fma(se, v_se, fma(sw, v_sw, fma(ne, v_ne, nw*v_nw))) — the arithmetic of the
+//   reference's compiled CPU grid sampler.
+// The round trip moves a sample by a few ulps, so for integer-valued coordinates
+// (RAFT's first iteration) floor(u) of neighbouring samples need not step by
+// exactly one.  Every sample therefore uses its own floor, and the staged window
+// is (2r+3)^2 cells: the per-sample floors span at most one extra row/column.
 //
-// Thread mapping: lanes = consecutive query pixels of one (pair, level, x-group),
-// so every output store is a coalesced 256-byte wave store.
+// MI355X mapping: one workgroup = QB consecutive query pixels x one level.
+//   phase 0  QB threads compute the 2(2r+1) sample positions of their query and
+//            the window origin (LDS);
+//   phase 1  each wave gathers whole windows of one query at a time into LDS —
+//            lanes walk consecutive cells of a window row, so one wave load
+//            touches a handful of 128-B lines instead of 64 (lane-per-query
+//            gathers thrash the 32 KiB L1 and become L2-bandwidth bound);
+//   phase 2  thread = (query, x-offset class): taps from LDS, fused sum, and
+//            every output store is a coalesced 256-B wave store along queries.
 #include "dxr_common.h"
 
 namespace {
 
+constexpr int FAR_ORIGIN = -(1 << 29);  // window origin of far / non-finite queries
+
 struct LookupGeom {
   int N;          // H * W query pixels per pair
   int levels;
-  int groups;     // x-offset groups per level
   int cout;       // levels * (2r+1)^2
   int lh[8], lw[8];
   long long loff[8];
@@ -48,111 +55,153 @@ __device__ __forceinline__ float sample_coord(float c, float sm1, float half_sm1
   return __fmul_rn(__fadd_rn(gn, 1.f), half_sm1);
 }
 
-template <int R, int OXG, typename PT>
-__global__ __launch_bounds__(256) void corr_lookup_kernel(const PT* __restrict__ pyr,
-                                                          const float* __restrict__ coords,
-                                                          float* __restrict__ out,
-                                                          LookupGeom g) {
-  constexpr int RD = 2 * R + 1;
-  const int q = blockIdx.x * 256 + threadIdx.x;
-  if (q >= g.N) return;
-  const int l = blockIdx.y / g.groups;
-  const int grp = blockIdx.y % g.groups;
-  const int b = blockIdx.z;
-  const int ox0 = grp * OXG;
+template <int R>
+struct LookupCfg {
+  static constexpr int RD = 2 * R + 1;     // samples per axis
+  static constexpr int WD = RD + 2;        // staged window side
+  static constexpr int NC = WD * WD;       // cells per window (odd: bank-friendly pitch)
+  static constexpr int NTHR = 128;         // two waves
+  static constexpr int QB = R <= 4 ? 32 : 16;  // queries per workgroup
+  static constexpr int NG = NTHR / QB;     // x-offset classes in phase 2
+  static constexpr int QPW = QB / (NTHR / 64);  // queries gathered per wave
+  static constexpr int CPL = (NC + 63) / 64;    // window cells per lane per query
+};
 
+template <int R, typename PT>
+__global__ __launch_bounds__(LookupCfg<R>::NTHR) void corr_lookup_kernel(const PT* __restrict__ pyr,
+                                                           const float* __restrict__ coords,
+                                                           float* __restrict__ out,
+                                                           LookupGeom g) {
+  using C = LookupCfg<R>;
+  constexpr int RD = C::RD, WD = C::WD, NC = C::NC, QB = C::QB, NG = C::NG;
+  constexpr int QPW = C::QPW, CPL = C::CPL;
+  __shared__ float cells[QB * NC];
+  __shared__ float sx[RD * QB];
+  __shared__ float sy[RD * QB];
+  __shared__ int org[2 * QB];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l = blockIdx.y, b = blockIdx.z;
+  const int q0 = blockIdx.x * QB;
   const int Hl = g.lh[l], Wl = g.lw[l];
-  float* obase = out + ((long long)b * g.cout + (long long)l * RD * RD) * g.N + q;
 
-  if (Hl == 1 || Wl == 1) {
-    // bilinear_sampler divides by zero (utils.py:61-62): the reference returns NaN.
-#pragma unroll
-    for (int j = 0; j < OXG; ++j) {
-      if (ox0 + j >= RD) break;
-#pragma unroll
-      for (int oy = 0; oy < RD; ++oy)
-        obase[(long long)((ox0 + j) * RD + oy) * g.N] = __builtin_nanf("");
+  // ---- phase 0: sample positions and window origin per query
+  if (tid < QB) {
+    const int q = q0 + tid;
+    float x = 0.f, y = 0.f;
+    if (q < g.N) {
+      const float inv = 1.f / (float)(1 << l);  // exact power of two
+      x = coords[((long long)b * 2 + 0) * g.N + q] * inv;
+      y = coords[((long long)b * 2 + 1) * g.N + q] * inv;
     }
-    return;
-  }
-
-  const float inv = 1.f / (float)(1 << l);  // exact power of two
-  const float xc = coords[((long long)b * 2 + 0) * g.N + q] * inv;
-  const float yc = coords[((long long)b * 2 + 1) * g.N + q] * inv;
-  const float wm1 = (float)(Wl - 1), hm1 = (float)(Hl - 1);
-  const float whalf = wm1 / 2.f, hhalf = hm1 / 2.f;
-
-  float ys[RD], xs[OXG];
+    const float wm1 = (float)(Wl - 1), hm1 = (float)(Hl - 1);
+    const float whalf = wm1 / 2.f, hhalf = hm1 / 2.f;
+    bool far = false;
+    int mx = 1 << 30, my = 1 << 30;
 #pragma unroll
-  for (int oy = 0; oy < RD; ++oy) ys[oy] = sample_coord(__fadd_rn(yc, (float)(oy - R)), hm1, hhalf);
-#pragma unroll
-  for (int j = 0; j < OXG; ++j) xs[j] = sample_coord(__fadd_rn(xc, (float)(ox0 + j - R)), wm1, whalf);
-
-  const float ybf = floorf(ys[0]);
-  const float xbf = floorf(xs[0]);
-  // Far-away or non-finite windows: every tap is outside the level (weights
-  // still carry NaN/inf through, as in the reference).
-  const bool near = fabsf(ybf) < 1.0e8f && fabsf(xbf) < 1.0e8f;
-  const int yb = near ? (int)ybf : -(1 << 28);
-  const int xb = near ? (int)xbf : -(1 << 28);
-
-  float fx[OXG], ex[OXG];
-#pragma unroll
-  for (int j = 0; j < OXG; ++j) {
-    fx[j] = __fsub_rn(xs[j], __fadd_rn(xbf, (float)j));
-    ex[j] = __fsub_rn(1.f, fx[j]);
-  }
-
-  const PT* img = pyr + g.loff[l] + ((long long)b * g.N + q) * ((long long)Hl * Wl);
-  bool colok[OXG + 1];
-#pragma unroll
-  for (int c = 0; c <= OXG; ++c) colok[c] = (unsigned)(xb + c) < (unsigned)Wl;
-
-  float prev[OXG + 1];
-#pragma unroll
-  for (int rr = 0; rr <= RD; ++rr) {
-    const int yy = yb + rr;
-    const bool rowok = (unsigned)yy < (unsigned)Hl;
-    float cur[OXG + 1];
-#pragma unroll
-    for (int c = 0; c <= OXG; ++c)
-      cur[c] = (rowok && colok[c]) ? load_cell(img + (long long)yy * Wl + (xb + c)) : 0.f;
-    if (rr > 0) {
-      const int oy = rr - 1;
-      const float n = __fsub_rn(ys[oy], __fadd_rn(ybf, (float)oy));
-      const float s = __fsub_rn(1.f, n);
-#pragma unroll
-      for (int j = 0; j < OXG; ++j) {
-        if (ox0 + j >= RD) break;
-        const float nw = __fmul_rn(s, ex[j]), ne = __fmul_rn(s, fx[j]);
-        const float sw = __fmul_rn(n, ex[j]), se = __fmul_rn(n, fx[j]);
-        float v = __fmul_rn(nw, prev[j]);
-        v = __builtin_fmaf(ne, prev[j + 1], v);
-        v = __builtin_fmaf(sw, cur[j], v);
-        v = __builtin_fmaf(se, cur[j + 1], v);
-        obase[(long long)((ox0 + j) * RD + oy) * g.N] = v;
+    for (int j = 0; j < RD; ++j) {
+      const float u = sample_coord(__fadd_rn(x, (float)(j - R)), wm1, whalf);
+      const float v = sample_coord(__fadd_rn(y, (float)(j - R)), hm1, hhalf);
+      sx[j * QB + tid] = u;
+      sy[j * QB + tid] = v;
+      const float fu = floorf(u), fv = floorf(v);
+      if (!(fabsf(fu) < 1.0e7f) || !(fabsf(fv) < 1.0e7f)) {
+        far = true;
+      } else {
+        mx = min(mx, (int)fu - j);
+        my = min(my, (int)fv - j);
       }
     }
+    // Windows entirely off the level hold only zeros: skip their loads.
+    if (!far && (mx + WD <= 0 || mx >= Wl || my + WD <= 0 || my >= Hl)) far = true;
+    org[tid] = far ? FAR_ORIGIN : mx;
+    org[QB + tid] = far ? FAR_ORIGIN : my;
+  }
+  __syncthreads();
+
+  // ---- phase 1: gather each query's window into LDS (zeros off the level).
+  // All of a wave's loads are issued before its first LDS store, so the
+  // QPW x CPL gathers are in flight together (one memory latency per wave).
+  float cellv[QPW][CPL];
 #pragma unroll
-    for (int c = 0; c <= OXG; ++c) prev[c] = cur[c];
+  for (int i = 0; i < QPW; ++i) {
+    const int qq = wave * QPW + i;
+    const int q = q0 + qq;
+    const int xlo = org[qq], ylo = org[QB + qq];
+    const bool live = q < g.N && xlo != FAR_ORIGIN;
+    const PT* img = pyr + g.loff[l] + ((long long)b * g.N + (live ? q : 0)) * ((long long)Hl * Wl);
+#pragma unroll
+    for (int m = 0; m < CPL; ++m) {
+      const int c = m * 64 + lane;
+      const int yy = ylo + c / WD, xx = xlo + c % WD;
+      cellv[i][m] = (live && c < NC && (unsigned)yy < (unsigned)Hl && (unsigned)xx < (unsigned)Wl)
+                    ? load_cell(img + (long long)yy * Wl + xx) : 0.f;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < QPW; ++i)
+#pragma unroll
+    for (int m = 0; m < CPL; ++m) {
+      const int c = m * 64 + lane;
+      if (c < NC) cells[(wave * QPW + i) * NC + c] = cellv[i][m];
+    }
+  __syncthreads();
+
+  // ---- phase 2: bilinear taps from LDS, coalesced stores along queries
+  const int qq = tid % QB;
+  const int q = q0 + qq;
+  if (q >= g.N) return;
+  const int xlo = org[qq], ylo = org[QB + qq];
+  const bool live = xlo != FAR_ORIGIN;
+  const float* cq = cells + qq * NC;
+  int row[RD];
+  float fn[RD], fs[RD];
+#pragma unroll
+  for (int oy = 0; oy < RD; ++oy) {
+    const float v = sy[oy * QB + qq];
+    const float fl = floorf(v);
+    fn[oy] = __fsub_rn(v, fl);
+    fs[oy] = __fsub_rn(1.f, fn[oy]);
+    row[oy] = live ? ((int)fl - ylo) * WD : 0;
+  }
+  float* ob = out + ((long long)b * g.cout + (long long)l * RD * RD) * g.N + q;
+  for (int ox = tid / QB; ox < RD; ox += NG) {
+    const float u = sx[ox * QB + qq];
+    const float fl = floorf(u);
+    const float fx = __fsub_rn(u, fl);
+    const float ex = __fsub_rn(1.f, fx);
+    const int col = live ? (int)fl - xlo : 0;
+#pragma unroll
+    for (int oy = 0; oy < RD; ++oy) {
+      float v00 = 0.f, v01 = 0.f, v10 = 0.f, v11 = 0.f;
+      if (live) {
+        const float* p = cq + row[oy] + col;
+        v00 = p[0]; v01 = p[1]; v10 = p[WD]; v11 = p[WD + 1];
+      }
+      const float nw = __fmul_rn(fs[oy], ex), ne = __fmul_rn(fs[oy], fx);
+      const float sw = __fmul_rn(fn[oy], ex), se = __fmul_rn(fn[oy], fx);
+      float v = __fmul_rn(nw, v00);
+      v = __builtin_fmaf(ne, v01, v);
+      v = __builtin_fmaf(sw, v10, v);
+      v = __builtin_fmaf(se, v11, v);
+      ob[(long long)(ox * RD + oy) * g.N] = v;
+    }
   }
 }
 
 template <int R, typename PT>
-int launch_lookup_r(const PT* pyr, const float* coords, float* out, LookupGeom g, int B,
+int launch_lookup_r(const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
                     hipStream_t stream) {
-  constexpr int RD = 2 * R + 1;
-  constexpr int OXG = RD <= 3 ? RD : (RD % 3 == 0 ? 3 : 4);
-  g.groups = (RD + OXG - 1) / OXG;
-  const dim3 grid((unsigned)((g.N + 255) / 256), (unsigned)(g.levels * g.groups), (unsigned)B);
-  hipLaunchKernelGGL((corr_lookup_kernel<R, OXG, PT>), grid, dim3(256), 0, stream, pyr, coords,
+  using C = LookupCfg<R>;
+  const dim3 grid((unsigned)((g.N + C::QB - 1) / C::QB), (unsigned)g.levels, (unsigned)B);
+  hipLaunchKernelGGL((corr_lookup_kernel<R, PT>), grid, dim3(C::NTHR), 0, stream, pyr, coords,
                      out, g);
   return dxr::launch_status();
 }
 
 template <typename PT>
-int launch_lookup(const PT* pyr, const float* coords, float* out, LookupGeom g, int B, int radius,
-                  hipStream_t stream) {
+int launch_lookup(const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
+                  int radius, hipStream_t stream) {
   switch (radius) {
     case 0: return launch_lookup_r<0, PT>(pyr, coords, out, g, B, stream);
     case 1: return launch_lookup_r<1, PT>(pyr, coords, out, g, B, stream);
@@ -183,7 +232,6 @@ extern "C" int dxr_corr_lookup(const void* pyramid, int pyr_dtype, int64_t B, in
   LookupGeom g;
   g.N = (int)(H * W);
   g.levels = num_levels;
-  g.groups = 1;
   g.cout = num_levels * rd * rd;
   for (int l = 0; l < 8; ++l) {
     g.lh[l] = l < L.n ? L.h[l] : 1;

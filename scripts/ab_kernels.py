@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Same-process A/B timing of kernel variants (MI355X_MICROARCH / §5.4 rule 24:
+interleaved rounds in ONE process).  Build variants are selected through
+DXR_BUILD_VARIANT (read by the launcher on every call).  Prints one JSON line.
+
+Usage: python scripts/ab_kernels.py [--workload sintel] [--variants 0,1,2,3] [--rounds 5]
+"""
+import argparse
+import json
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import bench  # noqa: E402  (workload table, algorithmic byte/flop formulas)
+import dexiraft_amd  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="sintel", choices=sorted(bench.WORKLOADS))
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--variants", default="0,1,2,3")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    (_, _), (H, W), _, _ = bench.WORKLOADS[a.workload]
+    dev = torch.device("cuda", 0)
+    f1, f2, coords = bench.make_inputs(a.batch, H, W, "f32", 7, dev)
+    variants = [int(v) for v in a.variants.split(",")]
+    times = {v: [] for v in variants}
+    ref = None
+    with torch.no_grad():
+        for v in variants:                      # correctness: variants are bit-identical
+            os.environ["DXR_BUILD_VARIANT"] = str(v)
+            cb = dexiraft_amd.CorrBlock(f1, f2)
+            if ref is None:
+                ref = cb._buf.clone()
+            assert torch.equal(cb._buf, ref), f"variant {v} differs from variant {variants[0]}"
+        for _ in range(a.rounds):
+            for v in variants:
+                os.environ["DXR_BUILD_VARIANT"] = str(v)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.reps):
+                    dexiraft_amd.CorrBlock(f1, f2)
+                e1.record()
+                torch.cuda.synchronize()
+                times[v].append(e0.elapsed_time(e1) / a.reps * 1e3)
+        cb = dexiraft_amd.CorrBlock(f1, f2)
+        for _ in range(3):
+            for c in coords:
+                cb(c)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            outs = [cb(c) for c in coords]
+        lk = []
+        for _ in range(a.rounds):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.reps):
+                g.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            lk.append(e0.elapsed_time(e1) / a.reps / len(coords) * 1e3)
+    flops = bench.build_flops(a.batch, H, W)
+    res = {"workload": a.workload, "batch": a.batch,
+           "build_us": {v: {"median": float(np.median(t)), "min": float(np.min(t))}
+                        for v, t in times.items()},
+           "build_tflops_median": {v: flops / (np.median(t) * 1e-6) / 1e12 for v, t in times.items()},
+           "lookup_us_median": float(np.median(lk)),
+           "lookup_gbs": bench.lookup_bytes(a.batch, H, W) / (np.median(lk) * 1e-6) / 1e9}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

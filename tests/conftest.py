@@ -45,7 +45,7 @@ def load_tiny(name: str) -> dict:
     with np.load(GOLDEN / f"tiny_{name}.npz") as z:
         d = {k: z[k] for k in z.files}
     d.update(manifest()["tiny"][name])
-    d["n_coords"] = sum(1 for k in d if k.startswith("coords"))
+    d["n_coords"] = sum(1 for k in d if k.startswith("coords") and k[6:].isdigit())
     return d
 
 

@@ -1,0 +1,138 @@
+"""CPU: the C-ABI library loads, exports exactly what include/dexiraft_corr.h
+declares, and validates arguments on the host before any launch (so these calls
+are safe without a GPU: they return before touching the device)."""
+from __future__ import annotations
+
+import ctypes
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+from conftest import REPO
+
+HEADER = REPO / "include" / "dexiraft_corr.h"
+DECL = re.compile(r"^\s*(?:int|int64_t|const char\*)\s+(dxr_\w+)\s*\(", re.M)
+
+
+def declared() -> set[str]:
+    return set(DECL.findall(HEADER.read_text()))
+
+
+@pytest.fixture(scope="module")
+def nat():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "_dxr_build_t", REPO / "optical-flow_dexi-raft_amd" / "build.py")
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    b.build()  # no-op when fresh; hipcc cross-compiles here otherwise
+    from dexiraft_amd import _native
+    _native.load()
+    return _native
+
+
+def test_header_declares_the_documented_entry_points():
+    assert declared() == {
+        "dxr_abi_version", "dxr_status_string", "dxr_last_hip_error", "dxr_pyramid_numel",
+        "dxr_pyramid_level_offset", "dxr_corr_pyramid_build", "dxr_corr_lookup",
+        "dxr_avg_pool2x2", "dxr_alt_corr_forward", "dxr_alt_corr_lookup"}
+
+
+def test_library_exports_every_declared_symbol(nat):
+    out = subprocess.run(["nm", "-D", "--defined-only", str(nat.LIB_PATH)], capture_output=True,
+                         text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T dxr_" in ln}
+    assert exported == declared()
+    assert set(nat.SIGNATURES) == declared()
+    lib = nat.load()
+    for name in declared():
+        assert isinstance(getattr(lib, name), ctypes._CFuncPtr)
+
+
+def test_library_is_gfx950_code(nat):
+    """The embedded HIP fat binary targets gfx950 (MI355X) only."""
+    blob = Path(nat.LIB_PATH).read_bytes()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    for other in (b"--gfx942", b"--gfx90a", b"--gfx1100"):
+        assert other not in blob
+
+
+def test_abi_version_and_status_strings(nat):
+    lib = nat.load()
+    assert lib.dxr_abi_version() == nat.ABI_VERSION == 1
+    assert lib.dxr_status_string(0) == b"ok"
+    assert lib.dxr_status_string(1) == b"invalid argument"
+    assert lib.dxr_status_string(2) == b"unsupported by this build"
+    assert lib.dxr_status_string(-1) == b"HIP launch error"
+    assert lib.dxr_status_string(77) == b"unknown status"
+    assert lib.dxr_last_hip_error() == 0
+
+
+@pytest.mark.parametrize("B,H,W,L", [(1, 55, 128, 4), (8, 47, 156, 4), (2, 12, 16, 4),
+                                     (1, 33, 40, 5), (3, 9, 11, 2), (1, 1, 1, 1)])
+def test_pyramid_geometry(nat, B, H, W, L):
+    lib = nat.load()
+    sizes = [(H, W)]
+    for _ in range(L - 1):
+        sizes.append((sizes[-1][0] // 2, sizes[-1][1] // 2))
+    n = H * W
+    offs = [0]
+    for h, w in sizes:
+        offs.append(offs[-1] + B * n * h * w)
+    assert lib.dxr_pyramid_numel(B, H, W, L) == offs[-1]
+    for lvl in range(L):
+        assert lib.dxr_pyramid_level_offset(B, H, W, lvl) == offs[lvl]
+
+
+def test_pyramid_geometry_rejects_empty_levels(nat):
+    lib = nat.load()
+    assert lib.dxr_pyramid_numel(1, 7, 30, 4) == -1     # 7 -> 3 -> 1 -> 0
+    assert lib.dxr_pyramid_numel(1, 8, 8, 4) > 0
+    assert lib.dxr_pyramid_numel(1, 8, 8, 0) == -1
+    assert lib.dxr_pyramid_level_offset(1, 8, 8, -1) == -1
+
+
+def test_host_side_validation_needs_no_gpu(nat):
+    lib = nat.load()
+    P = 1 << 12  # a non-null dummy address: never dereferenced on these paths
+    EINVAL, EUNSUP, OK = nat.DXR_EINVAL, nat.DXR_EUNSUPPORTED, nat.DXR_OK
+    b = lib.dxr_corr_pyramid_build
+    assert b(P, P, 0, -1, 256, 8, 8, 4, 16.0, P, 0, None) == EINVAL      # B < 0
+    assert b(P, P, 0, 1, 0, 8, 8, 4, 16.0, P, 0, None) == EINVAL        # D = 0
+    assert b(P, P, 0, 1, 256, 7, 30, 4, 16.0, P, 0, None) == EINVAL     # empty level
+    assert b(P, P, 0, 1, 256, 8, 8, 4, 0.0, P, 0, None) == EINVAL       # divisor 0
+    assert b(P, P, 0, 1, 256, 8, 8, 4, float("nan"), P, 0, None) == EINVAL
+    assert b(None, P, 0, 1, 256, 8, 8, 4, 16.0, P, 0, None) == EINVAL   # null input
+    assert b(P, P, 0, 0, 256, 8, 8, 4, 16.0, None, 0, None) == OK       # empty batch
+    assert b(P, P, 7, 1, 256, 8, 8, 4, 16.0, P, 0, None) == EUNSUP      # unknown dtype
+    lk = lib.dxr_corr_lookup
+    assert lk(P, 0, 1, 8, 8, 4, -1, P, P, None) == EINVAL               # radius < 0
+    assert lk(P, 0, 1, 8, 8, 4, 9, P, P, None) == EUNSUP                # radius > 8
+    assert lk(P, 0, 1, 8, 8, 9, 4, P, P, None) == EINVAL                # 9 levels
+    assert lk(P, 5, 1, 8, 8, 4, 4, P, P, None) == EINVAL                # unknown dtype
+    assert lk(P, 0, 0, 8, 8, 4, 4, None, None, None) == OK
+    assert lk(P, 0, 1, 8, 8, 4, 4, None, P, None) == EINVAL             # null coords
+    assert lib.dxr_avg_pool2x2(P, P, -1, 8, 8, None) == EINVAL
+    assert lib.dxr_avg_pool2x2(None, None, 0, 8, 8, None) == OK
+    assert lib.dxr_avg_pool2x2(P, P, 3, 1, 8, None) == OK               # nothing to pool
+    af = lib.dxr_alt_corr_forward
+    assert af(P, P, P, P, 1, 8, 8, 8, 8, 64, 1, -1, None) == EINVAL
+    assert af(P, P, P, P, 1, 8, 8, 8, 8, 64, 1, 7, None) == EUNSUP
+    assert af(P, P, P, P, 1, 8, 8, 8, 8, 0, 1, 4, None) == EINVAL
+    assert af(None, None, None, None, 1, 8, 8, 8, 8, 64, 0, 4, None) == OK
+    al = lib.dxr_alt_corr_lookup
+    ptrs = (ctypes.c_void_p * 4)(P, P, P, P)
+    assert al(P, ptrs, P, P, 1, 16, 16, 64, 4, 4, 0.0, None) == EINVAL  # divisor 0
+    assert al(P, ptrs, P, P, 1, 16, 16, 64, 4, 9, 16.0, None) == EUNSUP
+    assert al(P, None, P, P, 1, 16, 16, 64, 4, 4, 16.0, None) == EINVAL
+    assert lib.dxr_last_hip_error() == 0
+
+
+def test_check_maps_status_to_reference_exceptions(nat):
+    nat.check(0, "ok")
+    with pytest.raises(RuntimeError, match="invalid argument"):
+        nat.check(1, "x")
+    with pytest.raises(NotImplementedError):
+        nat.check(2, "x")

@@ -1,0 +1,151 @@
+"""CPU: pin the oracle against the reference's own outputs (golden fixtures).
+
+The fixtures come from running the reference core/corr.py here
+(tests/golden/make_golden.py).  These tests establish that the numpy
+restatement in oracle/ IS the reference's algorithm, so GPU tests may use it as
+the checker at sizes and for inputs the fixtures do not cover.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import datagen as dg
+import oracle
+from conftest import load_large, load_tiny, tiny_cases, tolerance_check
+
+
+def test_generator_is_pinned():
+    """Inputs are regenerated from seeds on the GPU box: the stream must not drift."""
+    assert dg.splitmix64(0, 3).tolist() == [16294208416658607535, 7960286522194355700,
+                                            487617019471545679]
+    np.testing.assert_array_equal(dg.uniform(7, 3), [0.3898297483912715, 0.01678829452815611,
+                                                      0.9007606806068834])
+    np.testing.assert_allclose(dg.normal(0, 4), [2.044272163028782, 1.045091417389922,
+                                                 0.34268650712041837, -0.1933658650337396],
+                               rtol=1e-15)
+    np.testing.assert_array_equal(dg.fmap(1, 1, 2, 2, 2)[0, 0],
+                                  np.array([[-1.2145813, 0.13394034], [1.9091979, -1.0727307]],
+                                           dtype=np.float32))
+
+
+@pytest.mark.parametrize("name", tiny_cases())
+def test_oracle_pyramid(name):
+    d = load_tiny(name)
+    rows = d["pyr_rows"]
+    p32 = oracle.corr_pyramid(d["fmap1"], d["fmap2"], d["num_levels"], np.float32)
+    p64 = oracle.corr_pyramid(d["fmap1"], d["fmap2"], d["num_levels"], np.float64)
+    for lvl in range(d["num_levels"]):
+        ref = d[f"pyr{lvl}"]
+        # float32 mirror: same op sequence; bit-exact on this host's BLAS, so allow
+        # only a last-ulp difference for other BLAS kernels.
+        tolerance_check(p32[lvl][rows], ref, 1e-6)
+        tolerance_check(p64[lvl][rows].astype(np.float32), ref, 1e-5)
+
+
+@pytest.mark.parametrize("name", [n for n in tiny_cases()
+                                  if load_tiny(n)["pyr_rows"].size == load_tiny(n)["B"] *
+                                  load_tiny(n)["H"] * load_tiny(n)["W"]])
+def test_oracle_lookup_bitexact_on_reference_pyramid(name):
+    """corr_lookup on the reference's pyramid reproduces the reference's bits
+    (grid_sample coordinate round trip and fused tap sum included)."""
+    d = load_tiny(name)
+    pyr = [d[f"pyr{lvl}"] for lvl in range(d["num_levels"])]
+    for k in range(d["n_coords"]):
+        got, ref = oracle.corr_lookup(pyr, d[f"coords{k}"], d["radius"]), d[f"out{k}"]
+        assert got.dtype == np.float32 and got.shape == ref.shape
+        assert np.array_equal(np.isnan(got), np.isnan(ref))
+        fin = ~np.isnan(ref)
+        assert np.array_equal(got[fin], ref[fin])
+
+
+@pytest.mark.parametrize("name", tiny_cases())
+def test_oracle_float64_path(name):
+    d = load_tiny(name)
+    pyr = oracle.corr_pyramid(d["fmap1"], d["fmap2"], d["num_levels"], np.float64)
+    for k in range(d["n_coords"]):
+        tolerance_check(oracle.corr_lookup(pyr, d[f"coords{k}"], d["radius"]), d[f"out{k}"], 1e-5)
+
+
+def test_nan_level_is_reference_behaviour():
+    """A 1-row/1-column level divides by zero in bilinear_sampler: all NaN."""
+    d = load_tiny("nanlevel")
+    assert d["pyr3"].shape[-2:] == (1, 2)
+    for k in range(d["n_coords"]):
+        out = d[f"out{k}"].reshape(1, 4, 81, 12, 16)
+        assert np.isnan(out[:, 3]).all() and not np.isnan(out[:, :3]).any()
+
+
+def _alt_kernel_literal(f1, f2, coords, r):
+    """Pure-Python restatement of correlation_kernel.cu:59-114 for ONE query and
+    one coordinate set: cell loop iy-major, each dot scattered (+=) to <= 4 taps."""
+    rd = 2 * r + 1
+    out = np.zeros(rd * rd)
+    x, y = np.float32(coords[0]), np.float32(coords[1])
+    # scalar_t = float in the kernel (:67-68): x - floor(x) rounds for small negative x
+    dx, dy = float(x - np.floor(x)), float(y - np.floor(y))
+    H2, W2, _ = f2.shape
+    for iy in range(rd + 1):
+        for ix in range(rd + 1):
+            h2 = int(np.floor(y)) - r + iy
+            w2 = int(np.floor(x)) - r + ix
+            s = float(f1 @ f2[h2, w2]) if (0 <= h2 < H2 and 0 <= w2 < W2) else 0.0
+            if iy > 0 and ix > 0:
+                out[(iy - 1) + rd * (ix - 1)] += s * dy * dx
+            if iy > 0 and ix < rd:
+                out[(iy - 1) + rd * ix] += s * dy * (1 - dx)
+            if iy < rd and ix > 0:
+                out[iy + rd * (ix - 1)] += s * (1 - dy) * dx
+            if iy < rd and ix < rd:
+                out[iy + rd * ix] += s * (1 - dy) * (1 - dx)
+    return out
+
+
+def test_alt_forward_matches_literal_kernel_restatement():
+    B, H1, W1, H2, W2, C, N, r = 1, 5, 6, 7, 8, 16, 2, 2
+    f1 = dg.normal(1, B * H1 * W1 * C).reshape(B, H1, W1, C)
+    f2 = dg.normal(2, B * H2 * W2 * C).reshape(B, H2, W2, C)
+    c = (dg.uniform(3, B * N * H1 * W1 * 2).reshape(B, N, H1, W1, 2) * 12 - 2).astype(np.float32)
+    got = oracle.alt_corr_forward(f1, f2, c, r)
+    for n in range(N):
+        for h in range(H1):
+            for w in range(W1):
+                ref = _alt_kernel_literal(f1[0, h, w], f2[0], c[0, n, h, w], r)
+                np.testing.assert_allclose(got[0, n, :, h, w], ref, rtol=1e-12, atol=1e-12)
+
+
+def test_alt_block_oracle_matches_reference_corrblock():
+    """AlternateCorrBlock == CorrBlock by linearity of pooling:
+    the only difference is grid_sample's coordinate round trip (a few ulps)."""
+    d = load_tiny("batch2_alt")
+    for k in range(d["n_coords"]):
+        got = oracle.alt_corr_block(d["fmap1"], d["fmap2"], d[f"coords{k}"], 4, d["radius"])
+        tolerance_check(got, d[f"out{k}"], 1e-5)
+
+
+def test_alt_block_oracle_raises_for_small_fmaps():
+    f = dg.fmap(5, 1, 8, 12, 20)
+    with pytest.raises(RuntimeError):
+        oracle.alt_corr_block(f, f, dg.coords(6, 1, 12, 20), 4, 4)
+
+
+def test_large_chairs_checksums():
+    """Benchmark-shape pin (C1 Chairs 46x62): regenerated inputs + float32 oracle
+    vs the reference's checksums and sampled entries."""
+    d = load_large("chairs")
+    B, D, H, W, r = d["B"], d["D"], d["H"], d["W"], d["radius"]
+    f1 = dg.fmap(d["fmap_seeds"][0], B, D, H, W, d["dist"])
+    f2 = dg.fmap(d["fmap_seeds"][1], B, D, H, W, d["dist"])
+    np.testing.assert_allclose([f1.astype(np.float64).sum(), f2.astype(np.float64).sum()],
+                               d["fmap_checksum"], rtol=0, atol=1e-6)
+    pyr = oracle.corr_pyramid(f1, f2, 4, np.float32)
+    for lvl in range(4):
+        flat = pyr[lvl].reshape(-1)
+        maxabs = float(d[f"pyr{lvl}_maxabs"])
+        assert np.abs(flat[d[f"pyr{lvl}_idx"]] - d[f"pyr{lvl}_val"]).max() <= 1e-6 * maxabs
+        np.testing.assert_allclose(flat.astype(np.float64).sum(), d[f"pyr{lvl}_sum"][0],
+                                   rtol=1e-6, atol=1e-3)
+    mode, scale, seed = d["coords"][0]
+    out = oracle.corr_lookup(pyr, dg.coords(int(seed), B, H, W, mode, float(scale)), r)
+    maxabs = float(d["out0_maxabs"])
+    assert np.abs(out.reshape(-1)[d["out0_idx"]] - d["out0_val"]).max() <= 1e-6 * maxabs
