@@ -11,8 +11,10 @@
  *
  * Reference interfaces replaced (paths relative to the reference repository):
  *   dxr_corr_pyramid_build   core/corr.py:13-27  CorrBlock.__init__ (matmul,
- *                            / sqrt(D), 3x F.avg_pool2d) and core/corr.py:52-60
- *                            CorrBlock.corr (num_levels = 1)
+ *                            / sqrt(D), 3x F.avg_pool2d)
+ *   dxr_corr_volume          core/corr.py:52-60  CorrBlock.corr (static)
+ *   dxr_pyramid_unpack/pack  core/corr.py:16,24,27 the corr_pyramid attribute
+ *                            (reference layout <-> paged storage)
  *   dxr_corr_lookup          core/corr.py:29-50  CorrBlock.__call__ together with
  *                            core/utils/utils.py:57-71 bilinear_sampler
  *                            (F.grid_sample, align_corners=True, zero padding)
@@ -25,10 +27,14 @@
  *
  * Layouts (all row-major, C-contiguous):
  *   fmap (CorrBlock)        [B, D, H, W]               (NCHW, as core/raft.py:139-142)
- *   pyramid level l         [B*H*W, H_l, W_l]          H_0 = H, H_l = floor(H_{l-1}/2)
- *                           levels stored back to back; element offset of level l
- *                           is dxr_pyramid_level_offset(B,H,W,l).  This is exactly
- *                           the reference's corr_pyramid[l] ([B*H*W,1,H_l,W_l]).
+ *   pyramid                 PAGED storage (opaque to callers; sizes and level
+ *                           offsets from dxr_pyramid_numel/_level_offset).  Level l
+ *                           has H_l = floor(H_{l-1}/2) rows, as F.avg_pool2d.  Levels
+ *                           0..3 are split into pages of 128 query pixels x one
+ *                           (8x16 >> l) tile of image-2 cells, each page contiguous
+ *                           and written by one build workgroup; levels >= 4 are
+ *                           row-major.  dxr_pyramid_unpack converts a level to the
+ *                           reference's corr_pyramid[l] layout [B*H*W, H_l, W_l].
  *   coords                  [B, 2, H, W] float32       channel 0 = x, 1 = y
  *                           (core/utils/utils.py:74-77)
  *   lookup output           [B, L*(2r+1)^2, H, W] float32, channel
@@ -94,6 +100,26 @@ int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int in_dtype,
                            int64_t B, int64_t D, int64_t H, int64_t W,
                            int num_levels, float divisor,
                            void* pyramid, int pyr_dtype, hipStream_t stream);
+
+/*
+ * CorrBlock.corr: the level-0 volume alone, row-major [B, H, W, 1, H, W]
+ * (= [B*H*W, H, W]) float32, divided by `divisor`.
+ */
+int dxr_corr_volume(const void* fmap1, const void* fmap2, int in_dtype,
+                    int64_t B, int64_t D, int64_t H, int64_t W, float divisor,
+                    float* out, hipStream_t stream);
+
+/*
+ * Convert one level between the paged pyramid and the reference layout
+ * [B*H*W, H_l, W_l] float32 (core/corr.py:22-27).  Padding cells of the paged
+ * storage are neither read nor written.
+ */
+int dxr_pyramid_unpack(const void* pyramid, int pyr_dtype, int64_t B, int64_t H,
+                       int64_t W, int num_levels, int level, float* out,
+                       hipStream_t stream);
+int dxr_pyramid_pack(const float* level_data, int64_t B, int64_t H, int64_t W,
+                     int num_levels, int level, void* pyramid, int pyr_dtype,
+                     hipStream_t stream);
 
 /*
  * Stage (c): radius-r bilinear lookup of every level around coords / 2^l.

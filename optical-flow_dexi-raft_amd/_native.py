@@ -33,6 +33,9 @@ SIGNATURES: dict[str, tuple[object, list[object]]] = {
     "dxr_pyramid_level_offset": (_i64, [_i64, _i64, _i64, _int]),
     "dxr_corr_pyramid_build": (_int, [_vp, _vp, _int, _i64, _i64, _i64, _i64, _int, _f32,
                                       _vp, _int, _vp]),
+    "dxr_corr_volume": (_int, [_vp, _vp, _int, _i64, _i64, _i64, _i64, _f32, _vp, _vp]),
+    "dxr_pyramid_unpack": (_int, [_vp, _int, _i64, _i64, _i64, _int, _int, _vp, _vp]),
+    "dxr_pyramid_pack": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _int, _vp]),
     "dxr_corr_lookup": (_int, [_vp, _int, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp]),
     "dxr_avg_pool2x2": (_int, [_vp, _vp, _i64, _i64, _i64, _vp]),
     "dxr_alt_corr_forward": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64,

@@ -117,8 +117,8 @@ class CorrBlock:
     ``[B, num_levels*(2r+1)^2, H, W]`` tensor in the reference's channel order.
 
     fp32 fmaps (the reference's dtype, core/raft.py:139-142) compute with exact
-    f32 MFMA and store an f32 pyramid; ``corr_pyramid`` then holds the
-    reference-layout ``[B*H*W, 1, H_l, W_l]`` levels as views of one buffer.
+    f32 MFMA and store an f32 pyramid.  The pyramid lives in one paged buffer
+    (``_buf``); ``corr_pyramid`` gives the reference-layout levels on demand.
     """
 
     def __init__(self, fmap1, fmap2, num_levels=4, radius=4):
@@ -150,11 +150,32 @@ class CorrBlock:
                 f1.data_ptr(), f2.data_ptr(), in_dt, B, D, H, W, num_levels, _sqrt_dim(D),
                 self._buf.data_ptr(), pyr_dt, nat.stream_of(f1))
         nat.check(st, "CorrBlock build (dxr_corr_pyramid_build)")
-        N = H * W
-        self.corr_pyramid = []
-        for lvl, (h, w) in enumerate(sizes):
-            off = lib.dxr_pyramid_level_offset(B, H, W, lvl)
-            self.corr_pyramid.append(self._buf[off:off + B * N * h * w].view(B * N, 1, h, w))
+        self._level_sizes = sizes
+        self._ref_pyramid = None
+
+    @property
+    def corr_pyramid(self):
+        """Reference-layout levels ``[B*H*W, 1, H_l, W_l]`` (core/corr.py:16-27).
+
+        The native pyramid is stored paged (one contiguous page per build
+        workgroup, include/dexiraft_corr.h); this list is materialised on first
+        access by ``dxr_pyramid_unpack`` and cached.  Values are float32 (bf16
+        pyramids are widened).  The lookup never needs it.
+        """
+        if self._ref_pyramid is None:
+            B, D, H, W = self._geom
+            lib = nat.load()
+            levels = []
+            with _Launch(self._device):
+                for lvl, (h, w) in enumerate(self._level_sizes):
+                    t = torch.empty((B * H * W, 1, h, w), dtype=torch.float32, device=self._device)
+                    st = lib.dxr_pyramid_unpack(self._buf.data_ptr(), self._pyr_dt, B, H, W,
+                                                self.num_levels, lvl, t.data_ptr(),
+                                                nat.stream_of(t))
+                    nat.check(st, "CorrBlock.corr_pyramid (dxr_pyramid_unpack)")
+                    levels.append(t)
+            self._ref_pyramid = levels
+        return self._ref_pyramid
 
     def __call__(self, coords):
         B, D, H, W = self._geom
@@ -181,10 +202,9 @@ class CorrBlock:
         f1, f2 = fmap1.contiguous(), fmap2.contiguous()
         lib = nat.load()
         with _Launch(fmap1.device):
-            st = lib.dxr_corr_pyramid_build(f1.data_ptr(), f2.data_ptr(), nat.DXR_F32, B, D, H,
-                                            W, 1, _sqrt_dim(D), out.data_ptr(), nat.DXR_F32,
-                                            nat.stream_of(f1))
-        nat.check(st, "CorrBlock.corr (dxr_corr_pyramid_build)")
+            st = lib.dxr_corr_volume(f1.data_ptr(), f2.data_ptr(), nat.DXR_F32, B, D, H, W,
+                                     _sqrt_dim(D), out.data_ptr(), nat.stream_of(f1))
+        nat.check(st, "CorrBlock.corr (dxr_corr_volume)")
         return out
 
 

@@ -7,7 +7,7 @@
 // registers, in the epilogue of the MFMA tile that produced it.
 //
 // GEMM view (per pair b): C[i, j] = sum_d f1[d, i] * f2[d, j], i = query pixel
-// (M = H*W), j = target pixel (N = H*W, taken as 2-D spatial tiles of image 2),
+// (M = H*W), j = target pixel (N = H*W, taken as 8 x 16 spatial tiles of image 2),
 // K = D.  MFMA orientation is transposed (rows = targets, cols = queries) so that
 // an accumulator lane owns ONE query and a 2-row x 16-col patch of targets:
 //   v_mfma_f32_32x32x2_f32 D layout: col = lane & 31, row = (reg&3) + 8*(reg>>2)
@@ -16,9 +16,14 @@
 //   holds spatial column r of that row.
 // A wave owns 32 queries x an 8x16 target tile (4 MFMA tiles: rows 2t, 2t+1),
 // so 2x2, 4x4 and 8x8 pooling all finish inside the wave: in-lane adds plus one
-// exchange between lane halves (lane ^ 32).  Floor-mode pooling falls out of the
-// per-level bounds checks (a pooled cell is written only if it exists at that
-// level).
+// exchange between lane halves (lane ^ 32).
+//
+// Output: the paged pyramid layout of dxr_common.h.  A workgroup computes exactly
+// one page per level (128 queries x one tile), stored contiguously, so the
+// epilogue streams 1 KiB-contiguous wave stores: level-0/1 values go through a
+// per-wave LDS transpose, level-2/3 values are already contiguous per wave.
+// (Scattered per-query row stores — 64 lines per wave store — cost more than the
+// MFMA loop itself: measured 346 vs 220 us at Sintel shape.)
 #include <cmath>
 #include <cstdlib>
 
@@ -26,16 +31,22 @@
 
 namespace {
 
-constexpr int TH = 8;            // target tile rows   (image-2 rows)
-constexpr int TW = 16;           // target tile cols
+constexpr int TH = dxr::PAGE_H;  // target tile rows   (image-2 rows)
+constexpr int TW = dxr::PAGE_W;  // target tile cols
 constexpr int NTGT = TH * TW;    // 128 targets per workgroup
+constexpr int WAVES = 4;         // waves split the 128 queries of a page
+constexpr int BM = 32 * WAVES;   // = dxr::PAGE_Q
+constexpr int NT = 64 * WAVES;
+constexpr int P0 = NTGT + 4;     // LDS pitch (floats) of a staged level-0 query row
+constexpr int P1 = 32 + 4;       // LDS pitch of a staged level-1 query block
+static_assert(BM == dxr::PAGE_Q, "one workgroup = one page");
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 struct BuildGeom {
   int D, H, W, N;       // N = H * W
   int levels;           // fused levels (1..4)
-  int tiles_w;          // ceil(W / TW)
+  int tiles_w, tiles_h; // tiles per image (TX, TY)
   float divisor;        // sqrt(D) in the reference
   float recip;          // 1/divisor when that is exact (power of two), else 0
   int lh[4], lw[4];     // level sizes
@@ -44,11 +55,9 @@ struct BuildGeom {
 
 // Global -> register staging of one BK slice of the query panel (A: [BK][BM])
 // and the target tile (B: [BK][TH][TW]).  VEC: W % 4 == 0, so every float4 is
-// fully inside or fully outside the map.
-template <bool VEC, int WAVES, int BK>
+// fully inside or fully outside the map; outside elements stage as zero.
+template <bool VEC, int BK>
 struct Stage {
-  static constexpr int NT = 64 * WAVES;
-  static constexpr int BM = 32 * WAVES;
   static constexpr int NA = VEC ? BK * BM / 4 / NT : BK * BM / NT;    // per-thread units
   static constexpr int NB = VEC ? BK * NTGT / 4 / NT : BK * NTGT / NT;
   static_assert(NA >= 1 && NB >= 1, "tile too small for the thread count");
@@ -130,19 +139,28 @@ __device__ __forceinline__ void store4(float* dst, const float* v, int nvalid, b
   }
 }
 
-template <bool VEC, int WAVES, int BK>
-__global__ __launch_bounds__(64 * WAVES) void corr_build_f32_kernel(
-    const float* __restrict__ f1, const float* __restrict__ f2,
-    float* __restrict__ pyr, BuildGeom g) {
-  constexpr int BM = 32 * WAVES;
+__device__ __forceinline__ float4 f4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float a, float b, float c, float d) {
+  *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+}
+
+// PAGED: write the paged pyramid (levels 1..4 fused).  !PAGED: write level 0
+// only, row-major [B*N][H][W] (CorrBlock.corr's [B,H,W,1,H,W] volume).
+template <bool VEC, int BK, bool PAGED>
+__global__ __launch_bounds__(NT) void corr_build_f32_kernel(const float* __restrict__ f1,
+                                                            const float* __restrict__ f2,
+                                                            float* __restrict__ pyr,
+                                                            BuildGeom g) {
   constexpr int KP = BK / 2;                        // MFMA k-pairs per stage
-  __shared__ float lds[2 * BK * (BM + NTGT)];       // [buf][A: BK*BM | B: BK*NTGT]
+  constexpr int LDS_K = 2 * BK * (BM + NTGT);       // double-buffered A | B stages
+  constexpr int LDS_E = WAVES * 16 * P0;            // epilogue: 16 level-0 rows per wave
+  __shared__ float lds[LDS_K > LDS_E ? LDS_K : LDS_E];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int th0 = (blockIdx.x / g.tiles_w) * TH;
-  const int tw0 = (blockIdx.x % g.tiles_w) * TW;
+  const int txi = blockIdx.x % g.tiles_w, tyi = blockIdx.x / g.tiles_w;
+  const int th0 = tyi * TH, tw0 = txi * TW;
   const int q0 = blockIdx.y * BM;
   const int b = blockIdx.z;
   const long long fstride = (long long)g.D * g.N;
@@ -164,7 +182,7 @@ __global__ __launch_bounds__(64 * WAVES) void corr_build_f32_kernel(
   auto As = [&](int buf) { return lds + buf * BK * (BM + NTGT); };
   auto Bs = [&](int buf) { return lds + buf * BK * (BM + NTGT) + BK * BM; };
 
-  Stage<VEC, WAVES, BK> st;
+  Stage<VEC, BK> st;
   const int nk = (g.D + BK - 1) / BK;
   st.load(f1b, f2b, 0, q0, th0, tw0, g, tid);
   st.store(As(0), Bs(0), tid);
@@ -175,24 +193,14 @@ __global__ __launch_bounds__(64 * WAVES) void corr_build_f32_kernel(
     if (ks + 1 < nk) st.load(f1b, f2b, (ks + 1) * BK, q0, th0, tw0, g, tid);
     const float* a_s = As(buf);
     const float* b_s = Bs(buf);
-    // Operand fragments are read one k-pair ahead of the MFMAs that use them,
-    // so the LDS latency hides under four 64-cycle MFMAs.
-    float bq[2], at[2][4];
-    bq[0] = a_s[khalf * BM + qry_off];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) at[0][t] = b_s[khalf * NTGT + 2 * t * TW + tgt_off];
 #pragma unroll
     for (int kp = 0; kp < KP; ++kp) {
-      const int cur = kp & 1, nxt = cur ^ 1;
-      if (kp + 1 < KP) {
-        const int k = 2 * (kp + 1) + khalf;
-        bq[nxt] = a_s[k * BM + qry_off];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) at[nxt][t] = b_s[k * NTGT + 2 * t * TW + tgt_off];
-      }
+      const int k = 2 * kp + khalf;
+      const float bq = a_s[k * BM + qry_off];
 #pragma unroll
       for (int t = 0; t < 4; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(at[cur][t], bq[cur], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(b_s[k * NTGT + 2 * t * TW + tgt_off], bq,
+                                                      acc[t], 0, 0, 0);
     }
     if (ks + 1 < nk) st.store(As(buf ^ 1), Bs(buf ^ 1), tid);
     __syncthreads();
@@ -200,12 +208,6 @@ __global__ __launch_bounds__(64 * WAVES) void corr_build_f32_kernel(
 
   // ---------------- epilogue: scale, level 0, fused pooling ----------------
   const int h = lane >> 5;                 // spatial row within each 2-row MFMA tile
-  const int qi = q0 + wave * 32 + j;       // this lane's query pixel
-  // Lanes l and l^32 share the query, so they leave together and the
-  // lane-half exchange below never reads an exited lane.
-  if (qi >= g.N) return;
-  const long long qimg = (long long)b * g.N + qi;
-
   // x / sqrt(D): a multiply is bit-identical when 1/sqrt(D) is exact (D = 4^k).
   if (g.recip != 0.f) {
 #pragma unroll
@@ -219,9 +221,10 @@ __global__ __launch_bounds__(64 * WAVES) void corr_build_f32_kernel(
       for (int r = 0; r < 16; ++r) acc[t][r] = acc[t][r] / g.divisor;
   }
 
-  // Level 0: lane writes 16 contiguous columns of row th0 + 2t + h.
-  {
-    float* img = pyr + g.loff[0] + qimg * g.N;
+  if constexpr (!PAGED) {
+    const int qi = q0 + wave * 32 + j;
+    if (qi >= g.N) return;
+    float* img = pyr + ((long long)b * g.N + qi) * g.N;
     const int nv = g.W - tw0;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -235,74 +238,122 @@ __global__ __launch_bounds__(64 * WAVES) void corr_build_f32_kernel(
         }
       }
     }
-  }
-  if (g.levels < 2) return;
+    return;
+  } else {
+    // Page index shared by all levels; each level's page holds 128 queries x
+    // (TH x TW >> l) cells, query-major.  This wave owns queries 32w .. 32w+31.
+    // Padding pages/cells (queries >= N, cells off the map) are written too: they
+    // hold zeros or pools of zeros and are never read.
+    const long long page = ((long long)b * gridDim.y + blockIdx.y) * ((long long)g.tiles_h *
+                           g.tiles_w) + (long long)tyi * g.tiles_w + txi;
+    float* wl = lds + wave * 16 * P0;     // this wave's private LDS region
 
-  // Level 1 (2x2): rows 2t / 2t+1 live in lane halves 0 / 1.  Both halves compute
-  // identical values in the reference's window order ((v00+v01)+v10)+v11.
-  float l1[4][8];
+    // Level 0: 16 queries per round staged as [q][8][16] rows, then streamed as
+    // 1 KiB wave stores (two 512-B query blocks per instruction).
+    float* pg0 = pyr + g.loff[0] + page * (BM * NTGT) + (long long)wave * 32 * NTGT;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
+    for (int r = 0; r < 2; ++r) {
+      if ((j >> 4) == r) {
+        float* row = wl + (j & 15) * P0 + h * TW;
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      const float o0 = acc[t][2 * m], o1 = acc[t][2 * m + 1];
-      const float p0 = __shfl_xor(o0, 32), p1 = __shfl_xor(o1, 32);
-      const float t0 = h ? p0 : o0, t1 = h ? p1 : o1;
-      const float b0 = h ? o0 : p0, b1 = h ? o1 : p1;
-      l1[t][m] = (((t0 + t1) + b0) + b1) * 0.25f;
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int c4 = 0; c4 < 4; ++c4)
+            st4(row + 2 * t * TW + 4 * c4, acc[t][4 * c4], acc[t][4 * c4 + 1],
+                acc[t][4 * c4 + 2], acc[t][4 * c4 + 3]);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int qq = 2 * k + (lane >> 5);
+        const int off = (lane & 31) * 4;
+        const float4 v = f4(wl + qq * P0 + off);
+        *reinterpret_cast<float4*>(pg0 + (r * 16 + qq) * NTGT + off) = v;
+      }
+      __syncthreads();
     }
-  }
-  {
-    const int lh = g.lh[1], lw = g.lw[1];
-    float* img = pyr + g.loff[1] + qimg * ((long long)lh * lw);
-    const int c0 = tw0 / 2 + 4 * h;
-    const bool vec = VEC && (lw % 4 == 0);
+    if (g.levels < 2) return;
+
+    // Level 1 (2x2): rows 2t / 2t+1 live in lane halves 0 / 1.  Both halves
+    // compute identical values in the reference's window order ((v00+v01)+v10)+v11.
+    float l1[4][8];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int row = th0 / 2 + t;
-      if (row < lh && c0 < lw) {
-        float v[4] = {l1[t][4 * h], l1[t][4 * h + 1], l1[t][4 * h + 2], l1[t][4 * h + 3]};
-        store4(img + (long long)row * lw + c0, v, lw - c0, vec);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const float o0 = acc[t][2 * m], o1 = acc[t][2 * m + 1];
+        const float p0 = __shfl_xor(o0, 32), p1 = __shfl_xor(o1, 32);
+        const float t0 = h ? p0 : o0, t1 = h ? p1 : o1;
+        const float b0 = h ? o0 : p0, b1 = h ? o1 : p1;
+        l1[t][m] = (((t0 + t1) + b0) + b1) * 0.25f;
       }
     }
-  }
-  if (g.levels < 3) return;
-
-  // Level 2 (4x4 of level 0 = 2x2 of level 1), fully in-lane.
-  float l2[2][4];
+    {
+      // stage [32 q][4][8] (pitch P1), stream 4 x 1 KiB
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+      for (int t = 0; t < 4; ++t)
+        st4(wl + j * P1 + t * 8 + 4 * h, l1[t][4 * h], l1[t][4 * h + 1], l1[t][4 * h + 2],
+            l1[t][4 * h + 3]);
+      __syncthreads();
+      float* pg1 = pyr + g.loff[1] + page * (BM * NTGT / 4) + (long long)wave * 32 * (NTGT / 4);
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
-      l2[u][n] = (((l1[2 * u][2 * n] + l1[2 * u][2 * n + 1]) + l1[2 * u + 1][2 * n]) +
-                  l1[2 * u + 1][2 * n + 1]) * 0.25f;
-  {
-    const int lh = g.lh[2], lw = g.lw[2];
-    float* img = pyr + g.loff[2] + qimg * ((long long)lh * lw);
-    const int row = th0 / 4 + h, c0 = tw0 / 4;
-    const bool vec = VEC && (lw % 4 == 0);
-    if (row < lh && c0 < lw) {
-      float v[4] = {l2[h][0], l2[h][1], l2[h][2], l2[h][3]};
-      store4(img + (long long)row * lw + c0, v, lw - c0, vec);
+      for (int k = 0; k < 4; ++k) {
+        const int qq = 8 * k + (lane >> 3);
+        const int off = (lane & 7) * 4;
+        *reinterpret_cast<float4*>(pg1 + qq * 32 + off) = f4(wl + qq * P1 + off);
+      }
     }
-  }
-  if (g.levels < 4) return;
+    if (g.levels < 3) return;
 
-  // Level 3 (8x8 of level 0): two cells per wave-tile; half h writes cell h.
-  {
-    float l3[2];
+    // Level 2 (4x4 of level 0 = 2x2 of level 1), in-lane; [q][2][4] per page,
+    // lane (j, h) writes row h: the wave's 64 x 16 B stores are one 1 KiB run.
+    float l2[2][4];
 #pragma unroll
-    for (int v = 0; v < 2; ++v)
-      l3[v] = (((l2[0][2 * v] + l2[0][2 * v + 1]) + l2[1][2 * v]) + l2[1][2 * v + 1]) * 0.25f;
-    const int lh = g.lh[3], lw = g.lw[3];
-    float* img = pyr + g.loff[3] + qimg * ((long long)lh * lw);
-    const int row = th0 / 8, col = tw0 / 8 + h;
-    if (row < lh && col < lw) img[(long long)row * lw + col] = l3[h];
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        l2[u][n] = (((l1[2 * u][2 * n] + l1[2 * u][2 * n + 1]) + l1[2 * u + 1][2 * n]) +
+                    l1[2 * u + 1][2 * n + 1]) * 0.25f;
+    {
+      float* pg2 = pyr + g.loff[2] + page * (BM * NTGT / 16) + (long long)wave * 32 * 8;
+      st4(pg2 + j * 8 + 4 * h, l2[h][0], l2[h][1], l2[h][2], l2[h][3]);
+    }
+    if (g.levels < 4) return;
+
+    // Level 3 (8x8 of level 0): [q][1][2] per page; lane (j, h) writes cell h.
+    {
+      float l3[2];
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+        l3[v] = (((l2[0][2 * v] + l2[0][2 * v + 1]) + l2[1][2 * v]) + l2[1][2 * v + 1]) * 0.25f;
+      float* pg3 = pyr + g.loff[3] + page * (BM * 2) + (long long)wave * 32 * 2;
+      pg3[j * 2 + h] = l3[h];
+    }
   }
 }
 
-// Generic floor-mode 2x2 average pool over [planes, H, W] (levels >= 4, and the
-// fmap pyramid of AlternateCorrBlock).  Window order matches F.avg_pool2d.
+// Floor-mode 2x2 average pool of one pyramid level into the next, for levels
+// beyond the fused four (any layout, addressed through dxr::cell_index).
+__global__ __launch_bounds__(256) void pool_level_kernel(float* __restrict__ pyr,
+                                                         dxr::LevelLayout src,
+                                                         dxr::LevelLayout dst, int B, int N) {
+  const long long per = (long long)dst.h * dst.w;
+  const long long total = (long long)B * N * per;
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const int x = (int)(idx % dst.w);
+    const int y = (int)((idx / dst.w) % dst.h);
+    const long long bq = idx / per;
+    const int b = (int)(bq / N), q = (int)(bq % N);
+    const float v00 = pyr[dxr::cell_index(src, b, q, 2 * y, 2 * x)];
+    const float v01 = pyr[dxr::cell_index(src, b, q, 2 * y, 2 * x + 1)];
+    const float v10 = pyr[dxr::cell_index(src, b, q, 2 * y + 1, 2 * x)];
+    const float v11 = pyr[dxr::cell_index(src, b, q, 2 * y + 1, 2 * x + 1)];
+    pyr[dxr::cell_index(dst, b, q, y, x)] = (((v00 + v01) + v10) + v11) * 0.25f;
+  }
+}
+
+// Row-major [planes, H, W] -> [planes, H/2, W/2] pool (AlternateCorrBlock's fmaps).
 __global__ __launch_bounds__(256) void avg_pool2x2_kernel(const float* __restrict__ in,
                                                           float* __restrict__ out,
                                                           long long planes, int H, int W) {
@@ -319,50 +370,106 @@ __global__ __launch_bounds__(256) void avg_pool2x2_kernel(const float* __restric
   }
 }
 
+// Reference layout [B*N][h][w] <-> paged level (pack: UNPACK=false).
+template <bool UNPACK, typename PT>
+__global__ __launch_bounds__(256) void repack_kernel(PT* __restrict__ pyr, float* __restrict__ ref,
+                                                     dxr::LevelLayout lay, int B, int N) {
+  const long long per = (long long)lay.h * lay.w;
+  const long long total = (long long)B * N * per;
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const int x = (int)(idx % lay.w);
+    const int y = (int)((idx / lay.w) % lay.h);
+    const long long bq = idx / per;
+    const int b = (int)(bq / N), q = (int)(bq % N);
+    const long long c = dxr::cell_index(lay, b, q, y, x);
+    if constexpr (UNPACK) {
+      if constexpr (sizeof(PT) == 2) ref[idx] = dxr::bf16_to_f32(pyr[c]);
+      else ref[idx] = pyr[c];
+    } else {
+      if constexpr (sizeof(PT) == 2) pyr[c] = dxr::f32_to_bf16(ref[idx]);
+      else pyr[c] = ref[idx];
+    }
+  }
+}
+
+unsigned grid_for(long long total) {
+  long long blocks = (total + 255) / 256;
+  if (blocks > 2048 * 8) blocks = 2048 * 8;
+  return (unsigned)(blocks < 1 ? 1 : blocks);
+}
+
 int launch_avg_pool(const float* in, float* out, long long planes, int H, int W,
                     hipStream_t stream) {
   const long long total = planes * (long long)(H / 2) * (W / 2);
   if (total == 0) return DXR_OK;
-  long long blocks = (total + 255) / 256;
-  if (blocks > 2048 * 8) blocks = 2048 * 8;
-  hipLaunchKernelGGL(avg_pool2x2_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
-                     in, out, planes, H, W);
+  hipLaunchKernelGGL(avg_pool2x2_kernel, dim3(grid_for(total)), dim3(256), 0, stream, in, out,
+                     planes, H, W);
   return dxr::launch_status();
 }
 
-// Tile variants (queries per workgroup = 32 * WAVES, K step BK).  Selected by
-// DXR_BUILD_VARIANT for same-process A/B timing; 0 is the tuned default.
-template <bool VEC, int WAVES, int BK>
-int launch_build_cfg(const float* f1, const float* f2, float* pyr, const BuildGeom& g,
-                     int tiles_t, int B, hipStream_t stream) {
-  constexpr int BM = 32 * WAVES;
-  const dim3 grid((unsigned)tiles_t, (unsigned)((g.N + BM - 1) / BM), (unsigned)B);
+template <bool VEC, int BK, bool PAGED>
+int launch_build_cfg(const float* f1, const float* f2, float* pyr, const BuildGeom& g, int B,
+                     hipStream_t stream) {
+  const dim3 grid((unsigned)(g.tiles_h * g.tiles_w), (unsigned)((g.N + BM - 1) / BM), (unsigned)B);
   if (grid.y > 65535) return DXR_EINVAL;
-  hipLaunchKernelGGL((corr_build_f32_kernel<VEC, WAVES, BK>), grid, dim3(64 * WAVES), 0, stream,
-                     f1, f2, pyr, g);
+  hipLaunchKernelGGL((corr_build_f32_kernel<VEC, BK, PAGED>), grid, dim3(NT), 0, stream, f1, f2,
+                     pyr, g);
   return dxr::launch_status();
 }
 
+// DXR_BUILD_VARIANT (same-process A/B timing only): 1 selects BK = 32.
 int build_variant() {
   const char* v = std::getenv("DXR_BUILD_VARIANT");
   return v ? std::atoi(v) : 0;
 }
 
-int launch_build_f32(bool vec, int variant, const float* f1, const float* f2, float* pyr,
-                     const BuildGeom& g, int tiles_t, int B, hipStream_t stream) {
-  if (!vec) return launch_build_cfg<false, 4, 16>(f1, f2, pyr, g, tiles_t, B, stream);
-  switch (variant) {
-    case 1: return launch_build_cfg<true, 4, 32>(f1, f2, pyr, g, tiles_t, B, stream);
-    case 2: return launch_build_cfg<true, 8, 16>(f1, f2, pyr, g, tiles_t, B, stream);
-    case 3: return launch_build_cfg<true, 8, 32>(f1, f2, pyr, g, tiles_t, B, stream);
-    default: return launch_build_cfg<true, 4, 16>(f1, f2, pyr, g, tiles_t, B, stream);
+template <bool PAGED>
+int launch_build_f32(bool vec, const float* f1, const float* f2, float* pyr, const BuildGeom& g,
+                     int B, hipStream_t stream) {
+  if (!vec) return launch_build_cfg<false, 16, PAGED>(f1, f2, pyr, g, B, stream);
+  if (build_variant() == 1) return launch_build_cfg<true, 32, PAGED>(f1, f2, pyr, g, B, stream);
+  return launch_build_cfg<true, 16, PAGED>(f1, f2, pyr, g, B, stream);
+}
+
+BuildGeom make_geom(int64_t D, int64_t H, int64_t W, float divisor, const dxr::Levels& L) {
+  BuildGeom g;
+  g.D = (int)D; g.H = (int)H; g.W = (int)W; g.N = (int)(H * W);
+  g.levels = L.n < 4 ? L.n : 4;
+  g.tiles_w = (int)((W + TW - 1) / TW);
+  g.tiles_h = (int)((H + TH - 1) / TH);
+  g.divisor = divisor;
+  int e2 = 0;
+  g.recip = (std::frexp(divisor, &e2) == 0.5f) ? 1.f / divisor : 0.f;  // exact iff 2^k
+  for (int l = 0; l < 4; ++l) {
+    g.lh[l] = l < L.n ? L.h[l] : 1;
+    g.lw[l] = l < L.n ? L.w[l] : 1;
+    g.loff[l] = l < L.n ? L.off[l] : 0;
   }
+  return g;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p % 16) == 0; }
+
+constexpr int PROCEED = -100;
+
+int check_build_args(const void* fmap1, const void* fmap2, int in_dtype, int64_t B, int64_t D,
+                     float divisor, const void* out, int out_dtype) {
+  if (D < 1 || D > (1 << 20) || !(divisor == divisor) || divisor == 0.f) return DXR_EINVAL;
+  if (B > 65535) return DXR_EINVAL;
+  if ((in_dtype != DXR_F32 && in_dtype != DXR_BF16) ||
+      (out_dtype != DXR_F32 && out_dtype != DXR_BF16))
+    return DXR_EINVAL;
+  if (B == 0) return DXR_OK;
+  if (!fmap1 || !fmap2 || !out) return DXR_EINVAL;
+  if (in_dtype != DXR_F32 || out_dtype != DXR_F32) return DXR_EUNSUPPORTED;
+  return PROCEED;
 }
 
 }  // namespace
 
-extern "C" int dxr_avg_pool2x2(const float* in, float* out, int64_t planes, int64_t H,
-                               int64_t W, hipStream_t stream) {
+extern "C" int dxr_avg_pool2x2(const float* in, float* out, int64_t planes, int64_t H, int64_t W,
+                               hipStream_t stream) {
   if (planes < 0 || H < 1 || W < 1 || H > (1 << 30) || W > (1 << 30)) return DXR_EINVAL;
   if (planes == 0 || H < 2 || W < 2) return DXR_OK;
   if (!in || !out) return DXR_EINVAL;
@@ -375,39 +482,78 @@ extern "C" int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int 
                                       int pyr_dtype, hipStream_t stream) {
   dxr::Levels L;
   if (!dxr::make_levels(B, H, W, num_levels, &L)) return DXR_EINVAL;
-  if (D < 1 || !(divisor == divisor) || divisor == 0.f) return DXR_EINVAL;
-  if (H * W > (1LL << 30) || D > (1 << 20)) return DXR_EINVAL;
-  if (B > 65535) return DXR_EINVAL;
-  if (B == 0) return DXR_OK;
-  if (!fmap1 || !fmap2 || !pyramid) return DXR_EINVAL;
-  if (in_dtype != DXR_F32 || pyr_dtype != DXR_F32) return DXR_EUNSUPPORTED;
-
-  BuildGeom g;
-  g.D = (int)D; g.H = (int)H; g.W = (int)W; g.N = (int)(H * W);
-  g.levels = num_levels < 4 ? num_levels : 4;
-  g.tiles_w = (int)((W + TW - 1) / TW);
-  g.divisor = divisor;
-  int e2 = 0;
-  g.recip = (std::frexp(divisor, &e2) == 0.5f) ? 1.f / divisor : 0.f;  // exact iff 2^k
-  for (int l = 0; l < 4; ++l) {
-    g.lh[l] = l < L.n ? L.h[l] : 1;
-    g.lw[l] = l < L.n ? L.w[l] : 1;
-    g.loff[l] = l < L.n ? L.off[l] : 0;
-  }
+  const int chk = check_build_args(fmap1, fmap2, in_dtype, B, D, divisor, pyramid, pyr_dtype);
+  if (chk != PROCEED) return chk;
+  const BuildGeom g = make_geom(D, H, W, divisor, L);
   float* pyr = static_cast<float*>(pyramid);
   const float* f1 = static_cast<const float*>(fmap1);
   const float* f2 = static_cast<const float*>(fmap2);
-  const bool vec = (W % 4) == 0 && ((uintptr_t)f1 % 16) == 0 && ((uintptr_t)f2 % 16) == 0 &&
-                   ((uintptr_t)pyr % 16) == 0;
-  const int tiles_t = (int)((H + TH - 1) / TH) * g.tiles_w;
-  int st = launch_build_f32(vec, build_variant(), f1, f2, pyr, g, tiles_t, (int)B, stream);
+  const bool vec = (W % 4) == 0 && aligned16(f1) && aligned16(f2) && aligned16(pyr);
+  int st = launch_build_f32<true>(vec, f1, f2, pyr, g, (int)B, stream);
   if (st != DXR_OK) return st;
-
   // Levels beyond the fused four: plain pooling passes, level l from level l-1.
-  for (int l = 4; l < L.n; ++l) {
-    st = launch_avg_pool(pyr + L.off[l - 1], pyr + L.off[l], B * H * W, L.h[l - 1], L.w[l - 1],
-                         stream);
+  for (int l = dxr::TILED_LEVELS; l < L.n; ++l) {
+    const long long total = B * H * W * (long long)L.h[l] * L.w[l];
+    hipLaunchKernelGGL(pool_level_kernel, dim3(grid_for(total)), dim3(256), 0, stream, pyr,
+                       L.lay[l - 1], L.lay[l], (int)B, (int)(H * W));
+    st = dxr::launch_status();
     if (st != DXR_OK) return st;
   }
   return DXR_OK;
+}
+
+extern "C" int dxr_corr_volume(const void* fmap1, const void* fmap2, int in_dtype, int64_t B,
+                               int64_t D, int64_t H, int64_t W, float divisor, float* out,
+                               hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, 1, &L)) return DXR_EINVAL;
+  const int chk = check_build_args(fmap1, fmap2, in_dtype, B, D, divisor, out, DXR_F32);
+  if (chk != PROCEED) return chk;
+  const BuildGeom g = make_geom(D, H, W, divisor, L);
+  const float* f1 = static_cast<const float*>(fmap1);
+  const float* f2 = static_cast<const float*>(fmap2);
+  const bool vec = (W % 4) == 0 && aligned16(f1) && aligned16(f2) && aligned16(out);
+  return launch_build_f32<false>(vec, f1, f2, out, g, (int)B, stream);
+}
+
+extern "C" int dxr_pyramid_unpack(const void* pyramid, int pyr_dtype, int64_t B, int64_t H,
+                                  int64_t W, int num_levels, int level, float* out,
+                                  hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, num_levels, &L) || level < 0 || level >= num_levels)
+    return DXR_EINVAL;
+  if (pyr_dtype != DXR_F32 && pyr_dtype != DXR_BF16) return DXR_EINVAL;
+  if (B == 0) return DXR_OK;
+  if (!pyramid || !out) return DXR_EINVAL;
+  const long long total = B * H * W * (long long)L.h[level] * L.w[level];
+  if (pyr_dtype == DXR_F32)
+    hipLaunchKernelGGL((repack_kernel<true, float>), dim3(grid_for(total)), dim3(256), 0, stream,
+                       const_cast<float*>(static_cast<const float*>(pyramid)), out, L.lay[level],
+                       (int)B, (int)(H * W));
+  else
+    hipLaunchKernelGGL((repack_kernel<true, uint16_t>), dim3(grid_for(total)), dim3(256), 0,
+                       stream, const_cast<uint16_t*>(static_cast<const uint16_t*>(pyramid)), out,
+                       L.lay[level], (int)B, (int)(H * W));
+  return dxr::launch_status();
+}
+
+extern "C" int dxr_pyramid_pack(const float* level_data, int64_t B, int64_t H, int64_t W,
+                                int num_levels, int level, void* pyramid, int pyr_dtype,
+                                hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, num_levels, &L) || level < 0 || level >= num_levels)
+    return DXR_EINVAL;
+  if (pyr_dtype != DXR_F32 && pyr_dtype != DXR_BF16) return DXR_EINVAL;
+  if (B == 0) return DXR_OK;
+  if (!pyramid || !level_data) return DXR_EINVAL;
+  const long long total = B * H * W * (long long)L.h[level] * L.w[level];
+  float* src = const_cast<float*>(level_data);
+  if (pyr_dtype == DXR_F32)
+    hipLaunchKernelGGL((repack_kernel<false, float>), dim3(grid_for(total)), dim3(256), 0, stream,
+                       static_cast<float*>(pyramid), src, L.lay[level], (int)B, (int)(H * W));
+  else
+    hipLaunchKernelGGL((repack_kernel<false, uint16_t>), dim3(grid_for(total)), dim3(256), 0,
+                       stream, static_cast<uint16_t*>(pyramid), src, L.lay[level], (int)B,
+                       (int)(H * W));
+  return dxr::launch_status();
 }

@@ -35,13 +35,40 @@ namespace {
 
 constexpr int FAR_ORIGIN = -(1 << 29);  // window origin of far / non-finite queries
 
+// Paged-pyramid addressing of one level (dxr_common.h), in shift/mask form:
+//   index = off + (b*qt + (q >> lqb)) * qstride + (q & (2^lqb - 1)) * S
+//         + ((y >> lth) * tx + (x >> ltw)) * pageS + (y & mh) * tw + (x & mw)
+// Row-major levels use lth = ltw = 30 (tile index 0 for in-range cells).
+struct LevelAddr {
+  int h, w;                 // true level size
+  int lth, ltw, mh, mw;     // tile shifts / masks
+  int tw, tx, lqb, qt;
+  long long off, qstride, S, pageS;
+};
+
 struct LookupGeom {
   int N;          // H * W query pixels per pair
   int levels;
   int cout;       // levels * (2r+1)^2
-  int lh[8], lw[8];
-  long long loff[8];
+  LevelAddr lv[8];
 };
+
+LevelAddr level_addr(const dxr::LevelLayout& y) {
+  LevelAddr a;
+  a.h = y.h; a.w = y.w; a.tw = y.tw; a.tx = y.tx; a.qt = y.qt; a.off = y.off;
+  a.S = (long long)y.th * y.tw;
+  if (y.qb > 1) {  // paged level: power-of-two tile dims and page size
+    a.lth = __builtin_ctz(y.th); a.ltw = __builtin_ctz(y.tw);
+    a.mh = y.th - 1; a.mw = y.tw - 1;
+    a.lqb = __builtin_ctz(y.qb);
+    a.pageS = (long long)y.qb * a.S;
+    a.qstride = (long long)y.ty * y.tx * a.pageS;
+  } else {         // row-major level
+    a.lth = 30; a.ltw = 30; a.mh = 0x3fffffff; a.mw = 0x3fffffff;
+    a.lqb = 0; a.pageS = 0; a.qstride = a.S;
+  }
+  return a;
+}
 
 template <typename PT>
 __device__ __forceinline__ float load_cell(const PT* p) {
@@ -83,7 +110,8 @@ __global__ __launch_bounds__(LookupCfg<R>::NTHR) void corr_lookup_kernel(const P
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l = blockIdx.y, b = blockIdx.z;
   const int q0 = blockIdx.x * QB;
-  const int Hl = g.lh[l], Wl = g.lw[l];
+  const LevelAddr A = g.lv[l];
+  const int Hl = A.h, Wl = A.w;
 
   // ---- phase 0: sample positions and window origin per query
   if (tid < QB) {
@@ -129,13 +157,17 @@ __global__ __launch_bounds__(LookupCfg<R>::NTHR) void corr_lookup_kernel(const P
     const int q = q0 + qq;
     const int xlo = org[qq], ylo = org[QB + qq];
     const bool live = q < g.N && xlo != FAR_ORIGIN;
-    const PT* img = pyr + g.loff[l] + ((long long)b * g.N + (live ? q : 0)) * ((long long)Hl * Wl);
+    const int qs = live ? q : 0;
+    const PT* img = pyr + A.off + ((long long)b * A.qt + (qs >> A.lqb)) * A.qstride +
+                    (long long)(qs & ((1 << A.lqb) - 1)) * A.S;
 #pragma unroll
     for (int m = 0; m < CPL; ++m) {
       const int c = m * 64 + lane;
       const int yy = ylo + c / WD, xx = xlo + c % WD;
-      cellv[i][m] = (live && c < NC && (unsigned)yy < (unsigned)Hl && (unsigned)xx < (unsigned)Wl)
-                    ? load_cell(img + (long long)yy * Wl + xx) : 0.f;
+      const bool in = live && c < NC && (unsigned)yy < (unsigned)Hl && (unsigned)xx < (unsigned)Wl;
+      const long long e = ((long long)(yy >> A.lth) * A.tx + (xx >> A.ltw)) * A.pageS +
+                          (yy & A.mh) * A.tw + (xx & A.mw);
+      cellv[i][m] = in ? load_cell(img + e) : 0.f;
     }
   }
 #pragma unroll
@@ -233,11 +265,7 @@ extern "C" int dxr_corr_lookup(const void* pyramid, int pyr_dtype, int64_t B, in
   g.N = (int)(H * W);
   g.levels = num_levels;
   g.cout = num_levels * rd * rd;
-  for (int l = 0; l < 8; ++l) {
-    g.lh[l] = l < L.n ? L.h[l] : 1;
-    g.lw[l] = l < L.n ? L.w[l] : 1;
-    g.loff[l] = l < L.n ? L.off[l] : 0;
-  }
+  for (int l = 0; l < L.n; ++l) g.lv[l] = level_addr(L.lay[l]);
   if (pyr_dtype == DXR_F32)
     return launch_lookup(static_cast<const float*>(pyramid), coords, out, g, (int)B, radius, stream);
   if (pyr_dtype == DXR_BF16)

@@ -22,30 +22,78 @@ inline int launch_status() {
   return DXR_OK;
 }
 
-// Pyramid geometry: level sizes follow F.avg_pool2d(2, stride=2) floor mode.
+// ---------------------------------------------------------------------------
+// Pyramid layout ("paged" correlation volume).
+//
+// Level sizes follow F.avg_pool2d(2, stride=2) floor mode: H_l = floor(H_{l-1}/2).
+// Storage is tiled so that each build workgroup owns one contiguous block:
+// a PAGE = (QB query pixels) x (one TH x TW tile of image-2 cells).  Levels 0..3
+// use QB = 128 and a level-0 tile of 8 x 16 cells, pooled to 4x8, 2x4, 1x2 at
+// levels 1..3 (so one page's pooled cells come from the same workgroup).  Pages
+// are padded: queries to a multiple of 128, image-2 to whole tiles.  Levels >= 4
+// are plain row-major images (QB = 1, one tile = the whole level).  The element
+// index of (pair b, query q, cell y, x) at a level is
+//   ((((b*QT + q/QB)*TY + y/TH)*TX + x/TW)*QB + q%QB)*(TH*TW) + (y%TH)*TW + x%TW
+// ---------------------------------------------------------------------------
+constexpr int PAGE_Q = 128;    // queries per page (levels 0..3)
+constexpr int PAGE_H = 8;      // level-0 tile rows
+constexpr int PAGE_W = 16;     // level-0 tile cols
+constexpr int TILED_LEVELS = 4;
+
+struct LevelLayout {
+  int h, w;          // true level size (floor-mode pooling)
+  int th, tw;        // tile rows / cols at this level
+  int ty, tx;        // tiles per image along y / x
+  int qb, qt;        // queries per page, query blocks per pair
+  long long off;     // element offset of the level in the pyramid buffer
+};
+
 struct Levels {
   int n;
   int h[8];
   int w[8];
   int64_t off[8];  // element offset of each level in the pyramid buffer
   int64_t numel;
+  LevelLayout lay[8];
 };
 
 inline bool make_levels(int64_t B, int64_t H, int64_t W, int num_levels, Levels* L) {
   if (B < 0 || H < 1 || W < 1 || num_levels < 1 || num_levels > 8) return false;
+  if (H * W > (1LL << 30)) return false;
   const int64_t N = H * W;
+  const int64_t qt = (N + PAGE_Q - 1) / PAGE_Q;
+  const int64_t ty = (H + PAGE_H - 1) / PAGE_H, tx = (W + PAGE_W - 1) / PAGE_W;
   int64_t off = 0, h = H, w = W;
   L->n = num_levels;
   for (int l = 0; l < num_levels; ++l) {
     if (l > 0) { h /= 2; w /= 2; }
     if (h < 1 || w < 1) return false;
+    LevelLayout& y = L->lay[l];
+    y.h = (int)h;
+    y.w = (int)w;
+    y.off = off;
+    if (l < TILED_LEVELS) {
+      y.th = PAGE_H >> l; y.tw = PAGE_W >> l;
+      y.ty = (int)ty; y.tx = (int)tx;
+      y.qb = PAGE_Q; y.qt = (int)qt;
+      off += B * qt * PAGE_Q * ty * tx * (int64_t)y.th * y.tw;
+    } else {
+      y.th = (int)h; y.tw = (int)w; y.ty = 1; y.tx = 1; y.qb = 1; y.qt = (int)N;
+      off += B * N * h * w;
+    }
     L->h[l] = (int)h;
     L->w[l] = (int)w;
-    L->off[l] = off;
-    off += B * N * h * w;
+    L->off[l] = y.off;
   }
   L->numel = off;
   return true;
+}
+
+// Element index of (pair b, query q, cell y, x) inside one level (see above).
+__host__ __device__ __forceinline__ long long cell_index(const LevelLayout& y, int b, int q, int cy,
+                                                        int cx) {
+  const long long page = (((long long)b * y.qt + q / y.qb) * y.ty + cy / y.th) * y.tx + cx / y.tw;
+  return y.off + (page * y.qb + q % y.qb) * (y.th * y.tw) + (cy % y.th) * y.tw + cx % y.tw;
 }
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t v) {

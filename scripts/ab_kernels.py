@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--workload", default="sintel", choices=sorted(bench.WORKLOADS))
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--variants", default="0,1,2,3")
+    ap.add_argument("--ablations", default="", help="timing-only variants (outputs not checked)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
@@ -31,7 +32,8 @@ def main():
     dev = torch.device("cuda", 0)
     f1, f2, coords = bench.make_inputs(a.batch, H, W, "f32", 7, dev)
     variants = [int(v) for v in a.variants.split(",")]
-    times = {v: [] for v in variants}
+    ablations = [int(v) for v in a.ablations.split(",") if v]
+    times = {v: [] for v in variants + ablations}
     ref = None
     with torch.no_grad():
         for v in variants:                      # correctness: variants are bit-identical
@@ -41,7 +43,7 @@ def main():
                 ref = cb._buf.clone()
             assert torch.equal(cb._buf, ref), f"variant {v} differs from variant {variants[0]}"
         for _ in range(a.rounds):
-            for v in variants:
+            for v in variants + ablations:
                 os.environ["DXR_BUILD_VARIANT"] = str(v)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -50,6 +52,7 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 times[v].append(e0.elapsed_time(e1) / a.reps * 1e3)
+        os.environ["DXR_BUILD_VARIANT"] = str(variants[0])
         cb = dexiraft_amd.CorrBlock(f1, f2)
         for _ in range(3):
             for c in coords:

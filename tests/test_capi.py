@@ -37,7 +37,8 @@ def test_header_declares_the_documented_entry_points():
     assert declared() == {
         "dxr_abi_version", "dxr_status_string", "dxr_last_hip_error", "dxr_pyramid_numel",
         "dxr_pyramid_level_offset", "dxr_corr_pyramid_build", "dxr_corr_lookup",
-        "dxr_avg_pool2x2", "dxr_alt_corr_forward", "dxr_alt_corr_lookup"}
+        "dxr_avg_pool2x2", "dxr_alt_corr_forward", "dxr_alt_corr_lookup", "dxr_corr_volume",
+        "dxr_pyramid_unpack", "dxr_pyramid_pack"}
 
 
 def test_library_exports_every_declared_symbol(nat):
@@ -73,14 +74,20 @@ def test_abi_version_and_status_strings(nat):
 @pytest.mark.parametrize("B,H,W,L", [(1, 55, 128, 4), (8, 47, 156, 4), (2, 12, 16, 4),
                                      (1, 33, 40, 5), (3, 9, 11, 2), (1, 1, 1, 1)])
 def test_pyramid_geometry(nat, B, H, W, L):
+    """Paged sizes: levels 0..3 in pages of 128 queries x (8x16 >> l) cells over
+    whole tiles; levels >= 4 row-major (include/dexiraft_corr.h)."""
     lib = nat.load()
-    sizes = [(H, W)]
-    for _ in range(L - 1):
-        sizes.append((sizes[-1][0] // 2, sizes[-1][1] // 2))
     n = H * W
+    qt, ty, tx = -(-n // 128), -(-H // 8), -(-W // 16)
     offs = [0]
-    for h, w in sizes:
-        offs.append(offs[-1] + B * n * h * w)
+    h, w = H, W
+    for lvl in range(L):
+        if lvl:
+            h, w = h // 2, w // 2
+        if lvl < 4:
+            offs.append(offs[-1] + B * qt * 128 * ty * tx * (8 >> lvl) * (16 >> lvl))
+        else:
+            offs.append(offs[-1] + B * n * h * w)
     assert lib.dxr_pyramid_numel(B, H, W, L) == offs[-1]
     for lvl in range(L):
         assert lib.dxr_pyramid_level_offset(B, H, W, lvl) == offs[lvl]
@@ -106,7 +113,10 @@ def test_host_side_validation_needs_no_gpu(nat):
     assert b(P, P, 0, 1, 256, 8, 8, 4, float("nan"), P, 0, None) == EINVAL
     assert b(None, P, 0, 1, 256, 8, 8, 4, 16.0, P, 0, None) == EINVAL   # null input
     assert b(P, P, 0, 0, 256, 8, 8, 4, 16.0, None, 0, None) == OK       # empty batch
-    assert b(P, P, 7, 1, 256, 8, 8, 4, 16.0, P, 0, None) == EUNSUP      # unknown dtype
+    assert b(P, P, 7, 1, 256, 8, 8, 4, 16.0, P, 0, None) == EINVAL      # unknown dtype
+    assert lib.dxr_corr_volume(P, P, 0, 1, 0, 8, 8, 16.0, P, None) == EINVAL
+    assert lib.dxr_pyramid_unpack(P, 0, 1, 8, 8, 4, 4, P, None) == EINVAL   # level >= L
+    assert lib.dxr_pyramid_pack(P, 1, 8, 8, 4, 0, P, 3, None) == EINVAL     # bad dtype
     lk = lib.dxr_corr_lookup
     assert lk(P, 0, 1, 8, 8, 4, -1, P, P, None) == EINVAL               # radius < 0
     assert lk(P, 0, 1, 8, 8, 4, 9, P, P, None) == EUNSUP                # radius > 8

@@ -64,13 +64,23 @@ def test_lookup_matches_reference(dx, name):
                                   if len(load_tiny(n)["pyr_rows"]) == load_tiny(n)["B"] *
                                   load_tiny(n)["H"] * load_tiny(n)["W"]])
 def test_lookup_bitexact_on_reference_pyramid(dx, name):
-    """dxr_corr_lookup on the reference's own pyramid reproduces its bits."""
+    """dxr_corr_lookup on the reference's own pyramid reproduces its bits.  The
+    reference levels are packed into a NaN-prefilled paged buffer (packing writes
+    only real cells), so any read of page padding would surface as NaN."""
     d = load_tiny(name)
     from dexiraft_amd import _native as nat
     lib = nat.load()
     B, H, W, L, r = d["B"], d["H"], d["W"], d["num_levels"], d["radius"]
-    buf = torch.cat([_t(d[f"pyr{lvl}"]).reshape(-1) for lvl in range(L)])
-    assert buf.numel() == lib.dxr_pyramid_numel(B, H, W, L)
+    buf = torch.full((lib.dxr_pyramid_numel(B, H, W, L),), float("nan"), device=DEV)
+    for lvl in range(L):
+        lev = _t(d[f"pyr{lvl}"])
+        st = lib.dxr_pyramid_pack(lev.data_ptr(), B, H, W, L, lvl, buf.data_ptr(), nat.DXR_F32,
+                                  nat.stream_of(lev))
+        assert st == 0
+        back = torch.empty_like(lev)
+        st = lib.dxr_pyramid_unpack(buf.data_ptr(), nat.DXR_F32, B, H, W, L, lvl,
+                                    back.data_ptr(), nat.stream_of(lev))
+        assert st == 0 and torch.equal(back, lev)          # pack/unpack round trip
     rd = 2 * r + 1
     for k in range(d["n_coords"]):
         c = _t(d[f"coords{k}"])
@@ -330,6 +340,16 @@ def test_side_stream(dx):
         out = dx.CorrBlock(f1, f2)(c)
     torch.cuda.current_stream().wait_stream(s)
     assert torch.equal(out, ref)
+
+
+def test_corr_pyramid_is_cached_reference_layout(dx):
+    f1, f2 = _pair(H=19, W=37, seed=103)
+    cb = dx.CorrBlock(f1, f2)
+    p = cb.corr_pyramid
+    assert p is cb.corr_pyramid
+    assert [tuple(t.shape) for t in p] == [(703, 1, 19, 37), (703, 1, 9, 18), (703, 1, 4, 9),
+                                           (703, 1, 2, 4)]
+    assert all(t.is_contiguous() and t.dtype == torch.float32 for t in p)
 
 
 def test_native_library_is_the_one_loaded(dx):
