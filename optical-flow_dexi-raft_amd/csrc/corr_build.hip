@@ -47,6 +47,7 @@ struct BuildGeom {
   int D, H, W, N;       // N = H * W
   int levels;           // fused levels (1..4)
   int tiles_w, tiles_h; // tiles per image (TX, TY)
+  int qt;               // query blocks (pages along queries) per pair
   float divisor;        // sqrt(D) in the reference
   float recip;          // 1/divisor when that is exact (power of two), else 0
   int lh[4], lw[4];     // level sizes
@@ -144,25 +145,185 @@ __device__ __forceinline__ void st4(float* p, float a, float b, float c, float d
   *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
 }
 
+template <typename OT>
+__device__ __forceinline__ OT to_out(float v) {
+  if constexpr (sizeof(OT) == 2) return dxr::f32_to_bf16(v);
+  else return v;
+}
+
+// Store 8 consecutive values (two float4 read from LDS) as OT: 16 B of bf16 or
+// 2 x 16 B of f32.
+template <typename OT>
+__device__ __forceinline__ void store8(OT* dst, const float* src) {
+  const float4 a = f4(src), c = f4(src + 4);
+  if constexpr (sizeof(OT) == 2) {
+    uint4 u;
+    u.x = (uint32_t)to_out<OT>(a.x) | ((uint32_t)to_out<OT>(a.y) << 16);
+    u.y = (uint32_t)to_out<OT>(a.z) | ((uint32_t)to_out<OT>(a.w) << 16);
+    u.z = (uint32_t)to_out<OT>(c.x) | ((uint32_t)to_out<OT>(c.y) << 16);
+    u.w = (uint32_t)to_out<OT>(c.z) | ((uint32_t)to_out<OT>(c.w) << 16);
+    *reinterpret_cast<uint4*>(dst) = u;
+  } else {
+    *reinterpret_cast<float4*>(dst) = a;
+    *reinterpret_cast<float4*>(dst + 4) = c;
+  }
+}
+
+// Paged epilogue (levels 0..3 of one page), shared by the f32 and bf16 builds.
+// acc holds this wave's 32 queries x 8x16 targets, already divided by sqrt(D).
+// Each level's page holds 128 queries x (TH x TW >> l) cells, query-major; this
+// wave owns queries 32w .. 32w+31.  Padding queries/cells are written too (zeros
+// or pools of zeros) and never read.  Every pooled value is computed from the
+// f32 values of the level above, in the reference's window order
+// ((v00+v01)+v10)+v11 (F.avg_pool2d), then rounded to OT once.
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+// 16-byte global store, optionally nontemporal (streamed past the caches' LRU).
+__device__ __forceinline__ void gst(float4* p, float4 v, bool nt) {
+  if (nt) {
+    const f32x4v w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<f32x4v*>(p));
+  } else {
+    *p = v;
+  }
+}
+
+template <typename OT, bool NTS = false>
+__device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT* __restrict__ pyr,
+                                               const BuildGeom& g, long long page, int wave,
+                                               int lane) {
+  const int j = lane & 31, h = lane >> 5;
+  float* wl = lds + wave * 16 * P0;     // this wave's private LDS region
+
+  // Level 0: 16 queries per round staged as [q][8][16] f32 rows, then streamed
+  // as 1 KiB wave stores.
+  OT* pg0 = pyr + g.loff[0] + page * (BM * NTGT) + (long long)wave * 32 * NTGT;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    if ((j >> 4) == r) {
+      float* row = wl + (j & 15) * P0 + h * TW;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4)
+          st4(row + 2 * t * TW + 4 * c4, acc[t][4 * c4], acc[t][4 * c4 + 1],
+              acc[t][4 * c4 + 2], acc[t][4 * c4 + 3]);
+    }
+    __syncthreads();
+    if constexpr (sizeof(OT) == 4) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int qq = 2 * k + (lane >> 5);
+        const int off = (lane & 31) * 4;
+        gst(reinterpret_cast<float4*>(pg0 + (r * 16 + qq) * NTGT + off), f4(wl + qq * P0 + off), NTS);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int qq = 4 * k + (lane >> 4);
+        const int off = (lane & 15) * 8;
+        store8<OT>(pg0 + (r * 16 + qq) * NTGT + off, wl + qq * P0 + off);
+      }
+    }
+    __syncthreads();
+  }
+  if (g.levels < 2) return;
+
+  // Level 1 (2x2): rows 2t / 2t+1 live in lane halves 0 / 1; both halves
+  // compute identical values.
+  float l1[4][8];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const float o0 = acc[t][2 * m], o1 = acc[t][2 * m + 1];
+      const float p0 = __shfl_xor(o0, 32), p1 = __shfl_xor(o1, 32);
+      const float t0 = h ? p0 : o0, t1 = h ? p1 : o1;
+      const float b0 = h ? o0 : p0, b1 = h ? o1 : p1;
+      l1[t][m] = (((t0 + t1) + b0) + b1) * 0.25f;
+    }
+  }
+  {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      st4(wl + j * P1 + t * 8 + 4 * h, l1[t][4 * h], l1[t][4 * h + 1], l1[t][4 * h + 2],
+          l1[t][4 * h + 3]);
+    __syncthreads();
+    OT* pg1 = pyr + g.loff[1] + page * (BM * NTGT / 4) + (long long)wave * 32 * (NTGT / 4);
+    if constexpr (sizeof(OT) == 4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int qq = 8 * k + (lane >> 3);
+        const int off = (lane & 7) * 4;
+        gst(reinterpret_cast<float4*>(pg1 + qq * 32 + off), f4(wl + qq * P1 + off), NTS);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int qq = 16 * k + (lane >> 2);
+        const int off = (lane & 3) * 8;
+        store8<OT>(pg1 + qq * 32 + off, wl + qq * P1 + off);
+      }
+    }
+  }
+  if (g.levels < 3) return;
+
+  // Level 2 (4x4 of level 0 = 2x2 of level 1), in-lane; lane (j, h) writes row h.
+  float l2[2][4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+      l2[u][n] = (((l1[2 * u][2 * n] + l1[2 * u][2 * n + 1]) + l1[2 * u + 1][2 * n]) +
+                  l1[2 * u + 1][2 * n + 1]) * 0.25f;
+  {
+    OT* pg2 = pyr + g.loff[2] + page * (BM * NTGT / 16) + (long long)wave * 32 * 8 + j * 8 + 4 * h;
+    if constexpr (sizeof(OT) == 4) {
+      st4(pg2, l2[h][0], l2[h][1], l2[h][2], l2[h][3]);
+    } else {
+      uint2 u;
+      u.x = (uint32_t)to_out<OT>(l2[h][0]) | ((uint32_t)to_out<OT>(l2[h][1]) << 16);
+      u.y = (uint32_t)to_out<OT>(l2[h][2]) | ((uint32_t)to_out<OT>(l2[h][3]) << 16);
+      *reinterpret_cast<uint2*>(pg2) = u;
+    }
+  }
+  if (g.levels < 4) return;
+
+  // Level 3 (8x8 of level 0): lane (j, h) writes cell h.
+  float l3[2];
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+    l3[v] = (((l2[0][2 * v] + l2[0][2 * v + 1]) + l2[1][2 * v]) + l2[1][2 * v + 1]) * 0.25f;
+  OT* pg3 = pyr + g.loff[3] + page * (BM * 2) + (long long)wave * 32 * 2;
+  pg3[j * 2 + h] = to_out<OT>(l3[h]);
+}
+
 // PAGED: write the paged pyramid (levels 1..4 fused).  !PAGED: write level 0
 // only, row-major [B*N][H][W] (CorrBlock.corr's [B,H,W,1,H,W] volume).
-template <bool VEC, int BK, bool PAGED>
-__global__ __launch_bounds__(NT) void corr_build_f32_kernel(const float* __restrict__ f1,
-                                                            const float* __restrict__ f2,
-                                                            float* __restrict__ pyr,
-                                                            BuildGeom g) {
+template <int BK>
+constexpr int build_lds_floats() {
+  return 2 * BK * (BM + NTGT) > WAVES * 16 * P0 ? 2 * BK * (BM + NTGT) : WAVES * 16 * P0;
+}
+
+// One page (128 queries x one 8x16 target tile of pair b): K loop + epilogue.
+// `page` is the flat page index ((b*QT + qblk)*TY + tyi)*TX + txi, which is also
+// the page's position in every paged level.
+template <bool VEC, int BK, bool PAGED, typename OT, bool NTS>
+__device__ __forceinline__ void build_page_f32(const float* __restrict__ f1,
+                                               const float* __restrict__ f2,
+                                               OT* __restrict__ pyr, const BuildGeom& g,
+                                               float* lds, long long page) {
   constexpr int KP = BK / 2;                        // MFMA k-pairs per stage
-  constexpr int LDS_K = 2 * BK * (BM + NTGT);       // double-buffered A | B stages
-  constexpr int LDS_E = WAVES * 16 * P0;            // epilogue: 16 level-0 rows per wave
-  __shared__ float lds[LDS_K > LDS_E ? LDS_K : LDS_E];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int txi = blockIdx.x % g.tiles_w, tyi = blockIdx.x / g.tiles_w;
+  const int tpi = g.tiles_w * g.tiles_h;
+  const int txi = (int)(page % g.tiles_w), tyi = (int)((page / g.tiles_w) % g.tiles_h);
+  const int qblk = (int)((page / tpi) % g.qt);
+  const int b = (int)(page / ((long long)tpi * g.qt));
   const int th0 = tyi * TH, tw0 = txi * TW;
-  const int q0 = blockIdx.y * BM;
-  const int b = blockIdx.z;
+  const int q0 = qblk * BM;
   const long long fstride = (long long)g.D * g.N;
   const float* f1b = f1 + b * fstride;
   const float* f2b = f2 + b * fstride;
@@ -222,6 +383,7 @@ __global__ __launch_bounds__(NT) void corr_build_f32_kernel(const float* __restr
   }
 
   if constexpr (!PAGED) {
+    static_assert(sizeof(OT) == 4, "row-major volume is float32");
     const int qi = q0 + wave * 32 + j;
     if (qi >= g.N) return;
     float* img = pyr + ((long long)b * g.N + qi) * g.N;
@@ -240,96 +402,203 @@ __global__ __launch_bounds__(NT) void corr_build_f32_kernel(const float* __restr
     }
     return;
   } else {
-    // Page index shared by all levels; each level's page holds 128 queries x
-    // (TH x TW >> l) cells, query-major.  This wave owns queries 32w .. 32w+31.
-    // Padding pages/cells (queries >= N, cells off the map) are written too: they
-    // hold zeros or pools of zeros and are never read.
-    const long long page = ((long long)b * gridDim.y + blockIdx.y) * ((long long)g.tiles_h *
-                           g.tiles_w) + (long long)tyi * g.tiles_w + txi;
-    float* wl = lds + wave * 16 * P0;     // this wave's private LDS region
-
-    // Level 0: 16 queries per round staged as [q][8][16] rows, then streamed as
-    // 1 KiB wave stores (two 512-B query blocks per instruction).
-    float* pg0 = pyr + g.loff[0] + page * (BM * NTGT) + (long long)wave * 32 * NTGT;
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      if ((j >> 4) == r) {
-        float* row = wl + (j & 15) * P0 + h * TW;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int c4 = 0; c4 < 4; ++c4)
-            st4(row + 2 * t * TW + 4 * c4, acc[t][4 * c4], acc[t][4 * c4 + 1],
-                acc[t][4 * c4 + 2], acc[t][4 * c4 + 3]);
-      }
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int qq = 2 * k + (lane >> 5);
-        const int off = (lane & 31) * 4;
-        const float4 v = f4(wl + qq * P0 + off);
-        *reinterpret_cast<float4*>(pg0 + (r * 16 + qq) * NTGT + off) = v;
-      }
-      __syncthreads();
-    }
-    if (g.levels < 2) return;
-
-    // Level 1 (2x2): rows 2t / 2t+1 live in lane halves 0 / 1.  Both halves
-    // compute identical values in the reference's window order ((v00+v01)+v10)+v11.
-    float l1[4][8];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const float o0 = acc[t][2 * m], o1 = acc[t][2 * m + 1];
-        const float p0 = __shfl_xor(o0, 32), p1 = __shfl_xor(o1, 32);
-        const float t0 = h ? p0 : o0, t1 = h ? p1 : o1;
-        const float b0 = h ? o0 : p0, b1 = h ? o1 : p1;
-        l1[t][m] = (((t0 + t1) + b0) + b1) * 0.25f;
-      }
-    }
-    {
-      // stage [32 q][4][8] (pitch P1), stream 4 x 1 KiB
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-        st4(wl + j * P1 + t * 8 + 4 * h, l1[t][4 * h], l1[t][4 * h + 1], l1[t][4 * h + 2],
-            l1[t][4 * h + 3]);
-      __syncthreads();
-      float* pg1 = pyr + g.loff[1] + page * (BM * NTGT / 4) + (long long)wave * 32 * (NTGT / 4);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int qq = 8 * k + (lane >> 3);
-        const int off = (lane & 7) * 4;
-        *reinterpret_cast<float4*>(pg1 + qq * 32 + off) = f4(wl + qq * P1 + off);
-      }
-    }
-    if (g.levels < 3) return;
-
-    // Level 2 (4x4 of level 0 = 2x2 of level 1), in-lane; [q][2][4] per page,
-    // lane (j, h) writes row h: the wave's 64 x 16 B stores are one 1 KiB run.
-    float l2[2][4];
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-        l2[u][n] = (((l1[2 * u][2 * n] + l1[2 * u][2 * n + 1]) + l1[2 * u + 1][2 * n]) +
-                    l1[2 * u + 1][2 * n + 1]) * 0.25f;
-    {
-      float* pg2 = pyr + g.loff[2] + page * (BM * NTGT / 16) + (long long)wave * 32 * 8;
-      st4(pg2 + j * 8 + 4 * h, l2[h][0], l2[h][1], l2[h][2], l2[h][3]);
-    }
-    if (g.levels < 4) return;
-
-    // Level 3 (8x8 of level 0): [q][1][2] per page; lane (j, h) writes cell h.
-    {
-      float l3[2];
-#pragma unroll
-      for (int v = 0; v < 2; ++v)
-        l3[v] = (((l2[0][2 * v] + l2[0][2 * v + 1]) + l2[1][2 * v]) + l2[1][2 * v + 1]) * 0.25f;
-      float* pg3 = pyr + g.loff[3] + page * (BM * 2) + (long long)wave * 32 * 2;
-      pg3[j * 2 + h] = l3[h];
-    }
+    paged_epilogue<OT, NTS>(acc, lds, pyr, g, page, wave, lane);
   }
+}
+
+// One page per workgroup (grid = TX*TY x QT x B).
+template <bool VEC, int BK, bool PAGED, typename OT = float, bool NTS = false>
+__global__ __launch_bounds__(NT) void corr_build_f32_kernel(const float* __restrict__ f1,
+                                                            const float* __restrict__ f2,
+                                                            OT* __restrict__ pyr, BuildGeom g) {
+  __shared__ float lds[build_lds_floats<BK>()];
+  const long long page =
+      ((long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  build_page_f32<VEC, BK, PAGED, OT, NTS>(f1, f2, pyr, g, lds, page);
+}
+
+// Persistent: gridDim.x resident workgroups walk the pages with stride
+// gridDim.x, so a page's store drain overlaps the next page's MFMA loop instead
+// of every workgroup on a CU storing in lockstep.  With TX*TY a multiple of 8
+// (e.g. 56 at Sintel shape) each XCD keeps one residue class of target tiles.
+template <bool VEC, int BK, typename OT = float, bool NTS = false>
+__global__ __launch_bounds__(NT) void corr_build_f32_persistent(const float* __restrict__ f1,
+                                                                const float* __restrict__ f2,
+                                                                OT* __restrict__ pyr,
+                                                                BuildGeom g, long long pages) {
+  __shared__ float lds[build_lds_floats<BK>()];
+  for (long long page = blockIdx.x; page < pages; page += gridDim.x) {
+    build_page_f32<VEC, BK, true, OT, NTS>(f1, f2, pyr, g, lds, page);
+    __syncthreads();  // the next page's prologue overwrites the epilogue's LDS
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bf16 build: v_mfma_f32_32x32x16_bf16, f32 accumulation, same tile, same
+// transposed orientation and the same paged epilogue.  Operand tiles are staged
+// in their natural [k][n] order (fmaps are NCHW: a k-row of a panel is
+// contiguous) — the target tile with its 32-column groups permuted into MFMA-row
+// order — and fragments are read with ds_read_b64_tr_b16, which hands each lane
+// one column (4 consecutive k) of a 4 x 16 block: two reads = one 8-element
+// operand (lane l: A[row l&31][k 8*(l>>5)+e]).  Row pitch 320 B makes those
+// reads conflict-free (rows 16 banks apart, the two 16-lane groups of a half 8
+// banks apart).
+// ---------------------------------------------------------------------------
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef short s8v __attribute__((ext_vector_type(8)));
+typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
+
+constexpr int BKH = 32;            // K per stage (two 16-deep MFMA steps)
+constexpr int PH = BM + 32;        // LDS row pitch in bf16 elements (320 B)
+static_assert(NTGT + 32 == PH, "A and B images share the pitch");
+constexpr int STAGE_H = 2 * BKH * PH;  // bf16 elements per stage (A image + B image)
+
+__device__ __forceinline__ s4v tr_read(const uint16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s4v*)(p));
+}
+
+// LDS column of target (tile row r in 0..7, tile col c in 0..15): MFMA tile
+// t = r/2, MFMA row j = (c & 3) + 4*(r & 1) + 8*(c >> 2) (inverse of tgt mapping).
+__device__ __forceinline__ int tgt_col(int r, int c) {
+  return (r >> 1) * 32 + (c & 3) + 4 * (r & 1) + 8 * (c >> 2);
+}
+
+template <bool VEC, typename OT>
+__global__ __launch_bounds__(NT) void corr_build_bf16_kernel(const uint16_t* __restrict__ f1,
+                                                             const uint16_t* __restrict__ f2,
+                                                             OT* __restrict__ pyr, BuildGeom g) {
+  constexpr int LDS_E = WAVES * 16 * P0 * 4;          // epilogue bytes
+  constexpr int LDS_K = 2 * STAGE_H * 2;              // two stages, bytes
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_K > LDS_E ? LDS_K : LDS_E];
+  uint16_t* lh = reinterpret_cast<uint16_t*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int txi = blockIdx.x % g.tiles_w, tyi = blockIdx.x / g.tiles_w;
+  const int th0 = tyi * TH, tw0 = txi * TW;
+  const int q0 = blockIdx.y * BM;
+  const int b = blockIdx.z;
+  const long long fstride = (long long)g.D * g.N;
+  const uint16_t* f1b = f1 + b * fstride;
+  const uint16_t* f2b = f2 + b * fstride;
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  // Staging units: VEC = 4 bf16 (8 B) per unit, 4 units per thread per image.
+  uint2 ra[4], rb[4];
+  uint16_t sa[16], sb[16];
+  auto load = [&](int k0) {
+    if constexpr (VEC) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int idx = tid + NT * s;
+        const int k = idx >> 5;
+        {
+          const int c = (idx & 31) * 4, kk = k0 + k, q = q0 + c;
+          ra[s] = (kk < g.D && q < g.N)
+                      ? *reinterpret_cast<const uint2*>(f1b + (long long)kk * g.N + q)
+                      : make_uint2(0u, 0u);
+        }
+        {
+          const int r = (idx >> 2) & 7, c = (idx & 3) * 4;
+          const int kk = k0 + k, hh = th0 + r, ww = tw0 + c;
+          rb[s] = (kk < g.D && hh < g.H && ww < g.W)
+                      ? *reinterpret_cast<const uint2*>(f2b + (long long)kk * g.N + hh * g.W + ww)
+                      : make_uint2(0u, 0u);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int idx = tid + NT * s;
+        const int k = idx >> 7, kk = k0 + k;
+        {
+          const int q = q0 + (idx & 127);
+          sa[s] = (kk < g.D && q < g.N) ? f1b[(long long)kk * g.N + q] : (uint16_t)0;
+        }
+        {
+          const int r = (idx >> 4) & 7, c = idx & 15, hh = th0 + r, ww = tw0 + c;
+          sb[s] = (kk < g.D && hh < g.H && ww < g.W) ? f2b[(long long)kk * g.N + hh * g.W + ww]
+                                                     : (uint16_t)0;
+        }
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    uint16_t* A = lh + buf * STAGE_H;
+    uint16_t* Bt = A + BKH * PH;
+    if constexpr (VEC) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int idx = tid + NT * s;
+        const int k = idx >> 5;
+        *reinterpret_cast<uint2*>(A + k * PH + (idx & 31) * 4) = ra[s];
+        const int r = (idx >> 2) & 7, c = (idx & 3) * 4;
+        *reinterpret_cast<uint2*>(Bt + k * PH + tgt_col(r, c)) = rb[s];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int idx = tid + NT * s;
+        const int k = idx >> 7;
+        A[k * PH + (idx & 127)] = sa[s];
+        Bt[k * PH + tgt_col((idx >> 4) & 7, idx & 15)] = sb[s];
+      }
+    }
+  };
+
+  // Per-lane transposed-read geometry: lane 4q+p of each 16-lane group addresses
+  // row q, columns 4p..4p+3 of its block; the block's columns are this lane
+  // group's 16 MFMA rows/cols, its rows the lane half's 8 k values (2 reads).
+  const int li = lane & 15;
+  const int rd_off = (li >> 2) * PH + 4 * (li & 3) + 16 * ((lane >> 4) & 1) + 8 * (lane >> 5) * PH;
+
+  const int nk = (g.D + BKH - 1) / BKH;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) load((ks + 1) * BKH);
+    const uint16_t* A = lh + buf * STAGE_H;
+    const uint16_t* Bt = A + BKH * PH;
+#pragma unroll
+    for (int kk = 0; kk < BKH; kk += 16) {
+      const uint16_t* pa = A + kk * PH + rd_off + wave * 32;
+      const s8v qv = __builtin_shufflevector(tr_read(pa), tr_read(pa + 4 * PH), 0, 1, 2, 3, 4, 5,
+                                             6, 7);
+      const bf8v qf = __builtin_bit_cast(bf8v, qv);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint16_t* pb = Bt + kk * PH + rd_off + t * 32;
+        const s8v tv = __builtin_shufflevector(tr_read(pb), tr_read(pb + 4 * PH), 0, 1, 2, 3, 4,
+                                               5, 6, 7);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8v, tv), qf, acc[t],
+                                                         0, 0, 0);
+      }
+    }
+    if (ks + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  if (g.recip != 0.f) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] *= g.recip;
+  } else {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = acc[t][r] / g.divisor;
+  }
+  const long long page = ((long long)b * gridDim.y + blockIdx.y) * ((long long)g.tiles_h *
+                         g.tiles_w) + (long long)tyi * g.tiles_w + txi;
+  paged_epilogue<OT, false>(acc, reinterpret_cast<float*>(smem), pyr, g, page, wave, lane);
 }
 
 // Floor-mode 2x2 average pool of one pyramid level into the next, for levels
@@ -408,13 +677,52 @@ int launch_avg_pool(const float* in, float* out, long long planes, int H, int W,
   return dxr::launch_status();
 }
 
-template <bool VEC, int BK, bool PAGED>
-int launch_build_cfg(const float* f1, const float* f2, float* pyr, const BuildGeom& g, int B,
+dim3 build_grid(const BuildGeom& g, int B) {
+  return dim3((unsigned)(g.tiles_h * g.tiles_w), (unsigned)((g.N + BM - 1) / BM), (unsigned)B);
+}
+
+template <bool VEC, int BK, bool PAGED, typename OT = float, bool NTS = false>
+int launch_build_cfg(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, int B,
                      hipStream_t stream) {
-  const dim3 grid((unsigned)(g.tiles_h * g.tiles_w), (unsigned)((g.N + BM - 1) / BM), (unsigned)B);
+  const dim3 grid = build_grid(g, B);
   if (grid.y > 65535) return DXR_EINVAL;
-  hipLaunchKernelGGL((corr_build_f32_kernel<VEC, BK, PAGED>), grid, dim3(NT), 0, stream, f1, f2,
-                     pyr, g);
+  hipLaunchKernelGGL((corr_build_f32_kernel<VEC, BK, PAGED, OT, NTS>), grid, dim3(NT), 0, stream,
+                     f1, f2, pyr, g);
+  return dxr::launch_status();
+}
+
+int resident_build_groups() {
+  static int n = [] {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    return cus * 4;  // 4 workgroups of 256 threads fit per CU (33 KB LDS, <= 128 VGPRs)
+  }();
+  return n;
+}
+
+template <bool VEC, int BK, typename OT = float, bool NTS = false>
+int launch_build_persistent(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, int B,
+                            hipStream_t stream) {
+  const long long pages = (long long)B * g.qt * g.tiles_h * g.tiles_w;
+  const long long groups = pages < resident_build_groups() ? pages : resident_build_groups();
+  hipLaunchKernelGGL((corr_build_f32_persistent<VEC, BK, OT, NTS>), dim3((unsigned)groups),
+                     dim3(NT), 0, stream, f1, f2, pyr, g, pages);
+  return dxr::launch_status();
+}
+
+template <typename OT>
+int launch_build_bf16(bool vec, const uint16_t* f1, const uint16_t* f2, OT* pyr,
+                      const BuildGeom& g, int B, hipStream_t stream) {
+  const dim3 grid = build_grid(g, B);
+  if (grid.y > 65535) return DXR_EINVAL;
+  if (vec)
+    hipLaunchKernelGGL((corr_build_bf16_kernel<true, OT>), grid, dim3(NT), 0, stream, f1, f2, pyr,
+                       g);
+  else
+    hipLaunchKernelGGL((corr_build_bf16_kernel<false, OT>), grid, dim3(NT), 0, stream, f1, f2, pyr,
+                       g);
   return dxr::launch_status();
 }
 
@@ -424,12 +732,23 @@ int build_variant() {
   return v ? std::atoi(v) : 0;
 }
 
-template <bool PAGED>
-int launch_build_f32(bool vec, const float* f1, const float* f2, float* pyr, const BuildGeom& g,
+// Variants (DXR_BUILD_VARIANT, for same-process A/B only): 0 one page per
+// workgroup, 1 the same with BK 32, 2 persistent, 3 persistent + nontemporal
+// stores, 4 one page per workgroup + nontemporal stores.
+template <bool PAGED, typename OT = float>
+int launch_build_f32(bool vec, const float* f1, const float* f2, OT* pyr, const BuildGeom& g,
                      int B, hipStream_t stream) {
-  if (!vec) return launch_build_cfg<false, 16, PAGED>(f1, f2, pyr, g, B, stream);
-  if (build_variant() == 1) return launch_build_cfg<true, 32, PAGED>(f1, f2, pyr, g, B, stream);
-  return launch_build_cfg<true, 16, PAGED>(f1, f2, pyr, g, B, stream);
+  if (!vec) return launch_build_cfg<false, 16, PAGED, OT>(f1, f2, pyr, g, B, stream);
+  if constexpr (PAGED) {
+    switch (build_variant()) {
+      case 1: return launch_build_cfg<true, 32, true, OT>(f1, f2, pyr, g, B, stream);
+      case 2: return launch_build_persistent<true, 16, OT, false>(f1, f2, pyr, g, B, stream);
+      case 3: return launch_build_persistent<true, 16, OT, true>(f1, f2, pyr, g, B, stream);
+      case 4: return launch_build_cfg<true, 16, true, OT, true>(f1, f2, pyr, g, B, stream);
+      default: break;
+    }
+  }
+  return launch_build_cfg<true, 16, PAGED, OT>(f1, f2, pyr, g, B, stream);
 }
 
 BuildGeom make_geom(int64_t D, int64_t H, int64_t W, float divisor, const dxr::Levels& L) {
@@ -438,6 +757,7 @@ BuildGeom make_geom(int64_t D, int64_t H, int64_t W, float divisor, const dxr::L
   g.levels = L.n < 4 ? L.n : 4;
   g.tiles_w = (int)((W + TW - 1) / TW);
   g.tiles_h = (int)((H + TH - 1) / TH);
+  g.qt = (int)((H * W + BM - 1) / BM);
   g.divisor = divisor;
   int e2 = 0;
   g.recip = (std::frexp(divisor, &e2) == 0.5f) ? 1.f / divisor : 0.f;  // exact iff 2^k
@@ -462,7 +782,6 @@ int check_build_args(const void* fmap1, const void* fmap2, int in_dtype, int64_t
     return DXR_EINVAL;
   if (B == 0) return DXR_OK;
   if (!fmap1 || !fmap2 || !out) return DXR_EINVAL;
-  if (in_dtype != DXR_F32 || out_dtype != DXR_F32) return DXR_EUNSUPPORTED;
   return PROCEED;
 }
 
@@ -485,12 +804,27 @@ extern "C" int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int 
   const int chk = check_build_args(fmap1, fmap2, in_dtype, B, D, divisor, pyramid, pyr_dtype);
   if (chk != PROCEED) return chk;
   const BuildGeom g = make_geom(D, H, W, divisor, L);
-  float* pyr = static_cast<float*>(pyramid);
-  const float* f1 = static_cast<const float*>(fmap1);
-  const float* f2 = static_cast<const float*>(fmap2);
-  const bool vec = (W % 4) == 0 && aligned16(f1) && aligned16(f2) && aligned16(pyr);
-  int st = launch_build_f32<true>(vec, f1, f2, pyr, g, (int)B, stream);
+  int st;
+  if (in_dtype == DXR_F32) {
+    const float* f1 = static_cast<const float*>(fmap1);
+    const float* f2 = static_cast<const float*>(fmap2);
+    const bool vec = (W % 4) == 0 && aligned16(f1) && aligned16(f2) && aligned16(pyramid);
+    st = pyr_dtype == DXR_F32
+             ? launch_build_f32<true>(vec, f1, f2, static_cast<float*>(pyramid), g, (int)B, stream)
+             : launch_build_f32<true>(vec, f1, f2, static_cast<uint16_t*>(pyramid), g, (int)B,
+                                      stream);
+  } else {
+    const uint16_t* f1 = static_cast<const uint16_t*>(fmap1);
+    const uint16_t* f2 = static_cast<const uint16_t*>(fmap2);
+    const bool vec = (W % 4) == 0 && ((uintptr_t)f1 % 8) == 0 && ((uintptr_t)f2 % 8) == 0 &&
+                     aligned16(pyramid);
+    st = pyr_dtype == DXR_F32
+             ? launch_build_bf16(vec, f1, f2, static_cast<float*>(pyramid), g, (int)B, stream)
+             : launch_build_bf16(vec, f1, f2, static_cast<uint16_t*>(pyramid), g, (int)B, stream);
+  }
   if (st != DXR_OK) return st;
+  if (L.n > dxr::TILED_LEVELS && pyr_dtype != DXR_F32) return DXR_EUNSUPPORTED;
+  float* pyr = static_cast<float*>(pyramid);
   // Levels beyond the fused four: plain pooling passes, level l from level l-1.
   for (int l = dxr::TILED_LEVELS; l < L.n; ++l) {
     const long long total = B * H * W * (long long)L.h[l] * L.w[l];
@@ -509,6 +843,7 @@ extern "C" int dxr_corr_volume(const void* fmap1, const void* fmap2, int in_dtyp
   if (!dxr::make_levels(B, H, W, 1, &L)) return DXR_EINVAL;
   const int chk = check_build_args(fmap1, fmap2, in_dtype, B, D, divisor, out, DXR_F32);
   if (chk != PROCEED) return chk;
+  if (in_dtype != DXR_F32) return DXR_EUNSUPPORTED;
   const BuildGeom g = make_geom(D, H, W, divisor, L);
   const float* f1 = static_cast<const float*>(fmap1);
   const float* f2 = static_cast<const float*>(fmap2);

@@ -276,6 +276,59 @@ def test_alternate_block_too_small_raises_like_reference(dx):
         dx.AlternateCorrBlock(f1, f2)
 
 
+# --------------------------------------------------------------------------- bf16 mode
+BF16_RTOL = 1e-2   # bf16 inputs + bf16 pyramid vs the f32 reference
+
+
+@pytest.mark.parametrize("name", ["fnet", "ragged", "batch2_alt", "small_r3"])
+def test_bf16_mode_within_its_tolerance(dx, name):
+    d = load_tiny(name)
+    f1, f2 = _t(d["fmap1"]).bfloat16(), _t(d["fmap2"]).bfloat16()
+    cb = dx.CorrBlock(f1, f2, num_levels=d["num_levels"], radius=d["radius"])
+    assert cb._buf.dtype == torch.bfloat16
+    rows = torch.from_numpy(d["pyr_rows"]).to(DEV)
+    for lvl in range(d["num_levels"]):
+        tolerance_check(cb.corr_pyramid[lvl][rows, 0].cpu().numpy(), d[f"pyr{lvl}"], BF16_RTOL)
+    # against the float64 oracle on the SAME bf16-rounded inputs only the bf16
+    # storage of the pyramid (<= 2^-9 of a value) and f32 accumulation remain
+    r1 = f1.float().cpu().numpy()
+    r2 = f2.float().cpu().numpy()
+    pyr = oracle.corr_pyramid(r1, r2, d["num_levels"], np.float64)
+    for lvl in range(d["num_levels"]):
+        got = cb.corr_pyramid[lvl][:, 0].cpu().numpy().astype(np.float64)
+        slack = 2.0 ** -8 * np.abs(pyr[lvl]) + 1e-5 * np.nanmax(np.abs(pyr[lvl]))
+        assert np.all((np.abs(got - pyr[lvl]) <= slack) | np.isnan(pyr[lvl]))
+    for k in range(d["n_coords"]):
+        out = cb(_t(d[f"coords{k}"]))
+        tolerance_check(out.cpu().numpy(), d[f"out{k}"], BF16_RTOL)
+
+
+def test_bf16_kitti_shape(dx):
+    """C3 shape (47x156: partial tiles, 8-byte staging) against the reference checksums."""
+    d = load_large("kitti")
+    B, D, H, W, r = d["B"], d["D"], d["H"], d["W"], d["radius"]
+    f1 = _t(dg.fmap(d["fmap_seeds"][0], B, D, H, W, d["dist"])).bfloat16()
+    f2 = _t(dg.fmap(d["fmap_seeds"][1], B, D, H, W, d["dist"])).bfloat16()
+    cb = dx.CorrBlock(f1, f2, radius=r)
+    for lvl in range(4):
+        a = cb.corr_pyramid[lvl].reshape(-1)
+        got = a[torch.from_numpy(d[f"pyr{lvl}_idx"]).to(DEV)].cpu().numpy()
+        assert np.abs(got - d[f"pyr{lvl}_val"]).max() <= BF16_RTOL * float(d[f"pyr{lvl}_maxabs"])
+    mode, scale, seed = d["coords"][0]
+    out = cb(_t(dg.coords(int(seed), B, H, W, mode, float(scale))))
+    got = out.reshape(-1)[torch.from_numpy(d["out0_idx"]).to(DEV)].cpu().numpy()
+    assert np.abs(got - d["out0_val"]).max() <= BF16_RTOL * float(d["out0_maxabs"])
+
+
+@pytest.mark.parametrize("variant", ["1", "2", "3", "4"])
+def test_build_variants_bit_identical(dx, variant, monkeypatch):
+    """Tuning variants (BK 32, persistent, nontemporal) produce the same bits."""
+    f1, f2 = _pair(B=2, H=47, W=156, seed=111, dist="fnet")
+    ref = dx.CorrBlock(f1, f2)._buf.clone()
+    monkeypatch.setenv("DXR_BUILD_VARIANT", variant)
+    assert torch.equal(dx.CorrBlock(f1, f2)._buf, ref)
+
+
 # --------------------------------------------------------------------------- edge cases / API
 def test_empty_batch(dx):
     f = torch.empty((0, 256, 20, 24), device=DEV)
