@@ -229,26 +229,34 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
   }
   if (g.levels < 2) return;
 
-  // Level 1 (2x2): rows 2t / 2t+1 live in lane halves 0 / 1; both halves
-  // compute identical values.
-  float l1[4][8];
+  // Levels 1 and 2, streamed one tile pair at a time to keep register pressure
+  // low: level-1 row t (2x2 pool of level-0 rows 2t, 2t+1, which live in lane
+  // halves 0 / 1; both halves compute identical values) goes to LDS at once, and
+  // the level-2 row u is pooled from level-1 rows 2u, 2u+1 while they are live.
+  float l2[2][4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
+  for (int u = 0; u < 2; ++u) {
+    float l1[2][8];
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      const float o0 = acc[t][2 * m], o1 = acc[t][2 * m + 1];
-      const float p0 = __shfl_xor(o0, 32), p1 = __shfl_xor(o1, 32);
-      const float t0 = h ? p0 : o0, t1 = h ? p1 : o1;
-      const float b0 = h ? o0 : p0, b1 = h ? o1 : p1;
-      l1[t][m] = (((t0 + t1) + b0) + b1) * 0.25f;
+    for (int s = 0; s < 2; ++s) {
+      const int t = 2 * u + s;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const float o0 = acc[t][2 * m], o1 = acc[t][2 * m + 1];
+        const float p0 = __shfl_xor(o0, 32), p1 = __shfl_xor(o1, 32);
+        const float t0 = h ? p0 : o0, t1 = h ? p1 : o1;
+        const float b0 = h ? o0 : p0, b1 = h ? o1 : p1;
+        l1[s][m] = (((t0 + t1) + b0) + b1) * 0.25f;
+      }
+      st4(wl + j * P1 + t * 8 + 4 * h, l1[s][4 * h], l1[s][4 * h + 1], l1[s][4 * h + 2],
+          l1[s][4 * h + 3]);
     }
-  }
-  {
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-      st4(wl + j * P1 + t * 8 + 4 * h, l1[t][4 * h], l1[t][4 * h + 1], l1[t][4 * h + 2],
-          l1[t][4 * h + 3]);
-    __syncthreads();
+    for (int n = 0; n < 4; ++n)
+      l2[u][n] = (((l1[0][2 * n] + l1[0][2 * n + 1]) + l1[1][2 * n]) + l1[1][2 * n + 1]) * 0.25f;
+  }
+  __syncthreads();
+  {
     OT* pg1 = pyr + g.loff[1] + page * (BM * NTGT / 4) + (long long)wave * 32 * (NTGT / 4);
     if constexpr (sizeof(OT) == 4) {
 #pragma unroll
@@ -268,23 +276,16 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
   }
   if (g.levels < 3) return;
 
-  // Level 2 (4x4 of level 0 = 2x2 of level 1), in-lane; lane (j, h) writes row h.
-  float l2[2][4];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-      l2[u][n] = (((l1[2 * u][2 * n] + l1[2 * u][2 * n + 1]) + l1[2 * u + 1][2 * n]) +
-                  l1[2 * u + 1][2 * n + 1]) * 0.25f;
+  // Level 2: [q][2][4] per page; lane (j, h) writes row h (a 1 KiB wave run).
   {
     OT* pg2 = pyr + g.loff[2] + page * (BM * NTGT / 16) + (long long)wave * 32 * 8 + j * 8 + 4 * h;
     if constexpr (sizeof(OT) == 4) {
       st4(pg2, l2[h][0], l2[h][1], l2[h][2], l2[h][3]);
     } else {
-      uint2 u;
-      u.x = (uint32_t)to_out<OT>(l2[h][0]) | ((uint32_t)to_out<OT>(l2[h][1]) << 16);
-      u.y = (uint32_t)to_out<OT>(l2[h][2]) | ((uint32_t)to_out<OT>(l2[h][3]) << 16);
-      *reinterpret_cast<uint2*>(pg2) = u;
+      uint2 w;
+      w.x = (uint32_t)to_out<OT>(l2[h][0]) | ((uint32_t)to_out<OT>(l2[h][1]) << 16);
+      w.y = (uint32_t)to_out<OT>(l2[h][2]) | ((uint32_t)to_out<OT>(l2[h][3]) << 16);
+      *reinterpret_cast<uint2*>(pg2) = w;
     }
   }
   if (g.levels < 4) return;
@@ -308,7 +309,31 @@ constexpr int build_lds_floats() {
 // One page (128 queries x one 8x16 target tile of pair b): K loop + epilogue.
 // `page` is the flat page index ((b*QT + qblk)*TY + tyi)*TX + txi, which is also
 // the page's position in every paged level.
-template <bool VEC, int BK, bool PAGED, typename OT, bool NTS>
+// x / sqrt(D) as the reference (core/corr.py:60): DIV = false multiplies by the
+// exact reciprocal (sqrt(D) a power of two, e.g. D = 256 -> 1/16: bit-identical);
+// DIV = true performs the IEEE division (compiled only where it is needed, as
+// its expansion costs registers).
+template <bool DIV>
+__device__ __forceinline__ void scale_acc(f32x16 (&acc)[4], const BuildGeom& g) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if constexpr (DIV) acc[t][r] = acc[t][r] / g.divisor;
+      else acc[t][r] *= g.recip;
+    }
+}
+
+// GLDS: stage operands with global_load_lds_dwordx4 (no staging registers).
+// Out-of-range rows/cols/queries read clamped, valid addresses: their values
+// only reach page padding (never read; pooled cells touching them fall outside
+// the floor-mode level bounds).  Requires W % 4 == 0 and D % BK == 0.
+__device__ __forceinline__ void glds16(const float* g, float* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g),
+                                   (__attribute__((address_space(3))) void*)(l), 16, 0, 0);
+}
+
+template <bool VEC, int BK, bool PAGED, typename OT, bool NTS, bool GLDS, bool DIV>
 __device__ __forceinline__ void build_page_f32(const float* __restrict__ f1,
                                                const float* __restrict__ f2,
                                                OT* __restrict__ pyr, const BuildGeom& g,
@@ -318,10 +343,13 @@ __device__ __forceinline__ void build_page_f32(const float* __restrict__ f1,
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
+  // Page coordinates in 32-bit arithmetic (pages < 2^31; 64-bit division expands
+  // to a long emulation loop on the GPU).
   const int tpi = g.tiles_w * g.tiles_h;
-  const int txi = (int)(page % g.tiles_w), tyi = (int)((page / g.tiles_w) % g.tiles_h);
-  const int qblk = (int)((page / tpi) % g.qt);
-  const int b = (int)(page / ((long long)tpi * g.qt));
+  const int pg = (int)page;
+  const int pimg = pg / tpi, pin = pg - pimg * tpi;
+  const int tyi = pin / g.tiles_w, txi = pin - tyi * g.tiles_w;
+  const int b = pimg / g.qt, qblk = pimg - b * g.qt;
   const int th0 = tyi * TH, tw0 = txi * TW;
   const int q0 = qblk * BM;
   const long long fstride = (long long)g.D * g.N;
@@ -343,15 +371,8 @@ __device__ __forceinline__ void build_page_f32(const float* __restrict__ f1,
   auto As = [&](int buf) { return lds + buf * BK * (BM + NTGT); };
   auto Bs = [&](int buf) { return lds + buf * BK * (BM + NTGT) + BK * BM; };
 
-  Stage<VEC, BK> st;
   const int nk = (g.D + BK - 1) / BK;
-  st.load(f1b, f2b, 0, q0, th0, tw0, g, tid);
-  st.store(As(0), Bs(0), tid);
-  __syncthreads();
-
-  for (int ks = 0; ks < nk; ++ks) {
-    const int buf = ks & 1;
-    if (ks + 1 < nk) st.load(f1b, f2b, (ks + 1) * BK, q0, th0, tw0, g, tid);
+  auto mfma_stage = [&](int buf) {
     const float* a_s = As(buf);
     const float* b_s = Bs(buf);
 #pragma unroll
@@ -363,24 +384,51 @@ __device__ __forceinline__ void build_page_f32(const float* __restrict__ f1,
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(b_s[k * NTGT + 2 * t * TW + tgt_off], bq,
                                                       acc[t], 0, 0, 0);
     }
-    if (ks + 1 < nk) st.store(As(buf ^ 1), Bs(buf ^ 1), tid);
+  };
+  if constexpr (GLDS) {
+    static_assert(BK == 16, "glds staging is laid out for BK = 16 (two k-rows per wave load)");
+    // Wave w fills k-row pairs 2w and 2w+1 of both tiles: one 1 KiB wave load
+    // per pair and tile, lane l -> (k = 2p + l/32, 16 B at column (l%32)*4), which
+    // is exactly the [k][128] LDS image (lane-linear destination).
+    const int qa = min(q0 + (lane & 31) * 4, g.N - 4);
+    const int r = (lane >> 2) & 7;
+    const long long tb = (long long)min(th0 + r, g.H - 1) * g.W + min(tw0 + (lane & 3) * 4, g.W - 4);
+    auto issue = [&](int k0, int buf) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int pr = 2 * wave + i;
+        const long long krow = (long long)(k0 + 2 * pr + khalf) * g.N;
+        glds16(f1b + krow + qa, As(buf) + pr * 256);
+        glds16(f2b + krow + tb, Bs(buf) + pr * 256);
+      }
+    };
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int ks = 0; ks < nk; ++ks) {
+      const int buf = ks & 1;
+      if (ks + 1 < nk) issue((ks + 1) * BK, buf ^ 1);
+      mfma_stage(buf);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    Stage<VEC, BK> st;
+    st.load(f1b, f2b, 0, q0, th0, tw0, g, tid);
+    st.store(As(0), Bs(0), tid);
+    __syncthreads();
+    for (int ks = 0; ks < nk; ++ks) {
+      const int buf = ks & 1;
+      if (ks + 1 < nk) st.load(f1b, f2b, (ks + 1) * BK, q0, th0, tw0, g, tid);
+      mfma_stage(buf);
+      if (ks + 1 < nk) st.store(As(buf ^ 1), Bs(buf ^ 1), tid);
+      __syncthreads();
+    }
   }
 
   // ---------------- epilogue: scale, level 0, fused pooling ----------------
   const int h = lane >> 5;                 // spatial row within each 2-row MFMA tile
-  // x / sqrt(D): a multiply is bit-identical when 1/sqrt(D) is exact (D = 4^k).
-  if (g.recip != 0.f) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[t][r] *= g.recip;
-  } else {
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[t][r] = acc[t][r] / g.divisor;
-  }
+  scale_acc<DIV>(acc, g);
 
   if constexpr (!PAGED) {
     static_assert(sizeof(OT) == 4, "row-major volume is float32");
@@ -406,29 +454,29 @@ __device__ __forceinline__ void build_page_f32(const float* __restrict__ f1,
   }
 }
 
-// One page per workgroup (grid = TX*TY x QT x B).
-template <bool VEC, int BK, bool PAGED, typename OT = float, bool NTS = false>
-__global__ __launch_bounds__(NT) void corr_build_f32_kernel(const float* __restrict__ f1,
+// One page per workgroup (grid = TX*TY x QT x B).  MINW = waves per SIMD the
+// register allocation must allow (0 = compiler's choice).
+template <bool VEC, int BK, bool PAGED, typename OT, bool NTS, int MINW, bool GLDS, bool DIV>
+__global__ __launch_bounds__(NT, MINW) void corr_build_f32_kernel(const float* __restrict__ f1,
                                                             const float* __restrict__ f2,
                                                             OT* __restrict__ pyr, BuildGeom g) {
   __shared__ float lds[build_lds_floats<BK>()];
   const long long page =
       ((long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-  build_page_f32<VEC, BK, PAGED, OT, NTS>(f1, f2, pyr, g, lds, page);
+  build_page_f32<VEC, BK, PAGED, OT, NTS, GLDS, DIV>(f1, f2, pyr, g, lds, page);
 }
 
 // Persistent: gridDim.x resident workgroups walk the pages with stride
 // gridDim.x, so a page's store drain overlaps the next page's MFMA loop instead
 // of every workgroup on a CU storing in lockstep.  With TX*TY a multiple of 8
 // (e.g. 56 at Sintel shape) each XCD keeps one residue class of target tiles.
-template <bool VEC, int BK, typename OT = float, bool NTS = false>
-__global__ __launch_bounds__(NT) void corr_build_f32_persistent(const float* __restrict__ f1,
-                                                                const float* __restrict__ f2,
-                                                                OT* __restrict__ pyr,
-                                                                BuildGeom g, long long pages) {
+template <bool VEC, int BK, typename OT, bool NTS, int MINW, bool GLDS, bool DIV>
+__global__ __launch_bounds__(NT, MINW) void corr_build_f32_persistent(
+    const float* __restrict__ f1, const float* __restrict__ f2, OT* __restrict__ pyr,
+    BuildGeom g, long long pages) {
   __shared__ float lds[build_lds_floats<BK>()];
   for (long long page = blockIdx.x; page < pages; page += gridDim.x) {
-    build_page_f32<VEC, BK, true, OT, NTS>(f1, f2, pyr, g, lds, page);
+    build_page_f32<VEC, BK, true, OT, NTS, GLDS, DIV>(f1, f2, pyr, g, lds, page);
     __syncthreads();  // the next page's prologue overwrites the epilogue's LDS
   }
 }
@@ -464,7 +512,7 @@ __device__ __forceinline__ int tgt_col(int r, int c) {
   return (r >> 1) * 32 + (c & 3) + 4 * (r & 1) + 8 * (c >> 2);
 }
 
-template <bool VEC, typename OT>
+template <bool VEC, typename OT, bool DIV>
 __global__ __launch_bounds__(NT) void corr_build_bf16_kernel(const uint16_t* __restrict__ f1,
                                                              const uint16_t* __restrict__ f2,
                                                              OT* __restrict__ pyr, BuildGeom g) {
@@ -585,17 +633,7 @@ __global__ __launch_bounds__(NT) void corr_build_bf16_kernel(const uint16_t* __r
     __syncthreads();
   }
 
-  if (g.recip != 0.f) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[t][r] *= g.recip;
-  } else {
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[t][r] = acc[t][r] / g.divisor;
-  }
+  scale_acc<DIV>(acc, g);
   const long long page = ((long long)b * gridDim.y + blockIdx.y) * ((long long)g.tiles_h *
                          g.tiles_w) + (long long)tyi * g.tiles_w + txi;
   paged_epilogue<OT, false>(acc, reinterpret_cast<float*>(smem), pyr, g, page, wave, lane);
@@ -681,34 +719,43 @@ dim3 build_grid(const BuildGeom& g, int B) {
   return dim3((unsigned)(g.tiles_h * g.tiles_w), (unsigned)((g.N + BM - 1) / BM), (unsigned)B);
 }
 
-template <bool VEC, int BK, bool PAGED, typename OT = float, bool NTS = false>
-int launch_build_cfg(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, int B,
-                     hipStream_t stream) {
+int resident_build_groups(int per_cu) {
+  static int cus = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n;
+  }();
+  return cus * per_cu;
+}
+
+// One f32 build configuration.  PERSIST: gridDim = resident workgroups
+// (MINW of 4-wave workgroups per CU) walking the pages.
+template <bool VEC, int BK, bool PAGED, typename OT, bool NTS, int MINW, bool GLDS, bool PERSIST>
+int launch_f32(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, int B,
+               hipStream_t stream) {
   const dim3 grid = build_grid(g, B);
   if (grid.y > 65535) return DXR_EINVAL;
-  hipLaunchKernelGGL((corr_build_f32_kernel<VEC, BK, PAGED, OT, NTS>), grid, dim3(NT), 0, stream,
-                     f1, f2, pyr, g);
-  return dxr::launch_status();
-}
-
-int resident_build_groups() {
-  static int n = [] {
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = 256;
-    return cus * 4;  // 4 workgroups of 256 threads fit per CU (33 KB LDS, <= 128 VGPRs)
-  }();
-  return n;
-}
-
-template <bool VEC, int BK, typename OT = float, bool NTS = false>
-int launch_build_persistent(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, int B,
-                            hipStream_t stream) {
-  const long long pages = (long long)B * g.qt * g.tiles_h * g.tiles_w;
-  const long long groups = pages < resident_build_groups() ? pages : resident_build_groups();
-  hipLaunchKernelGGL((corr_build_f32_persistent<VEC, BK, OT, NTS>), dim3((unsigned)groups),
-                     dim3(NT), 0, stream, f1, f2, pyr, g, pages);
+  if constexpr (PERSIST) {
+    static_assert(PAGED, "persistent build writes pages");
+    const long long pages = (long long)grid.x * grid.y * grid.z;
+    const long long cap = resident_build_groups(MINW > 0 ? MINW : 2);
+    const unsigned groups = (unsigned)(pages < cap ? pages : cap);
+    if (g.recip != 0.f)
+      hipLaunchKernelGGL((corr_build_f32_persistent<VEC, BK, OT, NTS, MINW, GLDS, false>),
+                         dim3(groups), dim3(NT), 0, stream, f1, f2, pyr, g, pages);
+    else
+      hipLaunchKernelGGL((corr_build_f32_persistent<VEC, BK, OT, NTS, MINW, GLDS, true>),
+                         dim3(groups), dim3(NT), 0, stream, f1, f2, pyr, g, pages);
+  } else {
+    if (g.recip != 0.f)
+      hipLaunchKernelGGL((corr_build_f32_kernel<VEC, BK, PAGED, OT, NTS, MINW, GLDS, false>), grid,
+                         dim3(NT), 0, stream, f1, f2, pyr, g);
+    else
+      hipLaunchKernelGGL((corr_build_f32_kernel<VEC, BK, PAGED, OT, NTS, MINW, GLDS, true>), grid,
+                         dim3(NT), 0, stream, f1, f2, pyr, g);
+  }
   return dxr::launch_status();
 }
 
@@ -717,38 +764,56 @@ int launch_build_bf16(bool vec, const uint16_t* f1, const uint16_t* f2, OT* pyr,
                       const BuildGeom& g, int B, hipStream_t stream) {
   const dim3 grid = build_grid(g, B);
   if (grid.y > 65535) return DXR_EINVAL;
-  if (vec)
-    hipLaunchKernelGGL((corr_build_bf16_kernel<true, OT>), grid, dim3(NT), 0, stream, f1, f2, pyr,
-                       g);
+  const bool div = g.recip == 0.f;
+  if (vec && !div)
+    hipLaunchKernelGGL((corr_build_bf16_kernel<true, OT, false>), grid, dim3(NT), 0, stream, f1,
+                       f2, pyr, g);
+  else if (vec)
+    hipLaunchKernelGGL((corr_build_bf16_kernel<true, OT, true>), grid, dim3(NT), 0, stream, f1, f2,
+                       pyr, g);
+  else if (!div)
+    hipLaunchKernelGGL((corr_build_bf16_kernel<false, OT, false>), grid, dim3(NT), 0, stream, f1,
+                       f2, pyr, g);
   else
-    hipLaunchKernelGGL((corr_build_bf16_kernel<false, OT>), grid, dim3(NT), 0, stream, f1, f2, pyr,
-                       g);
+    hipLaunchKernelGGL((corr_build_bf16_kernel<false, OT, true>), grid, dim3(NT), 0, stream, f1,
+                       f2, pyr, g);
   return dxr::launch_status();
 }
 
-// DXR_BUILD_VARIANT (same-process A/B timing only): 1 selects BK = 32.
+// DXR_BUILD_VARIANT selects a tuning variant (same-process A/B timing only).
 int build_variant() {
   const char* v = std::getenv("DXR_BUILD_VARIANT");
   return v ? std::atoi(v) : 0;
 }
 
-// Variants (DXR_BUILD_VARIANT, for same-process A/B only): 0 one page per
-// workgroup, 1 the same with BK 32, 2 persistent, 3 persistent + nontemporal
-// stores, 4 one page per workgroup + nontemporal stores.
+// Variants: 0 default; 1 register staging, 2 waves/SIMD; 2 register staging,
+// 3 waves/SIMD; 3 glds staging, 3 waves/SIMD; 4 glds staging, 4 waves/SIMD;
+// 5 = 3 persistent; 6 = 2 with nontemporal stores.
 template <bool PAGED, typename OT = float>
 int launch_build_f32(bool vec, const float* f1, const float* f2, OT* pyr, const BuildGeom& g,
                      int B, hipStream_t stream) {
-  if (!vec) return launch_build_cfg<false, 16, PAGED, OT>(f1, f2, pyr, g, B, stream);
+  if (!vec) return launch_f32<false, 16, PAGED, OT, false, 0, false, false>(f1, f2, pyr, g, B, stream);
   if constexpr (PAGED) {
+    const bool glds = g.D % 16 == 0;
     switch (build_variant()) {
-      case 1: return launch_build_cfg<true, 32, true, OT>(f1, f2, pyr, g, B, stream);
-      case 2: return launch_build_persistent<true, 16, OT, false>(f1, f2, pyr, g, B, stream);
-      case 3: return launch_build_persistent<true, 16, OT, true>(f1, f2, pyr, g, B, stream);
-      case 4: return launch_build_cfg<true, 16, true, OT, true>(f1, f2, pyr, g, B, stream);
+      case 1: return launch_f32<true, 16, true, OT, false, 0, false, false>(f1, f2, pyr, g, B, stream);
+      case 2: return launch_f32<true, 16, true, OT, false, 3, false, false>(f1, f2, pyr, g, B, stream);
+      case 3:
+        if (glds) return launch_f32<true, 16, true, OT, false, 3, true, false>(f1, f2, pyr, g, B, stream);
+        break;
+      case 4:
+        if (glds) return launch_f32<true, 16, true, OT, false, 4, true, false>(f1, f2, pyr, g, B, stream);
+        break;
+      case 5:
+        if (glds) return launch_f32<true, 16, true, OT, false, 3, true, true>(f1, f2, pyr, g, B, stream);
+        break;
+      case 6: return launch_f32<true, 16, true, OT, true, 3, false, false>(f1, f2, pyr, g, B, stream);
       default: break;
     }
+    return launch_f32<true, 16, true, OT, false, 3, false, false>(f1, f2, pyr, g, B, stream);
+  } else {
+    return launch_f32<true, 16, false, OT, false, 0, false, false>(f1, f2, pyr, g, B, stream);
   }
-  return launch_build_cfg<true, 16, PAGED, OT>(f1, f2, pyr, g, B, stream);
 }
 
 BuildGeom make_geom(int64_t D, int64_t H, int64_t W, float divisor, const dxr::Levels& L) {

@@ -320,7 +320,7 @@ def test_bf16_kitti_shape(dx):
     assert np.abs(got - d["out0_val"]).max() <= BF16_RTOL * float(d["out0_maxabs"])
 
 
-@pytest.mark.parametrize("variant", ["1", "2", "3", "4"])
+@pytest.mark.parametrize("variant", ["1", "2", "3", "4", "5", "6"])
 def test_build_variants_bit_identical(dx, variant, monkeypatch):
     """Tuning variants (BK 32, persistent, nontemporal) produce the same bits."""
     f1, f2 = _pair(B=2, H=47, W=156, seed=111, dist="fnet")
