@@ -512,8 +512,8 @@ __device__ __forceinline__ int tgt_col(int r, int c) {
   return (r >> 1) * 32 + (c & 3) + 4 * (r & 1) + 8 * (c >> 2);
 }
 
-template <bool VEC, typename OT, bool DIV>
-__global__ __launch_bounds__(NT) void corr_build_bf16_kernel(const uint16_t* __restrict__ f1,
+template <bool VEC, typename OT, bool DIV, int MINW>
+__global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_t* __restrict__ f1,
                                                              const uint16_t* __restrict__ f2,
                                                              OT* __restrict__ pyr, BuildGeom g) {
   constexpr int LDS_E = WAVES * 16 * P0 * 4;          // epilogue bytes
@@ -759,25 +759,30 @@ int launch_f32(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, in
   return dxr::launch_status();
 }
 
+template <bool VEC, int MINW, typename OT>
+int launch_bf16_w(const uint16_t* f1, const uint16_t* f2, OT* pyr, const BuildGeom& g, dim3 grid,
+                  hipStream_t stream) {
+  if (g.recip == 0.f)
+    hipLaunchKernelGGL((corr_build_bf16_kernel<VEC, OT, true, MINW>), grid, dim3(NT), 0, stream,
+                       f1, f2, pyr, g);
+  else
+    hipLaunchKernelGGL((corr_build_bf16_kernel<VEC, OT, false, MINW>), grid, dim3(NT), 0, stream,
+                       f1, f2, pyr, g);
+  return dxr::launch_status();
+}
+
+int build_variant();
+
+// bf16 variants: 0 default (3 waves/SIMD; the scalar-staging path keeps the
+// compiler's choice, it would spill at 3); 1 compiler-chosen occupancy.
 template <typename OT>
 int launch_build_bf16(bool vec, const uint16_t* f1, const uint16_t* f2, OT* pyr,
                       const BuildGeom& g, int B, hipStream_t stream) {
   const dim3 grid = build_grid(g, B);
   if (grid.y > 65535) return DXR_EINVAL;
-  const bool div = g.recip == 0.f;
-  if (vec && !div)
-    hipLaunchKernelGGL((corr_build_bf16_kernel<true, OT, false>), grid, dim3(NT), 0, stream, f1,
-                       f2, pyr, g);
-  else if (vec)
-    hipLaunchKernelGGL((corr_build_bf16_kernel<true, OT, true>), grid, dim3(NT), 0, stream, f1, f2,
-                       pyr, g);
-  else if (!div)
-    hipLaunchKernelGGL((corr_build_bf16_kernel<false, OT, false>), grid, dim3(NT), 0, stream, f1,
-                       f2, pyr, g);
-  else
-    hipLaunchKernelGGL((corr_build_bf16_kernel<false, OT, true>), grid, dim3(NT), 0, stream, f1,
-                       f2, pyr, g);
-  return dxr::launch_status();
+  if (!vec) return launch_bf16_w<false, 0>(f1, f2, pyr, g, grid, stream);
+  if (build_variant() == 1) return launch_bf16_w<true, 0>(f1, f2, pyr, g, grid, stream);
+  return launch_bf16_w<true, 3>(f1, f2, pyr, g, grid, stream);
 }
 
 // DXR_BUILD_VARIANT selects a tuning variant (same-process A/B timing only).

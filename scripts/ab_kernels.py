@@ -23,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="sintel", choices=sorted(bench.WORKLOADS))
     ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
     ap.add_argument("--variants", default="0,1,2,3")
     ap.add_argument("--ablations", default="", help="timing-only variants (outputs not checked)")
     ap.add_argument("--rounds", type=int, default=5)
@@ -30,7 +31,7 @@ def main():
     a = ap.parse_args()
     (_, _), (H, W), _, _ = bench.WORKLOADS[a.workload]
     dev = torch.device("cuda", 0)
-    f1, f2, coords = bench.make_inputs(a.batch, H, W, "f32", 7, dev)
+    f1, f2, coords = bench.make_inputs(a.batch, H, W, a.dtype, 7, dev)
     variants = [int(v) for v in a.variants.split(",")]
     ablations = [int(v) for v in a.ablations.split(",") if v]
     times = {v: [] for v in variants + ablations}
@@ -70,7 +71,7 @@ def main():
             torch.cuda.synchronize()
             lk.append(e0.elapsed_time(e1) / a.reps / len(coords) * 1e3)
     flops = bench.build_flops(a.batch, H, W)
-    res = {"workload": a.workload, "batch": a.batch,
+    res = {"workload": a.workload, "batch": a.batch, "dtype": a.dtype,
            "build_us": {v: {"median": float(np.median(t)), "min": float(np.min(t))}
                         for v, t in times.items()},
            "build_tflops_median": {v: flops / (np.median(t) * 1e-6) / 1e12 for v, t in times.items()},
