@@ -322,11 +322,18 @@ def test_bf16_kitti_shape(dx):
 
 @pytest.mark.parametrize("variant", ["1", "2", "3", "4", "5", "6"])
 def test_build_variants_bit_identical(dx, variant, monkeypatch):
-    """Tuning variants (BK 32, persistent, nontemporal) produce the same bits."""
+    """Tuning variants (occupancy, glds staging, persistent, nontemporal) produce
+    the same bits in every valid pyramid cell (page padding is never read and
+    its content is variant-specific), and the same lookups."""
     f1, f2 = _pair(B=2, H=47, W=156, seed=111, dist="fnet")
-    ref = dx.CorrBlock(f1, f2)._buf.clone()
+    c = _t(dg.coords(112, 2, 47, 156, "uniform", 12.0))
+    ref_cb = dx.CorrBlock(f1, f2)
+    ref, ref_out = ref_cb.corr_pyramid, ref_cb(c)
     monkeypatch.setenv("DXR_BUILD_VARIANT", variant)
-    assert torch.equal(dx.CorrBlock(f1, f2)._buf, ref)
+    cb = dx.CorrBlock(f1, f2)
+    for lvl, (a, b) in enumerate(zip(cb.corr_pyramid, ref)):
+        assert torch.equal(a, b), f"level {lvl}"
+    assert torch.equal(cb(c), ref_out)
 
 
 # --------------------------------------------------------------------------- edge cases / API
