@@ -76,6 +76,20 @@ def lookup_bytes(B, H, W, s_pyr=4):
     return B * H * W * (win * s_pyr + 8 + LEVELS * rd * rd * 4)
 
 
+def build_kernel(dtype, H, W):
+    """Which build kernel the library runs for this workload (csrc/corr_build.hip
+    launch_build_f32 / launch_build_bf16), and the MFMA work it executes per
+    algorithmic flop: the split f32 build issues six bf16 MFMA products per f32
+    product (exact hi+mid+lo operand split, f32 accumulation)."""
+    variant = os.environ.get("DXR_BUILD_VARIANT", "0")
+    if dtype == "bf16":
+        return "corr_build_bf16_kernel", 1, PEAK_BF16_TFLOPS, "bf16"
+    if D % 16 == 0 and W % 4 == 0 and variant in ("0", "7", "8", "9"):
+        return ("corr_build_split_kernel (f32 operands split exactly into 3 bf16, "
+                "bf16x6 MFMA, f32 accumulate)", 6, PEAK_BF16_TFLOPS, "bf16 MFMA, f32 accumulate")
+    return "corr_build_f32_kernel", 1, PEAK_F32_TFLOPS, "f32"
+
+
 def init_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -223,8 +237,8 @@ def main():
         value = pairs / elapsed
         s_in = 2 if dtype == "bf16" else 4
         flops = build_flops(B, H, W)
-        peak = PEAK_BF16_TFLOPS if dtype == "bf16" else PEAK_F32_TFLOPS
-        achieved = flops / (build_ms * 1e-3) / 1e12
+        kname, mfma_per_flop, peak, mfma_dtype = build_kernel(dtype, H, W)
+        achieved = mfma_per_flop * flops / (build_ms * 1e-3) / 1e12
         lb = lookup_bytes(B, H, W, s_pyr=s_in)
         res = {
             "metric": METRIC,
@@ -245,11 +259,14 @@ def main():
                 "pairs_per_gpu": B, "mode": args.mode, "parallelism": f"pairs sharded x{world}",
             },
             "roofline": {
-                "kernel": "corr_build_f32_kernel (stage a+b)",
+                "kernel": kname + " (stage a+b)",
                 "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                 "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                 "traffic": None,
+                "mfma_dtype": mfma_dtype,
                 "algorithmic_flops_per_launch": flops,
+                "mfma_flops_per_launch": mfma_per_flop * flops,
+                "f32_equivalent_tflops": round(flops / (build_ms * 1e-3) / 1e12, 2),
                 "avg_launch_us": round(build_ms * 1e3, 2),
             },
             "lookup_roofline": {

@@ -639,6 +639,188 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_
   paged_epilogue<OT, false>(acc, reinterpret_cast<float*>(smem), pyr, g, page, wave, lane);
 }
 
+// ---------------------------------------------------------------------------
+// f32 build on bf16 MFMA by exact 3-way operand split ("split" build).
+// Every f32 operand x is split as x = hi + mid + lo with hi, mid, lo bf16 and the
+// sum EXACT: hi = x with its low 16 bits cleared, mid = (x - hi) likewise, lo =
+// x - hi - mid (at most 8 significant bits, so exact in bf16; |x| in the normal
+// f32 range).  A product x*y is then the sum of nine exact bf16 x bf16 products;
+// the six kept here (hh, hm, mh, hl, lh, mm) leave out terms below 2^-24 |x y|,
+// i.e. below f32 rounding of the product itself, and are accumulated in f32 by
+// v_mfma_f32_32x32x16_bf16 — 6 x 32 cycles per 16 k against 8 x 64 for
+// v_mfma_f32_32x32x2_f32.  The result has f32-class error (tests compare it with
+// the f64 oracle at the same tolerance as the f32 MFMA build).
+//
+// Operands: the wave's 32 queries are loaded straight from global memory into
+// MFMA B-operand order (lane l: query l&31, k 8(l>>5)..+7) and split in
+// registers — no other wave reads them, so they skip LDS; the 8x16 target tile
+// (shared by the four waves) is split once per workgroup into three bf16 LDS
+// planes in the transposed-read layout of the bf16 build, double-buffered.
+// ---------------------------------------------------------------------------
+constexpr int BKS = 16;                 // K per stage
+constexpr int PLANE_S = BKS * PH;       // bf16 elements per split plane
+constexpr int STAGE_S = 3 * PLANE_S;    // hi, mid, lo planes
+
+struct Split3 {
+  uint32_t h, m, l;  // bf16 bit patterns in the high halves
+};
+
+__device__ __forceinline__ Split3 split3(float x) {
+  const uint32_t hb = __float_as_uint(x) & 0xffff0000u;
+  const float r1 = x - __uint_as_float(hb);
+  const uint32_t mb = __float_as_uint(r1) & 0xffff0000u;
+  const float r2 = r1 - __uint_as_float(mb);
+  return {hb, mb, __float_as_uint(r2)};
+}
+
+// bf16x2 word of the high halves of two f32 bit patterns (element a low).
+__device__ __forceinline__ uint32_t pack_hi(uint32_t a, uint32_t b) {
+  return __builtin_amdgcn_perm(b, a, 0x07060302u);
+}
+
+// ABL (timing-only ablations, never the default): 1 skips the epilogue stores,
+// 2 skips the MFMAs.
+template <typename OT, bool DIV, int MINW, int ABL = 0>
+__global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float* __restrict__ f1,
+                                                                    const float* __restrict__ f2,
+                                                                    OT* __restrict__ pyr,
+                                                                    BuildGeom g) {
+  constexpr int LDS_E = WAVES * 16 * P0 * 4;   // epilogue bytes
+  constexpr int LDS_K = 2 * STAGE_S * 2;       // two stages, bytes
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_K > LDS_E ? LDS_K : LDS_E];
+  uint16_t* lh = reinterpret_cast<uint16_t*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int txi = blockIdx.x % g.tiles_w, tyi = blockIdx.x / g.tiles_w;
+  const int th0 = tyi * TH, tw0 = txi * TW;
+  const int q0 = blockIdx.y * BM;
+  const int b = blockIdx.z;
+  const long long fstride = (long long)g.D * g.N;
+  const float* f1b = f1 + b * fstride;
+  const float* f2b = f2 + b * fstride;
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  // Query operand: lane -> (query q0 + 32 wave + (lane & 31), k rows 8 (lane >> 5) + e).
+  // Padding queries read a clamped, valid address (their outputs are page padding).
+  const int qa = min(q0 + wave * 32 + (lane & 31), g.N - 1);
+  const float* pa = f1b + (long long)(8 * (lane >> 5)) * g.N + qa;
+  // Target staging: 2 float4 per thread per stage, unit idx -> (k, tile row, col/4).
+  int bk[2], bcol[2];
+  long long boff[2];
+  bool bok[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int idx = tid + NT * s;
+    const int k = idx >> 5, r = (idx >> 2) & 7, c = (idx & 3) * 4;
+    bk[s] = k;
+    bcol[s] = tgt_col(r, c);
+    bok[s] = th0 + r < g.H && tw0 + c < g.W;
+    boff[s] = (long long)k * g.N + (long long)(th0 + r) * g.W + tw0 + c;
+  }
+
+  float an[8];
+  float4 bn[2];
+  auto load = [&](int k0) {
+    const long long ko = (long long)k0 * g.N;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) an[e] = pa[ko + (long long)e * g.N];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      bn[s] = bok[s] ? *reinterpret_cast<const float4*>(f2b + ko + boff[s])
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  s8v ah, am, al;   // split query operand of the current stage
+  auto split_a = [&]() {
+    uint32_t h[4], m[4], l[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const Split3 x = split3(an[2 * e]), y = split3(an[2 * e + 1]);
+      h[e] = pack_hi(x.h, y.h);
+      m[e] = pack_hi(x.m, y.m);
+      l[e] = pack_hi(x.l, y.l);
+    }
+    ah = __builtin_bit_cast(s8v, make_uint4(h[0], h[1], h[2], h[3]));
+    am = __builtin_bit_cast(s8v, make_uint4(m[0], m[1], m[2], m[3]));
+    al = __builtin_bit_cast(s8v, make_uint4(l[0], l[1], l[2], l[3]));
+  };
+  auto store_b = [&](int buf) {
+    uint16_t* P = lh + buf * STAGE_S;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const Split3 x = split3(bn[s].x), y = split3(bn[s].y), z = split3(bn[s].z),
+                   w = split3(bn[s].w);
+      const int o = bk[s] * PH + bcol[s];
+      *reinterpret_cast<uint2*>(P + o) = make_uint2(pack_hi(x.h, y.h), pack_hi(z.h, w.h));
+      *reinterpret_cast<uint2*>(P + PLANE_S + o) = make_uint2(pack_hi(x.m, y.m), pack_hi(z.m, w.m));
+      *reinterpret_cast<uint2*>(P + 2 * PLANE_S + o) =
+          make_uint2(pack_hi(x.l, y.l), pack_hi(z.l, w.l));
+    }
+  };
+
+  const int li = lane & 15;
+  const int rd_off = (li >> 2) * PH + 4 * (li & 3) + 16 * ((lane >> 4) & 1) + 8 * (lane >> 5) * PH;
+  auto frag = [&](const uint16_t* p) {
+    return __builtin_bit_cast(bf8v, __builtin_shufflevector(tr_read(p), tr_read(p + 4 * PH), 0, 1,
+                                                            2, 3, 4, 5, 6, 7));
+  };
+
+  const int nk = g.D / BKS;
+  load(0);
+  store_b(0);
+  split_a();
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) load((ks + 1) * BKS);
+    const bf8v qh = __builtin_bit_cast(bf8v, ah), qm = __builtin_bit_cast(bf8v, am),
+               ql = __builtin_bit_cast(bf8v, al);
+    const uint16_t* P = lh + buf * STAGE_S + rd_off;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const bf8v th = frag(P + t * 32), tm = frag(P + PLANE_S + t * 32),
+                 tl = frag(P + 2 * PLANE_S + t * 32);
+      if constexpr (ABL == 2) {
+        const s8v x = __builtin_bit_cast(s8v, th) ^ __builtin_bit_cast(s8v, tm) ^
+                      __builtin_bit_cast(s8v, tl) ^ __builtin_bit_cast(s8v, qh) ^
+                      __builtin_bit_cast(s8v, qm) ^ __builtin_bit_cast(s8v, ql);
+        acc[t][0] += (float)(x[0] + x[3] + x[5] + x[7]);
+        continue;
+      }
+      // small terms first
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, ql, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qh, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qm, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh, acc[t], 0, 0, 0);
+    }
+    if (ks + 1 < nk) {
+      store_b(buf ^ 1);
+      split_a();
+    }
+    __syncthreads();
+  }
+
+  scale_acc<DIV>(acc, g);
+  if constexpr (ABL == 1) {
+    float sum = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sum += acc[t][r];
+    if (sum == 1234.5f) pyr[tid] = to_out<OT>(sum);  // keeps the K loop live
+    return;
+  }
+  const long long page = ((long long)b * gridDim.y + blockIdx.y) * ((long long)g.tiles_h *
+                         g.tiles_w) + (long long)tyi * g.tiles_w + txi;
+  paged_epilogue<OT, false>(acc, reinterpret_cast<float*>(smem), pyr, g, page, wave, lane);
+}
+
 // Floor-mode 2x2 average pool of one pyramid level into the next, for levels
 // beyond the fused four (any layout, addressed through dxr::cell_index).
 __global__ __launch_bounds__(256) void pool_level_kernel(float* __restrict__ pyr,
@@ -785,15 +967,34 @@ int launch_build_bf16(bool vec, const uint16_t* f1, const uint16_t* f2, OT* pyr,
   return launch_bf16_w<true, 3>(f1, f2, pyr, g, grid, stream);
 }
 
+template <int MINW, typename OT, int ABL = 0>
+int launch_split(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, int B,
+                 hipStream_t stream) {
+  const dim3 grid = build_grid(g, B);
+  if (grid.y > 65535) return DXR_EINVAL;
+  if (g.recip == 0.f)
+    hipLaunchKernelGGL((corr_build_split_kernel<OT, true, MINW, ABL>), grid, dim3(NT), 0, stream,
+                       f1, f2, pyr, g);
+  else
+    hipLaunchKernelGGL((corr_build_split_kernel<OT, false, MINW, ABL>), grid, dim3(NT), 0, stream,
+                       f1, f2, pyr, g);
+  return dxr::launch_status();
+}
+
 // DXR_BUILD_VARIANT selects a tuning variant (same-process A/B timing only).
 int build_variant() {
   const char* v = std::getenv("DXR_BUILD_VARIANT");
   return v ? std::atoi(v) : 0;
 }
 
-// Variants: 0 default; 1 register staging, 2 waves/SIMD; 2 register staging,
-// 3 waves/SIMD; 3 glds staging, 3 waves/SIMD; 4 glds staging, 4 waves/SIMD;
-// 5 = 3 persistent; 6 = 2 with nontemporal stores.
+// Variants: 0 default (= 8, the split build, when D % 16 == 0, else 2);
+// f32-MFMA builds: 1 register staging,
+// 2 waves/SIMD; 2 register staging, 3 waves/SIMD; 3 glds staging, 3 waves/SIMD;
+// 4 glds staging, 4 waves/SIMD; 5 = 3 persistent; 6 = 2 with nontemporal
+// stores.  Measured (sintel, MI355X, r01i): 257 / 278 / 258 / 247 / 245 / 250 /
+// 257 us for variants 0(old default = 2) .. 6; 10 = 4.  Split builds (bf16x6
+// MFMA, f32-class error): 7 at 3 waves/SIMD, 8 at 4, 9 compiler-chosen —
+// r01k: 177 / 172 / 183 us against 289 us for the f32-MFMA build on that box.
 template <bool PAGED, typename OT = float>
 int launch_build_f32(bool vec, const float* f1, const float* f2, OT* pyr, const BuildGeom& g,
                      int B, hipStream_t stream) {
@@ -813,7 +1014,27 @@ int launch_build_f32(bool vec, const float* f1, const float* f2, OT* pyr, const 
         if (glds) return launch_f32<true, 16, true, OT, false, 3, true, true>(f1, f2, pyr, g, B, stream);
         break;
       case 6: return launch_f32<true, 16, true, OT, true, 3, false, false>(f1, f2, pyr, g, B, stream);
-      default: break;
+      case 7:
+        if (glds) return launch_split<3>(f1, f2, pyr, g, B, stream);
+        break;
+      case 8:
+        if (glds) return launch_split<4>(f1, f2, pyr, g, B, stream);
+        break;
+      case 9:
+        if (glds) return launch_split<2>(f1, f2, pyr, g, B, stream);
+        break;
+      case 91:  // timing-only ablations of the split build (outputs invalid)
+        if (glds) return launch_split<4, OT, 1>(f1, f2, pyr, g, B, stream);
+        break;
+      case 92:
+        if (glds) return launch_split<4, OT, 2>(f1, f2, pyr, g, B, stream);
+        break;
+      case 10:  // f32 MFMA build (glds staging, 4 waves/SIMD)
+        if (glds) return launch_f32<true, 16, true, OT, false, 4, true, false>(f1, f2, pyr, g, B, stream);
+        break;
+      default:
+        if (glds) return launch_split<4>(f1, f2, pyr, g, B, stream);
+        break;
     }
     return launch_f32<true, 16, true, OT, false, 3, false, false>(f1, f2, pyr, g, B, stream);
   } else {

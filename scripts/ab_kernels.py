@@ -28,15 +28,20 @@ def main():
     ap.add_argument("--ablations", default="", help="timing-only variants (outputs not checked)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--interleave", action="store_true",
+                    help="run the 12 lookups between builds (as bench.py does) and time builds only")
+    ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--side-stream", action="store_true", help="launch on a non-default stream")
     a = ap.parse_args()
     (_, _), (H, W), _, _ = bench.WORKLOADS[a.workload]
     dev = torch.device("cuda", 0)
-    f1, f2, coords = bench.make_inputs(a.batch, H, W, a.dtype, 7, dev)
+    f1, f2, coords = bench.make_inputs(a.batch, H, W, a.dtype, a.seed, dev)
     variants = [int(v) for v in a.variants.split(",")]
     ablations = [int(v) for v in a.ablations.split(",") if v]
     times = {v: [] for v in variants + ablations}
     ref = None
-    with torch.no_grad():
+    side = torch.cuda.Stream(device=dev) if a.side_stream else torch.cuda.current_stream(dev)
+    with torch.no_grad(), torch.cuda.stream(side):
         for v in variants:                      # correctness: variants are bit-identical
             os.environ["DXR_BUILD_VARIANT"] = str(v)
             cb = dexiraft_amd.CorrBlock(f1, f2)      # valid cells only (padding is never read)
@@ -47,6 +52,18 @@ def main():
         for _ in range(a.rounds):
             for v in variants + ablations:
                 os.environ["DXR_BUILD_VARIANT"] = str(v)
+                if a.interleave:
+                    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                           for _ in range(a.reps)]
+                    for e0, e1 in evs:
+                        e0.record()
+                        cb = dexiraft_amd.CorrBlock(f1, f2)
+                        e1.record()
+                        for c in coords:
+                            cb(c)
+                    torch.cuda.synchronize()
+                    times[v].append(float(np.mean([x.elapsed_time(y) for x, y in evs])) * 1e3)
+                    continue
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.reps):
@@ -72,7 +89,8 @@ def main():
             torch.cuda.synchronize()
             lk.append(e0.elapsed_time(e1) / a.reps / len(coords) * 1e3)
     flops = bench.build_flops(a.batch, H, W)
-    res = {"workload": a.workload, "batch": a.batch, "dtype": a.dtype,
+    res = {"workload": a.workload, "batch": a.batch, "dtype": a.dtype, "seed": a.seed,
+           "interleave": a.interleave, "side_stream": a.side_stream,
            "build_us": {v: {"median": float(np.median(t)), "min": float(np.min(t))}
                         for v, t in times.items()},
            "build_tflops_median": {v: flops / (np.median(t) * 1e-6) / 1e12 for v, t in times.items()},

@@ -320,13 +320,17 @@ def test_bf16_kitti_shape(dx):
     assert np.abs(got - d["out0_val"]).max() <= BF16_RTOL * float(d["out0_maxabs"])
 
 
-@pytest.mark.parametrize("variant", ["1", "2", "3", "4", "5", "6"])
-def test_build_variants_bit_identical(dx, variant, monkeypatch):
+# f32-MFMA build variants are checked against variant 2, split-build variants
+# against the default (the split build at 4 waves/SIMD).
+@pytest.mark.parametrize("variant,base", [("1", "2"), ("3", "2"), ("4", "2"), ("5", "2"),
+                                          ("6", "2"), ("10", "2"), ("7", "0"), ("9", "0")])
+def test_build_variants_bit_identical(dx, variant, base, monkeypatch):
     """Tuning variants (occupancy, glds staging, persistent, nontemporal) produce
     the same bits in every valid pyramid cell (page padding is never read and
     its content is variant-specific), and the same lookups."""
     f1, f2 = _pair(B=2, H=47, W=156, seed=111, dist="fnet")
     c = _t(dg.coords(112, 2, 47, 156, "uniform", 12.0))
+    monkeypatch.setenv("DXR_BUILD_VARIANT", base)
     ref_cb = dx.CorrBlock(f1, f2)
     ref, ref_out = ref_cb.corr_pyramid, ref_cb(c)
     monkeypatch.setenv("DXR_BUILD_VARIANT", variant)
@@ -334,6 +338,40 @@ def test_build_variants_bit_identical(dx, variant, monkeypatch):
     for lvl, (a, b) in enumerate(zip(cb.corr_pyramid, ref)):
         assert torch.equal(a, b), f"level {lvl}"
     assert torch.equal(cb(c), ref_out)
+
+
+@pytest.mark.parametrize("variant", ["0", "7"])
+def test_split_build_f32_accuracy(dx, variant, monkeypatch):
+    """The split build (f32 operands as exact hi+mid+lo bf16 triples, six bf16
+    MFMA products, f32 accumulation) has f32-class error: within RTOL of the
+    float64 oracle everywhere, and no worse than 2x the f32-MFMA build's own error."""
+    H, W = 55, 128
+    f1 = dg.fmap(51, 1, 256, H, W, "fnet")
+    f2 = dg.fmap(52, 1, 256, H, W, "fnet")
+    c = dg.coords(53, 1, H, W, "normal", 4.0)
+    pyr = oracle.corr_pyramid(f1, f2, 4, np.float64)
+    monkeypatch.setenv("DXR_BUILD_VARIANT", "10")           # f32 MFMA build
+    base = dx.CorrBlock(_t(f1), _t(f2)).corr_pyramid
+    monkeypatch.setenv("DXR_BUILD_VARIANT", variant)
+    cb = dx.CorrBlock(_t(f1), _t(f2))
+    for lvl in range(4):
+        got = cb.corr_pyramid[lvl][:, 0].cpu().numpy()
+        tolerance_check(got, pyr[lvl], RTOL)
+        e_split = np.abs(got - pyr[lvl]).max()
+        e_mfma = np.abs(base[lvl][:, 0].cpu().numpy() - pyr[lvl]).max()
+        print(f"level {lvl}: max|err| split {e_split:.3e}, f32 mfma {e_mfma:.3e}, "
+              f"max|ref| {np.abs(pyr[lvl]).max():.2f}")
+        assert e_split <= 2 * e_mfma + 1e-6
+    tolerance_check(cb(_t(c)).cpu().numpy(), oracle.corr_lookup(pyr, c, 4), RTOL)
+    for name in ("nanlevel", "batch2_alt", "min8"):          # D % 16 == 0, W % 4 == 0
+        d = load_tiny(name)
+        cb = dx.CorrBlock(_t(d["fmap1"]), _t(d["fmap2"]), num_levels=d["num_levels"],
+                          radius=d["radius"])
+        rows = torch.from_numpy(d["pyr_rows"]).to(DEV)
+        for lvl in range(d["num_levels"]):
+            tolerance_check(cb.corr_pyramid[lvl][rows, 0].cpu().numpy(), d[f"pyr{lvl}"], RTOL)
+        for k in range(d["n_coords"]):
+            tolerance_check(cb(_t(d[f"coords{k}"])).cpu().numpy(), d[f"out{k}"], RTOL)
 
 
 # --------------------------------------------------------------------------- edge cases / API
