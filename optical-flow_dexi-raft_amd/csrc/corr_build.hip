@@ -642,14 +642,19 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_
 // ---------------------------------------------------------------------------
 // f32 build on bf16 MFMA by exact 3-way operand split ("split" build).
 // Every f32 operand x is split as x = hi + mid + lo with hi, mid, lo bf16 and the
-// sum EXACT: hi = x with its low 16 bits cleared, mid = (x - hi) likewise, lo =
-// x - hi - mid (at most 8 significant bits, so exact in bf16; |x| in the normal
-// f32 range).  A product x*y is then the sum of nine exact bf16 x bf16 products;
-// the six kept here (hh, hm, mh, hl, lh, mm) leave out terms below 2^-24 |x y|,
-// i.e. below f32 rounding of the product itself, and are accumulated in f32 by
-// v_mfma_f32_32x32x16_bf16 — 6 x 32 cycles per 16 k against 8 x 64 for
-// v_mfma_f32_32x32x2_f32.  The result has f32-class error (tests compare it with
-// the f64 oracle at the same tolerance as the f32 MFMA build).
+// sum EXACT: hi = RNE_bf16(x), mid = RNE_bf16(x - hi), lo = x - hi - mid (the
+// residuals are multiples of ulp(x) spanning <= 16 and <= 8 significant bits, so
+// both subtractions and lo are exact; |x| in the normal f32 range).  A product
+// x*y is then the sum of nine exact bf16 x bf16 products; the six kept here (hh,
+// hm, mh, hl, lh, mm) leave out |mid*lo| + |lo*mid| + |lo*lo| <= 2^-25 |x y|,
+// below f32 rounding of the product itself.  Round-to-nearest splitting makes
+// the residuals sign-symmetric, so the dropped terms carry no bias (a truncating
+// split leaves them all with the sign of x*y: a -3e-8 relative shrink of every
+// sum, visible in the 49.5 M-cell checksums of the Sintel volume).  They are
+// accumulated in f32 by v_mfma_f32_32x32x16_bf16 — 6 x 32 cycles per 16 k
+// against 8 x 64 for v_mfma_f32_32x32x2_f32.  The result has f32-class error
+// (tests compare it with the f64 oracle at the same tolerance as the f32 MFMA
+// build, and its checksums with the reference's).
 //
 // Operands: the wave's 32 queries are loaded straight from global memory into
 // MFMA B-operand order (lane l: query l&31, k 8(l>>5)..+7) and split in
@@ -662,20 +667,30 @@ constexpr int PLANE_S = BKS * PH;       // bf16 elements per split plane
 constexpr int STAGE_S = 3 * PLANE_S;    // hi, mid, lo planes
 
 struct Split3 {
-  uint32_t h, m, l;  // bf16 bit patterns in the high halves
+  uint32_t h, m, l;  // bf16x2 words (first element in the low half)
 };
 
-__device__ __forceinline__ Split3 split3(float x) {
-  const uint32_t hb = __float_as_uint(x) & 0xffff0000u;
-  const float r1 = x - __uint_as_float(hb);
-  const uint32_t mb = __float_as_uint(r1) & 0xffff0000u;
-  const float r2 = r1 - __uint_as_float(mb);
-  return {hb, mb, __float_as_uint(r2)};
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+// v_cvt_pk_bf16_f32: round-to-nearest-even of two floats into one bf16x2 word.
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+  const f32x2_t v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
 
 // bf16x2 word of the high halves of two f32 bit patterns (element a low).
 __device__ __forceinline__ uint32_t pack_hi(uint32_t a, uint32_t b) {
   return __builtin_amdgcn_perm(b, a, 0x07060302u);
+}
+
+// Exact 3-way split of two floats (see above), packed for the MFMA operands.
+__device__ __forceinline__ Split3 split3(float a, float b) {
+  const uint32_t h = cvt_pk_bf16(a, b);
+  const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
+  const uint32_t m = cvt_pk_bf16(ra, rb);
+  const float la = ra - __uint_as_float(m << 16), lb = rb - __uint_as_float(m & 0xffff0000u);
+  return {h, m, pack_hi(__float_as_uint(la), __float_as_uint(lb))};
 }
 
 // ABL (timing-only ablations, never the default): 1 skips the epilogue stores,
@@ -739,10 +754,10 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     uint32_t h[4], m[4], l[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const Split3 x = split3(an[2 * e]), y = split3(an[2 * e + 1]);
-      h[e] = pack_hi(x.h, y.h);
-      m[e] = pack_hi(x.m, y.m);
-      l[e] = pack_hi(x.l, y.l);
+      const Split3 x = split3(an[2 * e], an[2 * e + 1]);
+      h[e] = x.h;
+      m[e] = x.m;
+      l[e] = x.l;
     }
     ah = __builtin_bit_cast(s8v, make_uint4(h[0], h[1], h[2], h[3]));
     am = __builtin_bit_cast(s8v, make_uint4(m[0], m[1], m[2], m[3]));
@@ -752,13 +767,11 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     uint16_t* P = lh + buf * STAGE_S;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const Split3 x = split3(bn[s].x), y = split3(bn[s].y), z = split3(bn[s].z),
-                   w = split3(bn[s].w);
+      const Split3 x = split3(bn[s].x, bn[s].y), z = split3(bn[s].z, bn[s].w);
       const int o = bk[s] * PH + bcol[s];
-      *reinterpret_cast<uint2*>(P + o) = make_uint2(pack_hi(x.h, y.h), pack_hi(z.h, w.h));
-      *reinterpret_cast<uint2*>(P + PLANE_S + o) = make_uint2(pack_hi(x.m, y.m), pack_hi(z.m, w.m));
-      *reinterpret_cast<uint2*>(P + 2 * PLANE_S + o) =
-          make_uint2(pack_hi(x.l, y.l), pack_hi(z.l, w.l));
+      *reinterpret_cast<uint2*>(P + o) = make_uint2(x.h, z.h);
+      *reinterpret_cast<uint2*>(P + PLANE_S + o) = make_uint2(x.m, z.m);
+      *reinterpret_cast<uint2*>(P + 2 * PLANE_S + o) = make_uint2(x.l, z.l);
     }
   };
 

@@ -18,6 +18,8 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import bench  # noqa: E402  (workload table, algorithmic byte/flop formulas)
 import dexiraft_amd  # noqa: E402
 
+SPLIT_VARIANTS = {0, 7, 8, 9}  # f32 builds on bf16 MFMA (exact operand split); D % 16 == 0
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -39,16 +41,17 @@ def main():
     variants = [int(v) for v in a.variants.split(",")]
     ablations = [int(v) for v in a.ablations.split(",") if v]
     times = {v: [] for v in variants + ablations}
-    ref = None
     side = torch.cuda.Stream(device=dev) if a.side_stream else torch.cuda.current_stream(dev)
     with torch.no_grad(), torch.cuda.stream(side):
-        for v in variants:                      # correctness: variants are bit-identical
+        ref = {}
+        for v in variants:  # correctness: variants of one family are bit-identical
             os.environ["DXR_BUILD_VARIANT"] = str(v)
             cb = dexiraft_amd.CorrBlock(f1, f2)      # valid cells only (padding is never read)
-            if ref is None:
-                ref = cb.corr_pyramid
-            assert all(torch.equal(x, y) for x, y in zip(cb.corr_pyramid, ref)), \
-                f"variant {v} differs from variant {variants[0]}"
+            fam = "split" if v in SPLIT_VARIANTS and a.dtype == "f32" else "mfma"
+            if fam not in ref:
+                ref[fam] = (v, cb.corr_pyramid)
+            assert all(torch.equal(x, y) for x, y in zip(cb.corr_pyramid, ref[fam][1])), \
+                f"variant {v} differs from variant {ref[fam][0]}"
         for _ in range(a.rounds):
             for v in variants + ablations:
                 os.environ["DXR_BUILD_VARIANT"] = str(v)
