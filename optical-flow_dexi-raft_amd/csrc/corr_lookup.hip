@@ -29,6 +29,8 @@
 //            gathers thrash the 32 KiB L1 and become L2-bandwidth bound);
 //   phase 2  thread = (query, x-offset class): taps from LDS, fused sum, and
 //            every output store is a coalesced 256-B wave store along queries.
+#include <cstdlib>
+
 #include "dxr_common.h"
 
 namespace {
@@ -94,7 +96,9 @@ struct LookupCfg {
   static constexpr int CPL = (NC + 63) / 64;    // window cells per lane per query
 };
 
-template <int R, typename PT>
+// ABL (timing-only ablations, DXR_LOOKUP_VARIANT; outputs invalid): bit 0 skips
+// the window gathers, bit 1 skips the output stores.
+template <int R, typename PT, int ABL = 0>
 __global__ __launch_bounds__(LookupCfg<R>::NTHR) void corr_lookup_kernel(const PT* __restrict__ pyr,
                                                            const float* __restrict__ coords,
                                                            float* __restrict__ out,
@@ -167,7 +171,8 @@ __global__ __launch_bounds__(LookupCfg<R>::NTHR) void corr_lookup_kernel(const P
       const bool in = live && c < NC && (unsigned)yy < (unsigned)Hl && (unsigned)xx < (unsigned)Wl;
       const long long e = ((long long)(yy >> A.lth) * A.tx + (xx >> A.ltw)) * A.pageS +
                           (yy & A.mh) * A.tw + (xx & A.mw);
-      cellv[i][m] = in ? load_cell(img + e) : 0.f;
+      if constexpr (ABL & 1) cellv[i][m] = in ? (float)(e & 7) : 0.f;
+      else cellv[i][m] = in ? load_cell(img + e) : 0.f;
     }
   }
 #pragma unroll
@@ -216,9 +221,227 @@ __global__ __launch_bounds__(LookupCfg<R>::NTHR) void corr_lookup_kernel(const P
       v = __builtin_fmaf(ne, v01, v);
       v = __builtin_fmaf(sw, v10, v);
       v = __builtin_fmaf(se, v11, v);
-      ob[(long long)(ox * RD + oy) * g.N] = v;
+      if constexpr (ABL & 2) {
+        if (v == 1234.5f) ob[(long long)(ox * RD + oy) * g.N] = v;
+      } else {
+        ob[(long long)(ox * RD + oy) * g.N] = v;
+      }
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Lookup, wide form (default).  Same arithmetic, sample by sample, as
+// corr_lookup_kernel above; the work of a workgroup (QB queries x one level) is
+// spread over NT = 512 threads so that no phase is a long per-thread chain:
+//   phase 0  one thread per (query, sample index j): both axes' coordinate
+//            round trips, floors and fractions; the window origin
+//            min_j(floor_j - j) and the far test are reduced over the query's
+//            G-lane group by shuffles; per-sample tap data {cell offset, f, 1-f}
+//            goes to LDS;
+//   phase 1  the QB windows are gathered as aligned vectors of V cells (V = 4 on
+//            the paged levels 0-2, whose tile rows hold >= 4 cells; 2 on level 3;
+//            1 on row-major levels), with 32-bit offsets from the workgroup's page
+//            base, into LDS rows of RS cells starting at the origin rounded down
+//            to a multiple of 4;
+//   phase 2  thread = (query, output class), stores along queries.
+// The narrow form's profile (r01, sintel: 1,600 VALU instructions per wave,
+// 1.7 waves per SIMD, 8.8 of 11.6 us left with gathers and stores removed) was
+// its per-thread instruction chains: the per-cell address arithmetic of the
+// gather, and phase 0 on a quarter of the threads.
+// ---------------------------------------------------------------------------
+template <int R>
+struct WideCfg {
+  static constexpr int RD = 2 * R + 1;
+  static constexpr int WD = RD + 2;                      // window side (cells)
+  static constexpr int RS = (WD + 3 + 3) & ~3;           // LDS row: 4-aligned start + WD
+  static constexpr int NQ = RS / 4;                      // 4-cell vectors per LDS row
+  static constexpr int QS = WD * RS + 4;                 // LDS cells per query (bank skew)
+  static constexpr int K = RD * RD;                      // outputs per query and level
+  static constexpr int NT = 512;
+  static constexpr int QB = R <= 4 ? 32 : 16;            // queries per workgroup
+  static constexpr int LG = RD <= 2 ? 1 : RD <= 4 ? 2 : RD <= 8 ? 3 : RD <= 16 ? 4 : 5;
+  static constexpr int G = 1 << LG;                      // lanes per query in phase 0
+  static constexpr int VSLOTS = QB * WD * NQ;            // 4-cell vectors per workgroup
+  static constexpr int VIT = (VSLOTS + NT - 1) / NT;
+  static constexpr int NCLS = NT / QB;                   // output classes
+  static_assert(QB * G <= NT, "one phase-0 slot per thread");
+  static_assert(G <= 64, "a query's lane group must sit in one wave");
+  static_assert(QB <= dxr::PAGE_Q && dxr::PAGE_Q % QB == 0, "a workgroup stays in one page");
+};
+
+// V consecutive cells of one tile row (or of a row-major level), widened to f32.
+template <int V, typename PT>
+__device__ __forceinline__ void load_vec(const PT* p, float* v) {
+  if constexpr (sizeof(PT) == 4 && V == 4) {
+    const float4 x = *reinterpret_cast<const float4*>(p);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  } else if constexpr (sizeof(PT) == 4 && V == 2) {
+    const float2 x = *reinterpret_cast<const float2*>(p);
+    v[0] = x.x; v[1] = x.y;
+  } else if constexpr (sizeof(PT) == 2 && V == 4) {
+    const uint2 x = *reinterpret_cast<const uint2*>(p);
+    v[0] = __uint_as_float(x.x << 16); v[1] = __uint_as_float(x.x & 0xffff0000u);
+    v[2] = __uint_as_float(x.y << 16); v[3] = __uint_as_float(x.y & 0xffff0000u);
+  } else if constexpr (sizeof(PT) == 2 && V == 2) {
+    const uint32_t x = *reinterpret_cast<const uint32_t*>(p);
+    v[0] = __uint_as_float(x << 16); v[1] = __uint_as_float(x & 0xffff0000u);
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) v[i] = load_cell(p + i);
+  }
+}
+
+// Phase 1 for one level type: V-cell vectors, 4 per LDS vector slot.
+template <int R, int V, typename PT>
+__device__ __forceinline__ void gather_windows(const PT* __restrict__ base, int qb0, const LevelAddr& A,
+                                               const int2* org, float* cells, int q0, int N,
+                                               int tid) {
+  using C = WideCfg<R>;
+  float4 v[C::VIT];
+#pragma unroll
+  for (int i = 0; i < C::VIT; ++i) {
+    const int s = tid + i * C::NT;
+    const int qq = s / (C::WD * C::NQ), rem = s - qq * (C::WD * C::NQ);
+    const int r = rem / C::NQ, k = rem - r * C::NQ;
+    float c[4] = {0.f, 0.f, 0.f, 0.f};
+    if (s < C::VSLOTS && q0 + qq < N) {
+      const int2 o = org[qq];
+      const int yy = o.y + r, x0 = (o.x & ~3) + 4 * k;
+      if (o.x != FAR_ORIGIN && (unsigned)yy < (unsigned)A.h && x0 >= 0 && x0 < A.w) {
+        const unsigned qoff = (unsigned)(qb0 + qq) * (unsigned)A.S;
+        const unsigned yoff = (unsigned)(yy >> A.lth) * (unsigned)A.tx;
+        const unsigned yin = (unsigned)((yy & A.mh) * A.tw);
+#pragma unroll
+        for (int h = 0; h < 4; h += V) {
+          const int x = x0 + h;
+          const unsigned e = qoff + (yoff + (unsigned)(x >> A.ltw)) * (unsigned)A.pageS + yin +
+                             (unsigned)(x & A.mw);
+          if (V == 4 || x < A.w) load_vec<V>(base + e, c + h);
+        }
+#pragma unroll
+        for (int h = 1; h < 4; ++h)
+          if (x0 + h >= A.w) c[h] = 0.f;   // past the level's right edge (tile padding)
+      }
+    }
+    v[i] = make_float4(c[0], c[1], c[2], c[3]);
+  }
+#pragma unroll
+  for (int i = 0; i < C::VIT; ++i) {
+    const int s = tid + i * C::NT;
+    if (s < C::VSLOTS) {
+      const int qq = s / (C::WD * C::NQ), rem = s - qq * (C::WD * C::NQ);
+      *reinterpret_cast<float4*>(cells + qq * C::QS + rem * 4) = v[i];
+    }
+  }
+}
+
+// ABL (timing-only ablations, outputs invalid): 4 returns at once, 5 after phase 0,
+// 6 after phase 1, 7 skips the gathers.
+template <int R, typename PT, int ABL = 0>
+__global__ __launch_bounds__(WideCfg<R>::NT) void corr_lookup_wide_kernel(
+    const PT* __restrict__ pyr, const float* __restrict__ coords, float* __restrict__ out,
+    LookupGeom g) {
+  using C = WideCfg<R>;
+  constexpr int RD = C::RD, WD = C::WD, RS = C::RS, K = C::K, QB = C::QB, G = C::G;
+  __shared__ __attribute__((aligned(16))) float cells[QB * C::QS];
+  __shared__ float4 xs[RD * QB];   // {column in the LDS row (int bits), fx, 1-fx, -}
+  __shared__ float4 ys[RD * QB];   // {row offset in LDS (int bits), fy, 1-fy, -}
+  __shared__ int2 org[QB];         // window origin (x, y) or FAR_ORIGIN
+
+  const int tid = threadIdx.x;
+  const int l = blockIdx.y, b = blockIdx.z;
+  const int q0 = blockIdx.x * QB;
+  const LevelAddr A = g.lv[l];
+  const int Hl = A.h, Wl = A.w;
+  if constexpr (ABL == 4) return;
+
+  // ---- phase 0
+  if (tid < QB * G) {
+    const int j = tid & (G - 1), qq = tid >> C::LG;
+    const int q = q0 + qq;
+    float cx = 0.f, cy = 0.f;
+    if (q < g.N) {
+      cx = coords[((long long)b * 2 + 0) * g.N + q];
+      cy = coords[((long long)b * 2 + 1) * g.N + q];
+    }
+    const float inv = 1.f / (float)(1 << l);  // exact power of two
+    const float wm1 = (float)(Wl - 1), hm1 = (float)(Hl - 1);
+    const float ux = sample_coord(__fadd_rn(cx * inv, (float)(j - R)), wm1, wm1 / 2.f);
+    const float uy = sample_coord(__fadd_rn(cy * inv, (float)(j - R)), hm1, hm1 / 2.f);
+    const float flx = floorf(ux), fly = floorf(uy);
+    const bool act = j < RD;
+    // a non-finite or huge sample makes its query far: FAR_ORIGIN propagates through the min
+    int mx = 0x7fffffff, my = 0x7fffffff;
+    if (act) {
+      const bool bad = !(fabsf(flx) < 1.0e7f) || !(fabsf(fly) < 1.0e7f);
+      mx = bad ? FAR_ORIGIN : (int)flx - j;
+      my = bad ? FAR_ORIGIN : (int)fly - j;
+    }
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) {
+      mx = min(mx, __shfl_xor(mx, o));
+      my = min(my, __shfl_xor(my, o));
+    }
+    // windows entirely off the level hold only zeros: no loads
+    const bool far = mx + WD <= 0 || mx >= Wl || my + WD <= 0 || my >= Hl;
+    if (j == 0) org[qq] = far ? make_int2(FAR_ORIGIN, FAR_ORIGIN) : make_int2(mx, my);
+    if (act) {
+      const float fx = __fsub_rn(ux, flx), fy = __fsub_rn(uy, fly);
+      const int col = far ? 0 : (int)flx - (mx & ~3);
+      const int row = far ? 0 : ((int)fly - my) * RS;
+      xs[j * QB + qq] = make_float4(__int_as_float(col), fx, __fsub_rn(1.f, fx), 0.f);
+      ys[j * QB + qq] = make_float4(__int_as_float(row), fy, __fsub_rn(1.f, fy), 0.f);
+    }
+  }
+  __syncthreads();
+  if constexpr (ABL == 5) {
+    if (xs[tid % (RD * QB)].y == 1234.5f) out[tid] = 0.f;
+    return;
+  }
+
+  // ---- phase 1 (zeros off the level and for far queries)
+  if constexpr (ABL != 7) {
+    const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
+    const int qb0 = q0 & ((1 << A.lqb) - 1);
+    if (A.lth == 30)
+      gather_windows<R, 1>(base, qb0, A, org, cells, q0, g.N, tid);
+    else if (A.tw >= 4)
+      gather_windows<R, 4>(base, qb0, A, org, cells, q0, g.N, tid);
+    else if (A.tw == 2)
+      gather_windows<R, 2>(base, qb0, A, org, cells, q0, g.N, tid);
+    else
+      gather_windows<R, 1>(base, qb0, A, org, cells, q0, g.N, tid);
+  }
+  __syncthreads();
+  if constexpr (ABL == 6) {
+    if (cells[tid] == 1234.5f) out[tid] = 0.f;
+    return;
+  }
+
+  // ---- phase 2
+  const int qq = tid % QB, cls = tid / QB;
+  if (q0 + qq >= g.N) return;
+  const float* cq = cells + qq * C::QS;
+  float* ob = out + ((long long)b * g.cout + (long long)l * K) * g.N + q0 + qq;
+  for (int k = cls; k < K; k += C::NCLS) {
+    const int ox = k / RD, oy = k - ox * RD;
+    const float4 xd = xs[ox * QB + qq], yd = ys[oy * QB + qq];
+    const float* p = cq + __float_as_int(yd.x) + __float_as_int(xd.x);
+    const float v00 = p[0], v01 = p[1], v10 = p[RS], v11 = p[RS + 1];
+    const float nw = __fmul_rn(yd.z, xd.z), ne = __fmul_rn(yd.z, xd.y);
+    const float sw = __fmul_rn(yd.y, xd.z), se = __fmul_rn(yd.y, xd.y);
+    float r = __fmul_rn(nw, v00);
+    r = __builtin_fmaf(ne, v01, r);
+    r = __builtin_fmaf(sw, v10, r);
+    r = __builtin_fmaf(se, v11, r);
+    ob[(unsigned)(k * g.N)] = r;
+  }
+}
+
+int lookup_variant() {
+  const char* v = std::getenv("DXR_LOOKUP_VARIANT");
+  return v ? std::atoi(v) : 0;
 }
 
 template <int R, typename PT>
@@ -226,8 +449,40 @@ int launch_lookup_r(const PT* pyr, const float* coords, float* out, const Lookup
                     hipStream_t stream) {
   using C = LookupCfg<R>;
   const dim3 grid((unsigned)((g.N + C::QB - 1) / C::QB), (unsigned)g.levels, (unsigned)B);
-  hipLaunchKernelGGL((corr_lookup_kernel<R, PT>), grid, dim3(C::NTHR), 0, stream, pyr, coords,
-                     out, g);
+  switch (lookup_variant()) {
+    case 91:
+      hipLaunchKernelGGL((corr_lookup_kernel<R, PT, 1>), grid, dim3(C::NTHR), 0, stream, pyr,
+                         coords, out, g);
+      break;
+    case 92:
+      hipLaunchKernelGGL((corr_lookup_kernel<R, PT, 2>), grid, dim3(C::NTHR), 0, stream, pyr,
+                         coords, out, g);
+      break;
+    case 93:
+      hipLaunchKernelGGL((corr_lookup_kernel<R, PT, 3>), grid, dim3(C::NTHR), 0, stream, pyr,
+                         coords, out, g);
+      break;
+    case 1:  // narrow form
+      hipLaunchKernelGGL((corr_lookup_kernel<R, PT>), grid, dim3(C::NTHR), 0, stream, pyr, coords,
+                         out, g);
+      break;
+    case 94: case 95: case 96: case 97: {
+      using W = WideCfg<R>;
+      const dim3 gw((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
+      const int v = lookup_variant();
+      if (v == 94) hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT, 4>), gw, dim3(W::NT), 0, stream, pyr, coords, out, g);
+      if (v == 95) hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT, 5>), gw, dim3(W::NT), 0, stream, pyr, coords, out, g);
+      if (v == 96) hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT, 6>), gw, dim3(W::NT), 0, stream, pyr, coords, out, g);
+      if (v == 97) hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT, 7>), gw, dim3(W::NT), 0, stream, pyr, coords, out, g);
+      break;
+    }
+    default: {
+      using W = WideCfg<R>;
+      const dim3 gw((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
+      hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT>), gw, dim3(W::NT), 0, stream, pyr,
+                         coords, out, g);
+    }
+  }
   return dxr::launch_status();
 }
 
