@@ -16,8 +16,11 @@ used.  Rank 0 prints ONE JSON line.
 Execution: the step is captured into two HIP graphs (build, lookups) and
 replayed — the launch-bound lookups would otherwise be host-bound in Python.
 HIP events between the two replays give the build kernel's duration inside the
-timed region (the roofline's ``achieved``).  ``--mode eager`` times plain
-Python calls instead.
+timed region (the roofline's ``achieved``; it includes the graph launch, so it
+reads a few percent above the rocprofv3 kernel duration — conservative).
+(Event-record nodes inside one K-step graph would exclude it, but ROCm torch
+refuses external events and raw hipEventRecord nodes did not record: r01.)
+``--mode eager`` times plain Python calls instead.
 """
 from __future__ import annotations
 
@@ -88,6 +91,19 @@ def build_kernel(dtype, H, W):
         return ("corr_build_split_kernel (f32 operands split exactly into 3 bf16, "
                 "bf16x6 MFMA, f32 accumulate)", 6, PEAK_BF16_TFLOPS, "bf16 MFMA, f32 accumulate")
     return "corr_build_f32_kernel", 1, PEAK_F32_TFLOPS, "f32"
+
+
+def pmc_traffic(kernel_prefix):
+    """Per-launch HBM bytes of a kernel from the newest committed PMC summary
+    (profiles/<round>/traffic.json, written by scripts/pmc_traffic.py from
+    separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench), or None."""
+    files = sorted((REPO / "profiles").glob("*/traffic.json"))
+    for f in reversed(files):
+        data = json.loads(f.read_text())
+        for name, rec in data.items():
+            if name.split("::")[-1].startswith(kernel_prefix):
+                return rec["traffic_bytes"], f"{f.relative_to(REPO)}: {rec['correction']}"
+    return None, None
 
 
 def init_dist():
@@ -190,6 +206,7 @@ def main():
     def lookups():
         state["outs"] = [state["cb"](c) for c in coords]
 
+    timing = "hip events between graph replays"
     with torch.no_grad(), torch.cuda.stream(stream):
         for _ in range(max(args.warmup, 1)):          # eager warmup (also JIT-free check)
             build()
@@ -207,6 +224,7 @@ def main():
                 run_look()
         else:
             run_build, run_look = build, lookups
+            timing = "hip events between eager launches"
         torch.cuda.synchronize()
 
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
@@ -239,6 +257,9 @@ def main():
         flops = build_flops(B, H, W)
         kname, mfma_per_flop, peak, mfma_dtype = build_kernel(dtype, H, W)
         achieved = mfma_per_flop * flops / (build_ms * 1e-3) / 1e12
+        kshort = kname.split(" ")[0]
+        b_traffic, b_src = pmc_traffic(kshort + "<")
+        l_traffic, l_src = pmc_traffic("corr_lookup_wide_kernel<")
         lb = lookup_bytes(B, H, W, s_pyr=s_in)
         res = {
             "metric": METRIC,
@@ -257,12 +278,13 @@ def main():
                 "workload": f"CorrBlock build + {ITERS} lookups, {args.workload} "
                             f"{img_h}x{img_w} (fmap {H}x{W}), D={D}, r={RADIUS}, L={LEVELS}",
                 "pairs_per_gpu": B, "mode": args.mode, "parallelism": f"pairs sharded x{world}",
+                "kernel_timing": timing,
             },
             "roofline": {
                 "kernel": kname + " (stage a+b)",
                 "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                 "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                "traffic": None,
+                "traffic": b_traffic, "traffic_source": b_src,
                 "mfma_dtype": mfma_dtype,
                 "algorithmic_flops_per_launch": flops,
                 "mfma_flops_per_launch": mfma_per_flop * flops,
@@ -270,11 +292,12 @@ def main():
                 "avg_launch_us": round(build_ms * 1e3, 2),
             },
             "lookup_roofline": {
-                "kernel": "corr_lookup_kernel (stage c)",
+                "kernel": "corr_lookup_wide_kernel (stage c)",
                 "bound": "hbm", "achieved": round(lb / (look_ms * 1e-3) / 1e9, 1),
                 "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(lb / (look_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
                 "algorithmic_bytes_per_launch": lb,
+                "traffic": l_traffic, "traffic_source": l_src,
                 "avg_launch_us": round(look_ms * 1e3, 2),
             },
             "build_bytes_per_launch": build_bytes(B, H, W, s_in, s_in),

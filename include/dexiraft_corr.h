@@ -57,7 +57,7 @@ extern "C" {
 /* HIP's own definition; repeating an identical typedef is legal in C11/C++. */
 typedef struct ihipStream_t* hipStream_t;
 
-#define DXR_ABI_VERSION 1
+#define DXR_ABI_VERSION 2
 
 enum dxr_status {
   DXR_OK = 0,
@@ -87,19 +87,36 @@ int64_t dxr_pyramid_numel(int64_t B, int64_t H, int64_t W, int num_levels);
 int64_t dxr_pyramid_level_offset(int64_t B, int64_t H, int64_t W, int level);
 
 /*
+ * Bytes of device workspace dxr_corr_pyramid_build can use for these shapes
+ * (0 = none): the exact hi/mid/lo bf16 split planes of both float32 fmaps
+ * (2 * B * 3 * D * H * W * 2 bytes; D % 16 == 0).  The caller allocates it; it
+ * is dead once the build's kernels have run (stream order).
+ */
+int64_t dxr_build_workspace_bytes(int64_t B, int64_t D, int64_t H, int64_t W,
+                                  int in_dtype);
+
+/*
  * Stage (a)+(b): all-pairs correlation fmap1^T . fmap2 / divisor and its
  * avg-pool pyramid, written in one pass (pooling fused into the MFMA epilogue).
  *   fmap1, fmap2 : [B, D, H, W], dtype in_dtype (DXR_F32 or DXR_BF16)
  *   divisor      : the reference divides by sqrt(D) (core/corr.py:60)
  *   pyramid      : dxr_pyramid_numel(B,H,W,num_levels) elements of pyr_dtype
  *   num_levels   : >= 1; every level must be at least 1 x 1
- * DXR_F32 inputs compute with exact-f32 MFMA (v_mfma_f32_32x32x2_f32); DXR_BF16
- * inputs use bf16 MFMA with f32 accumulation.
+ *   workspace    : NULL, or >= dxr_build_workspace_bytes(...) bytes, 16-byte
+ *                  aligned (a smaller or NULL workspace selects a build that
+ *                  needs none; results are identical)
+ * DXR_F32 inputs compute in f32 class: every f32 operand is split exactly into
+ * three bf16 parts and six bf16 x bf16 MFMA products per f32 product are
+ * accumulated in f32 (terms below 2^-25 |x y| dropped); with D % 16 != 0 the
+ * exact-f32 MFMA v_mfma_f32_32x32x2_f32 is used.  DXR_BF16 inputs use bf16 MFMA
+ * with f32 accumulation.
  */
 int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int in_dtype,
                            int64_t B, int64_t D, int64_t H, int64_t W,
                            int num_levels, float divisor,
-                           void* pyramid, int pyr_dtype, hipStream_t stream);
+                           void* pyramid, int pyr_dtype,
+                           void* workspace, int64_t workspace_bytes,
+                           hipStream_t stream);
 
 /*
  * CorrBlock.corr: the level-0 volume alone, row-major [B, H, W, 1, H, W]

@@ -116,8 +116,9 @@ class CorrBlock:
     (``dxr_corr_lookup``) returning a new contiguous float32
     ``[B, num_levels*(2r+1)^2, H, W]`` tensor in the reference's channel order.
 
-    fp32 fmaps (the reference's dtype, core/raft.py:139-142) compute with exact
-    f32 MFMA and store an f32 pyramid.  The pyramid lives in one paged buffer
+    fp32 fmaps (the reference's dtype, core/raft.py:139-142) compute in f32
+    class (exact three-way bf16 split of every operand, six bf16 MFMA products
+    per f32 product, f32 accumulation) and store an f32 pyramid.  The pyramid lives in one paged buffer
     (``_buf``); ``corr_pyramid`` gives the reference-layout levels on demand.
     """
 
@@ -145,10 +146,14 @@ class CorrBlock:
         self._buf = torch.empty(numel, dtype=pyr_torch, device=fmap1.device)
         f1 = fmap1.contiguous()
         f2 = fmap2.contiguous()
+        # Split-plane workspace (f32 fmaps): a temporary from torch's caching
+        # allocator, released in stream order after the build's kernels.
+        ws_bytes = lib.dxr_build_workspace_bytes(B, D, H, W, in_dt)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=fmap1.device) if ws_bytes else None
         with _Launch(self._device):
             st = lib.dxr_corr_pyramid_build(
                 f1.data_ptr(), f2.data_ptr(), in_dt, B, D, H, W, num_levels, _sqrt_dim(D),
-                self._buf.data_ptr(), pyr_dt, nat.stream_of(f1))
+                self._buf.data_ptr(), pyr_dt, nat.ptr(ws), ws_bytes, nat.stream_of(f1))
         nat.check(st, "CorrBlock build (dxr_corr_pyramid_build)")
         self._level_sizes = sizes
         self._ref_pyramid = None

@@ -820,7 +820,182 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
   }
 
   scale_acc<DIV>(acc, g);
-  if constexpr (ABL == 1) {
+  if constexpr (ABL == 1 || ABL == 4) {
+    float sum = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sum += acc[t][r];
+    if (sum == 1234.5f) pyr[tid] = to_out<OT>(sum);  // keeps the K loop live
+    return;
+  }
+  const long long page = ((long long)b * gridDim.y + blockIdx.y) * ((long long)g.tiles_h *
+                         g.tiles_w) + (long long)tyi * g.tiles_w + txi;
+  paged_epilogue<OT, false>(acc, reinterpret_cast<float*>(smem), pyr, g, page, wave, lane);
+}
+
+// ---------------------------------------------------------------------------
+// Pre-split f32 build ("presplit", the default for f32 fmaps with D % 16 == 0).
+// The same exact hi+mid+lo operand split and the same six bf16 MFMA products as
+// the split build above, but the split is done ONCE per fmap element by
+// split_planes_kernel into a workspace, instead of once per workgroup that reads
+// the element (55-56 times at Sintel).  The split build's profile (r01, sintel:
+// 113 us of its 173 us left with the MFMAs removed, ~195 VALU per wave and
+// k-step) was that in-loop split plus its staging; here the K loop issues no
+// VALU work beyond address increments.
+//
+// Workspace layout (16-byte chunks of 8 consecutive k of one pixel, bf16):
+//   chunk(fmap, b, plane, kb, pixel) at (((fmap*B + b)*3 + plane)*(D/8) + kb)*N + pixel
+// An MFMA operand lane (row = pixel, 8 k) is one chunk, so 32 lanes of a wave
+// read 512 contiguous bytes.  Query operands go global -> registers (each wave
+// reads only its own 32 queries); the 8x16 target tile, shared by the four
+// waves, goes global -> LDS by global_load_lds_dwordx4 into a 3-stage ring, in
+// slot order (target, k-half ^ target-row parity): that swizzle makes the
+// per-lane 16-byte fragment reads conflict-free.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void split_planes_kernel(const float* __restrict__ f1,
+                                                           const float* __restrict__ f2,
+                                                           uint4* __restrict__ ws, int B, int D,
+                                                           int N) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  const int kb = blockIdx.y;
+  const int fb = blockIdx.z;               // fmap * B + b
+  if (p >= N) return;
+  const float* src = (fb < B ? f1 + (long long)fb * D * N : f2 + (long long)(fb - B) * D * N) +
+                     (long long)kb * 8 * N + p;
+  float x[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) x[e] = src[(long long)e * N];
+  uint32_t h[4], m[4], l[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const Split3 v = split3(x[2 * e], x[2 * e + 1]);
+    h[e] = v.h; m[e] = v.m; l[e] = v.l;
+  }
+  const long long plane = (long long)(D / 8) * N;
+  uint4* dst = ws + (long long)fb * 3 * plane + (long long)kb * N + p;
+  dst[0] = make_uint4(h[0], h[1], h[2], h[3]);
+  dst[plane] = make_uint4(m[0], m[1], m[2], m[3]);
+  dst[2 * plane] = make_uint4(l[0], l[1], l[2], l[3]);
+}
+
+// Stage = one 16-deep k slice: target tile (3 planes x 128 targets x 2 k-halves
+// x 16 B, shared by the four waves) + query panel (4 waves x 3 planes x 2 halves
+// x 32 queries x 16 B; each wave's part is read only by that wave).
+constexpr int PS_B = 3 * NTGT * 2 * 16;      // 12 KiB
+constexpr int PS_AW = 3 * 2 * 32 * 16;       // 3 KiB per wave
+constexpr int PS_STAGE = PS_B + WAVES * PS_AW;
+
+__device__ __forceinline__ void glds_chunk(const uint4* g, unsigned char* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g),
+                                   (__attribute__((address_space(3))) void*)(l), 16, 0, 0);
+}
+
+// Both operands arrive by LDS-DMA only (no VGPR-destination loads in the loop,
+// so no compiler-inserted vmcnt(0)), NS stages in flight, a counted
+// s_waitcnt vmcnt and a raw s_barrier per k step (__syncthreads() would drain
+// the in-flight DMA: cdna_hip_programming.md §5 "Pipelining across barriers").
+// ABL (timing-only ablations, never the default): 1 skips the epilogue stores,
+// 2 skips the MFMAs, 3 skips the K loop, 4 = 1 + 2.
+template <typename OT, bool DIV, int MINW, int NS, int ABL = 0>
+__global__ __launch_bounds__(NT, MINW) void corr_build_presplit_kernel(const uint4* __restrict__ ws,
+                                                                       OT* __restrict__ pyr,
+                                                                       BuildGeom g, int B) {
+  constexpr int LDS_E = WAVES * 16 * P0 * 4;              // epilogue bytes
+  constexpr int LDS_K = NS * PS_STAGE;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_K > LDS_E ? LDS_K : LDS_E];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int txi = blockIdx.x % g.tiles_w, tyi = blockIdx.x / g.tiles_w;
+  const int th0 = tyi * TH, tw0 = txi * TW;
+  const int q0 = blockIdx.y * BM;
+  const int b = blockIdx.z;
+  const long long plane = (long long)(g.D / 8) * g.N;     // chunks per plane
+  const uint4* wa = ws + (long long)b * 3 * plane;          // fmap1 planes of pair b
+  const uint4* wb = ws + (long long)(B + b) * 3 * plane;    // fmap2 planes of pair b
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  // Query DMA: lane -> (k-half lane >> 5, query q0 + 32 wave + (lane & 31)); the
+  // LDS image [plane][half][32] is lane-linear, and so is the fragment read.
+  // Padding queries read a clamped, valid pixel (their outputs are page padding).
+  const int kh = lane >> 5;
+  const uint4* pa = wa + (long long)kh * g.N + min(q0 + wave * 32 + (lane & 31), g.N - 1);
+  // Target DMA: thread tid fills slot tid of each plane: target sp = tid >> 1,
+  // k-half (tid & 1) ^ (target row parity).  Off-image targets read clamped pixels.
+  const int sp = tid >> 1;
+  const int sr = sp >> 4, sc = sp & 15;
+  const int skh = (tid & 1) ^ (sr & 1);
+  const uint4* pb = wb + (long long)skh * g.N + (long long)min(th0 + sr, g.H - 1) * g.W +
+                    min(tw0 + sc, g.W - 1);
+  // Fragment read offset of tile t: target j of MFMA tile t is spatial
+  // (2t + ((j >> 2) & 1), (j & 3) + 4 (j >> 3)).
+  const int j = lane & 31;
+  const int rsp = ((j >> 2) & 1) * 16 + (j & 3) + 4 * (j >> 3);
+  const int rdb = (rsp * 2 + (kh ^ ((j >> 2) & 1))) * 16;
+  const int rda = PS_B + wave * PS_AW + lane * 16;
+
+  const int nk = g.D / 16;
+  auto issue = [&](int ks) {
+    unsigned char* st = smem + (ks % NS) * PS_STAGE;
+    const long long ko = (long long)ks * 2 * g.N;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) glds_chunk(pb + ko + p * plane, st + p * (NTGT * 2 * 16) + wave * 1024);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) glds_chunk(pa + ko + p * plane, st + PS_B + wave * PS_AW + p * 1024);
+  };
+  auto compute = [&](int ks) {
+    const unsigned char* st = smem + (ks % NS) * PS_STAGE;
+    const bf8v qh = *reinterpret_cast<const bf8v*>(st + rda);
+    const bf8v qm = *reinterpret_cast<const bf8v*>(st + rda + 1024);
+    const bf8v ql = *reinterpret_cast<const bf8v*>(st + rda + 2048);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const unsigned char* pt = st + rdb + t * 32 * 2 * 16;
+      const bf8v th = *reinterpret_cast<const bf8v*>(pt);
+      const bf8v tm = *reinterpret_cast<const bf8v*>(pt + NTGT * 2 * 16);
+      const bf8v tl = *reinterpret_cast<const bf8v*>(pt + 2 * NTGT * 2 * 16);
+      if constexpr (ABL == 2 || ABL == 4) {
+        const s8v x = __builtin_bit_cast(s8v, th) ^ __builtin_bit_cast(s8v, tm) ^
+                      __builtin_bit_cast(s8v, tl) ^ __builtin_bit_cast(s8v, qh) ^
+                      __builtin_bit_cast(s8v, qm) ^ __builtin_bit_cast(s8v, ql);
+        acc[t][0] += (float)(x[0] + x[3] + x[5] + x[7]);
+        continue;
+      }
+      // small terms first
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, ql, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qh, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qm, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh, acc[t], 0, 0, 0);
+    }
+  };
+
+  // Iteration ks: wait for stage ks (all but the 6 DMA ops of each younger stage
+  // in flight), raw barrier (the DMA data of every wave is then visible, and
+  // every wave has finished reading stage ks - 1), issue stage ks + NS - 1 into
+  // the slot stage ks - 1 used, compute stage ks.
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (ABL != 3 && s < nk) issue(s);
+  for (int ks = 0; ks < (ABL == 3 ? 0 : nk); ++ks) {
+    const int younger = min(NS - 2, nk - 1 - ks);   // stages issued after ks
+    if (NS >= 3 && younger >= 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (ks + NS - 1 < nk) issue(ks + NS - 1);
+    compute(ks);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();   // the epilogue reuses the ring's LDS
+
+  scale_acc<DIV>(acc, g);
+  if constexpr (ABL == 1 || ABL == 4) {
     float sum = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -994,13 +1169,41 @@ int launch_split(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, 
   return dxr::launch_status();
 }
 
+// Workspace of the presplit build: hi/mid/lo bf16 planes of both fmaps.
+long long presplit_ws_bytes(long long B, long long D, long long N) {
+  return 2LL * B * 3 * D * N * 2;
+}
+
+template <int MINW, int NS, typename OT, int ABL = 0>
+int launch_presplit(const float* f1, const float* f2, void* ws, OT* pyr, const BuildGeom& g,
+                    int B, hipStream_t stream) {
+  const dim3 grid = build_grid(g, B);
+  if (grid.y > 65535 || 2LL * B > 65535) return DXR_EINVAL;
+  uint4* w = static_cast<uint4*>(ws);
+  hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((g.N + 255) / 256), (unsigned)(g.D / 8),
+                                               (unsigned)(2 * B)),
+                     dim3(256), 0, stream, f1, f2, w, B, g.D, g.N);
+  const int st = dxr::launch_status();
+  if (st != DXR_OK) return st;
+  if (g.recip == 0.f)
+    hipLaunchKernelGGL((corr_build_presplit_kernel<OT, true, MINW, NS, ABL>), grid, dim3(NT), 0,
+                       stream, w, pyr, g, B);
+  else
+    hipLaunchKernelGGL((corr_build_presplit_kernel<OT, false, MINW, NS, ABL>), grid, dim3(NT), 0,
+                       stream, w, pyr, g, B);
+  return dxr::launch_status();
+}
+
 // DXR_BUILD_VARIANT selects a tuning variant (same-process A/B timing only).
 int build_variant() {
   const char* v = std::getenv("DXR_BUILD_VARIANT");
   return v ? std::atoi(v) : 0;
 }
 
-// Variants: 0 default (= 8, the split build, when D % 16 == 0, else 2);
+// Variants: 0 default (= 8, the split build, when D % 16 == 0 and W % 4 == 0;
+// else 2); presplit builds (need the workspace; r01 sintel: 181-190 us vs 178
+// for 8, operand staging L2 -> LDS bound, §DESIGN): 11 = 3-stage ring (72 KiB, 2 WG/CU),
+// 12 = 2 stages at 3 WG/CU, 13 = 2 stages at 2 WG/CU, 14 = 2 stages at 4 waves/SIMD;
 // f32-MFMA builds: 1 register staging,
 // 2 waves/SIMD; 2 register staging, 3 waves/SIMD; 3 glds staging, 3 waves/SIMD;
 // 4 glds staging, 4 waves/SIMD; 5 = 3 persistent; 6 = 2 with nontemporal
@@ -1010,7 +1213,21 @@ int build_variant() {
 // r01k: 177 / 172 / 183 us against 289 us for the f32-MFMA build on that box.
 template <bool PAGED, typename OT = float>
 int launch_build_f32(bool vec, const float* f1, const float* f2, OT* pyr, const BuildGeom& g,
-                     int B, hipStream_t stream) {
+                     int B, hipStream_t stream, void* ws = nullptr) {
+  if constexpr (PAGED) {
+    // presplit: any W (edge tiles read clamped pixels), needs D % 16 and the workspace
+    const int v = build_variant();
+    if (ws != nullptr && g.D % 16 == 0) {
+      if (v == 11) return launch_presplit<2, 3, OT>(f1, f2, ws, pyr, g, B, stream);
+      if (v == 12) return launch_presplit<3, 2, OT>(f1, f2, ws, pyr, g, B, stream);
+      if (v == 13) return launch_presplit<2, 2, OT>(f1, f2, ws, pyr, g, B, stream);
+      if (v == 14) return launch_presplit<4, 2, OT>(f1, f2, ws, pyr, g, B, stream);
+      if (v == 111) return launch_presplit<2, 3, OT, 1>(f1, f2, ws, pyr, g, B, stream);  // timing
+      if (v == 112) return launch_presplit<2, 3, OT, 2>(f1, f2, ws, pyr, g, B, stream);  // timing
+      if (v == 113) return launch_presplit<2, 3, OT, 3>(f1, f2, ws, pyr, g, B, stream);  // timing
+      if (v == 114) return launch_presplit<2, 3, OT, 4>(f1, f2, ws, pyr, g, B, stream);  // timing
+    }
+  }
   if (!vec) return launch_f32<false, 16, PAGED, OT, false, 0, false, false>(f1, f2, pyr, g, B, stream);
   if constexpr (PAGED) {
     const bool glds = g.D % 16 == 0;
@@ -1099,24 +1316,38 @@ extern "C" int dxr_avg_pool2x2(const float* in, float* out, int64_t planes, int6
   return launch_avg_pool(in, out, planes, (int)H, (int)W, stream);
 }
 
+extern "C" int64_t dxr_build_workspace_bytes(int64_t B, int64_t D, int64_t H, int64_t W,
+                                             int in_dtype) {
+  if (B < 1 || D < 1 || H < 1 || W < 1 || H * W > (1LL << 30)) return 0;
+  if (in_dtype != DXR_F32 || D % 16 != 0) return 0;
+  const int v = build_variant();   // only the presplit variants use a workspace
+  if (!((v >= 11 && v <= 14) || (v >= 111 && v <= 114))) return 0;
+  return presplit_ws_bytes(B, D, H * W);
+}
+
 extern "C" int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int in_dtype,
                                       int64_t B, int64_t D, int64_t H, int64_t W,
                                       int num_levels, float divisor, void* pyramid,
-                                      int pyr_dtype, hipStream_t stream) {
+                                      int pyr_dtype, void* workspace, int64_t workspace_bytes,
+                                      hipStream_t stream) {
   dxr::Levels L;
   if (!dxr::make_levels(B, H, W, num_levels, &L)) return DXR_EINVAL;
   const int chk = check_build_args(fmap1, fmap2, in_dtype, B, D, divisor, pyramid, pyr_dtype);
   if (chk != PROCEED) return chk;
+  if (workspace_bytes < 0 || (workspace != nullptr && !aligned16(workspace))) return DXR_EINVAL;
   const BuildGeom g = make_geom(D, H, W, divisor, L);
   int st;
   if (in_dtype == DXR_F32) {
     const float* f1 = static_cast<const float*>(fmap1);
     const float* f2 = static_cast<const float*>(fmap2);
     const bool vec = (W % 4) == 0 && aligned16(f1) && aligned16(f2) && aligned16(pyramid);
+    const int64_t need = dxr_build_workspace_bytes(B, D, H, W, in_dtype);
+    void* ws = (need > 0 && workspace != nullptr && workspace_bytes >= need) ? workspace : nullptr;
     st = pyr_dtype == DXR_F32
-             ? launch_build_f32<true>(vec, f1, f2, static_cast<float*>(pyramid), g, (int)B, stream)
+             ? launch_build_f32<true>(vec, f1, f2, static_cast<float*>(pyramid), g, (int)B, stream,
+                                      ws)
              : launch_build_f32<true>(vec, f1, f2, static_cast<uint16_t*>(pyramid), g, (int)B,
-                                      stream);
+                                      stream, ws);
   } else {
     const uint16_t* f1 = static_cast<const uint16_t*>(fmap1);
     const uint16_t* f2 = static_cast<const uint16_t*>(fmap2);

@@ -250,7 +250,7 @@ __global__ __launch_bounds__(LookupCfg<R>::NTHR) void corr_lookup_kernel(const P
 // its per-thread instruction chains: the per-cell address arithmetic of the
 // gather, and phase 0 on a quarter of the threads.
 // ---------------------------------------------------------------------------
-template <int R>
+template <int R, int NT_ = 512>
 struct WideCfg {
   static constexpr int RD = 2 * R + 1;
   static constexpr int WD = RD + 2;                      // window side (cells)
@@ -258,14 +258,15 @@ struct WideCfg {
   static constexpr int NQ = RS / 4;                      // 4-cell vectors per LDS row
   static constexpr int QS = WD * RS + 4;                 // LDS cells per query (bank skew)
   static constexpr int K = RD * RD;                      // outputs per query and level
-  static constexpr int NT = 512;
+  static constexpr int NT = NT_;
   static constexpr int QB = R <= 4 ? 32 : 16;            // queries per workgroup
   static constexpr int LG = RD <= 2 ? 1 : RD <= 4 ? 2 : RD <= 8 ? 3 : RD <= 16 ? 4 : 5;
   static constexpr int G = 1 << LG;                      // lanes per query in phase 0
   static constexpr int VSLOTS = QB * WD * NQ;            // 4-cell vectors per workgroup
   static constexpr int VIT = (VSLOTS + NT - 1) / NT;
   static constexpr int NCLS = NT / QB;                   // output classes
-  static_assert(QB * G <= NT, "one phase-0 slot per thread");
+  static constexpr int SIT = (QB * G + NT - 1) / NT;     // phase-0 slots per thread
+  static_assert((QB * G) % NT == 0 || QB * G < NT, "whole waves per phase-0 pass");
   static_assert(G <= 64, "a query's lane group must sit in one wave");
   static_assert(QB <= dxr::PAGE_Q && dxr::PAGE_Q % QB == 0, "a workgroup stays in one page");
 };
@@ -293,11 +294,11 @@ __device__ __forceinline__ void load_vec(const PT* p, float* v) {
 }
 
 // Phase 1 for one level type: V-cell vectors, 4 per LDS vector slot.
-template <int R, int V, typename PT>
+template <int R, int NT_, int V, typename PT>
 __device__ __forceinline__ void gather_windows(const PT* __restrict__ base, int qb0, const LevelAddr& A,
                                                const int2* org, float* cells, int q0, int N,
                                                int tid) {
-  using C = WideCfg<R>;
+  using C = WideCfg<R, NT_>;
   float4 v[C::VIT];
 #pragma unroll
   for (int i = 0; i < C::VIT; ++i) {
@@ -338,11 +339,11 @@ __device__ __forceinline__ void gather_windows(const PT* __restrict__ base, int 
 
 // ABL (timing-only ablations, outputs invalid): 4 returns at once, 5 after phase 0,
 // 6 after phase 1, 7 skips the gathers.
-template <int R, typename PT, int ABL = 0>
-__global__ __launch_bounds__(WideCfg<R>::NT) void corr_lookup_wide_kernel(
+template <int R, typename PT, int ABL = 0, int NT_ = 512>
+__global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
     const PT* __restrict__ pyr, const float* __restrict__ coords, float* __restrict__ out,
     LookupGeom g) {
-  using C = WideCfg<R>;
+  using C = WideCfg<R, NT_>;
   constexpr int RD = C::RD, WD = C::WD, RS = C::RS, K = C::K, QB = C::QB, G = C::G;
   __shared__ __attribute__((aligned(16))) float cells[QB * C::QS];
   __shared__ float4 xs[RD * QB];   // {column in the LDS row (int bits), fx, 1-fx, -}
@@ -357,8 +358,11 @@ __global__ __launch_bounds__(WideCfg<R>::NT) void corr_lookup_wide_kernel(
   if constexpr (ABL == 4) return;
 
   // ---- phase 0
-  if (tid < QB * G) {
-    const int j = tid & (G - 1), qq = tid >> C::LG;
+#pragma unroll
+  for (int it = 0; it < C::SIT; ++it) {
+    const int slot = tid + it * C::NT;
+    if (slot >= QB * G) break;   // whole waves
+    const int j = slot & (G - 1), qq = slot >> C::LG;
     const int q = q0 + qq;
     float cx = 0.f, cy = 0.f;
     if (q < g.N) {
@@ -405,13 +409,13 @@ __global__ __launch_bounds__(WideCfg<R>::NT) void corr_lookup_wide_kernel(
     const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
     const int qb0 = q0 & ((1 << A.lqb) - 1);
     if (A.lth == 30)
-      gather_windows<R, 1>(base, qb0, A, org, cells, q0, g.N, tid);
+      gather_windows<R, NT_, 1>(base, qb0, A, org, cells, q0, g.N, tid);
     else if (A.tw >= 4)
-      gather_windows<R, 4>(base, qb0, A, org, cells, q0, g.N, tid);
+      gather_windows<R, NT_, 4>(base, qb0, A, org, cells, q0, g.N, tid);
     else if (A.tw == 2)
-      gather_windows<R, 2>(base, qb0, A, org, cells, q0, g.N, tid);
+      gather_windows<R, NT_, 2>(base, qb0, A, org, cells, q0, g.N, tid);
     else
-      gather_windows<R, 1>(base, qb0, A, org, cells, q0, g.N, tid);
+      gather_windows<R, NT_, 1>(base, qb0, A, org, cells, q0, g.N, tid);
   }
   __syncthreads();
   if constexpr (ABL == 6) {
@@ -466,6 +470,20 @@ int launch_lookup_r(const PT* pyr, const float* coords, float* out, const Lookup
       hipLaunchKernelGGL((corr_lookup_kernel<R, PT>), grid, dim3(C::NTHR), 0, stream, pyr, coords,
                          out, g);
       break;
+    case 2: {  // wide form at 256 threads
+      using W = WideCfg<R, 256>;
+      const dim3 gw((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
+      hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT, 0, 256>), gw, dim3(256), 0, stream, pyr,
+                         coords, out, g);
+      break;
+    }
+    case 3: {  // wide form at 1024 threads
+      using W = WideCfg<R, 1024>;
+      const dim3 gw((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
+      hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT, 0, 1024>), gw, dim3(1024), 0, stream,
+                         pyr, coords, out, g);
+      break;
+    }
     case 94: case 95: case 96: case 97: {
       using W = WideCfg<R>;
       const dim3 gw((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
