@@ -188,12 +188,16 @@ __device__ __forceinline__ void gst(float4* p, float4 v, bool nt) {
   }
 }
 
+// `region`: this wave's LDS staging region; `qslot`: which 32 queries of the
+// page the wave holds; `active` = false keeps the barriers but stores nothing
+// (a wave whose page lies past the pyramid's last query page).
 template <typename OT, bool NTS = false>
 __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT* __restrict__ pyr,
-                                               const BuildGeom& g, long long page, int wave,
-                                               int lane) {
+                                               const BuildGeom& g, long long page, int region,
+                                               int qslot, bool active, int lane) {
   const int j = lane & 31, h = lane >> 5;
-  float* wl = lds + wave * 16 * P0;     // this wave's private LDS region
+  const int wave = qslot;
+  float* wl = lds + region * 16 * P0;   // this wave's private LDS region
 
   // Level 0: 16 queries per round staged as [q][8][16] f32 rows, then streamed
   // as 1 KiB wave stores.
@@ -215,14 +219,16 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
       for (int k = 0; k < 8; ++k) {
         const int qq = 2 * k + (lane >> 5);
         const int off = (lane & 31) * 4;
-        gst(reinterpret_cast<float4*>(pg0 + (r * 16 + qq) * NTGT + off), f4(wl + qq * P0 + off), NTS);
+        if (active)
+          gst(reinterpret_cast<float4*>(pg0 + (r * 16 + qq) * NTGT + off), f4(wl + qq * P0 + off),
+              NTS);
       }
     } else {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int qq = 4 * k + (lane >> 4);
         const int off = (lane & 15) * 8;
-        store8<OT>(pg0 + (r * 16 + qq) * NTGT + off, wl + qq * P0 + off);
+        if (active) store8<OT>(pg0 + (r * 16 + qq) * NTGT + off, wl + qq * P0 + off);
       }
     }
     __syncthreads();
@@ -258,7 +264,8 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
   __syncthreads();
   {
     OT* pg1 = pyr + g.loff[1] + page * (BM * NTGT / 4) + (long long)wave * 32 * (NTGT / 4);
-    if constexpr (sizeof(OT) == 4) {
+    if (!active) {
+    } else if constexpr (sizeof(OT) == 4) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int qq = 8 * k + (lane >> 3);
@@ -274,7 +281,7 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
       }
     }
   }
-  if (g.levels < 3) return;
+  if (g.levels < 3 || !active) return;   // no barriers below this point
 
   // Level 2: [q][2][4] per page; lane (j, h) writes row h (a 1 KiB wave run).
   {
@@ -450,7 +457,7 @@ __device__ __forceinline__ void build_page_f32(const float* __restrict__ f1,
     }
     return;
   } else {
-    paged_epilogue<OT, NTS>(acc, lds, pyr, g, page, wave, lane);
+    paged_epilogue<OT, NTS>(acc, lds, pyr, g, page, wave, wave, true, lane);
   }
 }
 
@@ -636,7 +643,7 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_
   scale_acc<DIV>(acc, g);
   const long long page = ((long long)b * gridDim.y + blockIdx.y) * ((long long)g.tiles_h *
                          g.tiles_w) + (long long)tyi * g.tiles_w + txi;
-  paged_epilogue<OT, false>(acc, reinterpret_cast<float*>(smem), pyr, g, page, wave, lane);
+  paged_epilogue<OT, false>(acc, reinterpret_cast<float*>(smem), pyr, g, page, wave, wave, true, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -820,7 +827,7 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
   }
 
   scale_acc<DIV>(acc, g);
-  if constexpr (ABL == 1 || ABL == 4) {
+  if constexpr (ABL == 1 || ABL == 4 || ABL == 5) {
     float sum = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -831,11 +838,11 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
   }
   const long long page = ((long long)b * gridDim.y + blockIdx.y) * ((long long)g.tiles_h *
                          g.tiles_w) + (long long)tyi * g.tiles_w + txi;
-  paged_epilogue<OT, false>(acc, reinterpret_cast<float*>(smem), pyr, g, page, wave, lane);
+  paged_epilogue<OT, false>(acc, reinterpret_cast<float*>(smem), pyr, g, page, wave, wave, true, lane);
 }
 
 // ---------------------------------------------------------------------------
-// Pre-split f32 build ("presplit", the default for f32 fmaps with D % 16 == 0).
+// Pre-split f32 build ("presplit", DXR_BUILD_VARIANT 11-14; not the default).
 // The same exact hi+mid+lo operand split and the same six bf16 MFMA products as
 // the split build above, but the split is done ONCE per fmap element by
 // split_planes_kernel into a workspace, instead of once per workgroup that reads
@@ -896,7 +903,8 @@ __device__ __forceinline__ void glds_chunk(const uint4* g, unsigned char* l) {
 // s_waitcnt vmcnt and a raw s_barrier per k step (__syncthreads() would drain
 // the in-flight DMA: cdna_hip_programming.md §5 "Pipelining across barriers").
 // ABL (timing-only ablations, never the default): 1 skips the epilogue stores,
-// 2 skips the MFMAs, 3 skips the K loop, 4 = 1 + 2.
+// 2 skips the MFMAs, 3 skips the K loop, 4 = 1 + 2, 5 skips the DMA and the
+// epilogue stores (LDS reads + MFMAs + barriers only).
 template <typename OT, bool DIV, int MINW, int NS, int ABL = 0>
 __global__ __launch_bounds__(NT, MINW) void corr_build_presplit_kernel(const uint4* __restrict__ ws,
                                                                        OT* __restrict__ pyr,
@@ -941,6 +949,7 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_presplit_kernel(const uin
 
   const int nk = g.D / 16;
   auto issue = [&](int ks) {
+    if constexpr (ABL == 5) return;
     unsigned char* st = smem + (ks % NS) * PS_STAGE;
     const long long ko = (long long)ks * 2 * g.N;
 #pragma unroll
@@ -995,7 +1004,7 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_presplit_kernel(const uin
   __builtin_amdgcn_s_barrier();   // the epilogue reuses the ring's LDS
 
   scale_acc<DIV>(acc, g);
-  if constexpr (ABL == 1 || ABL == 4) {
+  if constexpr (ABL == 1 || ABL == 4 || ABL == 5) {
     float sum = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -1006,7 +1015,7 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_presplit_kernel(const uin
   }
   const long long page = ((long long)b * gridDim.y + blockIdx.y) * ((long long)g.tiles_h *
                          g.tiles_w) + (long long)tyi * g.tiles_w + txi;
-  paged_epilogue<OT, false>(acc, reinterpret_cast<float*>(smem), pyr, g, page, wave, lane);
+  paged_epilogue<OT, false>(acc, reinterpret_cast<float*>(smem), pyr, g, page, wave, wave, true, lane);
 }
 
 // Floor-mode 2x2 average pool of one pyramid level into the next, for levels
@@ -1226,6 +1235,8 @@ int launch_build_f32(bool vec, const float* f1, const float* f2, OT* pyr, const 
       if (v == 112) return launch_presplit<2, 3, OT, 2>(f1, f2, ws, pyr, g, B, stream);  // timing
       if (v == 113) return launch_presplit<2, 3, OT, 3>(f1, f2, ws, pyr, g, B, stream);  // timing
       if (v == 114) return launch_presplit<2, 3, OT, 4>(f1, f2, ws, pyr, g, B, stream);  // timing
+      if (v == 115) return launch_presplit<2, 3, OT, 5>(f1, f2, ws, pyr, g, B, stream);  // timing
+      if (v == 125) return launch_presplit<3, 2, OT, 5>(f1, f2, ws, pyr, g, B, stream);  // timing
     }
   }
   if (!vec) return launch_f32<false, 16, PAGED, OT, false, 0, false, false>(f1, f2, pyr, g, B, stream);
@@ -1321,7 +1332,8 @@ extern "C" int64_t dxr_build_workspace_bytes(int64_t B, int64_t D, int64_t H, in
   if (B < 1 || D < 1 || H < 1 || W < 1 || H * W > (1LL << 30)) return 0;
   if (in_dtype != DXR_F32 || D % 16 != 0) return 0;
   const int v = build_variant();   // only the presplit variants use a workspace
-  if (!((v >= 11 && v <= 14) || (v >= 111 && v <= 114))) return 0;
+  if (!((v >= 11 && v <= 14) || (v >= 111 && v <= 115) || v == 125))
+    return 0;
   return presplit_ws_bytes(B, D, H * W);
 }
 

@@ -328,14 +328,23 @@ def test_bf16_kitti_shape(dx):
 
 # f32-MFMA build variants are checked against variant 2, split-build variants
 # against the default (the split build at 4 waves/SIMD).
+SPLIT_FAMILY = ["7", "8", "9", "11", "12", "13"]
+
+
 @pytest.mark.parametrize("variant,base", [("1", "2"), ("3", "2"), ("4", "2"), ("5", "2"),
-                                          ("6", "2"), ("10", "2"), ("7", "0"), ("9", "0")])
-def test_build_variants_bit_identical(dx, variant, base, monkeypatch):
-    """Tuning variants (occupancy, glds staging, persistent, nontemporal) produce
-    the same bits in every valid pyramid cell (page padding is never read and
-    its content is variant-specific), and the same lookups."""
-    f1, f2 = _pair(B=2, H=47, W=156, seed=111, dist="fnet")
-    c = _t(dg.coords(112, 2, 47, 156, "uniform", 12.0))
+                                          ("6", "2"), ("10", "2")] +
+                         [(v, "0") for v in SPLIT_FAMILY])
+@pytest.mark.parametrize("shape", [(2, 47, 156), (1, 55, 100)])
+def test_build_variants_bit_identical(dx, variant, base, shape, monkeypatch):
+    """Tuning variants (occupancy, glds staging, persistent, nontemporal, wide
+    workgroups, pre-split planes) produce the same bits in every valid pyramid
+    cell (page padding is never read and its content is variant-specific), and
+    the same lookups.  55 x 100 has an odd number of query pages (43) and of
+    target tiles per row (7): the wide builds' edge workgroups hold pages past
+    the pyramid, which they must not write."""
+    B, H, W = shape
+    f1, f2 = _pair(B=B, H=H, W=W, seed=111, dist="fnet")
+    c = _t(dg.coords(112, B, H, W, "uniform", 12.0))
     monkeypatch.setenv("DXR_BUILD_VARIANT", base)
     ref_cb = dx.CorrBlock(f1, f2)
     ref, ref_out = ref_cb.corr_pyramid, ref_cb(c)
@@ -346,7 +355,7 @@ def test_build_variants_bit_identical(dx, variant, base, monkeypatch):
     assert torch.equal(cb(c), ref_out)
 
 
-@pytest.mark.parametrize("variant", ["0", "7"])
+@pytest.mark.parametrize("variant", ["0", "7", "11"])
 def test_split_build_f32_accuracy(dx, variant, monkeypatch):
     """The split build (f32 operands as exact hi+mid+lo bf16 triples, six bf16
     MFMA products, f32 accumulation) has f32-class error: within RTOL of the
