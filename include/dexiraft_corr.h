@@ -18,6 +18,10 @@
  *   dxr_corr_lookup          core/corr.py:29-50  CorrBlock.__call__ together with
  *                            core/utils/utils.py:57-71 bilinear_sampler
  *                            (F.grid_sample, align_corners=True, zero padding)
+ *   dxr_corr_lookup_backward core/utils/utils.py:65 grid_sample backward
+ *                            (autograd of CorrBlock.__call__, train.py:175-178)
+ *   dxr_pyramid_backward     core/corr.py:25-27,58-60 avg_pool2d + division
+ *                            backward (autograd of CorrBlock.__init__)
  *   dxr_avg_pool2x2          core/corr.py:69-71  F.avg_pool2d(fmap, 2, stride=2)
  *                            in AlternateCorrBlock.__init__
  *   dxr_alt_corr_forward     alt_cuda_corr/correlation.cpp:23-33 `forward`
@@ -149,6 +153,30 @@ int dxr_pyramid_pack(const float* level_data, int64_t B, int64_t H, int64_t W,
 int dxr_corr_lookup(const void* pyramid, int pyr_dtype,
                     int64_t B, int64_t H, int64_t W, int num_levels, int radius,
                     const float* coords, float* out, hipStream_t stream);
+
+/*
+ * Backward of stage (c) (training: core/utils/utils.py:65 grid_sample under
+ * autograd, train.py:175-178): ADDS d loss / d pyramid of one lookup to
+ * grad_pyramid, a float32 buffer with the pyramid's paged layout and size
+ * (dxr_pyramid_numel; the caller zero-fills it once and may accumulate several
+ * lookups into it).  grad_out: [B, num_levels*(2r+1)^2, H, W] float32.  No
+ * coordinate gradient (the reference detaches coords, core/raft.py:170).
+ */
+int dxr_corr_lookup_backward(const float* coords, const float* grad_out,
+                             int64_t B, int64_t H, int64_t W, int num_levels,
+                             int radius, void* grad_pyramid, int grad_dtype,
+                             hipStream_t stream);
+
+/*
+ * Backward of stages (a)+(b) down to the volume: folds the gradient of every
+ * level down the avg-pool chain (core/corr.py:25-27) and divides by `divisor`
+ * (core/corr.py:60), writing d loss / d (fmap1^T fmap2) as row-major
+ * [B*H*W, H, W] float32.  The fmap gradients are then two plain GEMMs:
+ * dfmap1 = fmap2 . dV^T, dfmap2 = fmap1 . dV (per pair, [D, H*W]).
+ */
+int dxr_pyramid_backward(const void* grad_pyramid, int grad_dtype,
+                         int64_t B, int64_t H, int64_t W, int num_levels,
+                         float divisor, float* grad_volume, hipStream_t stream);
 
 /*
  * 2x2 / stride-2 average pool, floor mode, of [planes, H, W] float32 into

@@ -7,11 +7,20 @@ HIP kernels of ``libdexiraft_corr.so``; the Python side only validates,
 allocates (from torch's caching allocator) and launches on torch's current
 stream.  There is no CPU path: host tensors raise.
 
+Training: with float32 fmaps that require grad (under grad mode), the block is
+differentiable with respect to the fmaps, as the reference is through matmul /
+avg_pool2d / grid_sample (train.py:175-178).  Each lookup's backward adds its
+bilinear transpose into one gradient pyramid owned by the block
+(``dxr_corr_lookup_backward``); the build's backward runs once after all of
+them, folds that pyramid down the pooling chain (``dxr_pyramid_backward``) and
+takes the fmap gradients as two plain GEMMs (torch.bmm: rocBLAS).
+
 Differences from the reference, all loud:
   * host (CPU) tensors raise ``RuntimeError`` instead of running on the CPU;
-  * inputs that would need autograd (``requires_grad`` under grad mode) raise
-    ``NotImplementedError`` — the reference trains through matmul / avg_pool /
-    grid_sample (train.py:175-178); the native backward is a listed next item.
+  * coords that require grad raise ``NotImplementedError`` (the reference
+    detaches them, core/raft.py:170; no grid gradient is implemented), as do
+    bfloat16 fmaps that require grad and AlternateCorrBlock inputs that require
+    grad (the reference's alt_cuda_corr output carries no autograd graph).
 """
 from __future__ import annotations
 
@@ -40,11 +49,102 @@ def _require_device(t: torch.Tensor, name: str) -> None:
             f"{name} is on {t.device}; dexiraft_amd runs only on HIP devices (no CPU path)")
 
 
-def _require_no_grad(*ts: torch.Tensor) -> None:
+def _require_no_grad(*ts: torch.Tensor, what: str = "these inputs") -> None:
     if torch.is_grad_enabled() and any(t.requires_grad for t in ts):
         raise NotImplementedError(
-            "dexiraft_amd correlation is inference-only in this build: inputs require grad "
-            "(wrap the call in torch.no_grad() or detach the inputs)")
+            f"dexiraft_amd: no gradient is implemented for {what} (wrap the call in "
+            "torch.no_grad() or detach the inputs)")
+
+
+def _wants_grad(*ts: torch.Tensor) -> bool:
+    return torch.is_grad_enabled() and any(t.requires_grad for t in ts)
+
+
+def _volume_grads(ctx_needs, f1: torch.Tensor, f2: torch.Tensor, dv: torch.Tensor):
+    """d/d fmap of corr = f1^T f2 given dV = d loss / d corr ([B, N, N], already
+    divided by sqrt(D)): dF1 = F2 dV^T, dF2 = F1 dV (plain GEMMs, rocBLAS)."""
+    B, D, H, W = f1.shape
+    N = H * W
+    df1 = df2 = None
+    if ctx_needs[0]:
+        df1 = torch.bmm(f2.reshape(B, D, N), dv.transpose(1, 2)).reshape(B, D, H, W)
+    if ctx_needs[1]:
+        df2 = torch.bmm(f1.reshape(B, D, N), dv).reshape(B, D, H, W)
+    return df1, df2
+
+
+class _BuildGrad(torch.autograd.Function):
+    """Graph node of CorrBlock.__init__: returns a scalar token every lookup
+    consumes, so autograd runs this backward once, after every lookup's
+    backward has added into ``block._grad_pyr``."""
+
+    @staticmethod
+    def forward(ctx, fmap1, fmap2, block):
+        ctx.block = block
+        ctx.save_for_backward(fmap1, fmap2)
+        return fmap1.new_zeros(())
+
+    @staticmethod
+    def backward(ctx, _gtoken):
+        block = ctx.block
+        gp, block._grad_pyr = block._grad_pyr, None
+        if gp is None:
+            return None, None, None
+        f1, f2 = ctx.saved_tensors
+        B, D, H, W = block._geom
+        dv = torch.empty((B, H * W, H * W), dtype=torch.float32, device=f1.device)
+        lib = nat.load()
+        with _Launch(block._device):
+            st = lib.dxr_pyramid_backward(gp.data_ptr(), nat.DXR_F32, B, H, W, block.num_levels,
+                                          _sqrt_dim(D), dv.data_ptr(), nat.stream_of(dv))
+        nat.check(st, "CorrBlock backward (dxr_pyramid_backward)")
+        df1, df2 = _volume_grads(ctx.needs_input_grad, f1, f2, dv)
+        return df1, df2, None
+
+
+class _LookupGrad(torch.autograd.Function):
+    """Graph node of CorrBlock.__call__ (differentiable in the pyramid only)."""
+
+    @staticmethod
+    def forward(ctx, token, coords, block):
+        ctx.block = block
+        ctx.save_for_backward(coords)
+        return block._lookup(coords)
+
+    @staticmethod
+    def backward(ctx, gout):
+        block = ctx.block
+        (coords,) = ctx.saved_tensors
+        B, D, H, W = block._geom
+        if block._grad_pyr is None:
+            block._grad_pyr = torch.zeros(block._buf.numel(), dtype=torch.float32,
+                                          device=block._device)
+        g = gout.contiguous().float()
+        lib = nat.load()
+        with _Launch(block._device):
+            st = lib.dxr_corr_lookup_backward(coords.data_ptr(), g.data_ptr(), B, H, W,
+                                              block.num_levels, block.radius,
+                                              block._grad_pyr.data_ptr(), nat.DXR_F32,
+                                              nat.stream_of(g))
+        nat.check(st, "CorrBlock lookup backward (dxr_corr_lookup_backward)")
+        return gout.new_zeros(()), None, None
+
+
+class _VolumeGrad(torch.autograd.Function):
+    """CorrBlock.corr with autograd: backward = dV / sqrt(D), two GEMMs."""
+
+    @staticmethod
+    def forward(ctx, fmap1, fmap2):
+        ctx.save_for_backward(fmap1, fmap2)
+        return CorrBlock._volume(fmap1, fmap2)
+
+    @staticmethod
+    def backward(ctx, gout):
+        f1, f2 = ctx.saved_tensors
+        B, D, H, W = f1.shape
+        dv = gout.reshape(B, H * W, H * W).float() / _sqrt_dim(D)
+        df1, df2 = _volume_grads(ctx.needs_input_grad, f1, f2, dv)
+        return df1, df2
 
 
 def _fmap_geometry(fmap1: torch.Tensor, fmap2: torch.Tensor) -> tuple[int, int, int, int]:
@@ -97,7 +197,6 @@ class _Launch:
 
 def _check_coords(coords: torch.Tensor, B: int, H: int, W: int, device: torch.device) -> torch.Tensor:
     _require_device(coords, "coords")
-    _require_no_grad(coords)
     if coords.dim() != 4 or tuple(coords.shape) != (B, 2, H, W):
         raise RuntimeError(f"coords must be [B, 2, H, W] = {(B, 2, H, W)}, got {tuple(coords.shape)}")
     if coords.device != device:
@@ -126,7 +225,8 @@ class CorrBlock:
         self.num_levels = num_levels
         self.radius = radius
         B, D, H, W = _fmap_geometry(fmap1, fmap2)
-        _require_no_grad(fmap1, fmap2)
+        self._token = None
+        self._grad_pyr = None
         if not isinstance(num_levels, int) or num_levels < 1:
             raise ValueError(f"num_levels must be a positive int, got {num_levels!r}")
         if not isinstance(radius, int) or radius < 0:
@@ -138,6 +238,8 @@ class CorrBlock:
             in_dt, pyr_dt, pyr_torch = nat.DXR_BF16, nat.DXR_BF16, torch.bfloat16
         else:
             raise RuntimeError(f"fmaps must be float32 or bfloat16, got {fmap1.dtype}")
+        if pyr_dt != nat.DXR_F32:
+            _require_no_grad(fmap1, fmap2, what="bfloat16 fmaps")
         self._geom = (B, D, H, W)
         self._pyr_dt = pyr_dt
         self._device = fmap1.device
@@ -157,6 +259,8 @@ class CorrBlock:
         nat.check(st, "CorrBlock build (dxr_corr_pyramid_build)")
         self._level_sizes = sizes
         self._ref_pyramid = None
+        if _wants_grad(fmap1, fmap2):
+            self._token = _BuildGrad.apply(f1, f2, self)
 
     @property
     def corr_pyramid(self):
@@ -184,7 +288,14 @@ class CorrBlock:
 
     def __call__(self, coords):
         B, D, H, W = self._geom
+        _require_no_grad(coords, what="coords (the reference detaches them, core/raft.py:170)")
         c = _check_coords(coords, B, H, W, self._device)
+        if self._token is not None and torch.is_grad_enabled():
+            return _LookupGrad.apply(self._token, c, self)
+        return self._lookup(c)
+
+    def _lookup(self, c):
+        B, D, H, W = self._geom
         rd = 2 * self.radius + 1
         out = torch.empty((B, self.num_levels * rd * rd, H, W), dtype=torch.float32,
                           device=self._device)
@@ -198,9 +309,16 @@ class CorrBlock:
 
     @staticmethod
     def corr(fmap1, fmap2):
-        """``[B, H, W, 1, H, W]`` volume ``fmap1^T fmap2 / sqrt(D)`` (core/corr.py:52-60)."""
+        """``[B, H, W, 1, H, W]`` volume ``fmap1^T fmap2 / sqrt(D)`` (core/corr.py:52-60);
+        differentiable in the fmaps under grad mode."""
+        _fmap_geometry(fmap1, fmap2)
+        if _wants_grad(fmap1, fmap2) and fmap1.dtype == torch.float32:
+            return _VolumeGrad.apply(fmap1.contiguous(), fmap2.contiguous())
+        return CorrBlock._volume(fmap1, fmap2)
+
+    @staticmethod
+    def _volume(fmap1, fmap2):
         B, D, H, W = _fmap_geometry(fmap1, fmap2)
-        _require_no_grad(fmap1, fmap2)
         if fmap1.dtype != torch.float32:
             raise RuntimeError(f"CorrBlock.corr expects float32 fmaps, got {fmap1.dtype}")
         out = torch.empty((B, H, W, 1, H, W), dtype=torch.float32, device=fmap1.device)
@@ -227,7 +345,8 @@ class AlternateCorrBlock:
         self.num_levels = num_levels
         self.radius = radius
         B, D, H, W = _fmap_geometry(fmap1, fmap2)
-        _require_no_grad(fmap1, fmap2)
+        _require_no_grad(fmap1, fmap2, what="AlternateCorrBlock (the reference's alt_cuda_corr "
+                                            "output carries no autograd graph, core/corr.py:85-88)")
         if fmap1.dtype != torch.float32:
             raise RuntimeError(f"AlternateCorrBlock expects float32 fmaps, got {fmap1.dtype}")
         if not isinstance(num_levels, int) or num_levels < 1:
@@ -236,6 +355,7 @@ class AlternateCorrBlock:
             raise ValueError(f"radius must be a non-negative int, got {radius!r}")
         _level_sizes(H, W, num_levels + 1)  # the reference pools num_levels times
         self._geom = (B, D, H, W)
+        self._token = None   # never differentiable (see the check above)
         self._device = fmap1.device
         lib = nat.load()
         f1, f2 = fmap1.contiguous(), fmap2.contiguous()
@@ -260,7 +380,14 @@ class AlternateCorrBlock:
 
     def __call__(self, coords):
         B, D, H, W = self._geom
+        _require_no_grad(coords, what="coords (the reference detaches them, core/raft.py:170)")
         c = _check_coords(coords, B, H, W, self._device)
+        if self._token is not None and torch.is_grad_enabled():
+            return _LookupGrad.apply(self._token, c, self)
+        return self._lookup(c)
+
+    def _lookup(self, c):
+        B, D, H, W = self._geom
         rd = 2 * self.radius + 1
         out = torch.empty((B, self.num_levels * rd * rd, H, W), dtype=torch.float32,
                           device=self._device)

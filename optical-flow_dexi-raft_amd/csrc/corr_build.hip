@@ -1079,6 +1079,42 @@ __global__ __launch_bounds__(256) void repack_kernel(PT* __restrict__ pyr, float
   }
 }
 
+// Pyramid backward: the gradient of every level (paged, as the pyramid) folded
+// down the avg-pool chain (F.avg_pool2d backward: each covered cell of level l
+// receives 1/4 of its level-(l+1) cell's total gradient; the floor-mode
+// remainder row / column receives none), then divided by the divisor:
+// dV[b*N + q][y][x] = (d0 + (d1 + (d2 + ...) / 4) / 4) / divisor, row-major.
+struct LevelsArg {
+  int n;
+  dxr::LevelLayout lay[8];
+};
+
+template <bool DIV>
+__global__ __launch_bounds__(256) void pyramid_backward_kernel(const float* __restrict__ gp,
+                                                               float* __restrict__ dv, LevelsArg L,
+                                                               int B, int N, int H, int W,
+                                                               float divisor, float recip) {
+  const long long total = (long long)B * N * H * W;
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const int x = (int)(idx % W);
+    const long long r = idx / W;
+    const int y = (int)(r % H);
+    const long long bq = r / H;
+    const int b = (int)(bq / N), q = (int)(bq % N);
+    float t = 0.f;
+    for (int k = L.n - 1; k >= 0; --k) {
+      const int yk = y >> k, xk = x >> k;
+      if (yk >= L.lay[k].h || xk >= L.lay[k].w) continue;
+      const bool parent = k + 1 < L.n && (y >> (k + 1)) < L.lay[k + 1].h &&
+                          (x >> (k + 1)) < L.lay[k + 1].w;
+      const float d = gp[dxr::cell_index(L.lay[k], b, q, yk, xk)];
+      t = parent ? d + 0.25f * t : d;
+    }
+    dv[idx] = DIV ? t / divisor : t * recip;
+  }
+}
+
 unsigned grid_for(long long total) {
   long long blocks = (total + 255) / 256;
   if (blocks > 2048 * 8) blocks = 2048 * 8;
@@ -1212,7 +1248,7 @@ int build_variant() {
 // Variants: 0 default (= 8, the split build, when D % 16 == 0 and W % 4 == 0;
 // else 2); presplit builds (need the workspace; r01 sintel: 181-190 us vs 178
 // for 8, operand staging L2 -> LDS bound, §DESIGN): 11 = 3-stage ring (72 KiB, 2 WG/CU),
-// 12 = 2 stages at 3 WG/CU, 13 = 2 stages at 2 WG/CU, 14 = 2 stages at 4 waves/SIMD;
+// 12 = 2 stages at 3 WG/CU, 13 = 2 stages at 2 WG/CU;
 // f32-MFMA builds: 1 register staging,
 // 2 waves/SIMD; 2 register staging, 3 waves/SIMD; 3 glds staging, 3 waves/SIMD;
 // 4 glds staging, 4 waves/SIMD; 5 = 3 persistent; 6 = 2 with nontemporal
@@ -1230,7 +1266,6 @@ int launch_build_f32(bool vec, const float* f1, const float* f2, OT* pyr, const 
       if (v == 11) return launch_presplit<2, 3, OT>(f1, f2, ws, pyr, g, B, stream);
       if (v == 12) return launch_presplit<3, 2, OT>(f1, f2, ws, pyr, g, B, stream);
       if (v == 13) return launch_presplit<2, 2, OT>(f1, f2, ws, pyr, g, B, stream);
-      if (v == 14) return launch_presplit<4, 2, OT>(f1, f2, ws, pyr, g, B, stream);
       if (v == 111) return launch_presplit<2, 3, OT, 1>(f1, f2, ws, pyr, g, B, stream);  // timing
       if (v == 112) return launch_presplit<2, 3, OT, 2>(f1, f2, ws, pyr, g, B, stream);  // timing
       if (v == 113) return launch_presplit<2, 3, OT, 3>(f1, f2, ws, pyr, g, B, stream);  // timing
@@ -1332,7 +1367,7 @@ extern "C" int64_t dxr_build_workspace_bytes(int64_t B, int64_t D, int64_t H, in
   if (B < 1 || D < 1 || H < 1 || W < 1 || H * W > (1LL << 30)) return 0;
   if (in_dtype != DXR_F32 || D % 16 != 0) return 0;
   const int v = build_variant();   // only the presplit variants use a workspace
-  if (!((v >= 11 && v <= 14) || (v >= 111 && v <= 115) || v == 125))
+  if (!((v >= 11 && v <= 13) || (v >= 111 && v <= 115) || v == 125))
     return 0;
   return presplit_ws_bytes(B, D, H * W);
 }
@@ -1437,5 +1472,30 @@ extern "C" int dxr_pyramid_pack(const float* level_data, int64_t B, int64_t H, i
     hipLaunchKernelGGL((repack_kernel<false, uint16_t>), dim3(grid_for(total)), dim3(256), 0,
                        stream, static_cast<uint16_t*>(pyramid), src, L.lay[level], (int)B,
                        (int)(H * W));
+  return dxr::launch_status();
+}
+
+extern "C" int dxr_pyramid_backward(const void* grad_pyramid, int grad_dtype, int64_t B,
+                                    int64_t H, int64_t W, int num_levels, float divisor,
+                                    float* grad_volume, hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, num_levels, &L)) return DXR_EINVAL;
+  if (grad_dtype != DXR_F32) return grad_dtype == DXR_BF16 ? DXR_EUNSUPPORTED : DXR_EINVAL;
+  if (!(divisor == divisor) || divisor == 0.f) return DXR_EINVAL;
+  if (B == 0) return DXR_OK;
+  if (!grad_pyramid || !grad_volume) return DXR_EINVAL;
+  LevelsArg la;
+  la.n = L.n;
+  for (int l = 0; l < L.n; ++l) la.lay[l] = L.lay[l];
+  int e2 = 0;
+  const float recip = (std::frexp(divisor, &e2) == 0.5f) ? 1.f / divisor : 0.f;
+  const long long total = B * H * W * H * W;
+  const float* gp = static_cast<const float*>(grad_pyramid);
+  if (recip != 0.f)
+    hipLaunchKernelGGL(pyramid_backward_kernel<false>, dim3(grid_for(total)), dim3(256), 0, stream,
+                       gp, grad_volume, la, (int)B, (int)(H * W), (int)H, (int)W, divisor, recip);
+  else
+    hipLaunchKernelGGL(pyramid_backward_kernel<true>, dim3(grid_for(total)), dim3(256), 0, stream,
+                       gp, grad_volume, la, (int)B, (int)(H * W), (int)H, (int)W, divisor, recip);
   return dxr::launch_status();
 }

@@ -337,27 +337,16 @@ __device__ __forceinline__ void gather_windows(const PT* __restrict__ base, int 
   }
 }
 
-// ABL (timing-only ablations, outputs invalid): 4 returns at once, 5 after phase 0,
-// 6 after phase 1, 7 skips the gathers.
-template <int R, typename PT, int ABL = 0, int NT_ = 512>
-__global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
-    const PT* __restrict__ pyr, const float* __restrict__ coords, float* __restrict__ out,
-    LookupGeom g) {
+// Phase 0 of the wide lookup (forward and backward): per (query, sample) the
+// coordinate round trip, floor and fractions; per query the window origin and
+// the far flag.  Tap data goes to xs / ys, origins to org.
+template <int R, int NT_>
+__device__ __forceinline__ void wide_phase0(const float* __restrict__ coords, const LookupGeom& g,
+                                            const LevelAddr& A, int b, int l, int q0, int tid,
+                                            float4* xs, float4* ys, int2* org) {
   using C = WideCfg<R, NT_>;
-  constexpr int RD = C::RD, WD = C::WD, RS = C::RS, K = C::K, QB = C::QB, G = C::G;
-  __shared__ __attribute__((aligned(16))) float cells[QB * C::QS];
-  __shared__ float4 xs[RD * QB];   // {column in the LDS row (int bits), fx, 1-fx, -}
-  __shared__ float4 ys[RD * QB];   // {row offset in LDS (int bits), fy, 1-fy, -}
-  __shared__ int2 org[QB];         // window origin (x, y) or FAR_ORIGIN
-
-  const int tid = threadIdx.x;
-  const int l = blockIdx.y, b = blockIdx.z;
-  const int q0 = blockIdx.x * QB;
-  const LevelAddr A = g.lv[l];
+  constexpr int RD = C::RD, WD = C::WD, RS = C::RS, QB = C::QB, G = C::G;
   const int Hl = A.h, Wl = A.w;
-  if constexpr (ABL == 4) return;
-
-  // ---- phase 0
 #pragma unroll
   for (int it = 0; it < C::SIT; ++it) {
     const int slot = tid + it * C::NT;
@@ -398,6 +387,29 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
       ys[j * QB + qq] = make_float4(__int_as_float(row), fy, __fsub_rn(1.f, fy), 0.f);
     }
   }
+}
+
+// ABL (timing-only ablations, outputs invalid): 4 returns at once, 5 after phase 0,
+// 6 after phase 1, 7 skips the gathers.
+template <int R, typename PT, int ABL = 0, int NT_ = 512>
+__global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
+    const PT* __restrict__ pyr, const float* __restrict__ coords, float* __restrict__ out,
+    LookupGeom g) {
+  using C = WideCfg<R, NT_>;
+  constexpr int RD = C::RD, RS = C::RS, K = C::K, QB = C::QB;
+  __shared__ __attribute__((aligned(16))) float cells[QB * C::QS];
+  __shared__ float4 xs[RD * QB];   // {column in the LDS row (int bits), fx, 1-fx, -}
+  __shared__ float4 ys[RD * QB];   // {row offset in LDS (int bits), fy, 1-fy, -}
+  __shared__ int2 org[QB];         // window origin (x, y) or FAR_ORIGIN
+
+  const int tid = threadIdx.x;
+  const int l = blockIdx.y, b = blockIdx.z;
+  const int q0 = blockIdx.x * QB;
+  const LevelAddr A = g.lv[l];
+  if constexpr (ABL == 4) return;
+
+  // ---- phase 0
+  wide_phase0<R, NT_>(coords, g, A, b, l, q0, tid, xs, ys, org);
   __syncthreads();
   if constexpr (ABL == 5) {
     if (xs[tid % (RD * QB)].y == 1234.5f) out[tid] = 0.f;
@@ -441,6 +453,94 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
     r = __builtin_fmaf(se, v11, r);
     ob[(unsigned)(k * g.N)] = r;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Lookup backward (training: train.py:175-178 backpropagates through the
+// grid_sample calls of core/utils/utils.py:65).  The gradient of one query's
+// level-l image comes only from that query's (2r+1)^2 samples at level l, so a
+// workgroup (QB queries x one level, as the forward) owns its windows: the
+// bilinear transpose is accumulated in LDS and added into the gradient pyramid
+// (same paged layout as the pyramid) with plain read-modify-writes, no atomics.
+// The transpose is separable — every tap weight is the product of a row factor
+// (1-fy or fy) and a column factor (1-fx or fx) of the forward — so per query
+//   T[cy][ox]  = sum_oy  wy(oy, cy) * g[ox][oy]
+//   dW[cy][cx] = sum_ox  T[cy][ox] * wx(ox, cx)
+// a deterministic order (no LDS atomics).  Taps off the level get no gradient
+// (zero padding); far and non-finite queries contribute nothing.
+// ---------------------------------------------------------------------------
+template <int R>
+__global__ __launch_bounds__(512) void corr_lookup_backward_kernel(const float* __restrict__ coords,
+                                                                   const float* __restrict__ gout,
+                                                                   float* __restrict__ gpyr,
+                                                                   LookupGeom g) {
+  using C = WideCfg<R, 512>;
+  constexpr int RD = C::RD, WD = C::WD, RS = C::RS, K = C::K, QB = C::QB, NT = C::NT;
+  __shared__ float4 xs[RD * QB];
+  __shared__ float4 ys[RD * QB];
+  __shared__ int2 org[QB];
+  __shared__ float G[K * QB];              // [k][qq]
+  __shared__ float T[QB * WD * RD];        // [qq][cy][ox]
+
+  const int tid = threadIdx.x;
+  const int l = blockIdx.y, b = blockIdx.z;
+  const int q0 = blockIdx.x * QB;
+  const LevelAddr A = g.lv[l];
+  wide_phase0<R, 512>(coords, g, A, b, l, q0, tid, xs, ys, org);
+  for (int i = tid; i < K * QB; i += NT) {
+    const int k = i / QB, qq = i - k * QB, q = q0 + qq;
+    G[i] = q < g.N ? gout[((long long)b * g.cout + (long long)l * K + k) * g.N + q] : 0.f;
+  }
+  __syncthreads();
+
+  for (int e = tid; e < QB * WD * RD; e += NT) {
+    const int qq = e / (WD * RD), rem = e - qq * (WD * RD);
+    const int cy = rem / RD, ox = rem - cy * RD;
+    float acc = 0.f;
+#pragma unroll
+    for (int oy = 0; oy < RD; ++oy) {
+      const float4 yd = ys[oy * QB + qq];
+      const int row = __float_as_int(yd.x) / RS;
+      const float w = row == cy ? yd.z : (row + 1 == cy ? yd.y : 0.f);
+      acc = __builtin_fmaf(G[(ox * RD + oy) * QB + qq], w, acc);
+    }
+    T[e] = acc;
+  }
+  __syncthreads();
+
+  float* base = gpyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
+  const int qb0 = q0 & ((1 << A.lqb) - 1);
+  for (int e = tid; e < QB * WD * RS; e += NT) {
+    const int qq = e / (WD * RS), rem = e - qq * (WD * RS);
+    const int cy = rem / RS, cx = rem - cy * RS;
+    const int2 o = org[qq];
+    if (q0 + qq >= g.N || o.x == FAR_ORIGIN) continue;
+    const int yy = o.y + cy, xx = (o.x & ~3) + cx;
+    if ((unsigned)yy >= (unsigned)A.h || (unsigned)xx >= (unsigned)A.w) continue;
+    float acc = 0.f;
+    const float* t = T + (qq * WD + cy) * RD;
+#pragma unroll
+    for (int ox = 0; ox < RD; ++ox) {
+      const float4 xd = xs[ox * QB + qq];
+      const int col = __float_as_int(xd.x);
+      const float w = col == cx ? xd.z : (col + 1 == cx ? xd.y : 0.f);
+      acc = __builtin_fmaf(t[ox], w, acc);
+    }
+    const unsigned off = (unsigned)(qb0 + qq) * (unsigned)A.S +
+                         ((unsigned)((yy >> A.lth) * A.tx + (xx >> A.ltw))) * (unsigned)A.pageS +
+                         (unsigned)((yy & A.mh) * A.tw + (xx & A.mw));
+    base[off] += acc;
+  }
+}
+
+template <int R>
+int launch_lookup_backward_r(const float* coords, const float* gout, float* gpyr,
+                             const LookupGeom& g, int B, hipStream_t stream) {
+  using W = WideCfg<R, 512>;
+  const dim3 grid((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
+  hipLaunchKernelGGL((corr_lookup_backward_kernel<R>), grid, dim3(512), 0, stream, coords, gout,
+                     gpyr, g);
+  return dxr::launch_status();
 }
 
 int lookup_variant() {
@@ -545,4 +645,35 @@ extern "C" int dxr_corr_lookup(const void* pyramid, int pyr_dtype, int64_t B, in
     return launch_lookup(static_cast<const uint16_t*>(pyramid), coords, out, g, (int)B, radius,
                          stream);
   return DXR_EINVAL;
+}
+
+extern "C" int dxr_corr_lookup_backward(const float* coords, const float* grad_out, int64_t B,
+                                        int64_t H, int64_t W, int num_levels, int radius,
+                                        void* grad_pyramid, int grad_dtype, hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, num_levels, &L)) return DXR_EINVAL;
+  if (radius < 0) return DXR_EINVAL;
+  if (radius > 8) return DXR_EUNSUPPORTED;
+  if (grad_dtype != DXR_F32) return grad_dtype == DXR_BF16 ? DXR_EUNSUPPORTED : DXR_EINVAL;
+  if (B > 65535 || H * W > (1LL << 30)) return DXR_EINVAL;
+  if (B == 0) return DXR_OK;
+  if (!coords || !grad_out || !grad_pyramid) return DXR_EINVAL;
+  const int rd = 2 * radius + 1;
+  LookupGeom g;
+  g.N = (int)(H * W);
+  g.levels = num_levels;
+  g.cout = num_levels * rd * rd;
+  for (int l = 0; l < L.n; ++l) g.lv[l] = level_addr(L.lay[l]);
+  float* gp = static_cast<float*>(grad_pyramid);
+  switch (radius) {
+    case 0: return launch_lookup_backward_r<0>(coords, grad_out, gp, g, (int)B, stream);
+    case 1: return launch_lookup_backward_r<1>(coords, grad_out, gp, g, (int)B, stream);
+    case 2: return launch_lookup_backward_r<2>(coords, grad_out, gp, g, (int)B, stream);
+    case 3: return launch_lookup_backward_r<3>(coords, grad_out, gp, g, (int)B, stream);
+    case 4: return launch_lookup_backward_r<4>(coords, grad_out, gp, g, (int)B, stream);
+    case 5: return launch_lookup_backward_r<5>(coords, grad_out, gp, g, (int)B, stream);
+    case 6: return launch_lookup_backward_r<6>(coords, grad_out, gp, g, (int)B, stream);
+    case 7: return launch_lookup_backward_r<7>(coords, grad_out, gp, g, (int)B, stream);
+    default: return launch_lookup_backward_r<8>(coords, grad_out, gp, g, (int)B, stream);
+  }
 }

@@ -217,3 +217,91 @@ def alt_corr_block(fmap1: np.ndarray, fmap2: np.ndarray, coords: np.ndarray, num
         outs.append(alt_corr_forward(f1, f2, ci, radius, dtype)[:, 0])
     out = np.stack(outs, axis=1).reshape(B, -1, H, W)
     return out / out.dtype.type(np.sqrt(F32(D), dtype=F32))
+
+
+# --------------------------------------------------------------------------- backward
+# Gradients of the reference CorrBlock with respect to its fmaps (training,
+# train.py:175-178 backpropagates through core/corr.py).  coords are detached
+# by the reference (core/raft.py:170), so no coordinate gradient is restated.
+
+
+def bilinear_sample_backward(grad: np.ndarray, shape: tuple[int, int, int], x: np.ndarray,
+                             y: np.ndarray) -> np.ndarray:
+    """Gradient of ``bilinear_sample`` w.r.t. ``img`` (F.grid_sample backward,
+    zero padding, align_corners=True, core/utils/utils.py:65): every in-bounds
+    tap of sample k receives grad[p, k] times its weight.  float64 accumulation."""
+    P, H, W = shape
+    ix = sample_coord(x, W)
+    iy = sample_coord(y, H)
+    with np.errstate(invalid="ignore"):
+        x0 = np.floor(ix)
+        y0 = np.floor(iy)
+        w = ix - x0
+        e = F32(1) - w
+        n = iy - y0
+        s = F32(1) - n
+        wts = {(0, 0): s * e, (0, 1): s * w, (1, 0): n * e, (1, 1): n * w}
+    g = grad.astype(np.float64)
+    out = np.zeros((P, H * W), dtype=np.float64)
+    plane = np.broadcast_to(np.arange(P)[:, None], g.shape)
+    for (dy_, dx_), wt in wts.items():
+        yy, xx = y0 + dy_, x0 + dx_
+        with np.errstate(invalid="ignore"):
+            ok = np.isfinite(yy) & np.isfinite(xx) & (yy >= 0) & (yy <= H - 1) & (xx >= 0) & \
+                (xx <= W - 1)
+        idx = np.where(ok, yy, 0).astype(np.int64) * W + np.where(ok, xx, 0).astype(np.int64)
+        np.add.at(out, (plane[ok], idx[ok]), (g * wt.astype(np.float64))[ok])
+    return out.reshape(P, H, W)
+
+
+def corr_lookup_backward(level_shapes: list[tuple[int, int]], coords: np.ndarray, radius: int,
+                         grad_out: np.ndarray) -> list[np.ndarray]:
+    """Gradient of ``corr_lookup`` (core/corr.py:29-50) w.r.t. each pyramid level:
+    the channel split / permute inverted, then one grid_sample backward per level.
+    Returns float64 levels [B*H*W, H_l, W_l]."""
+    B, _, H, W = coords.shape
+    rd = 2 * radius + 1
+    c = np.asarray(coords, dtype=F32).transpose(0, 2, 3, 1).reshape(B * H * W, 2)
+    offs = np.arange(-radius, radius + 1, dtype=F32)
+    g = np.asarray(grad_out).transpose(0, 2, 3, 1).reshape(B * H * W, len(level_shapes), rd * rd)
+    grads = []
+    for lvl, (hl, wl) in enumerate(level_shapes):
+        cen = c / F32(2 ** lvl)
+        xs = np.broadcast_to(cen[:, 0, None, None] + offs[None, :, None], (B * H * W, rd, rd))
+        ys = np.broadcast_to(cen[:, 1, None, None] + offs[None, None, :], (B * H * W, rd, rd))
+        grads.append(bilinear_sample_backward(g[:, lvl], (B * H * W, hl, wl),
+                                              xs.reshape(-1, rd * rd), ys.reshape(-1, rd * rd)))
+    return grads
+
+
+def avg_pool2x2_backward(dy: np.ndarray, in_shape: tuple[int, int]) -> np.ndarray:
+    """F.avg_pool2d(2, stride=2) backward: each covered input cell gets dy / 4;
+    the floor-mode remainder row / column gets 0."""
+    H, W = in_shape
+    Ho, Wo = dy.shape[-2:]
+    dx = np.zeros(dy.shape[:-2] + (H, W), dtype=dy.dtype)
+    q = dy / dy.dtype.type(4)
+    for a in range(2):
+        for b in range(2):
+            dx[..., a:2 * Ho:2, b:2 * Wo:2] = q
+    return dx
+
+
+def corr_pyramid_backward(fmap1: np.ndarray, fmap2: np.ndarray,
+                          dlevels: list[np.ndarray]) -> tuple[np.ndarray, np.ndarray]:
+    """Gradient of CorrBlock.__init__ (core/corr.py:13-27, 52-60) w.r.t. the fmaps,
+    given the gradient of every pyramid level: the pooling chain backward
+    (level l receives level l+1's total gradient / 4), then / sqrt(D), then the
+    two matmul gradients dF1 = F2 dV^T, dF2 = F1 dV.  float64."""
+    B, D, H, W = fmap1.shape
+    N = H * W
+    tot = dlevels[-1].astype(np.float64)
+    for lvl in range(len(dlevels) - 2, -1, -1):
+        hl, wl = dlevels[lvl].shape[-2:]
+        tot = dlevels[lvl].astype(np.float64) + avg_pool2x2_backward(tot, (hl, wl))
+    dv = tot.reshape(B, N, N) / np.float64(np.sqrt(F32(D), dtype=F32))
+    f1 = fmap1.reshape(B, D, N).astype(np.float64)
+    f2 = fmap2.reshape(B, D, N).astype(np.float64)
+    df1 = np.matmul(f2, dv.transpose(0, 2, 1))
+    df2 = np.matmul(f1, dv)
+    return df1.reshape(B, D, H, W), df2.reshape(B, D, H, W)

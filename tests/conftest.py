@@ -70,3 +70,27 @@ def tolerance_check(got: np.ndarray, ref: np.ndarray, rtol_of_max: float) -> flo
     err = float(np.abs(got[fin].astype(np.float64) - ref[fin].astype(np.float64)).max())
     assert err <= rtol_of_max * scale, f"max err {err:.3e} > {rtol_of_max:.1e} * {scale:.3e}"
     return err / scale
+
+
+BACKWARD_CASES = ["bw_basic", "bw_batch2_r3", "bw_d256"]
+
+
+def load_backward(name: str) -> dict:
+    """A backward golden (tests/golden/make_backward_golden.py) with its inputs
+    regenerated from the recorded seeds: fmaps, coord sets, loss weights."""
+    import datagen as dg
+    with np.load(GOLDEN / f"{name}.npz") as z:
+        d = {k: z[k] for k in z.files}
+    B, D, H, W, r, L = (int(v) for v in d["meta"])
+    dist = str(d["dist"])
+    d.update(B=B, D=D, H=H, W=W, radius=r, num_levels=L)
+    d["fmap1"] = dg.fmap(int(d["fmap_seeds"][0]), B, D, H, W, dist)
+    d["fmap2"] = dg.fmap(int(d["fmap_seeds"][1]), B, D, H, W, dist)
+    np.testing.assert_allclose([d["fmap1"].astype(np.float64).sum(),
+                                d["fmap2"].astype(np.float64).sum()], d["fmap_checksum"],
+                               rtol=0, atol=1e-6)
+    rd = 2 * r + 1
+    d["coords"] = [dg.coords(int(seed), B, H, W, str(mode), float(scale))
+                   for mode, scale, seed in d["coord_sets"]]
+    d["weights"] = [dg.fmap(int(s), B, L * rd * rd, H, W, "normal") for s in d["weight_seeds"]]
+    return d

@@ -38,7 +38,8 @@ def test_header_declares_the_documented_entry_points():
         "dxr_abi_version", "dxr_status_string", "dxr_last_hip_error", "dxr_pyramid_numel",
         "dxr_pyramid_level_offset", "dxr_corr_pyramid_build", "dxr_corr_lookup",
         "dxr_avg_pool2x2", "dxr_alt_corr_forward", "dxr_alt_corr_lookup", "dxr_corr_volume",
-        "dxr_pyramid_unpack", "dxr_pyramid_pack", "dxr_build_workspace_bytes"}
+        "dxr_pyramid_unpack", "dxr_pyramid_pack", "dxr_build_workspace_bytes",
+        "dxr_corr_lookup_backward", "dxr_pyramid_backward"}
 
 
 def test_library_exports_every_declared_symbol(nat):
@@ -144,6 +145,15 @@ def test_host_side_validation_needs_no_gpu(nat):
     assert al(P, ptrs, P, P, 1, 16, 16, 64, 4, 4, 0.0, None) == EINVAL  # divisor 0
     assert al(P, ptrs, P, P, 1, 16, 16, 64, 4, 9, 16.0, None) == EUNSUP
     assert al(P, None, P, P, 1, 16, 16, 64, 4, 4, 16.0, None) == EINVAL
+    lb = lib.dxr_corr_lookup_backward
+    assert lb(P, P, 1, 8, 8, 4, -1, P, 0, None) == EINVAL               # radius < 0
+    assert lb(P, P, 1, 8, 8, 4, 4, P, 1, None) == EUNSUP                # bf16 gradients
+    assert lb(None, P, 1, 8, 8, 4, 4, P, 0, None) == EINVAL             # null coords
+    assert lb(None, None, 0, 8, 8, 4, 4, None, 0, None) == OK           # empty batch
+    pb = lib.dxr_pyramid_backward
+    assert pb(P, 0, 1, 8, 8, 4, 0.0, P, None) == EINVAL                 # divisor 0
+    assert pb(P, 0, 1, 7, 30, 4, 16.0, P, None) == EINVAL               # empty level
+    assert pb(P, 1, 1, 8, 8, 4, 16.0, P, None) == EUNSUP
     assert lib.dxr_last_hip_error() == 0
 
 

@@ -469,3 +469,79 @@ def test_native_library_is_the_one_loaded(dx):
     """The in-tree .so is mapped into this process (no silent fallback)."""
     maps = open("/proc/self/maps").read()
     assert str(dx.LIB_PATH) in maps
+
+
+# --------------------------------------------------------------------------- backward
+BW_RTOL = 1e-4   # of max|reference gradient|, as the forward's fp32 tolerance
+
+
+def _loss_backward(block_cls, f1, f2, coord_sets, weights, **kw):
+    f1 = f1.clone().requires_grad_(True)
+    f2 = f2.clone().requires_grad_(True)
+    cb = block_cls(f1, f2, **kw)
+    loss = 0.0
+    for c, w in zip(coord_sets, weights):
+        loss = loss + (cb(c) * w).sum()
+    loss.backward()
+    return f1.grad, f2.grad
+
+
+@pytest.mark.parametrize("name", ["bw_basic", "bw_batch2_r3", "bw_d256"])
+def test_backward_matches_reference_autograd_golden(dx, name):
+    """d loss / d fmaps through CorrBlock (build + 3 lookups) against the
+    reference's own autograd gradients (tests/golden/make_backward_golden.py)."""
+    from conftest import load_backward
+    d = load_backward(name)
+    g1, g2 = _loss_backward(dx.CorrBlock, _t(d["fmap1"]), _t(d["fmap2"]),
+                            [_t(c) for c in d["coords"]], [_t(w) for w in d["weights"]],
+                            num_levels=d["num_levels"], radius=d["radius"])
+    for got, ref in ((g1, d["dfmap1"]), (g2, d["dfmap2"])):
+        scale = np.abs(ref).max()
+        err = np.abs(got.cpu().numpy() - ref).max()
+        print(f"{name}: max|err| {err:.3e} of max|grad| {scale:.3e}")
+        assert err <= BW_RTOL * scale
+
+
+@pytest.mark.parametrize("shape", [(1, 256, 46, 62, 4), (2, 128, 23, 37, 3)])
+def test_backward_matches_torch_autograd(dx, shape):
+    """Chairs-size and a ragged batch-2 case against torch autograd of the
+    PyTorch restatement (tests/torch_ref.py) on the same device, 12 lookups."""
+    from torch_ref import TorchCorrBlock
+    B, D, H, W, r = shape
+    f1, f2 = _pair(B=B, D=D, H=H, W=W, seed=301, dist="fnet")
+    cs = [_t(dg.coords(310 + k, B, H, W, "normal", 4.0)) for k in range(12)]
+    ws = [_t(dg.fmap(330 + k, B, 4 * (2 * r + 1) ** 2, H, W)) for k in range(12)]
+    g1, g2 = _loss_backward(dx.CorrBlock, f1, f2, cs, ws, radius=r)
+    t1, t2 = _loss_backward(TorchCorrBlock, f1, f2, cs, ws, radius=r)
+    for got, ref in ((g1, t1), (g2, t2)):
+        scale = ref.abs().max().item()
+        err = (got - ref).abs().max().item()
+        print(f"{shape}: max|err| {err:.3e} of max|grad| {scale:.3e}")
+        assert err <= BW_RTOL * scale
+
+
+def test_backward_of_static_corr(dx):
+    """CorrBlock.corr is differentiable (core/corr.py:52-60 is a plain matmul)."""
+    f1, f2 = _pair(B=2, D=64, H=12, W=20, seed=341)
+    w = _t(dg.fmap(342, 2 * 12 * 20, 1, 12 * 20, 1)).reshape(2, 12, 20, 1, 12, 20)
+    a1, a2 = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
+    (dx.CorrBlock.corr(a1, a2) * w).sum().backward()
+    b1, b2 = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
+    v = torch.bmm(b1.reshape(2, 64, -1).transpose(1, 2), b2.reshape(2, 64, -1)) / 8.0
+    (v.reshape(2, 12, 20, 1, 12, 20) * w).sum().backward()
+    for got, ref in ((a1.grad, b1.grad), (a2.grad, b2.grad)):
+        assert (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
+def test_backward_only_flows_to_fmaps_that_require_grad(dx):
+    f1, f2 = _pair(B=1, D=32, H=12, W=16, seed=351)
+    a1 = f1.clone().requires_grad_(True)
+    cb = dx.CorrBlock(a1, f2)
+    c = _t(dg.coords(352, 1, 12, 16, "normal", 2.0))
+    cb(c).sum().backward()
+    assert a1.grad is not None and torch.isfinite(a1.grad).all()
+    with torch.no_grad():                       # inference calls on a grad block stay plain
+        out = cb(c)
+    assert out.grad_fn is None
+    with pytest.raises(NotImplementedError, match="coords"):
+        cb(c.clone().requires_grad_(True))

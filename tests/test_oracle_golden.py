@@ -149,3 +149,38 @@ def test_large_chairs_checksums():
     out = oracle.corr_lookup(pyr, dg.coords(int(seed), B, H, W, mode, float(scale)), r)
     maxabs = float(d["out0_maxabs"])
     assert np.abs(out.reshape(-1)[d["out0_idx"]] - d["out0_val"]).max() <= 1e-6 * maxabs
+
+
+# --------------------------------------------------------------------------- backward
+@pytest.mark.parametrize("name", ["bw_basic", "bw_batch2_r3", "bw_d256"])
+def test_oracle_backward_matches_reference_autograd(name):
+    """The float64 backward restatement (grid_sample scatter, avg-pool chain,
+    matmul gradients) reproduces the reference autograd's fmap gradients."""
+    from conftest import load_backward
+    d = load_backward(name)
+    L, r = d["num_levels"], d["radius"]
+    pyr = oracle.corr_pyramid(d["fmap1"], d["fmap2"], L, np.float64)
+    shapes = [p.shape[-2:] for p in pyr]
+    dl = [np.zeros(p.shape) for p in pyr]
+    for c, w in zip(d["coords"], d["weights"]):
+        for acc, g in zip(dl, oracle.corr_lookup_backward(shapes, c, r, w)):
+            acc += g
+    df1, df2 = oracle.corr_pyramid_backward(d["fmap1"], d["fmap2"], dl)
+    for got, ref in ((df1, d["dfmap1"]), (df2, d["dfmap2"])):
+        scale = np.abs(ref).max()
+        assert np.abs(got - ref).max() <= 1e-5 * scale
+
+
+@pytest.mark.parametrize("name", ["fnet", "small_r3", "batch2_alt"])
+def test_torch_restatement_matches_reference_forward(name):
+    """tests/torch_ref.py (the device-side autograd checker of the GPU backward
+    tests) reproduces the reference forward on CPU."""
+    import torch
+    from torch_ref import TorchCorrBlock
+    d = load_tiny(name)
+    cb = TorchCorrBlock(torch.from_numpy(d["fmap1"]), torch.from_numpy(d["fmap2"]),
+                        num_levels=d["num_levels"], radius=d["radius"])
+    for k in range(len(d["coords"])):
+        out = cb(torch.from_numpy(d[f"coords{k}"])).numpy()
+        ref = d[f"out{k}"]
+        assert np.abs(out - ref).max() <= 1e-5 * np.abs(ref).max()
