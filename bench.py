@@ -93,14 +93,22 @@ def build_kernel(dtype, H, W):
     return "corr_build_f32_kernel", 1, PEAK_F32_TFLOPS, "f32"
 
 
-def pmc_traffic(kernel_prefix):
-    """Per-launch HBM bytes of a kernel from the newest committed PMC summary
-    (profiles/<round>/traffic.json, written by scripts/pmc_traffic.py from
-    separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench), or None."""
-    files = sorted((REPO / "profiles").glob("*/traffic.json"))
+def alt_lookup_flops(B, H, W):
+    n = H * W
+    return 2.0 * B * n * LEVELS * (2 * RADIUS + 2) ** 2 * D
+
+
+def pmc_traffic(workload, kernel_prefix):
+    """Per-launch HBM bytes of a kernel from the newest committed PMC summary of
+    this workload (profiles/<round>/traffic*.json, written by
+    scripts/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes
+    of this bench), or None when that workload was not profiled."""
+    files = sorted((REPO / "profiles").glob("*/traffic*.json"))
     for f in reversed(files):
         data = json.loads(f.read_text())
-        for name, rec in data.items():
+        if data.get("workload") != workload:
+            continue
+        for name, rec in data.get("kernels", {}).items():
             if name.split("::")[-1].startswith(kernel_prefix):
                 return rec["traffic_bytes"], f"{f.relative_to(REPO)}: {rec['correction']}"
     return None, None
@@ -176,6 +184,8 @@ def main():
                     help="strong scaling: this many pairs per step split over the ranks (C4: 64)")
     ap.add_argument("--dtype", default=None, choices=["f32", "bf16"])
     ap.add_argument("--mode", default="graph", choices=["graph", "eager"])
+    ap.add_argument("--block", default="corr", choices=["corr", "alt"],
+                    help="corr: CorrBlock (full pyramid); alt: AlternateCorrBlock (on the fly, C5)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -200,8 +210,10 @@ def main():
 
     state = {}
 
+    block_cls = dexiraft_amd.CorrBlock if args.block == "corr" else dexiraft_amd.AlternateCorrBlock
+
     def build():
-        state["cb"] = dexiraft_amd.CorrBlock(f1, f2, radius=RADIUS)
+        state["cb"] = block_cls(f1, f2, radius=RADIUS)
 
     def lookups():
         state["outs"] = [state["cb"](c) for c in coords]
@@ -255,11 +267,7 @@ def main():
         value = pairs / elapsed
         s_in = 2 if dtype == "bf16" else 4
         flops = build_flops(B, H, W)
-        kname, mfma_per_flop, peak, mfma_dtype = build_kernel(dtype, H, W)
-        achieved = mfma_per_flop * flops / (build_ms * 1e-3) / 1e12
-        kshort = kname.split(" ")[0]
-        b_traffic, b_src = pmc_traffic(kshort + "<")
-        l_traffic, l_src = pmc_traffic("corr_lookup_wide_kernel<")
+        wl_key = f"{args.workload}_b{B}_{dtype}"
         lb = lookup_bytes(B, H, W, s_pyr=s_in)
         res = {
             "metric": METRIC,
@@ -275,12 +283,19 @@ def main():
             "dtype": dtype,
             "data": "synthetic (torch.randn fmaps, coords = grid + N(0,4^2) px)",
             "config": {
-                "workload": f"CorrBlock build + {ITERS} lookups, {args.workload} "
+                "workload": f"{'CorrBlock' if args.block == 'corr' else 'AlternateCorrBlock'} "
+                            f"build + {ITERS} lookups, {args.workload} "
                             f"{img_h}x{img_w} (fmap {H}x{W}), D={D}, r={RADIUS}, L={LEVELS}",
                 "pairs_per_gpu": B, "mode": args.mode, "parallelism": f"pairs sharded x{world}",
                 "kernel_timing": timing,
             },
-            "roofline": {
+        }
+        if args.block == "corr":
+            kname, mfma_per_flop, peak, mfma_dtype = build_kernel(dtype, H, W)
+            achieved = mfma_per_flop * flops / (build_ms * 1e-3) / 1e12
+            b_traffic, b_src = pmc_traffic(wl_key, kname.split(" ")[0] + "<")
+            l_traffic, l_src = pmc_traffic(wl_key, "corr_lookup_wide_kernel<")
+            res["roofline"] = {
                 "kernel": kname + " (stage a+b)",
                 "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                 "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
@@ -289,9 +304,10 @@ def main():
                 "algorithmic_flops_per_launch": flops,
                 "mfma_flops_per_launch": mfma_per_flop * flops,
                 "f32_equivalent_tflops": round(flops / (build_ms * 1e-3) / 1e12, 2),
+                "algorithmic_bytes_per_launch": build_bytes(B, H, W, s_in, s_in),
                 "avg_launch_us": round(build_ms * 1e3, 2),
-            },
-            "lookup_roofline": {
+            }
+            res["lookup_roofline"] = {
                 "kernel": "corr_lookup_wide_kernel (stage c)",
                 "bound": "hbm", "achieved": round(lb / (look_ms * 1e-3) / 1e9, 1),
                 "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -299,9 +315,22 @@ def main():
                 "algorithmic_bytes_per_launch": lb,
                 "traffic": l_traffic, "traffic_source": l_src,
                 "avg_launch_us": round(look_ms * 1e3, 2),
-            },
-            "build_bytes_per_launch": build_bytes(B, H, W, s_in, s_in),
-        }
+            }
+        else:
+            # on-the-fly lookups: (2r+2)^2 window dot products of length D per query
+            # and level, f32 FMA on the vector ALUs (SURVEY.md §8(d) stage d)
+            aflops = alt_lookup_flops(B, H, W)
+            achieved = aflops / (look_ms * 1e-3) / 1e12
+            a_traffic, a_src = pmc_traffic(wl_key, "alt_corr_kernel<")
+            res["roofline"] = {
+                "kernel": "alt_corr_kernel (stage d, per lookup)",
+                "bound": "valu", "achieved": round(achieved, 2), "peak": PEAK_F32_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_TFLOPS, 4),
+                "traffic": a_traffic, "traffic_source": a_src,
+                "algorithmic_flops_per_launch": aflops,
+                "avg_launch_us": round(look_ms * 1e3, 2),
+                "pool_and_layout_us_per_step": round(build_ms * 1e3, 2),
+            }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(H, W, args.cpu_seconds)
         print(json.dumps(res), flush=True)

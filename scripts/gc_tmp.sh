@@ -1,4 +1,6 @@
 set -u
-O=gpurun_out/s3q; mkdir -p $O
-export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -v -s --timeout 120 --timeout-method thread -p no:cacheprovider -k "backward or e2e" > $O/pytest.log 2>&1; rc=$?; echo "pytest rc=$rc"; grep -E "FAILED|passed|failed|max\|err|EPE" $O/pytest.log | tail -30
+bash scripts/gpu_profile.sh r01_cfg/sintel sintel_b1_f32 || exit $?
+bash scripts/gpu_profile.sh r01_cfg/kitti kitti_b8_bf16 --workload kitti --no-cpu-baseline || exit $?
+bash scripts/gpu_profile.sh r01_cfg/chairs chairs_b1_f32 --workload chairs --no-cpu-baseline || exit $?
+bash scripts/gpu_profile.sh r01_cfg/hd_alt 1080p_b1_f32 --workload 1080p --block alt --no-cpu-baseline || exit $?
+timeout -k 10 300 python -u bench.py --workload 1080p --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/r01_cfg/hd_corr.log 2>&1; echo "hd corr rc=$?"; tail -1 gpurun_out/r01_cfg/hd_corr.log
