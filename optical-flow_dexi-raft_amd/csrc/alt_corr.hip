@@ -20,6 +20,8 @@
 // butterfly transpose (each lane ends with one cell's sum), cell sums go to LDS,
 // and after one barrier every thread emits outputs for one query with coalesced
 // 256-byte wave stores along the query dimension.
+#include <cstdlib>
+
 #include "dxr_common.h"
 
 namespace {
@@ -174,6 +176,244 @@ __global__ __launch_bounds__(256) void alt_corr_kernel(const float* __restrict__
   }
 }
 
+// ---------------------------------------------------------------------------
+// MFMA form (default when C % 16 == 0, C <= 256).  A workgroup owns a 4 x 8
+// tile of query pixels and one level.  The queries' (2r+2)^2 windows overlap,
+// so it computes the dot products of its 32 queries with every cell of the
+// windows' union bounding box (clipped to the level) as a small GEMM on the
+// matrix cores, cells x queries x C, and keeps the entries that fall in each
+// query's own window.  Every fmap2 cell vector is then read once per workgroup
+// instead of once per query (the per-query form above re-reads 100 cell vectors
+// per query: 6.7 GB per 1080p lookup, 1.37 ms).  f32 class: both operands are
+// split exactly into hi/mid/lo bf16 (as the split build, csrc/corr_build.hip)
+// and six bf16 products are accumulated in f32; the query planes are split once
+// into LDS, cell vectors in registers as they arrive (one k step ahead).  Box
+// cells are walked in chunks of 4 waves x 32*NRB.  The bilinear combination and
+// the output follow the per-query form exactly.
+// ---------------------------------------------------------------------------
+typedef __bf16 abf8 __attribute__((ext_vector_type(8)));
+typedef float af16 __attribute__((ext_vector_type(16)));
+typedef __bf16 abf2 __attribute__((ext_vector_type(2)));
+typedef float af2 __attribute__((ext_vector_type(2)));
+
+constexpr int TQY = 4, TQX = 8, TQ = TQY * TQX;    // query tile (32 pixels)
+
+__device__ __forceinline__ uint32_t alt_cvt_pk(float a, float b) {
+  const af2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, abf2));
+}
+
+// Exact hi/mid/lo split of 8 floats into three 8 x bf16 operands.
+__device__ __forceinline__ void alt_split8(const float (&x)[8], uint4& h, uint4& m, uint4& l) {
+  uint32_t hh[4], mm[4], ll[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float a = x[2 * e], b = x[2 * e + 1];
+    const uint32_t hp = alt_cvt_pk(a, b);
+    const float ra = a - __uint_as_float(hp << 16), rb = b - __uint_as_float(hp & 0xffff0000u);
+    const uint32_t mp = alt_cvt_pk(ra, rb);
+    const float la = ra - __uint_as_float(mp << 16), lb = rb - __uint_as_float(mp & 0xffff0000u);
+    hh[e] = hp;
+    mm[e] = mp;
+    ll[e] = __builtin_amdgcn_perm(__float_as_uint(lb), __float_as_uint(la), 0x07060302u);
+  }
+  h = make_uint4(hh[0], hh[1], hh[2], hh[3]);
+  m = make_uint4(mm[0], mm[1], mm[2], mm[3]);
+  l = make_uint4(ll[0], ll[1], ll[2], ll[3]);
+}
+
+template <int R, int NRB, int CMAX>
+__global__ __launch_bounds__(256, 2) void alt_corr_mfma_kernel(const float* __restrict__ f1,
+                                                               const float* __restrict__ coords,
+                                                               float* __restrict__ out,
+                                                               AltGeom g, int W1, int tiles_x) {
+  constexpr int RD = 2 * R + 1, RD1 = RD + 1, NCELL = RD1 * RD1;
+  constexpr int CHUNK = 4 * 32 * NRB;                       // box cells per chunk
+  constexpr int KB = CMAX / 8;                              // 8-channel blocks
+  __shared__ __attribute__((aligned(16))) uint4 qplanes[3 * KB * TQ];   // [plane][kb][q]
+  __shared__ float S[TQ * NCELL];                           // window dot products
+  __shared__ int4 qinfo[TQ];                                // {x0, y0, live, -}
+  __shared__ int box[4];                                    // bx0, by0, bw, bh
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+  const AltLevel lv = g.lv[blockIdx.y];
+  const int z = blockIdx.z, bf = z / g.Nc;
+  const float* cz = coords + (long long)z * g.coord_zstride;
+  const float* f1b = f1 + (long long)bf * g.f1_bstride;
+  const float* f2b = lv.f2 + (long long)bf * lv.H2 * lv.W2 * g.C;
+  const int H1 = g.N / W1;
+  const int nkb = g.C / 8;
+
+  // ---- query coordinates, window origins, the windows' union box
+  if (tid < TQ) {
+    const int qy = ty * TQY + tid / TQX, qx = tx * TQX + tid % TQX;
+    int x0 = 0, y0 = 0, live = 0;
+    if (qy < H1 && qx < W1) {
+      const int q = qy * W1 + qx;
+      const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
+      const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
+      const float xf = floorf(x), yf = floorf(y);
+      if (fabsf(xf) < 1.0e8f && fabsf(yf) < 1.0e8f) {
+        x0 = (int)xf - R;
+        y0 = (int)yf - R;
+        // windows entirely off the level need no dot products
+        live = (x0 + RD1 > 0 && x0 < lv.W2 && y0 + RD1 > 0 && y0 < lv.H2) ? 1 : 0;
+      }
+    }
+    qinfo[tid] = make_int4(x0, y0, live, 0);
+    int lx0 = live ? max(x0, 0) : 0x7fffffff, ly0 = live ? max(y0, 0) : 0x7fffffff;
+    int lx1 = live ? min(x0 + RD1, lv.W2) : -1, ly1 = live ? min(y0 + RD1, lv.H2) : -1;
+#pragma unroll
+    for (int o = 1; o < TQ; o <<= 1) {
+      lx0 = min(lx0, __shfl_xor(lx0, o));
+      ly0 = min(ly0, __shfl_xor(ly0, o));
+      lx1 = max(lx1, __shfl_xor(lx1, o));
+      ly1 = max(ly1, __shfl_xor(ly1, o));
+    }
+    if (tid == 0) {
+      const bool any = lx1 > lx0;
+      box[0] = any ? lx0 : 0;
+      box[1] = any ? ly0 : 0;
+      box[2] = any ? lx1 - lx0 : 0;
+      box[3] = any ? ly1 - ly0 : 0;
+    }
+  }
+  for (int i = tid; i < TQ * NCELL; i += 256) S[i] = 0.f;
+  // query operand planes: unit (kb, q) -> f1[q][8 kb .. 8 kb + 8), split once
+  for (int u = tid; u < nkb * TQ; u += 256) {
+    const int kb = u / TQ, qq = u - kb * TQ;
+    const int qy = min(ty * TQY + qq / TQX, H1 - 1), qx = min(tx * TQX + qq % TQX, W1 - 1);
+    const float* src = f1b + (long long)(qy * W1 + qx) * g.C + kb * 8;
+    const float4 a = *reinterpret_cast<const float4*>(src);
+    const float4 c = *reinterpret_cast<const float4*>(src + 4);
+    const float x[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+    uint4 h, m, l;
+    alt_split8(x, h, m, l);
+    qplanes[(0 * KB + kb) * TQ + qq] = h;
+    qplanes[(1 * KB + kb) * TQ + qq] = m;
+    qplanes[(2 * KB + kb) * TQ + qq] = l;
+  }
+  __syncthreads();
+
+  const int bx0 = box[0], by0 = box[1], bw = box[2], bh = box[3];
+  const int ncells = bw * bh;
+  const int j = lane & 31, kh = lane >> 5;
+  const int4 qi = qinfo[j];                   // this lane's accumulator column (query j)
+  for (int c0 = 0; c0 < ncells; c0 += CHUNK) {
+    af16 acc[NRB];
+    const float* src[NRB];
+#pragma unroll
+    for (int rb = 0; rb < NRB; ++rb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[rb][r] = 0.f;
+      // A operand lane -> cell c0 + 32 (wave NRB + rb) + j, channels 8 kh .. + 8 per k16
+      const int c = min(c0 + (wave * NRB + rb) * 32 + j, ncells - 1);
+      const int cy = c / bw, cx = c - cy * bw;
+      src[rb] = f2b + ((long long)(by0 + cy) * lv.W2 + bx0 + cx) * g.C + 8 * kh;
+    }
+    // cell vectors one k step ahead in registers
+    float4 ca[NRB], cb[NRB];
+#pragma unroll
+    for (int rb = 0; rb < NRB; ++rb) {
+      ca[rb] = *reinterpret_cast<const float4*>(src[rb]);
+      cb[rb] = *reinterpret_cast<const float4*>(src[rb] + 4);
+    }
+    for (int ks = 0; ks < nkb / 2; ++ks) {
+      float4 na[NRB], nb[NRB];
+      if (ks + 1 < nkb / 2) {
+#pragma unroll
+        for (int rb = 0; rb < NRB; ++rb) {
+          na[rb] = *reinterpret_cast<const float4*>(src[rb] + (ks + 1) * 16);
+          nb[rb] = *reinterpret_cast<const float4*>(src[rb] + (ks + 1) * 16 + 4);
+        }
+      }
+      const abf8 qh = __builtin_bit_cast(abf8, qplanes[(0 * KB + 2 * ks + kh) * TQ + j]);
+      const abf8 qm = __builtin_bit_cast(abf8, qplanes[(1 * KB + 2 * ks + kh) * TQ + j]);
+      const abf8 ql = __builtin_bit_cast(abf8, qplanes[(2 * KB + 2 * ks + kh) * TQ + j]);
+#pragma unroll
+      for (int rb = 0; rb < NRB; ++rb) {
+        const float4 a = ca[rb], b = cb[rb];
+        const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint4 h, m, l;
+        alt_split8(x, h, m, l);
+        const abf8 th = __builtin_bit_cast(abf8, h), tm = __builtin_bit_cast(abf8, m),
+                   tl = __builtin_bit_cast(abf8, l);
+        // small terms first
+        acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm, acc[rb], 0, 0, 0);
+        acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh, acc[rb], 0, 0, 0);
+        acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, ql, acc[rb], 0, 0, 0);
+        acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qh, acc[rb], 0, 0, 0);
+        acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qm, acc[rb], 0, 0, 0);
+        acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh, acc[rb], 0, 0, 0);
+      }
+      if (ks + 1 < nkb / 2) {
+#pragma unroll
+        for (int rb = 0; rb < NRB; ++rb) {
+          ca[rb] = na[rb];
+          cb[rb] = nb[rb];
+        }
+      }
+    }
+    // keep the entries inside query j's window: D row = (r & 3) + 8 (r >> 2) + 4 kh
+    if (qi.z) {
+#pragma unroll
+      for (int rb = 0; rb < NRB; ++rb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int c = c0 + (wave * NRB + rb) * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+          if (c < ncells) {
+            const int cy = c / bw, cx = c - cy * bw;
+            const int iy = by0 + cy - qi.y, ix = bx0 + cx - qi.x;
+            if ((unsigned)iy < (unsigned)RD1 && (unsigned)ix < (unsigned)RD1)
+              S[j * NCELL + iy * RD1 + ix] = acc[rb][r];
+          }
+        }
+    }
+  }
+  __syncthreads();
+
+  // ---- bilinear combination, as the per-query form (reference order)
+  const int qq = tid & (TQ - 1), cls = tid / TQ;
+  const int qy = ty * TQY + qq / TQX, qx = tx * TQX + qq % TQX;
+  if (qy >= H1 || qx >= W1) return;
+  const int q = qy * W1 + qx;
+  const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
+  const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
+  const float dx = x - floorf(x), dy = y - floorf(y);
+  const float* s = S + qq * NCELL;
+  float* o = out + (long long)z * g.cout * g.N + (long long)lv.ch_off * g.N + q;
+  for (int ox = cls; ox < RD; ox += 256 / TQ) {
+#pragma unroll
+    for (int oy = 0; oy < RD; ++oy) {
+      const float s00 = s[oy * RD1 + ox], s01 = s[oy * RD1 + ox + 1];
+      const float s10 = s[(oy + 1) * RD1 + ox], s11 = s[(oy + 1) * RD1 + ox + 1];
+      float v = __fmul_rn(__fmul_rn(s00, 1.f - dy), 1.f - dx);
+      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s01, 1.f - dy), dx));
+      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s10, dy), 1.f - dx));
+      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s11, dy), dx));
+      o[(long long)(oy + RD * ox) * g.N] = v / g.divisor;
+    }
+  }
+}
+
+int alt_variant() {
+  const char* v = std::getenv("DXR_ALT_VARIANT");
+  return v ? std::atoi(v) : 0;
+}
+
+template <int R, int NRB>
+int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const AltGeom& g,
+                      int levels, int Z, int W1, hipStream_t stream) {
+  const int H1 = g.N / W1;
+  const int tiles_x = (W1 + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
+  const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)levels, (unsigned)Z);
+  if (g.C > 256) return DXR_EUNSUPPORTED;
+  hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256>), grid, dim3(256), 0, stream, f1, coords,
+                     out, g, W1, tiles_x);
+  return dxr::launch_status();
+}
+
 template <int R>
 int launch_alt_r(const float* f1, const float* coords, float* out, const AltGeom& g, int levels,
                  int Z, bool vec, hipStream_t stream) {
@@ -186,7 +426,26 @@ int launch_alt_r(const float* f1, const float* coords, float* out, const AltGeom
 }
 
 int launch_alt(const float* f1, const float* coords, float* out, const AltGeom& g, int levels,
-               int Z, int radius, bool vec, hipStream_t stream) {
+               int Z, int radius, bool vec, hipStream_t stream, int W1 = 0) {
+  // MFMA form: C a multiple of 16 (k16 steps) up to 256, 16-byte aligned rows.
+  // DXR_ALT_VARIANT 1 selects the per-query form, 2 / 3 the MFMA form with 2 / 4
+  // row blocks per wave (r = 4).
+  const int v = alt_variant();
+  if (vec && W1 > 0 && g.C % 16 == 0 && g.C <= 256 && v != 1) {
+    switch (radius) {
+      case 0: return launch_alt_mfma_r<0, 1>(f1, coords, out, g, levels, Z, W1, stream);
+      case 1: return launch_alt_mfma_r<1, 1>(f1, coords, out, g, levels, Z, W1, stream);
+      case 2: return launch_alt_mfma_r<2, 1>(f1, coords, out, g, levels, Z, W1, stream);
+      case 3: return launch_alt_mfma_r<3, 1>(f1, coords, out, g, levels, Z, W1, stream);
+      case 4:
+        if (v == 2) return launch_alt_mfma_r<4, 2>(f1, coords, out, g, levels, Z, W1, stream);
+        if (v == 3) return launch_alt_mfma_r<4, 4>(f1, coords, out, g, levels, Z, W1, stream);
+        return launch_alt_mfma_r<4, 1>(f1, coords, out, g, levels, Z, W1, stream);
+      case 5: return launch_alt_mfma_r<5, 1>(f1, coords, out, g, levels, Z, W1, stream);
+      case 6: return launch_alt_mfma_r<6, 1>(f1, coords, out, g, levels, Z, W1, stream);
+      default: return DXR_EUNSUPPORTED;
+    }
+  }
   switch (radius) {
     case 0: return launch_alt_r<0>(f1, coords, out, g, levels, Z, vec, stream);
     case 1: return launch_alt_r<1>(f1, coords, out, g, levels, Z, vec, stream);
@@ -227,7 +486,7 @@ extern "C" int dxr_alt_corr_forward(const float* fmap1, const float* fmap2, cons
   g.coord_qstride = 2;
   g.lv[0] = AltLevel{fmap2, (int)H2, (int)W2, 1.f, 0};
   const bool vec = (C % 4 == 0) && aligned16(fmap1) && aligned16(fmap2);
-  return launch_alt(fmap1, coords, corr, g, 1, (int)(B * Nc), radius, vec, stream);
+  return launch_alt(fmap1, coords, corr, g, 1, (int)(B * Nc), radius, vec, stream, (int)W1);
 }
 
 extern "C" int dxr_alt_corr_lookup(const float* fmap1, const float* const* fmap2_levels,
@@ -258,5 +517,5 @@ extern "C" int dxr_alt_corr_lookup(const float* fmap1, const float* const* fmap2
     vec = vec && aligned16(fmap2_levels[l]);
     g.lv[l] = AltLevel{fmap2_levels[l], L.h[l], L.w[l], 1.f / (float)(1 << l), l * rd * rd};
   }
-  return launch_alt(fmap1, coords, out, g, num_levels, (int)B, radius, vec, stream);
+  return launch_alt(fmap1, coords, out, g, num_levels, (int)B, radius, vec, stream, (int)W);
 }
