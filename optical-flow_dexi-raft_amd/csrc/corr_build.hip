@@ -54,6 +54,57 @@ struct BuildGeom {
   long long loff[4];    // element offset of each level
 };
 
+// Page coordinates of this workgroup.  3-D grid (tiles, query blocks, pairs), or
+// with REMAP a 1-D grid laid out for the per-XCD L2s: workgroup w runs on XCD
+// w % 8 (round-robin dispatch; used for speed only), the bijective remap of
+// cdna_hip_programming.md §5 gives each XCD a contiguous range of a linear
+// order, and that order walks strips of STRIP target tiles query-block-major,
+// so the ~128 workgroups an XCD holds at once share ~8 target panels and ~16
+// query panels (~3 MB of f32 operands: its L2) instead of every target panel.
+struct PageCoord {
+  int txi, tyi, qblk, b;
+  long long page;
+};
+
+constexpr int STRIP = 8;
+
+template <bool REMAP>
+__device__ __forceinline__ PageCoord page_coord(const BuildGeom& g) {
+  PageCoord c;
+  const int T = g.tiles_w * g.tiles_h;
+  if constexpr (!REMAP) {
+    c.txi = blockIdx.x % g.tiles_w;
+    c.tyi = blockIdx.x / g.tiles_w;
+    c.qblk = blockIdx.y;
+    c.b = blockIdx.z;
+  } else {
+    const long long per_pair = (long long)g.qt * T;
+    const long long nwg = (long long)gridDim.x;
+    const long long w = blockIdx.x;
+    const long long q8 = nwg / 8, r8 = nwg % 8, xcd = w % 8;
+    const long long wl = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + w / 8;
+    c.b = (int)(wl / per_pair);
+    long long rem = wl - c.b * per_pair;
+    const int nfull = T / STRIP;
+    int tile;
+    if (rem < (long long)nfull * g.qt * STRIP) {
+      const int st = (int)(rem / ((long long)g.qt * STRIP));
+      const int in = (int)(rem - (long long)st * g.qt * STRIP);
+      c.qblk = in / STRIP;
+      tile = st * STRIP + in % STRIP;
+    } else {
+      const int nl = T - nfull * STRIP;
+      const int in = (int)(rem - (long long)nfull * g.qt * STRIP);
+      c.qblk = in / nl;
+      tile = nfull * STRIP + in % nl;
+    }
+    c.txi = tile % g.tiles_w;
+    c.tyi = tile / g.tiles_w;
+  }
+  c.page = (((long long)c.b * g.qt + c.qblk) * g.tiles_h + c.tyi) * g.tiles_w + c.txi;
+  return c;
+}
+
 // Global -> register staging of one BK slice of the query panel (A: [BK][BM])
 // and the target tile (B: [BK][TH][TW]).  VEC: W % 4 == 0, so every float4 is
 // fully inside or fully outside the map; outside elements stage as zero.
@@ -519,7 +570,7 @@ __device__ __forceinline__ int tgt_col(int r, int c) {
   return (r >> 1) * 32 + (c & 3) + 4 * (r & 1) + 8 * (c >> 2);
 }
 
-template <bool VEC, typename OT, bool DIV, int MINW>
+template <bool VEC, typename OT, bool DIV, int MINW, bool REMAP = false>
 __global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_t* __restrict__ f1,
                                                              const uint16_t* __restrict__ f2,
                                                              OT* __restrict__ pyr, BuildGeom g) {
@@ -529,10 +580,11 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_
   uint16_t* lh = reinterpret_cast<uint16_t*>(smem);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int txi = blockIdx.x % g.tiles_w, tyi = blockIdx.x / g.tiles_w;
+  const PageCoord pc = page_coord<REMAP>(g);
+  const int txi = pc.txi, tyi = pc.tyi;
   const int th0 = tyi * TH, tw0 = txi * TW;
-  const int q0 = blockIdx.y * BM;
-  const int b = blockIdx.z;
+  const int q0 = pc.qblk * BM;
+  const int b = pc.b;
   const long long fstride = (long long)g.D * g.N;
   const uint16_t* f1b = f1 + b * fstride;
   const uint16_t* f2b = f2 + b * fstride;
@@ -641,8 +693,7 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_
   }
 
   scale_acc<DIV>(acc, g);
-  const long long page = ((long long)b * gridDim.y + blockIdx.y) * ((long long)g.tiles_h *
-                         g.tiles_w) + (long long)tyi * g.tiles_w + txi;
+  const long long page = pc.page;
   paged_epilogue<OT, false>(acc, reinterpret_cast<float*>(smem), pyr, g, page, wave, wave, true, lane);
 }
 
@@ -702,7 +753,7 @@ __device__ __forceinline__ Split3 split3(float a, float b) {
 
 // ABL (timing-only ablations, never the default): 1 skips the epilogue stores,
 // 2 skips the MFMAs.
-template <typename OT, bool DIV, int MINW, int ABL = 0>
+template <typename OT, bool DIV, int MINW, int ABL = 0, bool REMAP = false>
 __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float* __restrict__ f1,
                                                                     const float* __restrict__ f2,
                                                                     OT* __restrict__ pyr,
@@ -713,10 +764,11 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
   uint16_t* lh = reinterpret_cast<uint16_t*>(smem);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int txi = blockIdx.x % g.tiles_w, tyi = blockIdx.x / g.tiles_w;
+  const PageCoord pc = page_coord<REMAP>(g);
+  const int txi = pc.txi, tyi = pc.tyi;
   const int th0 = tyi * TH, tw0 = txi * TW;
-  const int q0 = blockIdx.y * BM;
-  const int b = blockIdx.z;
+  const int q0 = pc.qblk * BM;
+  const int b = pc.b;
   const long long fstride = (long long)g.D * g.N;
   const float* f1b = f1 + b * fstride;
   const float* f2b = f2 + b * fstride;
@@ -836,8 +888,7 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     if (sum == 1234.5f) pyr[tid] = to_out<OT>(sum);  // keeps the K loop live
     return;
   }
-  const long long page = ((long long)b * gridDim.y + blockIdx.y) * ((long long)g.tiles_h *
-                         g.tiles_w) + (long long)tyi * g.tiles_w + txi;
+  const long long page = pc.page;
   paged_epilogue<OT, false>(acc, reinterpret_cast<float*>(smem), pyr, g, page, wave, wave, true, lane);
 }
 
@@ -1134,6 +1185,11 @@ dim3 build_grid(const BuildGeom& g, int B) {
   return dim3((unsigned)(g.tiles_h * g.tiles_w), (unsigned)((g.N + BM - 1) / BM), (unsigned)B);
 }
 
+// 1-D grid of every page (REMAP launches).
+dim3 remap_grid(const BuildGeom& g, int B) {
+  return dim3((unsigned)((long long)B * g.qt * g.tiles_h * g.tiles_w));
+}
+
 int resident_build_groups(int per_cu) {
   static int cus = [] {
     int dev = 0, n = 256;
@@ -1174,15 +1230,15 @@ int launch_f32(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, in
   return dxr::launch_status();
 }
 
-template <bool VEC, int MINW, typename OT>
+template <bool VEC, int MINW, typename OT, bool REMAP = false>
 int launch_bf16_w(const uint16_t* f1, const uint16_t* f2, OT* pyr, const BuildGeom& g, dim3 grid,
                   hipStream_t stream) {
   if (g.recip == 0.f)
-    hipLaunchKernelGGL((corr_build_bf16_kernel<VEC, OT, true, MINW>), grid, dim3(NT), 0, stream,
-                       f1, f2, pyr, g);
+    hipLaunchKernelGGL((corr_build_bf16_kernel<VEC, OT, true, MINW, REMAP>), grid, dim3(NT), 0,
+                       stream, f1, f2, pyr, g);
   else
-    hipLaunchKernelGGL((corr_build_bf16_kernel<VEC, OT, false, MINW>), grid, dim3(NT), 0, stream,
-                       f1, f2, pyr, g);
+    hipLaunchKernelGGL((corr_build_bf16_kernel<VEC, OT, false, MINW, REMAP>), grid, dim3(NT), 0,
+                       stream, f1, f2, pyr, g);
   return dxr::launch_status();
 }
 
@@ -1197,20 +1253,23 @@ int launch_build_bf16(bool vec, const uint16_t* f1, const uint16_t* f2, OT* pyr,
   if (grid.y > 65535) return DXR_EINVAL;
   if (!vec) return launch_bf16_w<false, 0>(f1, f2, pyr, g, grid, stream);
   if (build_variant() == 1) return launch_bf16_w<true, 0>(f1, f2, pyr, g, grid, stream);
+  if (build_variant() == 2)
+    return launch_bf16_w<true, 3, OT, true>(f1, f2, pyr, g, remap_grid(g, B), stream);
   return launch_bf16_w<true, 3>(f1, f2, pyr, g, grid, stream);
 }
 
-template <int MINW, typename OT, int ABL = 0>
+template <int MINW, typename OT, int ABL = 0, bool REMAP = false>
 int launch_split(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, int B,
                  hipStream_t stream) {
-  const dim3 grid = build_grid(g, B);
-  if (grid.y > 65535) return DXR_EINVAL;
+  const dim3 grid = REMAP ? remap_grid(g, B) : build_grid(g, B);
+  if (!REMAP && grid.y > 65535) return DXR_EINVAL;
+  if ((long long)B * g.qt * g.tiles_h * g.tiles_w > (1LL << 31) - 1) return DXR_EINVAL;
   if (g.recip == 0.f)
-    hipLaunchKernelGGL((corr_build_split_kernel<OT, true, MINW, ABL>), grid, dim3(NT), 0, stream,
-                       f1, f2, pyr, g);
+    hipLaunchKernelGGL((corr_build_split_kernel<OT, true, MINW, ABL, REMAP>), grid, dim3(NT), 0,
+                       stream, f1, f2, pyr, g);
   else
-    hipLaunchKernelGGL((corr_build_split_kernel<OT, false, MINW, ABL>), grid, dim3(NT), 0, stream,
-                       f1, f2, pyr, g);
+    hipLaunchKernelGGL((corr_build_split_kernel<OT, false, MINW, ABL, REMAP>), grid, dim3(NT), 0,
+                       stream, f1, f2, pyr, g);
   return dxr::launch_status();
 }
 
@@ -1304,6 +1363,9 @@ int launch_build_f32(bool vec, const float* f1, const float* f2, OT* pyr, const 
         break;
       case 92:
         if (glds) return launch_split<4, OT, 2>(f1, f2, pyr, g, B, stream);
+        break;
+      case 40:  // split build, XCD-aware page order
+        if (glds) return launch_split<4, OT, 0, true>(f1, f2, pyr, g, B, stream);
         break;
       case 10:  // f32 MFMA build (glds staging, 4 waves/SIMD)
         if (glds) return launch_f32<true, 16, true, OT, false, 4, true, false>(f1, f2, pyr, g, B, stream);

@@ -326,9 +326,22 @@ def test_bf16_kitti_shape(dx):
     assert np.abs(got - d["out0_val"]).max() <= BF16_RTOL * float(d["out0_maxabs"])
 
 
+@pytest.mark.parametrize("variant", ["1", "2"])
+def test_bf16_build_variants_bit_identical(dx, variant, monkeypatch):
+    """bf16 build variants (occupancy; XCD-aware page order) write the same bits."""
+    f1, f2 = _pair(B=3, H=47, W=100, seed=121, dist="fnet")
+    f1, f2 = f1.bfloat16(), f2.bfloat16()
+    monkeypatch.setenv("DXR_BUILD_VARIANT", "0")
+    ref = dx.CorrBlock(f1, f2).corr_pyramid
+    monkeypatch.setenv("DXR_BUILD_VARIANT", variant)
+    got = dx.CorrBlock(f1, f2).corr_pyramid
+    for lvl, (a, b) in enumerate(zip(got, ref)):
+        assert torch.equal(a, b), f"level {lvl}"
+
+
 # f32-MFMA build variants are checked against variant 2, split-build variants
 # against the default (the split build at 4 waves/SIMD).
-SPLIT_FAMILY = ["7", "8", "9", "11", "12", "13"]
+SPLIT_FAMILY = ["7", "8", "9", "11", "12", "13", "40"]
 
 
 @pytest.mark.parametrize("variant,base", [("1", "2"), ("3", "2"), ("4", "2"), ("5", "2"),
