@@ -1244,8 +1244,9 @@ int launch_bf16_w(const uint16_t* f1, const uint16_t* f2, OT* pyr, const BuildGe
 
 int build_variant();
 
-// bf16 variants: 0 default (3 waves/SIMD; the scalar-staging path keeps the
-// compiler's choice, it would spill at 3); 1 compiler-chosen occupancy.
+// bf16 variants: 0 default (3 waves/SIMD, XCD-aware page order: r01 KITTI b8
+// 721 us vs 837 in grid order; the scalar-staging path keeps the compiler's
+// choice, it would spill at 3); 1 compiler-chosen occupancy; 3 grid order.
 template <typename OT>
 int launch_build_bf16(bool vec, const uint16_t* f1, const uint16_t* f2, OT* pyr,
                       const BuildGeom& g, int B, hipStream_t stream) {
@@ -1253,9 +1254,8 @@ int launch_build_bf16(bool vec, const uint16_t* f1, const uint16_t* f2, OT* pyr,
   if (grid.y > 65535) return DXR_EINVAL;
   if (!vec) return launch_bf16_w<false, 0>(f1, f2, pyr, g, grid, stream);
   if (build_variant() == 1) return launch_bf16_w<true, 0>(f1, f2, pyr, g, grid, stream);
-  if (build_variant() == 2)
-    return launch_bf16_w<true, 3, OT, true>(f1, f2, pyr, g, remap_grid(g, B), stream);
-  return launch_bf16_w<true, 3>(f1, f2, pyr, g, grid, stream);
+  if (build_variant() == 3) return launch_bf16_w<true, 3>(f1, f2, pyr, g, grid, stream);
+  return launch_bf16_w<true, 3, OT, true>(f1, f2, pyr, g, remap_grid(g, B), stream);
 }
 
 template <int MINW, typename OT, int ABL = 0, bool REMAP = false>
