@@ -753,7 +753,9 @@ __device__ __forceinline__ Split3 split3(float a, float b) {
 
 // ABL (timing-only ablations, never the default): 1 skips the epilogue stores,
 // 2 skips the MFMAs.
-template <typename OT, bool DIV, int MINW, int ABL = 0, bool REMAP = false>
+// BV: target staging width in floats — 4 (float4 units; W % 4 == 0) or 2
+// (float2 units; W even, e.g. Chairs' 62-wide fmaps).
+template <typename OT, bool DIV, int MINW, int ABL = 0, bool REMAP = false, int BV = 4>
 __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float* __restrict__ f1,
                                                                     const float* __restrict__ f2,
                                                                     OT* __restrict__ pyr,
@@ -783,14 +785,17 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
   // Padding queries read a clamped, valid address (their outputs are page padding).
   const int qa = min(q0 + wave * 32 + (lane & 31), g.N - 1);
   const float* pa = f1b + (long long)(8 * (lane >> 5)) * g.N + qa;
-  // Target staging: 2 float4 per thread per stage, unit idx -> (k, tile row, col/4).
-  int bk[2], bcol[2];
-  long long boff[2];
-  bool bok[2];
+  // Target staging: NBS units of BV floats per thread per stage,
+  // unit idx -> (k, tile row, col / BV).
+  constexpr int UPR = TW / BV;               // units per tile row
+  constexpr int NBS = BKS * NTGT / BV / NT;  // units per thread
+  int bk[NBS], bcol[NBS];
+  long long boff[NBS];
+  bool bok[NBS];
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
+  for (int s = 0; s < NBS; ++s) {
     const int idx = tid + NT * s;
-    const int k = idx >> 5, r = (idx >> 2) & 7, c = (idx & 3) * 4;
+    const int k = idx / (8 * UPR), r = (idx / UPR) & 7, c = (idx % UPR) * BV;
     bk[s] = k;
     bcol[s] = tgt_col(r, c);
     bok[s] = th0 + r < g.H && tw0 + c < g.W;
@@ -798,15 +803,22 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
   }
 
   float an[8];
-  float4 bn[2];
+  float4 bn[NBS];
   auto load = [&](int k0) {
     const long long ko = (long long)k0 * g.N;
 #pragma unroll
     for (int e = 0; e < 8; ++e) an[e] = pa[ko + (long long)e * g.N];
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
-      bn[s] = bok[s] ? *reinterpret_cast<const float4*>(f2b + ko + boff[s])
-                     : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = 0; s < NBS; ++s) {
+      if constexpr (BV == 4) {
+        bn[s] = bok[s] ? *reinterpret_cast<const float4*>(f2b + ko + boff[s])
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        const float2 v = bok[s] ? *reinterpret_cast<const float2*>(f2b + ko + boff[s])
+                                : make_float2(0.f, 0.f);
+        bn[s] = make_float4(v.x, v.y, 0.f, 0.f);
+      }
+    }
   };
   s8v ah, am, al;   // split query operand of the current stage
   auto split_a = [&]() {
@@ -825,12 +837,19 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
   auto store_b = [&](int buf) {
     uint16_t* P = lh + buf * STAGE_S;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const Split3 x = split3(bn[s].x, bn[s].y), z = split3(bn[s].z, bn[s].w);
+    for (int s = 0; s < NBS; ++s) {
       const int o = bk[s] * PH + bcol[s];
-      *reinterpret_cast<uint2*>(P + o) = make_uint2(x.h, z.h);
-      *reinterpret_cast<uint2*>(P + PLANE_S + o) = make_uint2(x.m, z.m);
-      *reinterpret_cast<uint2*>(P + 2 * PLANE_S + o) = make_uint2(x.l, z.l);
+      const Split3 x = split3(bn[s].x, bn[s].y);
+      if constexpr (BV == 4) {
+        const Split3 z = split3(bn[s].z, bn[s].w);
+        *reinterpret_cast<uint2*>(P + o) = make_uint2(x.h, z.h);
+        *reinterpret_cast<uint2*>(P + PLANE_S + o) = make_uint2(x.m, z.m);
+        *reinterpret_cast<uint2*>(P + 2 * PLANE_S + o) = make_uint2(x.l, z.l);
+      } else {
+        *reinterpret_cast<uint32_t*>(P + o) = x.h;
+        *reinterpret_cast<uint32_t*>(P + PLANE_S + o) = x.m;
+        *reinterpret_cast<uint32_t*>(P + 2 * PLANE_S + o) = x.l;
+      }
     }
   };
 
@@ -1258,18 +1277,18 @@ int launch_build_bf16(bool vec, const uint16_t* f1, const uint16_t* f2, OT* pyr,
   return launch_bf16_w<true, 3, OT, true>(f1, f2, pyr, g, remap_grid(g, B), stream);
 }
 
-template <int MINW, typename OT, int ABL = 0, bool REMAP = false>
+template <int MINW, typename OT, int ABL = 0, bool REMAP = false, int BV = 4>
 int launch_split(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, int B,
                  hipStream_t stream) {
   const dim3 grid = REMAP ? remap_grid(g, B) : build_grid(g, B);
   if (!REMAP && grid.y > 65535) return DXR_EINVAL;
   if ((long long)B * g.qt * g.tiles_h * g.tiles_w > (1LL << 31) - 1) return DXR_EINVAL;
   if (g.recip == 0.f)
-    hipLaunchKernelGGL((corr_build_split_kernel<OT, true, MINW, ABL, REMAP>), grid, dim3(NT), 0,
-                       stream, f1, f2, pyr, g);
+    hipLaunchKernelGGL((corr_build_split_kernel<OT, true, MINW, ABL, REMAP, BV>), grid, dim3(NT),
+                       0, stream, f1, f2, pyr, g);
   else
-    hipLaunchKernelGGL((corr_build_split_kernel<OT, false, MINW, ABL, REMAP>), grid, dim3(NT), 0,
-                       stream, f1, f2, pyr, g);
+    hipLaunchKernelGGL((corr_build_split_kernel<OT, false, MINW, ABL, REMAP, BV>), grid, dim3(NT),
+                       0, stream, f1, f2, pyr, g);
   return dxr::launch_status();
 }
 
@@ -1332,6 +1351,11 @@ int launch_build_f32(bool vec, const float* f1, const float* f2, OT* pyr, const 
       if (v == 115) return launch_presplit<2, 3, OT, 5>(f1, f2, ws, pyr, g, B, stream);  // timing
       if (v == 125) return launch_presplit<3, 2, OT, 5>(f1, f2, ws, pyr, g, B, stream);  // timing
     }
+  }
+  if constexpr (PAGED) {
+    // W even but not a multiple of 4 (Chairs: 62): the split build on float2 target units
+    if (!vec && g.D % 16 == 0 && g.W % 2 == 0 && build_variant() != 2 && ((uintptr_t)f2 % 8) == 0)
+      return launch_split<4, OT, 0, false, 2>(f1, f2, pyr, g, B, stream);
   }
   if (!vec) return launch_f32<false, 16, PAGED, OT, false, 0, false, false>(f1, f2, pyr, g, B, stream);
   if constexpr (PAGED) {

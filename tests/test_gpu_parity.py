@@ -546,6 +546,25 @@ def test_backward_of_static_corr(dx):
         assert (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
 
 
+def test_split_build_even_width_not_multiple_of_4(dx, monkeypatch):
+    """Chairs' 62-wide fmaps take the split build with float2 target units: f32
+    class against the float64 oracle, and no worse than the exact-f32 MFMA build."""
+    H, W = 46, 62
+    f1 = dg.fmap(61, 1, 256, H, W, "fnet")
+    f2 = dg.fmap(62, 1, 256, H, W, "fnet")
+    pyr = oracle.corr_pyramid(f1, f2, 4, np.float64)
+    monkeypatch.setenv("DXR_BUILD_VARIANT", "2")            # exact-f32 MFMA build
+    base = dx.CorrBlock(_t(f1), _t(f2)).corr_pyramid
+    monkeypatch.setenv("DXR_BUILD_VARIANT", "0")
+    cb = dx.CorrBlock(_t(f1), _t(f2))
+    for lvl in range(4):
+        got = cb.corr_pyramid[lvl][:, 0].cpu().numpy()
+        tolerance_check(got, pyr[lvl], RTOL)
+        e_split = np.abs(got - pyr[lvl]).max()
+        e_mfma = np.abs(base[lvl][:, 0].cpu().numpy() - pyr[lvl]).max()
+        assert e_split <= 2 * e_mfma + 1e-6
+
+
 def test_backward_only_flows_to_fmaps_that_require_grad(dx):
     f1, f2 = _pair(B=1, D=32, H=12, W=16, seed=351)
     a1 = f1.clone().requires_grad_(True)
