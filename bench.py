@@ -87,7 +87,7 @@ def build_kernel(dtype, H, W):
     variant = os.environ.get("DXR_BUILD_VARIANT", "0")
     if dtype == "bf16":
         return "corr_build_bf16_kernel", 1, PEAK_BF16_TFLOPS, "bf16"
-    if D % 16 == 0 and W % 4 == 0 and variant in ("0", "7", "8", "9"):
+    if D % 16 == 0 and W % 2 == 0 and variant in ("0", "7", "8", "9", "40"):
         return ("corr_build_split_kernel (f32 operands split exactly into 3 bf16, "
                 "bf16x6 MFMA, f32 accumulate)", 6, PEAK_BF16_TFLOPS, "bf16 MFMA, f32 accumulate")
     return "corr_build_f32_kernel", 1, PEAK_F32_TFLOPS, "f32"

@@ -440,13 +440,19 @@ def test_radius_and_levels_variants(dx):
         tolerance_check(got, ref, RTOL)
 
 
-def test_grad_inputs_raise(dx):
+def test_grad_inputs_without_a_backward_raise(dx):
+    """Autograd is supported for f32 CorrBlock only (§3.5): bf16 fmaps and the
+    alternate block raise loudly when their inputs require grad."""
     f1, f2 = _pair(H=16, W=16, seed=98)
     f1.requires_grad_(True)
+    dx.CorrBlock(f1, f2)                                    # differentiable
     with pytest.raises(NotImplementedError):
-        dx.CorrBlock(f1, f2)
+        dx.CorrBlock(f1.bfloat16(), f2.bfloat16())
+    with pytest.raises(NotImplementedError):
+        dx.AlternateCorrBlock(f1, f2, num_levels=3)
     with torch.no_grad():
-        dx.CorrBlock(f1, f2)
+        dx.CorrBlock(f1.bfloat16(), f2.bfloat16())
+        dx.AlternateCorrBlock(f1, f2, num_levels=3)
 
 
 def test_bad_coords_shape_raises(dx):
