@@ -912,271 +912,6 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
 }
 
 // ---------------------------------------------------------------------------
-// Warp-specialised split build ("ws"): persistent workgroups of 8 waves, one per
-// CU.  Waves 0-3 run the split build's K loop for page i (the same operands,
-// splits, MFMA order and pooling, so the same bits); at the end of the page they
-// hand the scaled accumulators and the pooled levels over through LDS, laid out
-// as the page will sit in HBM.  Waves 4-7 stream that hand-off buffer to HBM in
-// 16 slices, one per k step of page i+1, under the same barriers — the pyramid
-// writes (the split build's 42 us epilogue at Sintel, which its four in-phase
-// workgroups per CU cannot overlap with MFMA work) run behind the next page's
-// MFMAs.  Pages are taken in the XCD-aware strip order of page_coord: each XCD
-// walks a contiguous range, its 32 resident pages sharing ~12 operand panels.
-// ---------------------------------------------------------------------------
-constexpr int WS_RING = 2 * STAGE_S * 2;             // bytes: two stages of B planes
-constexpr int WS_L0 = BM * P0;                       // floats: [q][132]
-constexpr int WS_L1 = BM * P1;                       // floats: [q][36]
-constexpr int WS_L2 = BM * 8;                        // floats: [q][2][4]
-constexpr int WS_L3 = BM * 2;                        // floats: [q][2]
-constexpr int WS_LDS = WS_RING + 4 * (WS_L0 + WS_L1 + WS_L2 + WS_L3);
-
-// linear strip-order page index -> page coordinates (see page_coord)
-__device__ __forceinline__ PageCoord strip_page(const BuildGeom& g, long long wl) {
-  PageCoord c;
-  const int T = g.tiles_w * g.tiles_h;
-  const long long per_pair = (long long)g.qt * T;
-  c.b = (int)(wl / per_pair);
-  const long long rem = wl - c.b * per_pair;
-  const int nfull = T / STRIP;
-  int tile;
-  if (rem < (long long)nfull * g.qt * STRIP) {
-    const int st = (int)(rem / ((long long)g.qt * STRIP));
-    const int in = (int)(rem - (long long)st * g.qt * STRIP);
-    c.qblk = in / STRIP;
-    tile = st * STRIP + in % STRIP;
-  } else {
-    const int nl = T - nfull * STRIP;
-    const int in = (int)(rem - (long long)nfull * g.qt * STRIP);
-    c.qblk = in / nl;
-    tile = nfull * STRIP + in % nl;
-  }
-  c.txi = tile % g.tiles_w;
-  c.tyi = tile / g.tiles_w;
-  c.page = (((long long)c.b * g.qt + c.qblk) * g.tiles_h + c.tyi) * g.tiles_w + c.txi;
-  return c;
-}
-
-template <bool DIV>
-__global__ __launch_bounds__(512, 1) void corr_build_ws_kernel(const float* __restrict__ f1,
-                                                               const float* __restrict__ f2,
-                                                               float* __restrict__ pyr,
-                                                               BuildGeom g, long long npages) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[WS_LDS];
-  uint16_t* lh = reinterpret_cast<uint16_t*>(smem);
-  float* L0 = reinterpret_cast<float*>(smem + WS_RING);
-  float* L1 = L0 + WS_L0;
-  float* L2 = L1 + WS_L1;
-  float* L3 = L2 + WS_L2;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bool compute = wave < WAVES;
-  const int ct = tid & (NT - 1);            // thread index within its half
-  const int j = lane & 31, h = lane >> 5;
-
-  // this workgroup's pages: a contiguous slice of its XCD's range of the strip order
-  const long long G = gridDim.x;
-  const long long xcd = blockIdx.x % 8, local = blockIdx.x / 8;
-  const long long ng8 = G / 8 + (xcd < G % 8 ? 1 : 0);         // workgroups on this XCD
-  const long long q8 = npages / 8, r8 = npages % 8;
-  const long long xs = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
-  const long long xn = q8 + (xcd < r8 ? 1 : 0);
-
-  const int li = lane & 15;
-  const int rd_off = (li >> 2) * PH + 4 * (li & 3) + 16 * ((lane >> 4) & 1) + 8 * (lane >> 5) * PH;
-  auto frag = [&](const uint16_t* p) {
-    return __builtin_bit_cast(bf8v, __builtin_shufflevector(tr_read(p), tr_read(p + 4 * PH), 0, 1,
-                                                            2, 3, 4, 5, 6, 7));
-  };
-  const int nk = g.D / BKS;
-
-  long long prev = -1;                      // page held in the hand-off buffer
-  for (long long it = 0;; ++it) {
-    const long long li_ = local + it * ng8;
-    const bool have = li_ < xn;
-    if (!have && prev < 0) break;           // uniform over the workgroup
-    PageCoord pc;
-    pc.page = 0; pc.txi = pc.tyi = pc.qblk = pc.b = 0;
-    if (have) pc = strip_page(g, xs + li_);
-
-    // ---- compute-wave state (the split build's K loop)
-    f32x16 acc[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-    const int th0 = pc.tyi * TH, tw0 = pc.txi * TW;
-    const int q0 = pc.qblk * BM;
-    const long long fstride = (long long)g.D * g.N;
-    const float* f1b = f1 + pc.b * fstride;
-    const float* f2b = f2 + pc.b * fstride;
-    const int qa = min(q0 + wave * 32 + j, g.N - 1);
-    const float* pa = f1b + (long long)(8 * h) * g.N + qa;
-    int bk[2], bcol[2];
-    long long boff[2];
-    bool bok[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int idx = ct + NT * s;
-      const int k = idx >> 5, r = (idx >> 2) & 7, c = (idx & 3) * 4;
-      bk[s] = k;
-      bcol[s] = tgt_col(r, c);
-      bok[s] = th0 + r < g.H && tw0 + c < g.W;
-      boff[s] = (long long)k * g.N + (long long)(th0 + r) * g.W + tw0 + c;
-    }
-    float an[8];
-    float4 bn[2];
-    auto load = [&](int k0) {
-      const long long ko = (long long)k0 * g.N;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) an[e] = pa[ko + (long long)e * g.N];
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-        bn[s] = bok[s] ? *reinterpret_cast<const float4*>(f2b + ko + boff[s])
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
-    };
-    s8v ah, am, al;
-    auto split_a = [&]() {
-      uint32_t hh[4], mm[4], ll[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const Split3 x = split3(an[2 * e], an[2 * e + 1]);
-        hh[e] = x.h; mm[e] = x.m; ll[e] = x.l;
-      }
-      ah = __builtin_bit_cast(s8v, make_uint4(hh[0], hh[1], hh[2], hh[3]));
-      am = __builtin_bit_cast(s8v, make_uint4(mm[0], mm[1], mm[2], mm[3]));
-      al = __builtin_bit_cast(s8v, make_uint4(ll[0], ll[1], ll[2], ll[3]));
-    };
-    auto store_b = [&](int buf) {
-      uint16_t* P = lh + buf * STAGE_S;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const Split3 x = split3(bn[s].x, bn[s].y), z = split3(bn[s].z, bn[s].w);
-        const int o = bk[s] * PH + bcol[s];
-        *reinterpret_cast<uint2*>(P + o) = make_uint2(x.h, z.h);
-        *reinterpret_cast<uint2*>(P + PLANE_S + o) = make_uint2(x.m, z.m);
-        *reinterpret_cast<uint2*>(P + 2 * PLANE_S + o) = make_uint2(x.l, z.l);
-      }
-    };
-
-    // ---- store-wave state: the previous page's addresses
-    PageCoord pp;
-    pp.page = 0;
-    if (prev >= 0) pp = strip_page(g, prev);
-    const int sw = wave - WAVES;            // store wave 0..3
-    auto stream = [&](int ks) {
-      // level 0: queries 8 ks .. 8 ks + 7, 512 B each: lane -> (query, 16 B)
-      {
-        const int qq = 8 * ks + 2 * sw + h;
-        const int off = j * 4;
-        float* dst = pyr + g.loff[0] + pp.page * (BM * NTGT) + (long long)qq * NTGT + off;
-        *reinterpret_cast<float4*>(dst) = f4(L0 + qq * P0 + off);
-      }
-      if (g.levels >= 2 && ks < 4) {        // level 1: 32 queries x 128 B per slice
-        const int qq = 32 * ks + 8 * sw + (lane >> 3);
-        const int off = (lane & 7) * 4;
-        float* dst = pyr + g.loff[1] + pp.page * (BM * NTGT / 4) + (long long)qq * 32 + off;
-        *reinterpret_cast<float4*>(dst) = f4(L1 + qq * P1 + off);
-      }
-      if (g.levels >= 3 && ks == 4) {       // level 2: 4 KiB
-        float* dst = pyr + g.loff[2] + pp.page * (BM * NTGT / 16) + (sw * 64 + lane) * 4;
-        *reinterpret_cast<float4*>(dst) = f4(L2 + (sw * 64 + lane) * 4);
-      }
-      if (g.levels >= 4 && ks == 5 && sw == 0) {   // level 3: 1 KiB
-        float* dst = pyr + g.loff[3] + pp.page * (BM * 2) + lane * 4;
-        *reinterpret_cast<float4*>(dst) = f4(L3 + lane * 4);
-      }
-    };
-
-    if (compute && have) {
-      load(0);
-      store_b(0);
-      split_a();
-    }
-    __syncthreads();
-    for (int ks = 0; ks < nk; ++ks) {
-      if (compute) {
-        if (have) {
-          const int buf = ks & 1;
-          if (ks + 1 < nk) load((ks + 1) * BKS);
-          const bf8v qh = __builtin_bit_cast(bf8v, ah), qm = __builtin_bit_cast(bf8v, am),
-                     ql = __builtin_bit_cast(bf8v, al);
-          const uint16_t* P = lh + buf * STAGE_S + rd_off;
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const bf8v th = frag(P + t * 32), tm = frag(P + PLANE_S + t * 32),
-                       tl = frag(P + 2 * PLANE_S + t * 32);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm, acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh, acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, ql, acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qh, acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qm, acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh, acc[t], 0, 0, 0);
-          }
-          if (ks + 1 < nk) {
-            store_b(buf ^ 1);
-            split_a();
-          }
-        }
-      } else if (prev >= 0 && ks < 16) {
-        stream(ks);
-      }
-      __syncthreads();
-    }
-    if (!compute && prev >= 0)              // K shorter than 16 steps: finish the slices
-      for (int ks = nk; ks < 16; ++ks) stream(ks);
-
-    // ---- hand-off: compute waves write page `it` into LDS in page layout
-    __syncthreads();                        // store waves are done with the buffer
-    if (compute && have) {
-      scale_acc<DIV>(acc, g);
-      float* w0 = L0 + (wave * 32 + j) * P0 + h * TW;
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int c4 = 0; c4 < 4; ++c4)
-          st4(w0 + 2 * t * TW + 4 * c4, acc[t][4 * c4], acc[t][4 * c4 + 1], acc[t][4 * c4 + 2],
-              acc[t][4 * c4 + 3]);
-      if (g.levels >= 2) {
-        float l2[2][4];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          float l1[2][8];
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const int t = 2 * u + s;
-#pragma unroll
-            for (int m = 0; m < 8; ++m) {
-              const float o0 = acc[t][2 * m], o1 = acc[t][2 * m + 1];
-              const float p0 = __shfl_xor(o0, 32), p1 = __shfl_xor(o1, 32);
-              const float t0 = h ? p0 : o0, t1 = h ? p1 : o1;
-              const float b0 = h ? o0 : p0, b1 = h ? o1 : p1;
-              l1[s][m] = (((t0 + t1) + b0) + b1) * 0.25f;
-            }
-            st4(L1 + (wave * 32 + j) * P1 + t * 8 + 4 * h, l1[s][4 * h], l1[s][4 * h + 1],
-                l1[s][4 * h + 2], l1[s][4 * h + 3]);
-          }
-#pragma unroll
-          for (int n = 0; n < 4; ++n)
-            l2[u][n] =
-                (((l1[0][2 * n] + l1[0][2 * n + 1]) + l1[1][2 * n]) + l1[1][2 * n + 1]) * 0.25f;
-        }
-        if (g.levels >= 3)
-          st4(L2 + (wave * 32 + j) * 8 + 4 * h, l2[h][0], l2[h][1], l2[h][2], l2[h][3]);
-        if (g.levels >= 4) {
-          float l3[2];
-#pragma unroll
-          for (int v = 0; v < 2; ++v)
-            l3[v] = (((l2[0][2 * v] + l2[0][2 * v + 1]) + l2[1][2 * v]) + l2[1][2 * v + 1]) * 0.25f;
-          L3[(wave * 32 + j) * 2 + h] = l3[h];
-        }
-      }
-    }
-    __syncthreads();
-    prev = have ? xs + li_ : -1;
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Pre-split f32 build ("presplit", DXR_BUILD_VARIANT 11-14; not the default).
 // The same exact hi+mid+lo operand split and the same six bf16 MFMA products as
 // the split build above, but the split is done ONCE per fmap element by
@@ -1557,20 +1292,6 @@ int launch_split(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, 
   return dxr::launch_status();
 }
 
-int launch_ws(const float* f1, const float* f2, float* pyr, const BuildGeom& g, int B,
-              hipStream_t stream) {
-  const long long npages = (long long)B * g.qt * g.tiles_h * g.tiles_w;
-  const long long cap = resident_build_groups(1);
-  const unsigned groups = (unsigned)(npages < cap ? npages : cap);
-  if (g.recip == 0.f)
-    hipLaunchKernelGGL((corr_build_ws_kernel<true>), dim3(groups), dim3(2 * NT), 0, stream, f1,
-                       f2, pyr, g, npages);
-  else
-    hipLaunchKernelGGL((corr_build_ws_kernel<false>), dim3(groups), dim3(2 * NT), 0, stream, f1,
-                       f2, pyr, g, npages);
-  return dxr::launch_status();
-}
-
 // Workspace of the presplit build: hi/mid/lo bf16 planes of both fmaps.
 long long presplit_ws_bytes(long long B, long long D, long long N) {
   return 2LL * B * 3 * D * N * 2;
@@ -1666,10 +1387,6 @@ int launch_build_f32(bool vec, const float* f1, const float* f2, OT* pyr, const 
         break;
       case 92:
         if (glds) return launch_split<4, OT, 2>(f1, f2, pyr, g, B, stream);
-        break;
-      case 50:  // warp-specialised split build (persistent, hand-off through LDS)
-        if constexpr (sizeof(OT) == 4)
-          if (glds) return launch_ws(f1, f2, reinterpret_cast<float*>(pyr), g, B, stream);
         break;
       case 40:  // split build, XCD-aware page order
         if (glds) return launch_split<4, OT, 0, true>(f1, f2, pyr, g, B, stream);

@@ -18,7 +18,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import bench  # noqa: E402  (workload table, algorithmic byte/flop formulas)
 import dexiraft_amd  # noqa: E402
 
-SPLIT_VARIANTS = {0, 7, 8, 9, 11, 12, 13, 40, 50}  # f32 builds on bf16 MFMA (exact operand split); D % 16 == 0
+SPLIT_VARIANTS = {0, 7, 8, 9, 11, 12, 13, 40}  # f32 builds on bf16 MFMA (exact operand split); D % 16 == 0
 
 
 def main():
