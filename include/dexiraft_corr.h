@@ -26,6 +26,8 @@
  *                            in AlternateCorrBlock.__init__
  *   dxr_alt_corr_forward     alt_cuda_corr/correlation.cpp:23-33 `forward`
  *                            (alt_cuda_corr/correlation_kernel.cu:260-286)
+ *   dxr_alt_corr_backward    alt_cuda_corr/correlation.cpp:36-48 `backward`
+ *                            (alt_cuda_corr/correlation_kernel.cu:288-320)
  *   dxr_alt_corr_lookup      core/corr.py:74-91  AlternateCorrBlock.__call__
  *                            (all levels in one launch, / sqrt(D) fused)
  *
@@ -195,6 +197,24 @@ int dxr_alt_corr_forward(const float* fmap1, const float* fmap2,
                          int64_t B, int64_t H1, int64_t W1, int64_t H2,
                          int64_t W2, int64_t C, int64_t Nc, int radius,
                          hipStream_t stream);
+
+/*
+ * Stage (d), reference-FFI backward: alt_cuda_corr.backward(fmap1, fmap2, coords,
+ * corr_grad, radius) (correlation.cpp:36-48, correlation_kernel.cu:122-256,288-320).
+ *   corr_grad  : [B, Nc, (2r+1)^2, H1, W1] float32 (the forward's output layout)
+ *   fmap1_grad : [B, H1, W1, C]  fully overwritten
+ *   fmap2_grad : [B, H2, W2, C]  zero-filled on `stream`, then accumulated with
+ *                atomics (summation order, hence the last bits, is not fixed —
+ *                as in the reference)
+ * The reference's third output, coords_grad, is identically zero; the caller
+ * allocates it.  Radius 0..6.
+ */
+int dxr_alt_corr_backward(const float* fmap1, const float* fmap2,
+                          const float* coords, const float* corr_grad,
+                          float* fmap1_grad, float* fmap2_grad,
+                          int64_t B, int64_t H1, int64_t W1, int64_t H2,
+                          int64_t W2, int64_t C, int64_t Nc, int radius,
+                          hipStream_t stream);
 
 /*
  * Stage (d), fused form used by AlternateCorrBlock.__call__: every level in one

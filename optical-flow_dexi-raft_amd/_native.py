@@ -43,6 +43,8 @@ SIGNATURES: dict[str, tuple[object, list[object]]] = {
     "dxr_pyramid_backward": (_int, [_vp, _int, _i64, _i64, _i64, _int, _f32, _vp, _vp]),
     "dxr_alt_corr_forward": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64,
                                     _i64, _int, _vp]),
+    "dxr_alt_corr_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64,
+                                     _i64, _i64, _i64, _int, _vp]),
     "dxr_alt_corr_lookup": (_int, [_vp, ctypes.POINTER(_vp), _vp, _vp, _i64, _i64, _i64, _i64,
                                    _int, _int, _f32, _vp]),
 }

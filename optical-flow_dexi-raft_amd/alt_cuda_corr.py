@@ -1,7 +1,8 @@
 """Drop-in for the reference's pybind module ``alt_cuda_corr``.
 
 Mirrors alt_cuda_corr/correlation.cpp:23-54: ``forward(fmap1, fmap2, coords,
-radius) -> [corr]`` with fmap1 ``[B, H1, W1, C]``, fmap2 ``[B, H2, W2, C]``,
+radius) -> [corr]`` and ``backward(fmap1, fmap2, coords, corr_grad, radius) ->
+[fmap1_grad, fmap2_grad, coords_grad]`` with fmap1 ``[B, H1, W1, C]``, fmap2 ``[B, H2, W2, C]``,
 coords ``[B, N, H1, W1, 2]`` (all float32, contiguous, on the device) and
 ``corr`` ``[B, N, (2r+1)^2, H1, W1]``, channel ``iy + (2r+1)*ix``.  Argument
 errors raise ``RuntimeError`` like the reference's ``TORCH_CHECK``
@@ -48,11 +49,38 @@ def forward(fmap1: torch.Tensor, fmap2: torch.Tensor, coords: torch.Tensor, radi
     return [corr]
 
 
-def backward(fmap1, fmap2, coords, corr_grad, radius):
-    """alt_cuda_corr.backward (correlation.cpp:36-48) — not yet native.
+def backward(fmap1: torch.Tensor, fmap2: torch.Tensor, coords: torch.Tensor,
+             corr_grad: torch.Tensor, radius: int):
+    """alt_cuda_corr.backward (correlation.cpp:36-48, correlation_kernel.cu:122-256,288-320).
 
-    The reference never reaches it (core/corr.py wraps no autograd.Function) and
-    it leaves coords_grad zero (correlation_kernel.cu:307).  Raising here keeps
-    the failure loud rather than returning wrong gradients.
+    Returns ``[fmap1_grad, fmap2_grad, coords_grad]``; coords_grad is zero, as in
+    the reference (correlation_kernel.cu:307).  fmap2_grad is accumulated with
+    atomics, so its last bits depend on the summation order (also as in the
+    reference).  The reference's core/corr.py never calls it (AlternateCorrBlock
+    wraps no autograd.Function); this is the FFI surface only.
     """
-    raise NotImplementedError("alt_cuda_corr.backward is not implemented in dexiraft_amd yet")
+    for t, n in ((fmap1, "fmap1"), (fmap2, "fmap2"), (coords, "coords"),
+                 (corr_grad, "corr_grad")):
+        _check_input(t, n)
+    if fmap1.dim() != 4 or fmap2.dim() != 4 or coords.dim() != 5 or coords.shape[-1] != 2:
+        raise RuntimeError("expected fmap1 [B,H1,W1,C], fmap2 [B,H2,W2,C], coords [B,N,H1,W1,2]")
+    B, H1, W1, C = (int(s) for s in fmap1.shape)
+    B2, H2, W2, C2 = (int(s) for s in fmap2.shape)
+    Bc, N, Hc, Wc, _ = (int(s) for s in coords.shape)
+    if B2 != B or C2 != C or Bc != B or (Hc, Wc) != (H1, W1):
+        raise RuntimeError("fmap1 / fmap2 / coords shapes are inconsistent")
+    rd = 2 * int(radius) + 1
+    if tuple(corr_grad.shape) != (B, N, rd * rd, H1, W1):
+        raise RuntimeError(f"corr_grad must be [B, N, (2r+1)^2, H1, W1] = "
+                           f"{[B, N, rd * rd, H1, W1]}, got {list(corr_grad.shape)}")
+    fmap1_grad = torch.empty_like(fmap1)
+    fmap2_grad = torch.empty_like(fmap2)
+    coords_grad = torch.zeros_like(coords)
+    lib = nat.load()
+    with torch.cuda.device(fmap1.device):
+        st = lib.dxr_alt_corr_backward(fmap1.data_ptr(), fmap2.data_ptr(), coords.data_ptr(),
+                                       corr_grad.data_ptr(), fmap1_grad.data_ptr(),
+                                       fmap2_grad.data_ptr(), B, H1, W1, H2, W2, C, N,
+                                       int(radius), nat.stream_of(fmap1))
+    nat.check(st, "alt_cuda_corr.backward (dxr_alt_corr_backward)")
+    return [fmap1_grad, fmap2_grad, coords_grad]

@@ -460,6 +460,110 @@ int launch_alt(const float* f1, const float* coords, float* out, const AltGeom& 
 
 bool aligned16(const void* p) { return ((uintptr_t)p % 16) == 0; }
 
+// ---------------------------------------------------------------------------
+// alt_cuda_corr.backward, reference-FFI form (correlation_kernel.cu:122-256,
+// launched by :288-320).  For query q of pair b and coordinate set n, cell
+// (iy, ix) in [0, 2r+1]^2 — (h2, w2) = (floor(y) - r + iy, floor(x) - r + ix) —
+// receives the transpose of the forward's bilinear scatter (:197-216):
+//   g = [iy>0, ix>0]  G(iy-1, ix-1) dy dx   + [iy>0, ix<rd]  G(iy-1, ix) dy (1-dx)
+//     + [iy<rd, ix>0] G(iy, ix-1) (1-dy) dx + [iy<rd, ix<rd] G(iy, ix) (1-dy)(1-dx)
+// with G(oy, ox) = corr_grad[b][n][oy + rd*ox][q]; every in-bounds cell then adds
+// g * fmap2[cell] to fmap1_grad[q] and g * fmap1[q] to fmap2_grad[cell]
+// (:218-233; atomics there too).  coords_grad is zero (:307).
+//
+// MI355X mapping: one wave per query pixel.  Lane L owns channels c0 + L + 64j
+// (j < 4) of a 256-channel slab, so each fmap2[cell] read is four 256-byte
+// coalesced dword loads and each fmap2_grad update four 256-byte hardware
+// global_atomic_add_f32 (full rate on contiguous lines).  The (2r+1)^2 weights of
+// the query are loaded once across the lanes and broadcast per cell with
+// v_readlane (the cell loops are unrolled, so the lane index is a constant).
+// fmap1_grad[q] is owned by the wave: written once per slab, no atomics.
+template <int R>
+__global__ __launch_bounds__(256) void alt_corr_backward_kernel(
+    const float* __restrict__ f1, const float* __restrict__ f2, const float* __restrict__ coords,
+    const float* __restrict__ cgrad, float* __restrict__ f1g, float* __restrict__ f2g, int N,
+    int H2, int W2, int C, int Nc) {
+  constexpr int RD = 2 * R + 1, RR = RD * RD, NG = (RR + 63) / 64;
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  const int b = blockIdx.y;
+  if (q >= N) return;  // whole wave; the kernel has no block barrier
+  const float* f1q = f1 + ((long long)b * N + q) * C;
+  float* f1gq = f1g + ((long long)b * N + q) * C;
+  const float* f2b = f2 + (long long)b * H2 * W2 * C;
+  float* f2gb = f2g + (long long)b * H2 * W2 * C;
+  for (int c0 = 0; c0 < C; c0 += 256) {
+    float a[4], acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + lane + 64 * j;
+      a[j] = c < C ? f1q[c] : 0.f;
+      acc[j] = 0.f;
+    }
+    for (int n = 0; n < Nc; ++n) {
+      const long long z = (long long)b * Nc + n;
+      const float x = coords[(z * N + q) * 2], y = coords[(z * N + q) * 2 + 1];
+      const float fx = floorf(x), fy = floorf(y);
+      const float dx = x - fx, dy = y - fy;
+      const int x0 = (int)fx - R, y0 = (int)fy - R;
+      int gv[NG];
+#pragma unroll
+      for (int k = 0; k < NG; ++k) {
+        const int i = lane + 64 * k;
+        gv[k] = i < RR ? __float_as_int(cgrad[(z * RR + i) * N + q]) : 0;
+      }
+      auto G = [&](int oy, int ox) {
+        const int i = oy + RD * ox;
+        return __int_as_float(__builtin_amdgcn_readlane(gv[i / 64], i % 64));
+      };
+#pragma unroll
+      for (int iy = 0; iy <= RD; ++iy) {
+        const int h2 = y0 + iy;
+        if (h2 < 0 || h2 >= H2) continue;
+#pragma unroll
+        for (int ix = 0; ix <= RD; ++ix) {
+          const int w2 = x0 + ix;
+          if (w2 < 0 || w2 >= W2) continue;
+          float g = 0.f;
+          if (iy > 0 && ix > 0) g += G(iy - 1, ix - 1) * dy * dx;
+          if (iy > 0 && ix < RD) g += G(iy - 1, ix) * dy * (1.f - dx);
+          if (iy < RD && ix > 0) g += G(iy, ix - 1) * (1.f - dy) * dx;
+          if (iy < RD && ix < RD) g += G(iy, ix) * (1.f - dy) * (1.f - dx);
+          const long long cell = ((long long)h2 * W2 + w2) * C;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int c = c0 + lane + 64 * j;
+            if (c < C) {
+              acc[j] += g * f2b[cell + c];
+              unsafeAtomicAdd(f2gb + cell + c, g * a[j]);
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + lane + 64 * j;
+      if (c < C) f1gq[c] = acc[j];
+    }
+  }
+}
+
+struct AltBwd {
+  const float *f1, *f2, *coords, *cgrad;
+  float *f1g, *f2g;
+  int B, N, H2, W2, C, Nc;
+};
+
+template <int R>
+int launch_alt_backward_r(const AltBwd& a, hipStream_t stream) {
+  const dim3 grid((unsigned)((a.N + 3) / 4), (unsigned)a.B);
+  hipLaunchKernelGGL((alt_corr_backward_kernel<R>), grid, dim3(256), 0, stream, a.f1, a.f2,
+                     a.coords, a.cgrad, a.f1g, a.f2g, a.N, a.H2, a.W2, a.C, a.Nc);
+  return dxr::launch_status();
+}
+
+
 }  // namespace
 
 extern "C" int dxr_alt_corr_forward(const float* fmap1, const float* fmap2, const float* coords,
@@ -487,6 +591,38 @@ extern "C" int dxr_alt_corr_forward(const float* fmap1, const float* fmap2, cons
   g.lv[0] = AltLevel{fmap2, (int)H2, (int)W2, 1.f, 0};
   const bool vec = (C % 4 == 0) && aligned16(fmap1) && aligned16(fmap2);
   return launch_alt(fmap1, coords, corr, g, 1, (int)(B * Nc), radius, vec, stream, (int)W1);
+}
+
+extern "C" int dxr_alt_corr_backward(const float* fmap1, const float* fmap2, const float* coords,
+                                     const float* corr_grad, float* fmap1_grad,
+                                     float* fmap2_grad, int64_t B, int64_t H1, int64_t W1,
+                                     int64_t H2, int64_t W2, int64_t C, int64_t Nc, int radius,
+                                     hipStream_t stream) {
+  if (B < 0 || H1 < 1 || W1 < 1 || H2 < 1 || W2 < 1 || C < 1 || Nc < 0 || radius < 0)
+    return DXR_EINVAL;
+  if (radius > 6) return DXR_EUNSUPPORTED;
+  if (H1 * W1 > (1LL << 30) || H2 * W2 > (1LL << 30) || B > 65535 || C > (1 << 20))
+    return DXR_EINVAL;
+  if (B == 0) return DXR_OK;
+  if (!fmap1 || !fmap2 || !fmap1_grad || !fmap2_grad) return DXR_EINVAL;
+  if (Nc > 0 && (!coords || !corr_grad)) return DXR_EINVAL;
+  // fmap2_grad accumulates atomically from zero, as the reference's torch::zeros output.
+  hipError_t e = hipMemsetAsync(fmap2_grad, 0, (size_t)(B * H2 * W2 * C) * sizeof(float), stream);
+  if (e != hipSuccess) {
+    dxr::set_last_hip_error(e);
+    return DXR_EHIP;
+  }
+  const AltBwd a{fmap1, fmap2, coords, corr_grad, fmap1_grad, fmap2_grad, (int)B,
+                 (int)(H1 * W1), (int)H2, (int)W2, (int)C, (int)Nc};
+  switch (radius) {
+    case 0: return launch_alt_backward_r<0>(a, stream);
+    case 1: return launch_alt_backward_r<1>(a, stream);
+    case 2: return launch_alt_backward_r<2>(a, stream);
+    case 3: return launch_alt_backward_r<3>(a, stream);
+    case 4: return launch_alt_backward_r<4>(a, stream);
+    case 5: return launch_alt_backward_r<5>(a, stream);
+    default: return launch_alt_backward_r<6>(a, stream);
+  }
 }
 
 extern "C" int dxr_alt_corr_lookup(const float* fmap1, const float* const* fmap2_levels,

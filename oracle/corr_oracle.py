@@ -194,6 +194,58 @@ def alt_corr_forward(fmap1: np.ndarray, fmap2: np.ndarray, coords: np.ndarray, r
     return out.reshape(B, N, rd * rd, H1, W1)
 
 
+def alt_corr_backward(fmap1: np.ndarray, fmap2: np.ndarray, coords: np.ndarray,
+                      corr_grad: np.ndarray, radius: int, dtype=np.float64):
+    """alt_cuda_corr.backward, alt_cuda_corr/correlation_kernel.cu:122-256 + :288-320.
+
+    ``corr_grad``: [B, N, (2r+1)^2, H1, W1].  Returns (fmap1_grad [B, H1, W1, C],
+    fmap2_grad [B, H2, W2, C], coords_grad = zeros [B, N, H1, W1, 2] (:307)).
+    Cell (iy, ix) of a query's (2r+2)^2 window gets g = the corr_grad taps of the
+    up-to-four outputs it feeds, weighted dy*dx, dy*(1-dx), (1-dy)*dx,
+    (1-dy)*(1-dx) (:197-216, output index oy + rd*ox); in-bounds cells add
+    g*fmap2[cell] to fmap1_grad[q] and g*fmap1[q] to fmap2_grad[cell] (:218-233).
+    It is the adjoint of alt_corr_forward in fmap1 and in fmap2
+    (tests/test_oracle_golden.py checks that identity).
+    """
+    B, H1, W1, C = fmap1.shape
+    _, H2, W2, _ = fmap2.shape
+    N = coords.shape[1]
+    Q = H1 * W1
+    rd = 2 * radius + 1
+    f1 = fmap1.astype(dtype).reshape(B, Q, C)
+    f2 = fmap2.astype(dtype)
+    G = np.asarray(corr_grad).astype(dtype).reshape(B, N, rd * rd, Q)
+    c = np.asarray(coords, dtype=F32).reshape(B, N, Q, 2)
+    x0, y0 = np.floor(c[..., 0]), np.floor(c[..., 1])
+    dx, dy = (c[..., 0] - x0).astype(dtype), (c[..., 1] - y0).astype(dtype)
+    x0i, y0i = x0.astype(np.int64), y0.astype(np.int64)
+    bidx = np.arange(B)[:, None, None]
+    f1g = np.zeros((B, Q, C), dtype=dtype)
+    f2g = np.zeros((B, H2, W2, C), dtype=dtype)
+    for iy in range(rd + 1):
+        for ix in range(rd + 1):
+            g = np.zeros((B, N, Q), dtype=dtype)
+            if iy > 0 and ix > 0:
+                g += G[:, :, (iy - 1) + rd * (ix - 1)] * dy * dx
+            if iy > 0 and ix < rd:
+                g += G[:, :, (iy - 1) + rd * ix] * dy * (1 - dx)
+            if iy < rd and ix > 0:
+                g += G[:, :, iy + rd * (ix - 1)] * (1 - dy) * dx
+            if iy < rd and ix < rd:
+                g += G[:, :, iy + rd * ix] * (1 - dy) * (1 - dx)
+            h2 = y0i - radius + iy
+            w2 = x0i - radius + ix
+            ok = (h2 >= 0) & (h2 < H2) & (w2 >= 0) & (w2 < W2)
+            g = np.where(ok, g, 0)
+            h2, w2 = np.where(ok, h2, 0), np.where(ok, w2, 0)
+            f1g += np.einsum("bnq,bnqc->bqc", g, f2[bidx, h2, w2])
+            for b in range(B):
+                np.add.at(f2g[b], (h2[b].ravel(), w2[b].ravel()),
+                          (g[b][..., None] * f1[b][None]).reshape(-1, C))
+    return (f1g.reshape(B, H1, W1, C), f2g,
+            np.zeros((B, N, H1, W1, 2), dtype=dtype))
+
+
 def alt_corr_block(fmap1: np.ndarray, fmap2: np.ndarray, coords: np.ndarray, num_levels: int = 4,
                    radius: int = 4, dtype=np.float64) -> np.ndarray:
     """AlternateCorrBlock(fmap1, fmap2)(coords), core/corr.py:63-91.

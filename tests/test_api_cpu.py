@@ -40,8 +40,9 @@ def test_host_tensors_raise_static_and_ffi():
     with pytest.raises(RuntimeError, match="CUDA tensor"):
         dx.alt_cuda_corr.forward(torch.zeros(1, 4, 4, 8), torch.zeros(1, 4, 4, 8),
                                  torch.zeros(1, 1, 4, 4, 2), 4)
-    with pytest.raises(NotImplementedError):
-        dx.alt_cuda_corr.backward(None, None, None, None, 4)
+    with pytest.raises(RuntimeError, match="CUDA tensor"):
+        z = torch.zeros(1, 4, 4, 8)
+        dx.alt_cuda_corr.backward(z, z, torch.zeros(1, 1, 4, 4, 2), torch.zeros(1, 1, 81, 4, 4), 4)
 
 
 def test_non_tensor_input_raises_type_error():

@@ -39,7 +39,7 @@ def test_header_declares_the_documented_entry_points():
         "dxr_pyramid_level_offset", "dxr_corr_pyramid_build", "dxr_corr_lookup",
         "dxr_avg_pool2x2", "dxr_alt_corr_forward", "dxr_alt_corr_lookup", "dxr_corr_volume",
         "dxr_pyramid_unpack", "dxr_pyramid_pack", "dxr_build_workspace_bytes",
-        "dxr_corr_lookup_backward", "dxr_pyramid_backward"}
+        "dxr_corr_lookup_backward", "dxr_pyramid_backward", "dxr_alt_corr_backward"}
 
 
 def test_library_exports_every_declared_symbol(nat):
@@ -150,6 +150,13 @@ def test_host_side_validation_needs_no_gpu(nat):
     assert lb(P, P, 1, 8, 8, 4, 4, P, 1, None) == EUNSUP                # bf16 gradients
     assert lb(None, P, 1, 8, 8, 4, 4, P, 0, None) == EINVAL             # null coords
     assert lb(None, None, 0, 8, 8, 4, 4, None, 0, None) == OK           # empty batch
+    ab = lib.dxr_alt_corr_backward
+    assert ab(P, P, P, P, P, P, 1, 8, 8, 8, 8, 64, 1, -1, None) == EINVAL   # radius < 0
+    assert ab(P, P, P, P, P, P, 1, 8, 8, 8, 8, 64, 1, 7, None) == EUNSUP    # radius > 6
+    assert ab(P, P, P, P, P, P, 1, 8, 8, 8, 8, 0, 1, 4, None) == EINVAL     # C = 0
+    assert ab(P, P, None, P, P, P, 1, 8, 8, 8, 8, 64, 1, 4, None) == EINVAL  # null coords
+    assert ab(P, P, P, P, None, P, 1, 8, 8, 8, 8, 64, 1, 4, None) == EINVAL  # null fmap1_grad
+    assert ab(None, None, None, None, None, None, 0, 8, 8, 8, 8, 64, 1, 4, None) == OK
     pb = lib.dxr_pyramid_backward
     assert pb(P, 0, 1, 8, 8, 4, 0.0, P, None) == EINVAL                 # divisor 0
     assert pb(P, 0, 1, 7, 30, 4, 16.0, P, None) == EINVAL               # empty level

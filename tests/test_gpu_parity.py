@@ -276,6 +276,27 @@ def test_alt_cuda_corr_forward_ffi(dx):
         dx.alt_cuda_corr.forward(_t(f1).transpose(1, 2), _t(f2), _t(c), r)
 
 
+@pytest.mark.parametrize("C,N,r", [(300, 2, 3), (64, 1, 4), (20, 1, 0)])
+def test_alt_cuda_corr_backward_ffi(dx, C, N, r):
+    """alt_cuda_corr.backward vs the oracle (pinned to the forward by adjointness):
+    windows partly outside fmap2, H2 != H1, C spanning two 256-channel slabs with a
+    ragged tail.  fmap2_grad is summed with atomics, so the bar is the north-star
+    tolerance, not bit equality."""
+    B, H1, W1, H2, W2 = 2, 9, 13, 7, 11
+    rd = 2 * r + 1
+    f1 = dg.normal(91, B * H1 * W1 * C).reshape(B, H1, W1, C).astype(np.float32)
+    f2 = dg.normal(92, B * H2 * W2 * C).reshape(B, H2, W2, C).astype(np.float32)
+    c = (dg.uniform(93, B * N * H1 * W1 * 2).reshape(B, N, H1, W1, 2) * 16 - 3).astype(np.float32)
+    g = dg.normal(94, B * N * rd * rd * H1 * W1).reshape(B, N, rd * rd, H1, W1).astype(np.float32)
+    r1, r2, _ = oracle.alt_corr_backward(f1, f2, c, g, r)
+    g1, g2, gc = dx.alt_cuda_corr.backward(_t(f1), _t(f2), _t(c), _t(g), r)
+    tolerance_check(g1.cpu().numpy(), r1, RTOL)
+    tolerance_check(g2.cpu().numpy(), r2, RTOL)
+    assert tuple(gc.shape) == c.shape and not gc.any()
+    with pytest.raises(RuntimeError):
+        dx.alt_cuda_corr.backward(_t(f1), _t(f2), _t(c), _t(g[:, :, 1:]), r)
+
+
 def test_alternate_block_too_small_raises_like_reference(dx):
     f1, f2 = _pair(H=15, W=40, seed=81)
     with pytest.raises(RuntimeError):

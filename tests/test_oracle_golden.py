@@ -114,6 +114,29 @@ def test_alt_forward_matches_literal_kernel_restatement():
                 np.testing.assert_allclose(got[0, n, :, h, w], ref, rtol=1e-12, atol=1e-12)
 
 
+@pytest.mark.parametrize("r", [0, 2, 4])
+def test_alt_backward_is_the_adjoint_of_the_forward(r):
+    """alt_cuda_corr.backward has no runnable reference here (CUDA-only) and no
+    golden; it is pinned to the forward restatement above by linearity: for any
+    direction d, <corr_grad, forward(d, fmap2)> = <fmap1_grad, d> and
+    <corr_grad, forward(fmap1, d)> = <fmap2_grad, d> (windows partly outside)."""
+    B, H1, W1, H2, W2, C, N = 2, 5, 7, 6, 9, 12, 2
+    rd = 2 * r + 1
+    f1 = dg.normal(11, B * H1 * W1 * C).reshape(B, H1, W1, C)
+    f2 = dg.normal(12, B * H2 * W2 * C).reshape(B, H2, W2, C)
+    c = (dg.uniform(13, B * N * H1 * W1 * 2).reshape(B, N, H1, W1, 2) * 14 - 3).astype(np.float32)
+    g = dg.normal(14, B * N * rd * rd * H1 * W1).reshape(B, N, rd * rd, H1, W1)
+    g1, g2, gc = oracle.alt_corr_backward(f1, f2, c, g, r)
+    assert g1.shape == f1.shape and g2.shape == f2.shape and not gc.any()
+    for seed in (15, 16):
+        d1 = dg.normal(seed, f1.size).reshape(f1.shape)
+        d2 = dg.normal(seed + 10, f2.size).reshape(f2.shape)
+        lhs1 = float((g * oracle.alt_corr_forward(d1, f2, c, r)).sum())
+        lhs2 = float((g * oracle.alt_corr_forward(f1, d2, c, r)).sum())
+        np.testing.assert_allclose(float((g1 * d1).sum()), lhs1, rtol=1e-11, atol=1e-11)
+        np.testing.assert_allclose(float((g2 * d2).sum()), lhs2, rtol=1e-11, atol=1e-11)
+
+
 def test_alt_block_oracle_matches_reference_corrblock():
     """AlternateCorrBlock == CorrBlock by linearity of pooling:
     the only difference is grid_sample's coordinate round trip (a few ulps)."""
