@@ -318,13 +318,22 @@ def main():
             }
         else:
             # on-the-fly lookups: (2r+2)^2 window dot products of length D per query
-            # and level, f32 FMA on the vector ALUs (SURVEY.md §8(d) stage d)
+            # and level, f32-class arithmetic (SURVEY.md §8(d) stage d).  The default
+            # kernel (D % 16 == 0, D <= 256) runs them as split-bf16 MFMA GEMMs over
+            # each 4x8 query tile's union box of cells; the issued MFMA work depends on
+            # the coordinates (box size), so the roofline prices the algorithmic window
+            # FLOPs against the f32 peak, as for an f32 kernel.
             aflops = alt_lookup_flops(B, H, W)
             achieved = aflops / (look_ms * 1e-3) / 1e12
-            a_traffic, a_src = pmc_traffic(wl_key, "alt_corr_kernel<")
+            mfma_alt = D % 16 == 0 and D <= 256 and os.environ.get("DXR_ALT_VARIANT") != "1"
+            akern = "alt_corr_mfma_kernel" if mfma_alt else "alt_corr_kernel"
+            a_traffic, a_src = pmc_traffic(wl_key, akern + "<")
             res["roofline"] = {
-                "kernel": "alt_corr_kernel (stage d, per lookup)",
-                "bound": "valu", "achieved": round(achieved, 2), "peak": PEAK_F32_TFLOPS,
+                "kernel": akern + (" (split-bf16 MFMA over the union box of 4x8-query windows, "
+                                   "f32 accumulate)" if mfma_alt else " (per-query VALU)")
+                + " (stage d, per lookup)",
+                "bound": "mfma" if mfma_alt else "valu", "achieved": round(achieved, 2),
+                "peak": PEAK_F32_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_TFLOPS, 4),
                 "traffic": a_traffic, "traffic_source": a_src,
                 "algorithmic_flops_per_launch": aflops,
