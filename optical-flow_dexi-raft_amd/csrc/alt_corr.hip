@@ -226,7 +226,8 @@ template <int R, int NRB, int CMAX>
 __global__ __launch_bounds__(256, 2) void alt_corr_mfma_kernel(const float* __restrict__ f1,
                                                                const float* __restrict__ coords,
                                                                float* __restrict__ out,
-                                                               AltGeom g, int W1, int tiles_x) {
+                                                               AltGeom g, int W1, int tiles_x,
+                                                               int remap) {
   constexpr int RD = 2 * R + 1, RD1 = RD + 1, NCELL = RD1 * RD1;
   constexpr int CHUNK = 4 * 32 * NRB;                       // box cells per chunk
   constexpr int KB = CMAX / 8;                              // 8-channel blocks
@@ -236,7 +237,15 @@ __global__ __launch_bounds__(256, 2) void alt_corr_mfma_kernel(const float* __re
   __shared__ int box[4];                                    // bx0, by0, bw, bh
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+  // Workgroups are dealt round-robin to the 8 XCDs; with `remap` XCD k takes the
+  // k-th contiguous band of tiles instead, so neighbouring tiles (whose boxes
+  // overlap) share one L2 (the bijection of csrc/corr_build.hip's page_coord).
+  int tile = blockIdx.x;
+  if (remap) {
+    const int n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = tile % 8;
+    tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + tile / 8;
+  }
+  const int tx = tile % tiles_x, ty = tile / tiles_x;
   const AltLevel lv = g.lv[blockIdx.y];
   const int z = blockIdx.z, bf = z / g.Nc;
   const float* cz = coords + (long long)z * g.coord_zstride;
@@ -410,7 +419,7 @@ int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const Al
   const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)levels, (unsigned)Z);
   if (g.C > 256) return DXR_EUNSUPPORTED;
   hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256>), grid, dim3(256), 0, stream, f1, coords,
-                     out, g, W1, tiles_x);
+                     out, g, W1, tiles_x, alt_variant() == 4 ? 0 : 1);
   return dxr::launch_status();
 }
 
@@ -429,7 +438,7 @@ int launch_alt(const float* f1, const float* coords, float* out, const AltGeom& 
                int Z, int radius, bool vec, hipStream_t stream, int W1 = 0) {
   // MFMA form: C a multiple of 16 (k16 steps) up to 256, 16-byte aligned rows.
   // DXR_ALT_VARIANT 1 selects the per-query form, 2 / 3 the MFMA form with 2 / 4
-  // row blocks per wave (r = 4).
+  // row blocks per wave (r = 4), 4 the MFMA form in plain (round-robin XCD) tile order.
   const int v = alt_variant();
   if (vec && W1 > 0 && g.C % 16 == 0 && g.C <= 256 && v != 1) {
     switch (radius) {
