@@ -55,9 +55,17 @@ def is_stale() -> bool:
     return any(p.stat().st_mtime > t for p in _deps())
 
 
+# Per-file flags.  corr_build.hip: no SLP vectorisation — packed f32 VALU
+# (v_pk_add_f32) beside MFMAs costs more issue cycles than the scalar pair it
+# replaces (MI355X_MICROARCH.md, cycle constants); measured r01: split build
+# 192 -> 182 us at Sintel, other kernels neutral.
+FILE_FLAGS = {"corr_build.hip": ["-fno-slp-vectorize"]}
+
+
 def _compile(src: Path, extra: list[str]) -> Path:
     obj = BUILD_DIR / (src.stem + ".o")
-    cmd = [hipcc(), *CXXFLAGS, *extra, "-c", str(src), "-o", str(obj)]
+    cmd = [hipcc(), *CXXFLAGS, *FILE_FLAGS.get(src.name, []), *extra, "-c", str(src), "-o",
+           str(obj)]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{' '.join(cmd)}\n{res.stderr}")
