@@ -30,6 +30,11 @@
  *                            (alt_cuda_corr/correlation_kernel.cu:288-320)
  *   dxr_alt_corr_lookup      core/corr.py:74-91  AlternateCorrBlock.__call__
  *                            (all levels in one launch, / sqrt(D) fused)
+ *   dxr_corr_lookup_conv1x1  core/corr.py:29-50 CorrBlock.__call__ followed by
+ *                            core/update.py:90 F.relu(self.convc1(corr))
+ *                            (BasicMotionEncoder; :71 SmallMotionEncoder)
+ *   dxr_conv1x1_pack_weight  core/update.py:83 / :66 the convc1 weight,
+ *                            rearranged once into the fused kernel's operand layout
  *
  * Layouts (all row-major, C-contiguous):
  *   fmap (CorrBlock)        [B, D, H, W]               (NCHW, as core/raft.py:139-142)
@@ -63,7 +68,7 @@ extern "C" {
 /* HIP's own definition; repeating an identical typedef is legal in C11/C++. */
 typedef struct ihipStream_t* hipStream_t;
 
-#define DXR_ABI_VERSION 2
+#define DXR_ABI_VERSION 3
 
 enum dxr_status {
   DXR_OK = 0,
@@ -168,6 +173,30 @@ int dxr_corr_lookup_backward(const float* coords, const float* grad_out,
                              int64_t B, int64_t H, int64_t W, int num_levels,
                              int radius, void* grad_pyramid, int grad_dtype,
                              hipStream_t stream);
+
+/*
+ * Stage (c) fused with the motion encoder's 1x1 convolution (SURVEY.md §8(f)
+ * row 2; inference):
+ *   out[b,o,h,w] = act(bias[o] + sum_c weight[o,c] * lookup(coords)[b,c,h,w])
+ * lookup() is dxr_corr_lookup (bit-identical samples), the contraction runs in
+ * f32 class (exact three-way bf16 split of both operands, f32 accumulation).
+ *   weight_packed : dxr_conv1x1_pack_weight of the [cout, cin] float32 weight,
+ *                   cin = num_levels*(2r+1)^2 (dxr_conv1x1_packed_bytes bytes:
+ *                   float32 [ceil(cin/16)*2][cout][8], zero padded)
+ *   bias          : [cout] float32 or NULL;  relu: 1 = F.relu, 0 = none
+ *   out           : [B, cout, H, W] float32
+ * Supported: radius 3 or 4, num_levels <= 4, cout a multiple of 32 (<= 4096);
+ * other valid requests return DXR_EUNSUPPORTED.
+ */
+int64_t dxr_conv1x1_packed_bytes(int64_t cout, int64_t cin);
+int dxr_conv1x1_pack_weight(const float* weight, int64_t cout, int64_t cin,
+                            void* packed, hipStream_t stream);
+int dxr_corr_lookup_conv1x1(const void* pyramid, int pyr_dtype,
+                            int64_t B, int64_t H, int64_t W, int num_levels,
+                            int radius, const float* coords,
+                            const void* weight_packed, const float* bias,
+                            int64_t cout, int relu, float* out,
+                            hipStream_t stream);
 
 /*
  * Backward of stages (a)+(b) down to the volume: folds the gradient of every

@@ -59,7 +59,7 @@ def is_stale() -> bool:
 # (v_pk_add_f32) beside MFMAs costs more issue cycles than the scalar pair it
 # replaces (MI355X_MICROARCH.md, cycle constants); measured r01: split build
 # 192 -> 182 us at Sintel, other kernels neutral.
-FILE_FLAGS = {"corr_build.hip": ["-fno-slp-vectorize"]}
+FILE_FLAGS = {"corr_build.hip": ["-fno-slp-vectorize"], "corr_lookup.hip": ["-fno-slp-vectorize"]}
 
 
 def _compile(src: Path, extra: list[str]) -> Path:

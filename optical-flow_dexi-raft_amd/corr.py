@@ -206,6 +206,31 @@ def _check_coords(coords: torch.Tensor, B: int, H: int, W: int, device: torch.de
     return coords.contiguous()
 
 
+_PACKED_CACHE: dict = {}
+
+
+def _packed_weight(weight: torch.Tensor, device: torch.device) -> torch.Tensor:
+    """A [Cout, Cin] conv weight in the fused kernel's operand layout
+    (dxr_conv1x1_pack_weight), cached per (storage, version, shape) so the 12 GRU
+    iterations pack it once."""
+    key = (weight.data_ptr(), weight._version, tuple(weight.shape), weight.dtype, str(device))
+    hit = _PACKED_CACHE.get(key)
+    if hit is not None:
+        return hit[1]
+    cout, cin = (int(s) for s in weight.shape)
+    w = weight.detach().float().contiguous()
+    lib = nat.load()
+    planes = torch.empty(lib.dxr_conv1x1_packed_bytes(cout, cin), dtype=torch.uint8, device=device)
+    with _Launch(device):
+        st = lib.dxr_conv1x1_pack_weight(w.data_ptr(), cout, cin, planes.data_ptr(),
+                                          nat.stream_of(w))
+    nat.check(st, "conv1x1 weight packing (dxr_conv1x1_pack_weight)")
+    if len(_PACKED_CACHE) > 16:
+        _PACKED_CACHE.clear()
+    _PACKED_CACHE[key] = (weight, planes)   # keeps the weight alive: its pointer stays unique
+    return planes
+
+
 class CorrBlock:
     """All-pairs correlation pyramid + radius-r lookup (reference core/corr.py:12-60).
 
@@ -305,6 +330,52 @@ class CorrBlock:
                                      self.num_levels, self.radius, c.data_ptr(),
                                      out.data_ptr(), nat.stream_of(c))
         nat.check(st, "CorrBlock lookup (dxr_corr_lookup)")
+        return out
+
+    def lookup_conv1x1(self, coords, weight, bias=None, relu=True):
+        """Lookup fused with the motion encoder's first 1x1 convolution:
+        ``F.relu(F.conv2d(self(coords), weight, bias))`` in one launch
+        (``dxr_corr_lookup_conv1x1``).
+
+        Replaces ``corr = corr_fn(coords1)`` (core/raft.py:172) followed by
+        ``cor = F.relu(self.convc1(corr))`` in BasicMotionEncoder.forward
+        (core/update.py:90; SmallMotionEncoder :71): pass ``convc1.weight`` and
+        ``convc1.bias``.  Returns a new contiguous float32 ``[B, Cout, H, W]``.
+        The samples are bit-identical to ``__call__``'s; the contraction runs in
+        f32 class on the matrix cores.  Inference only (raises under grad for
+        inputs that require grad).  Supported: radius 3/4, num_levels <= 4,
+        Cout a multiple of 32 (the reference's 256 and 96).
+        """
+        B, D, H, W = self._geom
+        _require_no_grad(coords, weight, *(() if bias is None else (bias,)),
+                         what="CorrBlock.lookup_conv1x1 (inference fusion)")
+        if self._token is not None and torch.is_grad_enabled():
+            raise NotImplementedError("CorrBlock.lookup_conv1x1 is inference-only; call the "
+                                      "block and convc1 separately to train through them")
+        c = _check_coords(coords, B, H, W, self._device)
+        rd = 2 * self.radius + 1
+        cin = self.num_levels * rd * rd
+        _require_device(weight, "weight")
+        if weight.dim() == 4 and tuple(weight.shape[2:]) == (1, 1):
+            weight = weight.reshape(weight.shape[0], weight.shape[1])
+        if weight.dim() != 2 or int(weight.shape[1]) != cin:
+            raise RuntimeError(f"weight must be [Cout, {cin}, 1, 1] (or [Cout, {cin}]), "
+                               f"got {tuple(weight.shape)}")
+        cout = int(weight.shape[0])
+        if bias is not None:
+            _require_device(bias, "bias")
+            if tuple(bias.shape) != (cout,):
+                raise RuntimeError(f"bias must be [{cout}], got {tuple(bias.shape)}")
+            bias = bias.detach().float().contiguous()
+        planes = _packed_weight(weight, self._device)
+        out = torch.empty((B, cout, H, W), dtype=torch.float32, device=self._device)
+        lib = nat.load()
+        with _Launch(self._device):
+            st = lib.dxr_corr_lookup_conv1x1(self._buf.data_ptr(), self._pyr_dt, B, H, W,
+                                             self.num_levels, self.radius, c.data_ptr(),
+                                             planes.data_ptr(), nat.ptr(bias), cout, int(bool(relu)),
+                                             out.data_ptr(), nat.stream_of(c))
+        nat.check(st, "CorrBlock.lookup_conv1x1 (dxr_corr_lookup_conv1x1)")
         return out
 
     @staticmethod

@@ -293,13 +293,14 @@ __device__ __forceinline__ void load_vec(const PT* p, float* v) {
   }
 }
 
-// Phase 1 for one level type: V-cell vectors, 4 per LDS vector slot.
+// Phase 1 for one level type: V-cell vectors, 4 per LDS vector slot.  Split in
+// a load half (registers) and a store half (LDS) so a caller can keep several
+// levels' gathers in flight at once (the fused motion kernel).
 template <int R, int NT_, int V, typename PT>
-__device__ __forceinline__ void gather_windows(const PT* __restrict__ base, int qb0, const LevelAddr& A,
-                                               const int2* org, float* cells, int q0, int N,
-                                               int tid) {
+__device__ __forceinline__ void gather_load(const PT* __restrict__ base, int qb0, const LevelAddr& A,
+                                            const int2* org, int q0, int N, int tid,
+                                            float4 (&v)[WideCfg<R, NT_>::VIT]) {
   using C = WideCfg<R, NT_>;
-  float4 v[C::VIT];
 #pragma unroll
   for (int i = 0; i < C::VIT; ++i) {
     const int s = tid + i * C::NT;
@@ -327,6 +328,12 @@ __device__ __forceinline__ void gather_windows(const PT* __restrict__ base, int 
     }
     v[i] = make_float4(c[0], c[1], c[2], c[3]);
   }
+}
+
+template <int R, int NT_>
+__device__ __forceinline__ void gather_store(const float4 (&v)[WideCfg<R, NT_>::VIT], float* cells,
+                                             int tid) {
+  using C = WideCfg<R, NT_>;
 #pragma unroll
   for (int i = 0; i < C::VIT; ++i) {
     const int s = tid + i * C::NT;
@@ -335,6 +342,15 @@ __device__ __forceinline__ void gather_windows(const PT* __restrict__ base, int 
       *reinterpret_cast<float4*>(cells + qq * C::QS + rem * 4) = v[i];
     }
   }
+}
+
+template <int R, int NT_, int V, typename PT>
+__device__ __forceinline__ void gather_windows(const PT* __restrict__ base, int qb0, const LevelAddr& A,
+                                               const int2* org, float* cells, int q0, int N,
+                                               int tid) {
+  float4 v[WideCfg<R, NT_>::VIT];
+  gather_load<R, NT_, V>(base, qb0, A, org, q0, N, tid, v);
+  gather_store<R, NT_>(v, cells, tid);
 }
 
 // Phase 0 of the wide lookup (forward and backward): per (query, sample) the
@@ -621,6 +637,309 @@ int launch_lookup(const PT* pyr, const float* coords, float* out, const LookupGe
   }
 }
 
+// ---------------------------------------------------------------------------
+// Lookup fused with the motion encoder's first 1x1 convolution (SURVEY.md
+// §8(f) row 2):
+//   out[b, o, q] = act(bias[o] + sum_c Wt[o, c] * corr[b, c, q])
+// where corr is this file's lookup output (channel c = l*(2r+1)^2 + ix*(2r+1) + iy,
+// core/corr.py:29-50) and Wt the convc1 weight of core/update.py:83 / :90
+// (BasicMotionEncoder, F.relu(self.convc1(corr)), 324 -> 256) or :66 / :71
+// (SmallMotionEncoder, 196 -> 96).  The reference writes the 9.1 MB lookup
+// tensor (Sintel), reads it back in the convolution and writes the conv output
+// before a separate ReLU pass; here the lookup vector of a query never leaves
+// the CU.
+//
+// One workgroup = 32 query pixels, 8 waves.  Per level: the lookup's phase 0
+// and phase 1 (the forward kernel's code), then phase 2 computes the samples
+// with the same arithmetic (bit-identical values) and stores each as an exact
+// hi/mid/lo bf16 split into LDS planes [plane][k/8][query][8] — the B operand
+// of v_mfma_f32_32x32x16_bf16 as it stands.  Then a (Cout x 32 x Cin) GEMM on
+// the matrix cores, f32 class like the build (six bf16 products per f32
+// product, small terms first, f32 accumulation): wave w owns output rows
+// 32w.., its A operand the pre-split weight planes (dxr_conv1x1_split_weight,
+// [plane][k/8][Cout] uint4, hot in L2), bias + ReLU in registers, coalesced
+// 128-B stores along queries into [B, Cout, H, W].
+// ---------------------------------------------------------------------------
+typedef __bf16 mbf8 __attribute__((ext_vector_type(8)));
+typedef float mf16 __attribute__((ext_vector_type(16)));
+
+template <int R>
+struct MotionCfg {
+  using C = WideCfg<R, 512>;
+  static constexpr int LMAX = 4;                          // levels staged in LDS
+  static constexpr int KP = (LMAX * C::K + 15) & ~15;     // input channels, padded to k steps
+  static constexpr int KB = KP / 8;                       // 8-channel blocks
+  static constexpr int NKS = KP / 16;                     // k steps
+  static_assert(C::QB == 32, "one 32-query MFMA column block per workgroup");
+};
+
+// hi / mid / lo bf16 bits of x (each round-to-nearest; x = hi + mid + lo exactly
+// for finite x up to the bf16 range of the residuals).
+__device__ __forceinline__ void split3(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
+  h = dxr::f32_to_bf16(x);
+  const float r1 = __fsub_rn(x, dxr::bf16_to_f32(h));
+  m = dxr::f32_to_bf16(r1);
+  l = dxr::f32_to_bf16(__fsub_rn(r1, dxr::bf16_to_f32(m)));
+}
+
+// The convc1 weight [Cout, Cin] f32 rearranged as [Cin_pad/8][Cout][8] (zero
+// padded): one k step of a lane's A operand is 32 contiguous bytes.  Kept in
+// f32 and split in registers by the fused kernel: 4 bytes per weight streamed
+// from L2 instead of 6 for pre-split planes (the stream is the GEMM's bound:
+// ~70 GB/s of L2 reads per CU, MI355X_MICROARCH.md "gather into LDS").
+__global__ __launch_bounds__(256) void conv1x1_pack_weight_kernel(const float* __restrict__ w,
+                                                                  int cout, int cin, int kbw,
+                                                                  float4* __restrict__ packed) {
+  const int u = blockIdx.x * 256 + threadIdx.x;
+  if (u >= kbw * cout) return;
+  const int kb = u / cout, o = u - kb * cout;
+  float x[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = kb * 8 + e;
+    x[e] = c < cin ? w[(long long)o * cin + c] : 0.f;
+  }
+  packed[2LL * u] = make_float4(x[0], x[1], x[2], x[3]);
+  packed[2LL * u + 1] = make_float4(x[4], x[5], x[6], x[7]);
+}
+
+// NT threads per workgroup (1024 by default: the four levels' lookup phases
+// are latency-bound at 8 waves per CU).  With 16 waves the GEMM splits K in two
+// halves per output block: waves 8..15 add their partial accumulators through
+// LDS (the lookup's staging area, free by then).
+// ABL (timing-only ablations, outputs invalid): 1 skips the GEMM's MFMAs and
+// weight loads, 2 skips the lookup phases.
+template <int R, typename PT, int NT = 1024, int PF = 4, int ABL = 0>
+__global__ __launch_bounds__(NT) void corr_lookup_conv1x1_kernel(
+    const PT* __restrict__ pyr, const float* __restrict__ coords, const float4* __restrict__ wpk,
+    const float* __restrict__ bias, float* __restrict__ out, LookupGeom g, int cout, int relu) {
+  using C = WideCfg<R, NT>;
+  using M = MotionCfg<R>;
+  constexpr int RD = C::RD, RS = C::RS, K = C::K, QB = C::QB, KB = M::KB;
+  constexpr int NW = NT / 64, KSPLIT = NW >= 16 ? 2 : 1;
+  static_assert(NW == 8 || NW == 16, "8 output blocks of 32 per pass");
+  // lookup staging (cells | xs | ys | org), reused as the K-split reduction area
+  constexpr int CELLS_B = QB * C::QS * 4, XS_B = M::LMAX * RD * QB * 16, ORG_B = M::LMAX * QB * 8;
+  constexpr int STAGE_B = CELLS_B + 2 * XS_B + ORG_B, RED_B = KSPLIT > 1 ? 8 * 16 * 64 * 4 : 0;
+  __shared__ __attribute__((aligned(16))) char stage[STAGE_B > RED_B ? STAGE_B : RED_B];
+  __shared__ __attribute__((aligned(16))) uint4 cpl[3 * KB * QB];   // [plane][kb][q] x 8 bf16
+  float* cells = reinterpret_cast<float*>(stage);
+  float4* xs = reinterpret_cast<float4*>(stage + CELLS_B);   // per level, as the lookup's phase 0
+  float4* ys = reinterpret_cast<float4*>(stage + CELLS_B + XS_B);
+  int2* org = reinterpret_cast<int2*>(stage + CELLS_B + 2 * XS_B);
+  float* red = reinterpret_cast<float*>(stage);
+  uint16_t* cph = reinterpret_cast<uint16_t*>(cpl);
+
+  const int tid = threadIdx.x;
+  const int b = blockIdx.y;
+  const int q0 = blockIdx.x * QB;
+  const int cin = g.cout;                  // levels * (2r+1)^2 <= M::KP
+  const int kpad = (cin + 15) & ~15;
+
+  // GEMM roles: wave -> output block (wave % 8) + 8i, K half (wave / 8).  The A
+  // operand (weight fragments, f32, split in registers) streams from L2 with PF
+  // k steps in flight; the first PF are requested before the lookup phases.
+  const int lane = tid & 63, wave = tid >> 6, j = lane & 31, kh = lane >> 5;
+  const int wob = wave & 7, khalf = wave >> 3;
+  const int nks = kpad / 16;
+  const int kbeg = khalf * nks / KSPLIT, kend = (khalf + 1) * nks / KSPLIT;
+  const int nob = cout / 32;
+  float4 wbuf[PF][2];
+  auto wload = [&](float4* dst, int ob, int ks) {
+    const float4* wp = wpk + 2 * ((long long)(2 * ks + kh) * cout + ob * 32 + j);
+    dst[0] = wp[0];
+    dst[1] = wp[1];
+  };
+  auto preload = [&](int ob) {
+#pragma unroll
+    for (int s = 0; s < PF; ++s) wload(wbuf[s], ob, min(kbeg + s, kend - 1));
+  };
+  if (ABL != 1 && wob < nob) preload(wob);
+
+  // zero the channel padding [cin, kpad) of the three planes
+  {
+    const int np = kpad - cin;
+    for (int i = tid; i < 3 * QB * np; i += NT) {
+      const int p = i / (QB * np), rem = i - p * (QB * np);
+      const int qq = rem / np, c = cin + rem - qq * np;
+      cph[((p * KB + (c >> 3)) * QB + qq) * 8 + (c & 7)] = 0;
+    }
+  }
+
+  // phase 0 of every level, then every level's window gathers in flight at
+  // once (registers), then per level: windows -> LDS, samples -> operand planes
+#pragma unroll
+  for (int l = 0; l < (ABL == 2 ? 0 : M::LMAX); ++l)
+    if (l < g.levels)
+      wide_phase0<R, NT>(coords, g, g.lv[l], b, l, q0, tid, xs + l * RD * QB, ys + l * RD * QB,
+                         org + l * QB);
+  __syncthreads();
+  float4 win[M::LMAX][C::VIT];
+#pragma unroll
+  for (int l = 0; l < (ABL == 2 ? 0 : M::LMAX); ++l) {
+    if (l < g.levels) {
+      const LevelAddr& A = g.lv[l];
+      const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
+      const int qb0 = q0 & ((1 << A.lqb) - 1);
+      // paged levels 0..3: level-l tiles are (16 >> l) cells wide
+      if (l < 3)
+        gather_load<R, NT, 4>(base, qb0, A, org + l * QB, q0, g.N, tid, win[l]);
+      else
+        gather_load<R, NT, 2>(base, qb0, A, org + l * QB, q0, g.N, tid, win[l]);
+    }
+  }
+#pragma unroll
+  for (int l = 0; l < (ABL == 2 ? 0 : M::LMAX); ++l) {
+    if (l >= g.levels) break;
+    gather_store<R, NT>(win[l], cells, tid);
+    __syncthreads();
+    {
+      const float4* xl = xs + l * RD * QB;
+      const float4* yl = ys + l * RD * QB;
+      const int qq = tid % QB, cls = tid / QB;
+      const bool live = q0 + qq < g.N;
+      const float* cq = cells + qq * C::QS;
+      for (int k = cls; k < K; k += C::NCLS) {
+        const int ox = k / RD, oy = k - ox * RD;
+        const float4 xd = xl[ox * QB + qq], yd = yl[oy * QB + qq];
+        const float* p = cq + __float_as_int(yd.x) + __float_as_int(xd.x);
+        const float v00 = p[0], v01 = p[1], v10 = p[RS], v11 = p[RS + 1];
+        const float nw = __fmul_rn(yd.z, xd.z), ne = __fmul_rn(yd.z, xd.y);
+        const float sw = __fmul_rn(yd.y, xd.z), se = __fmul_rn(yd.y, xd.y);
+        float r = __fmul_rn(nw, v00);
+        r = __builtin_fmaf(ne, v01, r);
+        r = __builtin_fmaf(sw, v10, r);
+        r = __builtin_fmaf(se, v11, r);
+        if (!live) r = 0.f;                // queries past N: finite zeros
+        uint16_t h, m, lo;
+        split3(r, h, m, lo);
+        const int c = l * K + k;
+        const int e = ((c >> 3) * QB + qq) * 8 + (c & 7);
+        cph[e] = h;
+        cph[KB * QB * 8 + e] = m;
+        cph[2 * KB * QB * 8 + e] = lo;
+      }
+    }
+    __syncthreads();   // cells are rewritten by the next level (and the staging
+                       // area becomes the reduction area after the last one)
+  }
+  if constexpr (ABL == 2) __syncthreads();
+
+  // ---- (Cout x 32 queries x Cin) GEMM, f32 class
+  const int q = q0 + j;
+  for (int ob0 = 0; ob0 < nob; ob0 += 8) {   // uniform trip count: barriers inside
+    const int ob = ob0 + wob;
+    const bool act = ob < nob;
+    mf16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    if (ABL != 1 && act) {
+      if (ob0 > 0) preload(ob);
+      // One k step: split the weight fragment of slot sl in registers, refill the
+      // slot PF steps ahead (unconditionally, clamped: a conditional refill makes
+      // the compiler wait for it at once), six MFMAs.
+      auto kstep = [&](int ks, int sl, bool refill) {
+        // keep each step's split behind its own waits: hoisted into the previous
+        // step's MFMA shadow, it makes that step wait for the refill in flight
+        __builtin_amdgcn_sched_barrier(0);
+        const int kb = 2 * ks + kh;
+        uint4 wh, wm, wl;
+        {
+          const float4 a = wbuf[sl][0], c = wbuf[sl][1];
+          const float x[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+          dxr::split8(x, wh, wm, wl);
+        }
+        if (refill) wload(wbuf[sl], ob, min(ks + PF, kend - 1));
+        const mbf8 th = __builtin_bit_cast(mbf8, wh);
+        const mbf8 tm = __builtin_bit_cast(mbf8, wm);
+        const mbf8 tl = __builtin_bit_cast(mbf8, wl);
+        const mbf8 qh = __builtin_bit_cast(mbf8, cpl[(0 * KB + kb) * QB + j]);
+        const mbf8 qm = __builtin_bit_cast(mbf8, cpl[(1 * KB + kb) * QB + j]);
+        const mbf8 ql = __builtin_bit_cast(mbf8, cpl[(2 * KB + kb) * QB + j]);
+        // small terms first
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, ql, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qm, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh, acc, 0, 0, 0);
+      };
+      const int nfull = kbeg + (kend - kbeg) / PF * PF;
+#pragma unroll 1
+      for (int k0 = kbeg; k0 < nfull; k0 += PF) {
+#pragma unroll
+        for (int sl = 0; sl < PF; ++sl) kstep(k0 + sl, sl, true);
+      }
+#pragma unroll
+      for (int sl = 0; sl < PF; ++sl)   // tail: no refills
+        if (nfull + sl < kend) kstep(nfull + sl, sl, false);
+    }
+    if constexpr (KSPLIT > 1) {
+      // the upper K half hands its partial sums to the lower half's wave
+      if (khalf == 1 && act) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) red[(wob * 16 + r) * 64 + lane] = acc[r];
+      }
+      __syncthreads();
+      if (khalf == 0 && act) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] += red[(wob * 16 + r) * 64 + lane];
+      }
+      __syncthreads();
+    }
+    if (khalf == 0 && act && q < g.N) {
+      float* ob_out = out + (long long)b * cout * g.N + q;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int orow = ob * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+        float v = acc[r] + (bias ? bias[orow] : 0.f);
+        if (relu && v < 0.f) v = 0.f;      // NaN stays NaN, as torch.relu
+        ob_out[(long long)orow * g.N] = v;
+      }
+    }
+  }
+}
+
+template <int R, typename PT, int NT, int PF, int ABL = 0>
+void launch_conv1x1_k(dim3 grid, hipStream_t stream, const PT* pyr, const float* coords,
+                      const float4* wpl, const float* bias, float* out, const LookupGeom& g,
+                      int cout, int relu) {
+  hipLaunchKernelGGL((corr_lookup_conv1x1_kernel<R, PT, NT, PF, ABL>), grid, dim3(NT), 0, stream,
+                     pyr, coords, wpl, bias, out, g, cout, relu);
+}
+
+template <int R, typename PT>
+int launch_lookup_conv1x1_r(const PT* pyr, const float* coords, const float4* wpl,
+                            const float* bias, float* out, const LookupGeom& g, int B, int cout,
+                            int relu, hipStream_t stream) {
+  using C = WideCfg<R, 1024>;
+  if (g.cout > MotionCfg<R>::KP) return DXR_EUNSUPPORTED;
+  const dim3 grid((unsigned)((g.N + C::QB - 1) / C::QB), (unsigned)B);
+  // DXR_MOTION_VARIANT (A/B only): 1 = 512 threads; 91 / 92 ablations.
+  const char* v = std::getenv("DXR_MOTION_VARIANT");
+  const int var = v ? std::atoi(v) : 0;
+  if (var == 1)
+    launch_conv1x1_k<R, PT, 512, 4>(grid, stream, pyr, coords, wpl, bias, out, g, cout, relu);
+  else if (var == 91)
+    launch_conv1x1_k<R, PT, 1024, 4, 1>(grid, stream, pyr, coords, wpl, bias, out, g, cout, relu);
+  else if (var == 92)
+    launch_conv1x1_k<R, PT, 1024, 4, 2>(grid, stream, pyr, coords, wpl, bias, out, g, cout, relu);
+  else
+    launch_conv1x1_k<R, PT, 1024, 4>(grid, stream, pyr, coords, wpl, bias, out, g, cout, relu);
+  return dxr::launch_status();
+}
+
+template <typename PT>
+int launch_lookup_conv1x1(const PT* pyr, const float* coords, const float4* wpl, const float* bias,
+                          float* out, const LookupGeom& g, int B, int radius, int cout, int relu,
+                          hipStream_t stream) {
+  switch (radius) {
+    case 3: return launch_lookup_conv1x1_r<3, PT>(pyr, coords, wpl, bias, out, g, B, cout, relu, stream);
+    case 4: return launch_lookup_conv1x1_r<4, PT>(pyr, coords, wpl, bias, out, g, B, cout, relu, stream);
+    default: return DXR_EUNSUPPORTED;
+  }
+}
+
 }  // namespace
 
 extern "C" int dxr_corr_lookup(const void* pyramid, int pyr_dtype, int64_t B, int64_t H,
@@ -676,4 +995,48 @@ extern "C" int dxr_corr_lookup_backward(const float* coords, const float* grad_o
     case 7: return launch_lookup_backward_r<7>(coords, grad_out, gp, g, (int)B, stream);
     default: return launch_lookup_backward_r<8>(coords, grad_out, gp, g, (int)B, stream);
   }
+}
+
+extern "C" int64_t dxr_conv1x1_packed_bytes(int64_t cout, int64_t cin) {
+  if (cout < 1 || cin < 1) return -1;
+  return ((cin + 15) / 16 * 16) * cout * 4;
+}
+
+extern "C" int dxr_conv1x1_pack_weight(const float* weight, int64_t cout, int64_t cin,
+                                       void* packed, hipStream_t stream) {
+  if (cout < 1 || cin < 1 || cout > (1 << 20) || cin > (1 << 20)) return DXR_EINVAL;
+  if (!weight || !packed) return DXR_EINVAL;
+  const int kbw = (int)((cin + 15) / 16 * 2);
+  const long long units = (long long)kbw * cout;
+  hipLaunchKernelGGL(conv1x1_pack_weight_kernel, dim3((unsigned)((units + 255) / 256)), dim3(256),
+                     0, stream, weight, (int)cout, (int)cin, kbw, static_cast<float4*>(packed));
+  return dxr::launch_status();
+}
+
+extern "C" int dxr_corr_lookup_conv1x1(const void* pyramid, int pyr_dtype, int64_t B, int64_t H,
+                                       int64_t W, int num_levels, int radius, const float* coords,
+                                       const void* weight_packed, const float* bias, int64_t cout,
+                                       int relu, float* out, hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, num_levels, &L)) return DXR_EINVAL;
+  if (radius < 0 || cout < 1) return DXR_EINVAL;
+  if (radius != 3 && radius != 4) return DXR_EUNSUPPORTED;
+  if (num_levels > 4 || cout % 32 != 0 || cout > 4096) return DXR_EUNSUPPORTED;
+  if (B > 65535 || H * W > (1LL << 30)) return DXR_EINVAL;
+  if (B == 0) return DXR_OK;
+  if (!pyramid || !coords || !weight_packed || !out) return DXR_EINVAL;
+  const int rd = 2 * radius + 1;
+  LookupGeom g;
+  g.N = (int)(H * W);
+  g.levels = num_levels;
+  g.cout = num_levels * rd * rd;
+  for (int l = 0; l < L.n; ++l) g.lv[l] = level_addr(L.lay[l]);
+  const float4* wpl = static_cast<const float4*>(weight_packed);
+  if (pyr_dtype == DXR_F32)
+    return launch_lookup_conv1x1(static_cast<const float*>(pyramid), coords, wpl, bias, out, g,
+                                 (int)B, radius, (int)cout, relu, stream);
+  if (pyr_dtype == DXR_BF16)
+    return launch_lookup_conv1x1(static_cast<const uint16_t*>(pyramid), coords, wpl, bias, out, g,
+                                 (int)B, radius, (int)cout, relu, stream);
+  return DXR_EINVAL;
 }

@@ -108,4 +108,32 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
   return (uint16_t)(u >> 16);
 }
 
+// Exact hi/mid/lo split of 8 floats into three 8 x bf16 MFMA operands
+// (x = hi + mid + lo; hi and mid round to nearest, lo keeps the residual's top
+// 16 bits).  Used by the split-bf16 f32-class MFMA kernels.
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+  typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  const f2_t v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf2_t));
+}
+
+__device__ __forceinline__ void split8(const float (&x)[8], uint4& h, uint4& m, uint4& l) {
+  uint32_t hh[4], mm[4], ll[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float a = x[2 * e], b = x[2 * e + 1];
+    const uint32_t hp = cvt_pk_bf16(a, b);
+    const float ra = a - __uint_as_float(hp << 16), rb = b - __uint_as_float(hp & 0xffff0000u);
+    const uint32_t mp = cvt_pk_bf16(ra, rb);
+    const float la = ra - __uint_as_float(mp << 16), lb = rb - __uint_as_float(mp & 0xffff0000u);
+    hh[e] = hp;
+    mm[e] = mp;
+    ll[e] = __builtin_amdgcn_perm(__float_as_uint(lb), __float_as_uint(la), 0x07060302u);
+  }
+  h = make_uint4(hh[0], hh[1], hh[2], hh[3]);
+  m = make_uint4(mm[0], mm[1], mm[2], mm[3]);
+  l = make_uint4(ll[0], ll[1], ll[2], ll[3]);
+}
+
 }  // namespace dxr

@@ -357,3 +357,24 @@ def corr_pyramid_backward(fmap1: np.ndarray, fmap2: np.ndarray,
     df1 = np.matmul(f2, dv.transpose(0, 2, 1))
     df2 = np.matmul(f1, dv)
     return df1.reshape(B, D, H, W), df2.reshape(B, D, H, W)
+
+
+def motion_conv1x1(corr: np.ndarray, weight: np.ndarray, bias: np.ndarray | None = None,
+                   relu: bool = True, dtype=np.float64) -> np.ndarray:
+    """First layer of the motion encoder on the lookup output:
+    ``F.relu(self.convc1(corr))`` (core/update.py:90 BasicMotionEncoder, :71
+    SmallMotionEncoder; ``convc1 = nn.Conv2d(cor_planes, Cout, 1, padding=0)``,
+    :83 / :66).  A 1x1 convolution is a per-pixel matrix product:
+    ``out[b, o, h, w] = bias[o] + sum_c weight[o, c] * corr[b, c, h, w]``.
+
+    ``corr``: [B, Cin, H, W]; ``weight``: [Cout, Cin] or [Cout, Cin, 1, 1].
+    """
+    B, C, H, W = corr.shape
+    w = weight.reshape(weight.shape[0], -1).astype(dtype)
+    assert w.shape[1] == C
+    out = np.einsum("oc,bcn->bon", w, corr.reshape(B, C, H * W).astype(dtype))
+    if bias is not None:
+        out = out + bias.astype(dtype)[None, :, None]
+    if relu:
+        out = np.where(out < 0, out.dtype.type(0), out)   # NaN stays NaN (torch.relu)
+    return out.reshape(B, -1, H, W)

@@ -94,3 +94,26 @@ def load_backward(name: str) -> dict:
                    for mode, scale, seed in d["coord_sets"]]
     d["weights"] = [dg.fmap(int(s), B, L * rd * rd, H, W, "normal") for s in d["weight_seeds"]]
     return d
+
+
+MOTION_CASES = ["motion_basic", "motion_small_b2"]
+
+
+def load_motion(name: str) -> dict:
+    """A lookup + convc1 golden (tests/golden/make_motion_golden.py) with its
+    inputs regenerated from the seeds: fmaps, coords, convc1 weight and bias."""
+    import datagen as dg
+    with np.load(GOLDEN / f"{name}.npz") as z:
+        d = {k: z[k] for k in z.files}
+    B, D, H, W, r, cout, cin, i = (int(v) for v in d["case"])
+    dist = str(d["dist"])
+    d.update(B=B, D=D, H=H, W=W, radius=r, cout=cout, cin=cin)
+    d["fmap1"] = dg.fmap(6000 + 10 * i, B, D, H, W, dist)
+    d["fmap2"] = dg.fmap(6001 + 10 * i, B, D, H, W, dist)
+    np.testing.assert_allclose([d["fmap1"].astype(np.float64).sum(),
+                                d["fmap2"].astype(np.float64).sum()], d["fmap_checksum"],
+                               rtol=0, atol=1e-6)
+    mode, scale = (str(v) for v in d["coord"])
+    d["coords"] = dg.coords(6002 + 10 * i, B, H, W, mode, float(scale))
+    d["weight"], d["bias"] = dg.conv1x1_weights(i, cout, cin)
+    return d

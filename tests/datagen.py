@@ -80,3 +80,11 @@ def coords(seed: int, B: int, H: int, W: int, mode: str = "normal", scale: float
     else:
         raise ValueError(mode)
     return (grid + d.reshape(B, 2, H, W)).astype(np.float32)
+
+
+def conv1x1_weights(i: int, cout: int, cin: int):
+    """Motion-encoder convc1 weight [cout, cin] ~ N(0, 1/cin) and bias [cout] ~
+    N(0, 0.25) for fixture case i (tests/golden/make_motion_golden.py)."""
+    w = fmap(5000 + 10 * i, 1, 1, cout, cin, "normal")[0, 0] / np.float32(np.sqrt(cin))
+    b = fmap(5001 + 10 * i, 1, 1, 1, cout, "normal")[0, 0, 0] * np.float32(0.5)
+    return w.astype(np.float32), b.astype(np.float32)

@@ -39,7 +39,8 @@ def test_header_declares_the_documented_entry_points():
         "dxr_pyramid_level_offset", "dxr_corr_pyramid_build", "dxr_corr_lookup",
         "dxr_avg_pool2x2", "dxr_alt_corr_forward", "dxr_alt_corr_lookup", "dxr_corr_volume",
         "dxr_pyramid_unpack", "dxr_pyramid_pack", "dxr_build_workspace_bytes",
-        "dxr_corr_lookup_backward", "dxr_pyramid_backward", "dxr_alt_corr_backward"}
+        "dxr_corr_lookup_backward", "dxr_pyramid_backward", "dxr_alt_corr_backward",
+        "dxr_conv1x1_packed_bytes", "dxr_conv1x1_pack_weight", "dxr_corr_lookup_conv1x1"}
 
 
 def test_library_exports_every_declared_symbol(nat):
@@ -63,7 +64,7 @@ def test_library_is_gfx950_code(nat):
 
 def test_abi_version_and_status_strings(nat):
     lib = nat.load()
-    assert lib.dxr_abi_version() == nat.ABI_VERSION == 2
+    assert lib.dxr_abi_version() == nat.ABI_VERSION == 3
     assert lib.dxr_status_string(0) == b"ok"
     assert lib.dxr_status_string(1) == b"invalid argument"
     assert lib.dxr_status_string(2) == b"unsupported by this build"
@@ -157,6 +158,18 @@ def test_host_side_validation_needs_no_gpu(nat):
     assert ab(P, P, None, P, P, P, 1, 8, 8, 8, 8, 64, 1, 4, None) == EINVAL  # null coords
     assert ab(P, P, P, P, None, P, 1, 8, 8, 8, 8, 64, 1, 4, None) == EINVAL  # null fmap1_grad
     assert ab(None, None, None, None, None, None, 0, 8, 8, 8, 8, 64, 1, 4, None) == OK
+    assert lib.dxr_conv1x1_packed_bytes(256, 324) == 336 * 256 * 4
+    assert lib.dxr_conv1x1_packed_bytes(0, 324) == -1
+    assert lib.dxr_conv1x1_pack_weight(P, 0, 324, P, None) == EINVAL
+    assert lib.dxr_conv1x1_pack_weight(None, 256, 324, P, None) == EINVAL
+    lc = lib.dxr_corr_lookup_conv1x1
+    assert lc(P, 0, 1, 8, 8, 4, -1, P, P, P, 256, 1, P, None) == EINVAL     # radius < 0
+    assert lc(P, 0, 1, 8, 8, 4, 2, P, P, P, 256, 1, P, None) == EUNSUP     # radius 2
+    assert lc(P, 0, 1, 8, 8, 4, 4, P, P, P, 100, 1, P, None) == EUNSUP     # Cout % 32
+    assert lc(P, 0, 1, 64, 64, 5, 4, P, P, P, 256, 1, P, None) == EUNSUP   # 5 levels
+    assert lc(P, 0, 1, 8, 8, 4, 4, P, None, P, 256, 1, P, None) == EINVAL  # null weights
+    assert lc(P, 7, 1, 8, 8, 4, 4, P, P, P, 256, 1, P, None) == EINVAL     # unknown dtype
+    assert lc(None, 0, 0, 8, 8, 4, 4, None, None, None, 256, 1, None, None) == OK
     pb = lib.dxr_pyramid_backward
     assert pb(P, 0, 1, 8, 8, 4, 0.0, P, None) == EINVAL                 # divisor 0
     assert pb(P, 0, 1, 7, 30, 4, 16.0, P, None) == EINVAL               # empty level

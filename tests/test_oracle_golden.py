@@ -207,3 +207,19 @@ def test_torch_restatement_matches_reference_forward(name):
         out = cb(torch.from_numpy(d[f"coords{k}"])).numpy()
         ref = d[f"out{k}"]
         assert np.abs(out - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("name", ["motion_basic", "motion_small_b2"])
+def test_oracle_motion_conv1x1(name):
+    """Lookup + ``F.relu(convc1(corr))`` (core/update.py:90 / :71) against the
+    reference encoder's output (tests/golden/make_motion_golden.py)."""
+    from conftest import load_motion
+    d = load_motion(name)
+    pyr = oracle.corr_pyramid(d["fmap1"], d["fmap2"], 4, np.float32)
+    corr = oracle.corr_lookup(pyr, d["coords"], d["radius"])
+    np.testing.assert_allclose(corr.astype(np.float64).sum(), d["corr_checksum"][0],
+                               rtol=1e-6, atol=1e-3)
+    got = oracle.motion_conv1x1(corr, d["weight"], d["bias"])
+    assert got.shape == d["out"].shape == (d["B"], d["cout"], d["H"], d["W"])
+    tolerance_check(got.astype(np.float32), d["out"], 1e-5)
+    assert (got == 0).any() and (got > 0).any()   # the ReLU clips part of the output
