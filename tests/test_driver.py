@@ -1,0 +1,123 @@
+"""CPU: the inference driver around the correlation path:
+InputPadder against the reference's own pad amounts (tests/golden/padder.json,
+made by tests/golden/make_padder_golden.py), the .flo format of
+core/utils/frame_utils.py:70-99, and the sharded pair loop with its flow gather
+at world size 2 (gloo; RCCL on GPUs)."""
+from __future__ import annotations
+
+import json
+import os
+import socket
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from dexiraft_amd.driver import FLO_TAG, InputPadder, infer_pairs, read_flo, write_flo
+
+GOLDEN = Path(__file__).resolve().parent / "golden" / "padder.json"
+
+
+@pytest.mark.parametrize("case", json.loads(GOLDEN.read_text()),
+                         ids=lambda c: f"{c['dims'][0]}x{c['dims'][1]}-{c['mode']}")
+def test_input_padder_matches_reference(case):
+    h, w = case["dims"]
+    p = InputPadder((1, 3, h, w), mode=case["mode"])
+    assert p._pad == case["pad"]
+    x = torch.arange(3 * h * w, dtype=torch.float32).reshape(1, 3, h, w)
+    (y,) = p.pad(x)
+    assert list(y.shape[-2:]) == case["padded"]
+    assert y.shape[-2] % 8 == 0 and y.shape[-1] % 8 == 0
+    assert float(y[..., :2, :2].sum()) == case["corner_sum"]
+    assert torch.equal(p.unpad(y), x) == case["roundtrip"] is True
+
+
+def test_flo_layout_and_roundtrip(tmp_path):
+    """Header float32 202021.25, int32 width, int32 height, then (u, v) pairs row by row."""
+    rng = np.random.default_rng(0)
+    uv = rng.standard_normal((5, 7, 2)).astype(np.float32)
+    f = tmp_path / "a.flo"
+    write_flo(f, uv)
+    raw = f.read_bytes()
+    assert len(raw) == 12 + 5 * 7 * 2 * 4
+    assert np.frombuffer(raw[:4], "<f4")[0] == np.float32(FLO_TAG)
+    assert np.frombuffer(raw[4:12], "<i4").tolist() == [7, 5]
+    body = np.frombuffer(raw[12:], "<f4").reshape(5, 14)
+    np.testing.assert_array_equal(body[:, 0::2], uv[..., 0])   # frame_utils.py:93-95
+    np.testing.assert_array_equal(body[:, 1::2], uv[..., 1])
+    np.testing.assert_array_equal(read_flo(f), uv)
+    write_flo(tmp_path / "b.flo", torch.from_numpy(uv).permute(2, 0, 1))   # [2, H, W] input
+    assert (tmp_path / "b.flo").read_bytes() == raw
+    (tmp_path / "bad.flo").write_bytes(b"\0" * 16)
+    with pytest.raises(ValueError):
+        read_flo(tmp_path / "bad.flo")
+
+
+class ToyModel:
+    """Stands in for RAFT(test_mode=True) (core/raft.py:192-193): flow = a fixed
+    function of the padded pair, so sharded and single-process runs must agree."""
+
+    def __call__(self, a, b, iters=12, test_mode=True):
+        assert test_mode and a.shape[-2] % 8 == 0 and a.shape[-1] % 8 == 0
+        flow = torch.stack([(a - b).mean(1)[0], (a * b).mean(1)[0] * iters])[None]
+        return flow[..., ::8, ::8], flow
+
+
+def _pairs(P=5, H=20, W=30):
+    g = torch.Generator().manual_seed(3)
+    return torch.rand((P, 3, H, W), generator=g), torch.rand((P, 3, H, W), generator=g)
+
+
+def test_infer_pairs_single_process(tmp_path):
+    i1, i2 = _pairs()
+    paths = [tmp_path / f"frame{k:04d}.flo" for k in range(5)]
+    flows = infer_pairs(ToyModel(), i1, i2, iters=4, flo_paths=paths)
+    assert flows.shape == (5, 2, 20, 30)
+    padder = InputPadder(i1.shape)
+    for k in range(5):
+        a, b = padder.pad(i1[k:k + 1], i2[k:k + 1])
+        ref = padder.unpad(ToyModel()(a, b, iters=4)[1][0])
+        assert torch.equal(flows[k], ref)
+        np.testing.assert_array_equal(read_flo(paths[k]), ref.permute(1, 2, 0).numpy())
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_dir, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        i1, i2 = _pairs()
+        paths = [Path(out_dir) / f"frame{k:04d}.flo" for k in range(5)]
+        flows = infer_pairs(ToyModel(), i1, i2, iters=4, flo_paths=paths)
+        local = infer_pairs(ToyModel(), i1, i2, iters=4, gather=False)
+        q.put((rank, flows.numpy(), local.shape[0]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_infer_pairs_world2_gathers_every_flow(tmp_path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    res = sorted((q.get(timeout=10) for _ in range(2)), key=lambda r: r[0])
+    ref = infer_pairs(ToyModel(), *_pairs(), iters=4).numpy()
+    for rank, flows, n_local in res:
+        np.testing.assert_array_equal(flows, ref)
+    assert [r[2] for r in res] == [3, 2]          # pair_range(5, 2, r)
+    for k in range(5):                              # every pair written once, by its owner
+        np.testing.assert_array_equal(read_flo(tmp_path / f"frame{k:04d}.flo"),
+                                      ref[k].transpose(1, 2, 0))
