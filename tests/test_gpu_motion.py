@@ -147,3 +147,37 @@ def test_fused_unsupported_and_grad_raise(dx):
         cb.lookup_conv1x1(c, w)
     with torch.no_grad():
         assert cb.lookup_conv1x1(c, w).shape == (1, 256, 16, 16)
+
+
+@pytest.mark.parametrize("levels,r", [(1, 4), (2, 4), (3, 3)])
+def test_fused_fewer_levels(dx, levels, r):
+    """num_levels < 4 (Cin = L*(2r+1)^2 padded to whole k steps inside the kernel)."""
+    B, D, H, W = 2, 64, 19, 27
+    f1, f2 = _t(dg.fmap(80, B, D, H, W, "fnet")), _t(dg.fmap(81, B, D, H, W, "fnet"))
+    c = _t(dg.coords(82, B, H, W, "normal", 3.0))
+    cin = levels * (2 * r + 1) ** 2
+    w = _t(dg.fmap(83, 1, 1, 64, cin)[0, 0] / np.float32(np.sqrt(cin)))
+    b = _t(dg.fmap(84, 1, 1, 1, 64)[0, 0, 0])
+    cb = dx.CorrBlock(f1, f2, num_levels=levels, radius=r)
+    got = cb.lookup_conv1x1(c, w, b).cpu().numpy()
+    tolerance_check(got, _ref64(cb(c), w, b).astype(np.float32), RTOL)
+
+
+def test_fused_far_and_nan_coords(dx):
+    """Far coordinates give zero samples (bias only); a NaN coordinate makes that
+    pixel's samples NaN, so its outputs are NaN exactly where the unfused path's are."""
+    B, D, H, W = 1, 64, 16, 24
+    f1, f2 = _t(dg.fmap(90, B, D, H, W)), _t(dg.fmap(91, B, D, H, W))
+    c = dg.coords(92, B, H, W, "normal", 2.0)
+    c[0, 0, 3, 5] = 1e6           # far
+    c[0, 1, 7, 9] = np.nan        # non-finite
+    c = _t(c)
+    w = _t(dg.fmap(93, 1, 1, 256, 324)[0, 0] / np.float32(18.0))
+    b = _t(dg.fmap(94, 1, 1, 1, 256)[0, 0, 0])
+    cb = dx.CorrBlock(f1, f2)
+    corr = cb(c)
+    got = cb.lookup_conv1x1(c, w, b, relu=False).cpu().numpy()
+    ref = _ref64(corr, w, b, relu=False).astype(np.float32)
+    tolerance_check(got, ref, RTOL)       # identical NaN pattern, finite entries within 1e-4
+    np.testing.assert_allclose(got[0, :, 3, 5], b.cpu().numpy(), rtol=0, atol=1e-6)
+    assert np.isnan(got[0, :, 7, 9]).all()
