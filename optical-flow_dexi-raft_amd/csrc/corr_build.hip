@@ -1265,7 +1265,11 @@ int build_variant();
 
 // bf16 variants: 0 default (3 waves/SIMD, XCD-aware page order: r01 KITTI b8
 // 721 us vs 837 in grid order; the scalar-staging path keeps the compiler's
-// choice, it would spill at 3); 1 compiler-chosen occupancy; 3 grid order.
+// choice, it would spill at 3); 1 compiler-chosen occupancy; 3 grid order;
+// 6 = 0 at 2 waves/SIMD.  Tried and removed (r01, KITTI b8): operand stages two
+// ahead from two register sets, with all 20 fragment reads of a stage issued
+// before its MFMAs: 660-704 us vs 645-662 — the K loop is not load- or
+// LDS-latency-bound.
 template <typename OT>
 int launch_build_bf16(bool vec, const uint16_t* f1, const uint16_t* f2, OT* pyr,
                       const BuildGeom& g, int B, hipStream_t stream) {
@@ -1274,6 +1278,8 @@ int launch_build_bf16(bool vec, const uint16_t* f1, const uint16_t* f2, OT* pyr,
   if (!vec) return launch_bf16_w<false, 0>(f1, f2, pyr, g, grid, stream);
   if (build_variant() == 1) return launch_bf16_w<true, 0>(f1, f2, pyr, g, grid, stream);
   if (build_variant() == 3) return launch_bf16_w<true, 3>(f1, f2, pyr, g, grid, stream);
+  if (build_variant() == 6)  // 2 waves/SIMD: 628-640 vs 645-662 us (KITTI b8, within noise)
+    return launch_bf16_w<true, 2, OT, true>(f1, f2, pyr, g, remap_grid(g, B), stream);
   return launch_bf16_w<true, 3, OT, true>(f1, f2, pyr, g, remap_grid(g, B), stream);
 }
 

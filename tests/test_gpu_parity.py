@@ -347,10 +347,12 @@ def test_bf16_kitti_shape(dx):
     assert np.abs(got - d["out0_val"]).max() <= BF16_RTOL * float(d["out0_maxabs"])
 
 
-@pytest.mark.parametrize("variant", ["1", "3"])
-def test_bf16_build_variants_bit_identical(dx, variant, monkeypatch):
-    """bf16 build variants (occupancy; XCD-aware page order) write the same bits."""
-    f1, f2 = _pair(B=3, H=47, W=100, seed=121, dist="fnet")
+@pytest.mark.parametrize("variant", ["1", "3", "6"])
+@pytest.mark.parametrize("D", [256, 96])
+def test_bf16_build_variants_bit_identical(dx, variant, D, monkeypatch):
+    """bf16 build variants (occupancy; XCD-aware page order; an odd stage count
+    at D = 96) write the same bits."""
+    f1, f2 = _pair(B=3, D=D, H=47, W=100, seed=121, dist="fnet")
     f1, f2 = f1.bfloat16(), f2.bfloat16()
     monkeypatch.setenv("DXR_BUILD_VARIANT", "0")
     ref = dx.CorrBlock(f1, f2).corr_pyramid
