@@ -186,6 +186,9 @@ def main():
     ap.add_argument("--mode", default="graph", choices=["graph", "eager"])
     ap.add_argument("--block", default="corr", choices=["corr", "alt"],
                     help="corr: CorrBlock (full pyramid); alt: AlternateCorrBlock (on the fly, C5)")
+    ap.add_argument("--layout", default="nchw", choices=["nchw", "nhwc"],
+                    help="fmap memory format: nchw (the reference's) or nhwc (channels-last "
+                         "encoders, SURVEY §8(f) row 4)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -206,6 +209,9 @@ def main():
         B = args.batch or b_default
     dtype = args.dtype or dt_default
     f1, f2, coords = make_inputs(B, H, W, dtype, seed=1234 + rank, dev=dev)
+    if args.layout == "nhwc":
+        f1 = f1.contiguous(memory_format=torch.channels_last)
+        f2 = f2.contiguous(memory_format=torch.channels_last)
     stream = torch.cuda.Stream(device=dev)
 
     state = {}
@@ -286,7 +292,8 @@ def main():
                 "workload": f"{'CorrBlock' if args.block == 'corr' else 'AlternateCorrBlock'} "
                             f"build + {ITERS} lookups, {args.workload} "
                             f"{img_h}x{img_w} (fmap {H}x{W}), D={D}, r={RADIUS}, L={LEVELS}",
-                "pairs_per_gpu": B, "mode": args.mode, "parallelism": f"pairs sharded x{world}",
+                "pairs_per_gpu": B, "fmap_layout": args.layout, "mode": args.mode,
+                "parallelism": f"pairs sharded x{world}",
                 "kernel_timing": timing,
             },
         }

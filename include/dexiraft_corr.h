@@ -24,6 +24,9 @@
  *                            backward (autograd of CorrBlock.__init__)
  *   dxr_avg_pool2x2          core/corr.py:69-71  F.avg_pool2d(fmap, 2, stride=2)
  *                            in AlternateCorrBlock.__init__
+ *   dxr_avg_pool2x2_nhwc     core/corr.py:70-71 the same pool on channels-last fmaps
+ *   dxr_transpose            core/corr.py:82-83 fmap.permute(0, 2, 3, 1).contiguous()
+ *                            (NCHW <-> NHWC)
  *   dxr_alt_corr_forward     alt_cuda_corr/correlation.cpp:23-33 `forward`
  *                            (alt_cuda_corr/correlation_kernel.cu:260-286)
  *   dxr_alt_corr_backward    alt_cuda_corr/correlation.cpp:36-48 `backward`
@@ -68,7 +71,7 @@ extern "C" {
 /* HIP's own definition; repeating an identical typedef is legal in C11/C++. */
 typedef struct ihipStream_t* hipStream_t;
 
-#define DXR_ABI_VERSION 3
+#define DXR_ABI_VERSION 4
 
 enum dxr_status {
   DXR_OK = 0,
@@ -215,6 +218,23 @@ int dxr_pyramid_backward(const void* grad_pyramid, int grad_dtype,
  */
 int dxr_avg_pool2x2(const float* in, float* out, int64_t planes,
                     int64_t H, int64_t W, hipStream_t stream);
+
+/*
+ * Channels-last fmaps.
+ *
+ * dxr_transpose: batched [B, rows, cols] -> [B, cols, rows] of float32
+ * (dtype DXR_F32) or bfloat16 (DXR_BF16) elements; NCHW -> NHWC is rows = C,
+ * cols = H*W (core/corr.py:82-83 `permute(0, 2, 3, 1).contiguous()`), NHWC ->
+ * NCHW the reverse.  Bit-exact.
+ *
+ * dxr_avg_pool2x2_nhwc: F.avg_pool2d(x, 2, stride=2) (core/corr.py:70-71) of a
+ * channels-last [B, H, W, C] float32 tensor into [B, H/2, W/2, C]; bit-identical
+ * to dxr_avg_pool2x2 on the NCHW tensor (same four values, same summation order).
+ */
+int dxr_transpose(const void* in, void* out, int dtype, int64_t B, int64_t rows,
+                  int64_t cols, hipStream_t stream);
+int dxr_avg_pool2x2_nhwc(const float* in, float* out, int64_t B, int64_t H,
+                         int64_t W, int64_t C, hipStream_t stream);
 
 /*
  * Stage (d), reference-FFI form: alt_cuda_corr.forward(fmap1, fmap2, coords,

@@ -15,7 +15,7 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_PATH = Path(__file__).resolve().with_name("libdexiraft_corr.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 DXR_OK, DXR_EINVAL, DXR_EUNSUPPORTED, DXR_EHIP = 0, 1, 2, -1
 DXR_F32, DXR_BF16 = 0, 1
@@ -49,6 +49,8 @@ SIGNATURES: dict[str, tuple[object, list[object]]] = {
     "dxr_conv1x1_pack_weight": (_int, [_vp, _i64, _i64, _vp, _vp]),
     "dxr_corr_lookup_conv1x1": (_int, [_vp, _int, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp,
                                        _i64, _int, _vp, _vp]),
+    "dxr_transpose": (_int, [_vp, _vp, _int, _i64, _i64, _i64, _vp]),
+    "dxr_avg_pool2x2_nhwc": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _vp]),
     "dxr_alt_corr_lookup": (_int, [_vp, ctypes.POINTER(_vp), _vp, _vp, _i64, _i64, _i64, _i64,
                                    _int, _int, _f32, _vp]),
 }

@@ -176,6 +176,63 @@ def _level_sizes(H: int, W: int, num_levels: int) -> list[tuple[int, int]]:
     return sizes
 
 
+def _channels_last(t: torch.Tensor) -> bool:
+    """A channels-last (NHWC-strided) 4-D fmap that is not also NCHW-contiguous."""
+    return t.is_contiguous(memory_format=torch.channels_last) and not t.is_contiguous()
+
+
+def _dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return nat.DXR_F32
+    if t.dtype == torch.bfloat16:
+        return nat.DXR_BF16
+    raise RuntimeError(f"fmaps must be float32 or bfloat16, got {t.dtype}")
+
+
+def _nchw(t: torch.Tensor) -> torch.Tensor:
+    """NCHW-contiguous fmap (no autograd graph: callers use it only without grad).
+
+    Channels-last fmaps (encoders emitting NHWC) go through
+    one native tiled transpose (``dxr_transpose``); other layouts through
+    ``.contiguous()`` (a no-op for the reference's own NCHW fmaps).
+    """
+    if not _channels_last(t):
+        return t.contiguous()
+    B, D, H, W = (int(s) for s in t.shape)
+    out = torch.empty((B, D, H, W), dtype=t.dtype, device=t.device)
+    with _Launch(t.device):
+        st = nat.load().dxr_transpose(t.data_ptr(), out.data_ptr(), _dtype_code(t), B, H * W, D,
+                                      nat.stream_of(t))
+    nat.check(st, "NHWC -> NCHW fmap (dxr_transpose)")
+    return out
+
+
+def _nhwc(t: torch.Tensor) -> torch.Tensor:
+    """``t.permute(0, 2, 3, 1).contiguous()`` (core/corr.py:82-83): a free view of a
+    channels-last fmap, one native tiled transpose (``dxr_transpose``) otherwise."""
+    if _channels_last(t):
+        return t.permute(0, 2, 3, 1)
+    t = t.contiguous()
+    B, D, H, W = (int(s) for s in t.shape)
+    out = torch.empty((B, H, W, D), dtype=t.dtype, device=t.device)
+    with _Launch(t.device):
+        st = nat.load().dxr_transpose(t.data_ptr(), out.data_ptr(), _dtype_code(t), B, D, H * W,
+                                      nat.stream_of(t))
+    nat.check(st, "NCHW -> NHWC fmap (dxr_transpose)")
+    return out
+
+
+def _pool_nhwc(t: torch.Tensor) -> torch.Tensor:
+    """F.avg_pool2d(x, 2, stride=2) of a channels-last fmap held as [B, H, W, C]."""
+    B, H, W, C = (int(s) for s in t.shape)
+    out = torch.empty((B, H // 2, W // 2, C), dtype=t.dtype, device=t.device)
+    with _Launch(t.device):
+        st = nat.load().dxr_avg_pool2x2_nhwc(t.data_ptr(), out.data_ptr(), B, H, W, C,
+                                             nat.stream_of(t))
+    nat.check(st, "AlternateCorrBlock pooling (dxr_avg_pool2x2_nhwc)")
+    return out
+
+
 class _Launch:
     """Runs a native call with fmap's device current (multi-GPU processes)."""
 
@@ -271,8 +328,10 @@ class CorrBlock:
         lib = nat.load()
         numel = lib.dxr_pyramid_numel(B, H, W, num_levels)
         self._buf = torch.empty(numel, dtype=pyr_torch, device=fmap1.device)
-        f1 = fmap1.contiguous()
-        f2 = fmap2.contiguous()
+        if _wants_grad(fmap1, fmap2):
+            f1, f2 = fmap1.contiguous(), fmap2.contiguous()   # tracked by autograd
+        else:
+            f1, f2 = _nchw(fmap1), _nchw(fmap2)
         # Split-plane workspace (f32 fmaps): a temporary from torch's caching
         # allocator, released in stream order after the build's kernels.
         ws_bytes = lib.dxr_build_workspace_bytes(B, D, H, W, in_dt)
@@ -393,7 +452,7 @@ class CorrBlock:
         if fmap1.dtype != torch.float32:
             raise RuntimeError(f"CorrBlock.corr expects float32 fmaps, got {fmap1.dtype}")
         out = torch.empty((B, H, W, 1, H, W), dtype=torch.float32, device=fmap1.device)
-        f1, f2 = fmap1.contiguous(), fmap2.contiguous()
+        f1, f2 = _nchw(fmap1), _nchw(fmap2)
         lib = nat.load()
         with _Launch(fmap1.device):
             st = lib.dxr_corr_volume(f1.data_ptr(), f2.data_ptr(), nat.DXR_F32, B, D, H, W,
@@ -428,26 +487,38 @@ class AlternateCorrBlock:
         self._geom = (B, D, H, W)
         self._token = None   # never differentiable (see the check above)
         self._device = fmap1.device
-        lib = nat.load()
-        f1, f2 = fmap1.contiguous(), fmap2.contiguous()
-        self.pyramid = [(f1, f2)]
-        with _Launch(self._device):
-            stream = nat.stream_of(f1)
-            for _ in range(num_levels):
-                p1, p2 = self.pyramid[-1]
-                h, w = p1.shape[-2:]
-                q1 = torch.empty((B, D, h // 2, w // 2), dtype=torch.float32, device=f1.device)
-                q2 = torch.empty_like(q1)
-                for src, dst in ((p1, q1), (p2, q2)):
-                    st = lib.dxr_avg_pool2x2(src.data_ptr(), dst.data_ptr(), B * D, h, w, stream)
-                    nat.check(st, "AlternateCorrBlock pooling (dxr_avg_pool2x2)")
-                self.pyramid.append((q1, q2))
-        # Channels-last copies once per block (the reference re-permutes on every
-        # call, core/corr.py:82-83): one coalesced 1 KiB vector per cell.
-        self._f1_nhwc = f1.permute(0, 2, 3, 1).contiguous()
-        self._f2_nhwc = [self.pyramid[i][1].permute(0, 2, 3, 1).contiguous()
-                         for i in range(num_levels)]
+        # NHWC operands (core/corr.py:82-83 permutes on every call; here once per
+        # block): a free view of channels-last fmaps, one tiled transpose otherwise.
+        # Only full-res fmap1 and the pooled fmap2 levels are used (core/corr.py:82-83),
+        # so only those are pooled; ``pyramid`` materialises the rest on demand.
+        self._fmaps = (fmap1, fmap2)
+        self._pyramid = None
+        self._f1_nhwc = _nhwc(fmap1)
+        self._f2_nhwc = [_nhwc(fmap2)]
+        for _ in range(1, num_levels):
+            self._f2_nhwc.append(_pool_nhwc(self._f2_nhwc[-1]))
         self._f2_ptrs = (ctypes.c_void_p * num_levels)(*[t.data_ptr() for t in self._f2_nhwc])
+
+    @property
+    def pyramid(self):
+        """The reference's ``pyramid`` (core/corr.py:66-72): ``num_levels + 1`` pairs
+        ``(fmap1_i, fmap2_i)`` of 2x2-pooled fmaps, ``[B, D, H_i, W_i]`` float32.
+
+        Entry 0 is the caller's fmaps; the pooled entries are channels-last
+        tensors (values bit-identical to F.avg_pool2d), materialised on first access
+        — the lookup needs only full-res fmap1 and fmap2's first num_levels levels.
+        """
+        if self._pyramid is None:
+            p1 = [self._f1_nhwc]
+            p2 = list(self._f2_nhwc)
+            while len(p1) < self.num_levels + 1:
+                p1.append(_pool_nhwc(p1[-1]))
+            while len(p2) < self.num_levels + 1:
+                p2.append(_pool_nhwc(p2[-1]))
+            pyr = [self._fmaps]
+            pyr += [(a.permute(0, 3, 1, 2), b.permute(0, 3, 1, 2)) for a, b in zip(p1[1:], p2[1:])]
+            self._pyramid = pyr
+        return self._pyramid
 
     def __call__(self, coords):
         B, D, H, W = self._geom

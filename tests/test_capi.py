@@ -40,7 +40,8 @@ def test_header_declares_the_documented_entry_points():
         "dxr_avg_pool2x2", "dxr_alt_corr_forward", "dxr_alt_corr_lookup", "dxr_corr_volume",
         "dxr_pyramid_unpack", "dxr_pyramid_pack", "dxr_build_workspace_bytes",
         "dxr_corr_lookup_backward", "dxr_pyramid_backward", "dxr_alt_corr_backward",
-        "dxr_conv1x1_packed_bytes", "dxr_conv1x1_pack_weight", "dxr_corr_lookup_conv1x1"}
+        "dxr_conv1x1_packed_bytes", "dxr_conv1x1_pack_weight", "dxr_corr_lookup_conv1x1",
+        "dxr_transpose", "dxr_avg_pool2x2_nhwc"}
 
 
 def test_library_exports_every_declared_symbol(nat):
@@ -64,7 +65,7 @@ def test_library_is_gfx950_code(nat):
 
 def test_abi_version_and_status_strings(nat):
     lib = nat.load()
-    assert lib.dxr_abi_version() == nat.ABI_VERSION == 3
+    assert lib.dxr_abi_version() == nat.ABI_VERSION == 4
     assert lib.dxr_status_string(0) == b"ok"
     assert lib.dxr_status_string(1) == b"invalid argument"
     assert lib.dxr_status_string(2) == b"unsupported by this build"
@@ -136,6 +137,15 @@ def test_host_side_validation_needs_no_gpu(nat):
     assert lib.dxr_avg_pool2x2(P, P, -1, 8, 8, None) == EINVAL
     assert lib.dxr_avg_pool2x2(None, None, 0, 8, 8, None) == OK
     assert lib.dxr_avg_pool2x2(P, P, 3, 1, 8, None) == OK               # nothing to pool
+    tr = lib.dxr_transpose
+    assert tr(P, P, 2, 1, 8, 8, None) == EINVAL                         # unknown dtype
+    assert tr(P, P, 0, -1, 8, 8, None) == EINVAL
+    assert tr(None, None, 0, 1, 0, 8, None) == OK                       # empty
+    assert tr(None, P, 1, 1, 8, 8, None) == EINVAL                      # null input
+    pn = lib.dxr_avg_pool2x2_nhwc
+    assert pn(P, P, 1, 8, 8, 0, None) == EINVAL                         # no channels
+    assert pn(None, None, 1, 1, 8, 64, None) == OK                      # nothing to pool
+    assert pn(None, P, 1, 8, 8, 64, None) == EINVAL
     af = lib.dxr_alt_corr_forward
     assert af(P, P, P, P, 1, 8, 8, 8, 8, 64, 1, -1, None) == EINVAL
     assert af(P, P, P, P, 1, 8, 8, 8, 8, 64, 1, 7, None) == EUNSUP
