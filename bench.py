@@ -147,30 +147,53 @@ def make_inputs(B, H, W, dtype, seed, dev):
     return f1, f2, coords
 
 
-def cpu_baseline(H, W, budget_s):
-    """Time the numpy oracle (oracle/, float32: the reference's op sequence —
-    matmul, /sqrt(D), 3x 2x2 avg-pool, 12 x 4-level bilinear lookups) on host cores."""
+def cpu_baseline(H, W, budget_s, impl="torch"):
+    """Time the reference's op sequence on host cores over a bounded sample.
+
+    impl "torch" (default; SURVEY.md §8(d) "CPU reference timing"): the plain-PyTorch
+    restatement tests/torch_ref.py (bmm, / sqrt(D), 3x F.avg_pool2d, 12 x 4
+    F.grid_sample + cat + permute — core/corr.py's ops, pinned to the reference's
+    goldens) on torch's CPU threads.  impl "numpy": the numpy oracle (oracle/,
+    float32), matmul on BLAS threads, lookups single-threaded.
+    """
     sys.path.insert(0, str(REPO / "tests"))
     import datagen as dg
-    import oracle
-    from threadpoolctl import threadpool_info
     f1 = dg.fmap(0, 1, D, H, W)
     f2 = dg.fmap(1, 1, D, H, W)
     cs = [dg.coords(100 + k, 1, H, W, "normal", 4.0) for k in range(ITERS)]
-    pairs, t0 = 0, time.perf_counter()
-    while True:
-        pyr = oracle.corr_pyramid(f1, f2, LEVELS, np.float32)
-        for c in cs:
-            oracle.corr_lookup(pyr, c, RADIUS)
-        pairs += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or pairs >= 50:
-            break
-    threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    if impl == "torch":
+        import torch_ref
+        threads = torch.get_num_threads()
+        t1, t2 = torch.from_numpy(f1), torch.from_numpy(f2)
+        tc = [torch.from_numpy(c) for c in cs]
+
+        def one_pair():
+            blk = torch_ref.TorchCorrBlock(t1, t2, LEVELS, RADIUS)
+            for c in tc:
+                blk(c)
+        what = f"torch CPU restatement of core/corr.py (tests/torch_ref.py), {threads} torch threads"
+    else:
+        import oracle
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+
+        def one_pair():
+            pyr = oracle.corr_pyramid(f1, f2, LEVELS, np.float32)
+            for c in cs:
+                oracle.corr_lookup(pyr, c, RADIUS)
+        what = f"numpy float32 oracle; matmul on {threads} BLAS threads, lookups single-threaded"
+    with torch.no_grad():
+        one_pair()                                   # warm-up (allocator, thread pool)
+        pairs, t0 = 0, time.perf_counter()
+        while True:
+            one_pair()
+            pairs += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s or pairs >= 50:
+                break
     return {"value": pairs / el, "unit": "pairs/s", "cores": threads, "kind": "port",
             "sample": f"{pairs} pair(s) of fmap {H}x{W}, D={D}: build + {ITERS} lookups, "
-                      f"numpy float32 oracle, {el:.1f} s; matmul on {threads} BLAS threads, "
-                      f"lookups single-threaded"}
+                      f"{el:.1f} s; {what}"}
 
 
 def main():
@@ -191,6 +214,8 @@ def main():
                          "encoders, SURVEY §8(f) row 4)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-impl", default="torch", choices=["torch", "numpy"],
+                    help="CPU baseline: torch restatement of core/corr.py (default) or numpy oracle")
     args = ap.parse_args()
 
     world, rank, local = init_dist()
@@ -358,7 +383,7 @@ def main():
                 "pool_and_layout_us_per_step": round(build_ms * 1e3, 2),
             }
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(H, W, args.cpu_seconds)
+            res["cpu_baseline"] = cpu_baseline(H, W, args.cpu_seconds, args.cpu_impl)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
