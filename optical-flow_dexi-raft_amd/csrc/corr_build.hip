@@ -1269,7 +1269,8 @@ int build_variant();
 // 6 = 0 at 2 waves/SIMD.  Tried and removed (r01, KITTI b8): operand stages two
 // ahead from two register sets, with all 20 fragment reads of a stage issued
 // before its MFMAs: 660-704 us vs 645-662 — the K loop is not load- or
-// LDS-latency-bound.
+// LDS-latency-bound.  64-deep K stages (half the barriers, 80 KB LDS, 2 workgroups
+// per CU): 862 vs 669 us at KITTI b8, 108 vs 86 us at Sintel — nor barrier-bound.
 template <typename OT>
 int launch_build_bf16(bool vec, const uint16_t* f1, const uint16_t* f2, OT* pyr,
                       const BuildGeom& g, int B, hipStream_t stream) {
