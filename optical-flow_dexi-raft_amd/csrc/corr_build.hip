@@ -1263,7 +1263,8 @@ int launch_bf16_w(const uint16_t* f1, const uint16_t* f2, OT* pyr, const BuildGe
 
 int build_variant();
 
-// bf16 variants: 0 default (3 waves/SIMD, XCD-aware page order: r01 KITTI b8
+// bf16 variants: 0 default (launch bound 3 waves/SIMD; compiled at 120 VGPRs = 4,
+// matching the 4 workgroups per CU its 40 KB of LDS allows; XCD-aware page order: r01 KITTI b8
 // 721 us vs 837 in grid order; the scalar-staging path keeps the compiler's
 // choice, it would spill at 3); 1 compiler-chosen occupancy; 3 grid order;
 // 6 = 0 at 2 waves/SIMD.  Tried and removed (r01, KITTI b8): operand stages two
