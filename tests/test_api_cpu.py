@@ -62,3 +62,29 @@ def test_coords_grid_matches_reference_definition():
 def test_sqrt_dim_is_the_references_float32_sqrt(dim):
     from dexiraft_amd.corr import _sqrt_dim
     assert _sqrt_dim(dim) == float(torch.sqrt(torch.tensor(dim).float()))
+
+
+def test_channels_last_classification():
+    """Which fmaps take the native layout path: NHWC-strided
+    4-D tensors that are not also NCHW-contiguous (degenerate shapes are both)."""
+    from dexiraft_amd.corr import _channels_last
+    x = torch.zeros(2, 8, 5, 7)
+    assert not _channels_last(x)
+    assert _channels_last(x.contiguous(memory_format=torch.channels_last))
+    assert not _channels_last(torch.zeros(2, 1, 5, 7).contiguous(memory_format=torch.channels_last))
+    assert not _channels_last(x.transpose(2, 3))                      # other strides: .contiguous()
+
+
+def test_host_channels_last_fmaps_raise():
+    f = torch.zeros(1, 16, 16, 16).contiguous(memory_format=torch.channels_last)
+    for ctor in (dx.CorrBlock, dx.AlternateCorrBlock):
+        with pytest.raises(RuntimeError):
+            ctor(f, f)
+
+
+def test_bench_cpu_baseline_torch_restatement():
+    """bench.py's cpu_baseline leg: the torch restatement of core/corr.py, bounded."""
+    import bench
+    res = bench.cpu_baseline(8, 12, 0.05, "torch")
+    assert res["kind"] == "port" and res["unit"] == "pairs/s" and res["value"] > 0
+    assert res["cores"] >= 1 and "torch_ref" in res["sample"]
