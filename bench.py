@@ -7,19 +7,23 @@ lookups with 12 different coordinate sets, exactly the reference's per-forward
 usage (core/raft.py:147, :169-173).  Inputs (fmaps [B,256,H/8,W/8] float32,
 coords = grid + N(0, 4^2) px) are synthetic and resident in HBM before timing.
 
-Launch: ``python bench.py [--gpus N --steps K --warmup W]``; for N > 1 the driver
-runs it under torch.distributed.run, one rank per GPU.  Pairs are independent,
-so each rank processes its own pairs (weak scaling, no collective on the data
-path); ranks are bracketed by barriers and the max elapsed time over ranks is
-used.  Rank 0 prints ONE JSON line.
+Launch: ``python bench.py [--gpus N --steps K --warmup W]``.  With ``--gpus N > 1``
+and no WORLD_SIZE in the environment, this process starts
+``torch.distributed.run`` with N ranks (one per GPU, RCCL) as a child before it
+touches any GPU, and exits with its status; under a launcher, WORLD_SIZE must
+equal --gpus.  Pairs are independent, so each rank processes its own pairs (weak
+scaling, no collective on the data path); ranks are bracketed by barriers and
+the max elapsed time over ranks is used.  After timing, a float64 checksum of
+every pair's 12th lookup output is all-gathered over RCCL (shard.gather_pairs)
+and reported.  Rank 0 prints ONE JSON line.
 
-Execution: the step is captured into two HIP graphs (build, lookups) and
-replayed — the launch-bound lookups would otherwise be host-bound in Python.
-HIP events between the two replays give the build kernel's duration inside the
-timed region (the roofline's ``achieved``; it includes the graph launch, so it
-reads a few percent above the rocprofv3 kernel duration — conservative).
-(Event-record nodes inside one K-step graph would exclude it, but ROCm torch
-refuses external events and raw hipEventRecord nodes did not record: r01.)
+Execution (``--mode graph``, default): ``value`` is timed on ONE HIP graph per
+step (build + 12 lookups), replayed K times — the launch-bound lookups would
+otherwise be host-bound in Python.  Kernel durations for the rooflines come from
+two more graphs timed with HIP events on the launch stream: KB back-to-back
+builds and 4 x 12 back-to-back lookups, each divided by its launch count, so the
+graph-launch cost is amortised and what remains per launch is the kernel plus
+one same-stream kernel boundary (~1.5 us, MI355X_MICROARCH.md "boundary").
 ``--mode eager`` times plain Python calls instead.
 """
 from __future__ import annotations
@@ -27,6 +31,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -42,6 +48,7 @@ METRIC = "frame pairs/sec (corr build + 12 lookups) @436x1024, 1–8 GPU; % MFMA
 PEAK_F32_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 PEAK_BF16_TFLOPS = 2500.0    # dense BF16 MFMA
 PEAK_HBM_GBS = 8000.0        # HBM3E spec
+SPLIT_PRODUCTS = 6           # bf16 MFMA products per f32 product in the split build
 
 # name -> (image H, W after InputPadder, fmap H, W, default pairs per GPU, dtype)
 WORKLOADS = {
@@ -51,6 +58,8 @@ WORKLOADS = {
     "1080p": ((1088, 1920), (136, 240), 1, "f32"),
 }
 D, RADIUS, LEVELS, ITERS = 256, 4, 4, 12
+KB_BUILDS = 8                # builds per kernel-timing graph
+KL_REPS = 4                  # x 12 lookups per kernel-timing graph
 
 
 def level_sizes(H, W, L=LEVELS):
@@ -80,16 +89,17 @@ def lookup_bytes(B, H, W, s_pyr=4):
 
 
 def build_kernel(dtype, H, W):
-    """Which build kernel the library runs for this workload (csrc/corr_build.hip
-    launch_build_f32 / launch_build_bf16), and the MFMA work it executes per
-    algorithmic flop: the split f32 build issues six bf16 MFMA products per f32
-    product (exact hi+mid+lo operand split, f32 accumulation)."""
-    variant = os.environ.get("DXR_BUILD_VARIANT", "0")
+    """The build kernel the library runs for this workload (csrc/corr_build.hip
+    launch_build_f32 / launch_build_bf16) and the ceiling of the arithmetic it
+    runs: the split f32 build issues six bf16 MFMA products per f32 product
+    (exact hi+mid+lo operand split, f32 accumulation), so its binding ceiling is
+    2.5 PF / 6 = 417 TF f32-equivalent; the f32 peak (157.3 TF) is §8(d)'s."""
     if dtype == "bf16":
         return "corr_build_bf16_kernel", 1, PEAK_BF16_TFLOPS, "bf16"
-    if D % 16 == 0 and W % 2 == 0 and variant in ("0", "7", "8", "9", "40"):
+    if D % 16 == 0 and W % 2 == 0:
         return ("corr_build_split_kernel (f32 operands split exactly into 3 bf16, "
-                "bf16x6 MFMA, f32 accumulate)", 6, PEAK_BF16_TFLOPS, "bf16 MFMA, f32 accumulate")
+                "bf16x6 MFMA, f32 accumulate)", SPLIT_PRODUCTS, PEAK_BF16_TFLOPS,
+                "bf16 MFMA, f32 accumulate")
     return "corr_build_f32_kernel", 1, PEAK_F32_TFLOPS, "f32"
 
 
@@ -103,7 +113,9 @@ def pmc_traffic(workload, kernel_prefix):
     this workload (profiles/<round>/traffic*.json, written by
     scripts/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes
     of this bench), or None when that workload was not profiled."""
-    files = sorted((REPO / "profiles").glob("*/traffic*.json"))
+    files = sorted((REPO / "profiles").glob("*/traffic*.json")) + \
+        sorted((REPO / "profiles").glob("*/*/traffic*.json"))
+    files.sort(key=lambda f: f.relative_to(REPO / "profiles").parts[0])
     for f in reversed(files):
         data = json.loads(f.read_text())
         if data.get("workload") != workload:
@@ -114,10 +126,32 @@ def pmc_traffic(workload, kernel_prefix):
     return None, None
 
 
-def init_dist():
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def relaunch_distributed(gpus: int, script: str | None = None,
+                         argv: list[str] | None = None) -> int:
+    """--gpus N > 1 without a launcher: run this script under torch.distributed.run
+    (N ranks, rendezvous on 127.0.0.1) as a CHILD process — never exec: nothing in
+    this process has touched the GPU — and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", script or str(Path(__file__).resolve()),
+           *(sys.argv[1:] if argv is None else argv)]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def init_dist(gpus: int):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {gpus}; they must agree")
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -147,8 +181,19 @@ def make_inputs(B, H, W, dtype, seed, dev):
     return f1, f2, coords
 
 
-def cpu_baseline(H, W, budget_s, impl="torch"):
-    """Time the reference's op sequence on host cores over a bounded sample.
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(H, W, budget_s, impl="torch", reps=5):
+    """Time the reference's op sequence on host cores: warm-up 1, then the median
+    of at least ``reps`` single-pair repetitions (more while within ``budget_s``).
 
     impl "torch" (default; SURVEY.md §8(d) "CPU reference timing"): the plain-PyTorch
     restatement tests/torch_ref.py (bmm, / sqrt(D), 3x F.avg_pool2d, 12 x 4
@@ -182,18 +227,41 @@ def cpu_baseline(H, W, budget_s, impl="torch"):
             for c in cs:
                 oracle.corr_lookup(pyr, c, RADIUS)
         what = f"numpy float32 oracle; matmul on {threads} BLAS threads, lookups single-threaded"
+    times = []
     with torch.no_grad():
         one_pair()                                   # warm-up (allocator, thread pool)
-        pairs, t0 = 0, time.perf_counter()
-        while True:
+        t_start = time.perf_counter()
+        while len(times) < reps or (time.perf_counter() - t_start < budget_s and len(times) < 50):
+            t0 = time.perf_counter()
             one_pair()
-            pairs += 1
-            el = time.perf_counter() - t0
-            if el >= budget_s or pairs >= 50:
-                break
-    return {"value": pairs / el, "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{pairs} pair(s) of fmap {H}x{W}, D={D}: build + {ITERS} lookups, "
-                      f"{el:.1f} s; {what}"}
+            times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return {"value": round(1.0 / med, 4), "unit": "pairs/s", "cores": threads,
+            "nproc": os.cpu_count(), "cpu_model": _cpu_model(), "kind": "port",
+            "median_of": len(times), "median_s_per_pair": round(med, 4),
+            "sample": f"{len(times)} single-pair reps (median) of fmap {H}x{W}, D={D}: build + "
+                      f"{ITERS} lookups, {sum(times):.1f} s; {what}"}
+
+
+def _timed_graph(fn, stream, pool, count):
+    """Capture ``fn`` (``count`` launches of one kernel) into a graph sharing
+    ``pool``; return a callable giving the mean ms per launch over ``reps``
+    replays, timed with HIP events on ``stream``."""
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=stream, pool=pool):
+        fn()
+
+    def measure(reps):
+        g.replay()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(reps)]
+        for a, b in ev:
+            a.record(stream)
+            g.replay()
+            b.record(stream)
+        torch.cuda.synchronize()
+        return float(np.mean([a.elapsed_time(b) for a, b in ev])) / count
+    return measure
 
 
 def main():
@@ -218,10 +286,12 @@ def main():
                     help="CPU baseline: torch restatement of core/corr.py (default) or numpy oracle")
     args = ap.parse_args()
 
-    world, rank, local = init_dist()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_distributed(args.gpus))
+    world, rank, local = init_dist(args.gpus)
     dev = torch.device("cuda", local if world > 1 else 0)
     import dexiraft_amd
-    from dexiraft_amd.shard import max_over_ranks, pair_range
+    from dexiraft_amd.shard import gather_pairs, max_over_ranks, pair_range
     dexiraft_amd.load_native()
 
     (img_h, img_w), (H, W), b_default, dt_default = WORKLOADS[args.workload]
@@ -230,8 +300,10 @@ def main():
         B = stop - start
         if B < 1:
             raise SystemExit(f"--total-pairs {args.total_pairs} leaves rank {rank} without pairs")
+        total = args.total_pairs
     else:
         B = args.batch or b_default
+        total = world * B
     dtype = args.dtype or dt_default
     f1, f2, coords = make_inputs(B, H, W, dtype, seed=1234 + rank, dev=dev)
     if args.layout == "nhwc":
@@ -240,7 +312,6 @@ def main():
     stream = torch.cuda.Stream(device=dev)
 
     state = {}
-
     block_cls = dexiraft_amd.CorrBlock if args.block == "corr" else dexiraft_amd.AlternateCorrBlock
 
     def build():
@@ -249,70 +320,70 @@ def main():
     def lookups():
         state["outs"] = [state["cb"](c) for c in coords]
 
-    timing = "hip events between graph replays"
+    def step():
+        build()
+        lookups()
+
+    timing = "hip events around graphs of back-to-back launches, divided by the launch count"
     with torch.no_grad(), torch.cuda.stream(stream):
-        for _ in range(max(args.warmup, 1)):          # eager warmup (also JIT-free check)
-            build()
-            lookups()
+        for _ in range(max(args.warmup, 1)):          # eager warmup (also a JIT-free check)
+            step()
         torch.cuda.synchronize()
         if args.mode == "graph":
-            g_build, g_look = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_build, stream=stream):
-                build()
-            with torch.cuda.graph(g_look, stream=stream, pool=g_build.pool()):
-                lookups()
-            run_build, run_look = g_build.replay, g_look.replay
             # The whole step (build + 12 lookups) as ONE graph: what a serving loop
-            # replays; `value` is timed on it.  The split graphs above give the
-            # per-kernel durations (HIP events between their replays).
+            # replays; `value` is timed on it.
             g_step = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_step, stream=stream):
-                build()
-                lookups()
+                step()
             for _ in range(max(args.warmup, 1)):
-                run_build()
-                run_look()
                 g_step.replay()
+            run_step = g_step.replay
         else:
-            run_build, run_look = build, lookups
-            timing = "hip events between eager launches"
+            run_step = step
+            timing = "hip events around eager launches"
         torch.cuda.synchronize()
 
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-                torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
         barrier(world)
         t0 = time.perf_counter()
-        for e0, e1, e2 in evs:
-            e0.record(stream)
-            run_build()
-            e1.record(stream)
-            run_look()
-            e2.record(stream)
+        for _ in range(args.steps):
+            run_step()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         barrier(world)
-        elapsed_split = elapsed
-        if args.mode == "graph":
-            barrier(world)
-            t0 = time.perf_counter()
-            for _ in range(args.steps):
-                g_step.replay()
-            torch.cuda.synchronize()
-            elapsed = time.perf_counter() - t0
-            barrier(world)
 
-    build_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in evs]))
-    look_ms = float(np.mean([b.elapsed_time(c) for _, b, c in evs])) / ITERS
+        # correctness record: float64 checksum of each pair's 12th lookup (of the
+        # last timed replay), gathered from every rank over RCCL (the only
+        # collective; outside the timed region)
+        local_sums = state["outs"][-1].double().sum(dim=(1, 2, 3))
+        sums = gather_pairs(local_sums, total)
+        finite = bool(torch.isfinite(sums).all().item())
+
+        # Kernel-timing pass (outside the timed region).
+        if args.mode == "graph":
+            keep = dict(state)            # the step graph's own tensors stay allocated
+            pool = g_step.pool()
+            kb = KB_BUILDS if H * W <= 16384 else 3
+            t_build = _timed_graph(lambda: [build() for _ in range(kb)], stream, pool, kb)
+            t_look = _timed_graph(lambda: [state["cb"](c) for _ in range(KL_REPS) for c in coords],
+                                  stream, pool, KL_REPS * ITERS)
+            build_ms, look_ms = t_build(5), t_look(5)
+            del keep
+        else:
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            ev[0].record(stream)
+            build()
+            ev[1].record(stream)
+            lookups()
+            ev[2].record(stream)
+            torch.cuda.synchronize()
+            build_ms, look_ms = ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]) / ITERS
+
     elapsed = max_over_ranks(elapsed, device=dev)
-    elapsed_split = max_over_ranks(elapsed_split, device=dev)
-    if world > 1:
-        # Correctness sanity outside the timed region: every rank's last lookup is finite.
-        ok = torch.tensor([float(torch.isfinite(state["outs"][-1]).all())], device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        assert ok.item() == 1.0
+    if not finite:
+        raise SystemExit("bench.py: non-finite lookup output")
 
     if rank == 0:
-        pairs = (args.total_pairs if args.total_pairs is not None else world * B) * args.steps
+        pairs = total * args.steps
         value = pairs / elapsed
         s_in = 2 if dtype == "bf16" else 4
         flops = build_flops(B, H, W)
@@ -337,40 +408,43 @@ def main():
                             f"{img_h}x{img_w} (fmap {H}x{W}), D={D}, r={RADIUS}, L={LEVELS}",
                 "pairs_per_gpu": B, "fmap_layout": args.layout, "mode": args.mode,
                 "parallelism": f"pairs sharded x{world}",
-                "kernel_timing": timing,
-                "step_timing": ("one HIP graph per step (build + 12 lookups); "
-                                f"{elapsed_split / args.steps * 1e3:.4f} ms/step with the build and "
-                                "the lookups in two graphs (the kernel-timing pass)")
+                "step_timing": "one HIP graph per step (build + 12 lookups)"
                                if args.mode == "graph" else "eager launches",
+                "kernel_timing": timing,
+            },
+            "pair_checksums": {
+                "what": "float64 sum of each pair's 12th lookup output, all-gathered over "
+                        f"{'RCCL' if world > 1 else 'no collective (1 rank)'}",
+                "pairs": int(sums.numel()), "sum_of_sums": float(sums.sum().item()),
+                "first": [round(float(v), 3) for v in sums[:4].tolist()],
             },
         }
         if args.block == "corr":
             kname, mfma_per_flop, pipe_peak, mfma_dtype = build_kernel(dtype, H, W)
-            # achieved = ALGORITHMIC flops (2*B*N^2*D) per launch / launch time, priced
-            # against the dense MFMA peak of the path's arithmetic type: f32 (157.3 TF)
-            # for f32 fmaps, bf16 (2.5 PF) for bf16 fmaps.  The split f32 build issues
-            # 6 bf16 MFMA products per f32 product; its bf16-pipe occupancy is reported
-            # beside it ("bf16_pipe"), not as the roofline.
-            peak = PEAK_BF16_TFLOPS if dtype == "bf16" else PEAK_F32_TFLOPS
+            # achieved = ALGORITHMIC flops (2*B*N^2*D) per launch / launch time.
+            # Ceiling = the dense MFMA peak of the arithmetic actually run: bf16 fmaps
+            # 2.5 PF; f32 fmaps on the split build 2.5 PF / 6 = 417 TF f32-equivalent
+            # (its bf16 pipe); the exact-f32 build 157.3 TF.  frac_f32_peak keeps
+            # SURVEY §8(d)'s f32 pricing beside it.
             achieved = flops / (build_ms * 1e-3) / 1e12
+            ceiling = pipe_peak / mfma_per_flop
             b_traffic, b_src = pmc_traffic(wl_key, kname.split(" ")[0] + "<")
             l_traffic, l_src = pmc_traffic(wl_key, "corr_lookup_wide_kernel<")
+            bb = build_bytes(B, H, W, s_in, s_in)
             res["roofline"] = {
                 "kernel": kname + " (stage a+b)",
-                "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
-                "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                "bound": "mfma", "achieved": round(achieved, 2), "peak": round(ceiling, 1),
+                "unit": "TFLOP/s", "frac": round(achieved / ceiling, 4),
+                "peak_basis": (f"dense bf16 MFMA 2.5 PF / {mfma_per_flop} products per f32 product"
+                               if mfma_per_flop > 1 else f"dense {mfma_dtype} MFMA peak"),
+                "frac_f32_peak": None if dtype == "bf16" else round(achieved / PEAK_F32_TFLOPS, 4),
                 "traffic": b_traffic, "traffic_source": b_src,
                 "mfma_dtype": mfma_dtype,
                 "algorithmic_flops_per_launch": flops,
-                "algorithmic_bytes_per_launch": build_bytes(B, H, W, s_in, s_in),
+                "algorithmic_bytes_per_launch": bb,
+                "hbm_frac": round(bb / (build_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
                 "avg_launch_us": round(build_ms * 1e3, 2),
             }
-            if mfma_per_flop > 1:
-                issued = mfma_per_flop * flops / (build_ms * 1e-3) / 1e12
-                res["roofline"]["bf16_pipe"] = {
-                    "mfma_flops_per_launch": mfma_per_flop * flops,
-                    "issued_tflops": round(issued, 2), "peak": pipe_peak,
-                    "frac": round(issued / pipe_peak, 4)}
             res["lookup_roofline"] = {
                 "kernel": "corr_lookup_wide_kernel (stage c)",
                 "bound": "hbm", "achieved": round(lb / (look_ms * 1e-3) / 1e9, 1),
@@ -382,22 +456,16 @@ def main():
             }
         else:
             # on-the-fly lookups: (2r+2)^2 window dot products of length D per query
-            # and level, f32-class arithmetic (SURVEY.md §8(d) stage d).  The default
-            # kernel (D % 16 == 0, D <= 256) runs them as split-bf16 MFMA GEMMs over
-            # each 4x8 query tile's union box of cells; the issued MFMA work depends on
-            # the coordinates (box size), so the roofline prices the algorithmic window
-            # FLOPs against the f32 peak, as for an f32 kernel.
+            # and level, f32-class arithmetic (SURVEY.md §8(d) stage d), priced at
+            # the f32 peak; the default kernel runs them as split-bf16 MFMA GEMMs.
             aflops = alt_lookup_flops(B, H, W)
             achieved = aflops / (look_ms * 1e-3) / 1e12
-            mfma_alt = D % 16 == 0 and D <= 256 and os.environ.get("DXR_ALT_VARIANT") != "1"
-            akern = "alt_corr_mfma_kernel" if mfma_alt else "alt_corr_kernel"
+            akern = "alt_corr_mfma_kernel"
             a_traffic, a_src = pmc_traffic(wl_key, akern + "<")
             res["roofline"] = {
-                "kernel": akern + (" (split-bf16 MFMA over the union box of 4x8-query windows, "
-                                   "f32 accumulate)" if mfma_alt else " (per-query VALU)")
-                + " (stage d, per lookup)",
-                "bound": "mfma" if mfma_alt else "valu", "achieved": round(achieved, 2),
-                "peak": PEAK_F32_TFLOPS,
+                "kernel": akern + " (split-bf16 MFMA over query-tile window boxes, f32 "
+                                  "accumulate; stage d, per lookup)",
+                "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F32_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_TFLOPS, 4),
                 "traffic": a_traffic, "traffic_source": a_src,
                 "algorithmic_flops_per_launch": aflops,

@@ -11,7 +11,8 @@
  *
  * Reference interfaces replaced (paths relative to the reference repository):
  *   dxr_corr_pyramid_build   core/corr.py:13-27  CorrBlock.__init__ (matmul,
- *                            / sqrt(D), 3x F.avg_pool2d)
+ *                            / sqrt(D), 3x F.avg_pool2d); NCHW or channels-last
+ *                            fmaps (core/extractor.py:166-192 -> core/raft.py:139-148)
  *   dxr_corr_volume          core/corr.py:52-60  CorrBlock.corr (static)
  *   dxr_pyramid_unpack/pack  core/corr.py:16,24,27 the corr_pyramid attribute
  *                            (reference layout <-> paged storage)
@@ -41,6 +42,7 @@
  *
  * Layouts (all row-major, C-contiguous):
  *   fmap (CorrBlock)        [B, D, H, W]               (NCHW, as core/raft.py:139-142)
+ *                           or [B, H, W, D] (DXR_NHWC)
  *   pyramid                 PAGED storage (opaque to callers; sizes and level
  *                           offsets from dxr_pyramid_numel/_level_offset).  Level l
  *                           has H_l = floor(H_{l-1}/2) rows, as F.avg_pool2d.  Levels
@@ -71,7 +73,7 @@ extern "C" {
 /* HIP's own definition; repeating an identical typedef is legal in C11/C++. */
 typedef struct ihipStream_t* hipStream_t;
 
-#define DXR_ABI_VERSION 4
+#define DXR_ABI_VERSION 5
 
 enum dxr_status {
   DXR_OK = 0,
@@ -83,6 +85,16 @@ enum dxr_status {
 enum dxr_dtype {
   DXR_F32 = 0,
   DXR_BF16 = 1          /* storage as IEEE bfloat16 bit patterns (uint16) */
+};
+
+enum dxr_layout {
+  DXR_NCHW = 0,         /* fmaps [B, D, H, W] (core/raft.py:139-142)              */
+  DXR_NHWC = 1          /* fmaps [B, H, W, D] (channels-last encoders, §8(f) row 4) */
+};
+
+enum dxr_build_algo {
+  DXR_BUILD_AUTO = 0,       /* f32 fmaps: split build where its layout allows  */
+  DXR_BUILD_EXACT_F32 = 1   /* f32 fmaps: exact-f32 MFMA build (v_mfma_f32_32x32x2_f32) */
 };
 
 /* ABI version of the loaded library (== DXR_ABI_VERSION it was built with). */
@@ -101,35 +113,26 @@ int64_t dxr_pyramid_numel(int64_t B, int64_t H, int64_t W, int num_levels);
 int64_t dxr_pyramid_level_offset(int64_t B, int64_t H, int64_t W, int level);
 
 /*
- * Bytes of device workspace dxr_corr_pyramid_build can use for these shapes
- * (0 = none): the exact hi/mid/lo bf16 split planes of both float32 fmaps
- * (2 * B * 3 * D * H * W * 2 bytes; D % 16 == 0).  The caller allocates it; it
- * is dead once the build's kernels have run (stream order).
- */
-int64_t dxr_build_workspace_bytes(int64_t B, int64_t D, int64_t H, int64_t W,
-                                  int in_dtype);
-
-/*
  * Stage (a)+(b): all-pairs correlation fmap1^T . fmap2 / divisor and its
  * avg-pool pyramid, written in one pass (pooling fused into the MFMA epilogue).
- *   fmap1, fmap2 : [B, D, H, W], dtype in_dtype (DXR_F32 or DXR_BF16)
+ *   fmap1, fmap2 : [B, D, H, W] (fmap_layout DXR_NCHW) or [B, H, W, D]
+ *                  (DXR_NHWC), dtype in_dtype (DXR_F32 or DXR_BF16)
  *   divisor      : the reference divides by sqrt(D) (core/corr.py:60)
  *   pyramid      : dxr_pyramid_numel(B,H,W,num_levels) elements of pyr_dtype
+ *                  (levels beyond 4 need pyr_dtype DXR_F32)
  *   num_levels   : >= 1; every level must be at least 1 x 1
- *   workspace    : NULL, or >= dxr_build_workspace_bytes(...) bytes, 16-byte
- *                  aligned (a smaller or NULL workspace selects a build that
- *                  needs none; results are identical)
+ *   algo         : DXR_BUILD_AUTO, or DXR_BUILD_EXACT_F32 (f32 fmaps only)
  * DXR_F32 inputs compute in f32 class: every f32 operand is split exactly into
  * three bf16 parts and six bf16 x bf16 MFMA products per f32 product are
- * accumulated in f32 (terms below 2^-25 |x y| dropped); with D % 16 != 0 the
- * exact-f32 MFMA v_mfma_f32_32x32x2_f32 is used.  DXR_BF16 inputs use bf16 MFMA
- * with f32 accumulation.
+ * accumulated in f32 (terms below 2^-25 |x y| dropped); with D % 16 != 0, odd W
+ * or DXR_BUILD_EXACT_F32 the exact-f32 MFMA v_mfma_f32_32x32x2_f32 is used.
+ * DXR_BF16 inputs use bf16 MFMA with f32 accumulation.  NHWC and NCHW inputs
+ * of the same values give bit-identical pyramids.
  */
 int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int in_dtype,
-                           int64_t B, int64_t D, int64_t H, int64_t W,
-                           int num_levels, float divisor,
-                           void* pyramid, int pyr_dtype,
-                           void* workspace, int64_t workspace_bytes,
+                           int fmap_layout, int64_t B, int64_t D, int64_t H,
+                           int64_t W, int num_levels, float divisor,
+                           void* pyramid, int pyr_dtype, int algo,
                            hipStream_t stream);
 
 /*

@@ -15,10 +15,12 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_PATH = Path(__file__).resolve().with_name("libdexiraft_corr.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 DXR_OK, DXR_EINVAL, DXR_EUNSUPPORTED, DXR_EHIP = 0, 1, 2, -1
 DXR_F32, DXR_BF16 = 0, 1
+DXR_NCHW, DXR_NHWC = 0, 1
+DXR_BUILD_AUTO, DXR_BUILD_EXACT_F32 = 0, 1
 
 # Every symbol include/dexiraft_corr.h declares, with its ctypes signature.
 _i64 = ctypes.c_int64
@@ -31,9 +33,8 @@ SIGNATURES: dict[str, tuple[object, list[object]]] = {
     "dxr_last_hip_error": (_int, []),
     "dxr_pyramid_numel": (_i64, [_i64, _i64, _i64, _int]),
     "dxr_pyramid_level_offset": (_i64, [_i64, _i64, _i64, _int]),
-    "dxr_build_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64, _int]),
-    "dxr_corr_pyramid_build": (_int, [_vp, _vp, _int, _i64, _i64, _i64, _i64, _int, _f32,
-                                      _vp, _int, _vp, _i64, _vp]),
+    "dxr_corr_pyramid_build": (_int, [_vp, _vp, _int, _int, _i64, _i64, _i64, _i64, _int, _f32,
+                                      _vp, _int, _int, _vp]),
     "dxr_corr_volume": (_int, [_vp, _vp, _int, _i64, _i64, _i64, _i64, _f32, _vp, _vp]),
     "dxr_pyramid_unpack": (_int, [_vp, _int, _i64, _i64, _i64, _int, _int, _vp, _vp]),
     "dxr_pyramid_pack": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _int, _vp]),

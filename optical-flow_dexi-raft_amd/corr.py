@@ -73,31 +73,47 @@ def _volume_grads(ctx_needs, f1: torch.Tensor, f2: torch.Tensor, dv: torch.Tenso
     return df1, df2
 
 
+class _GradState:
+    """What the backward of a differentiable CorrBlock needs: its geometry and
+    the gradient pyramid the lookups' backwards add into.  Held by the block
+    and by the autograd nodes, it references neither the block nor the graph,
+    so no reference cycle keeps the pyramid (``block._buf``) or the gradient
+    pyramid alive after the step: both are freed by refcount."""
+
+    __slots__ = ("geom", "num_levels", "radius", "device", "numel", "grad_pyr")
+
+    def __init__(self, geom, num_levels, radius, device, numel):
+        self.geom, self.num_levels, self.radius = geom, num_levels, radius
+        self.device, self.numel = device, numel
+        self.grad_pyr = None
+
+
 class _BuildGrad(torch.autograd.Function):
     """Graph node of CorrBlock.__init__: returns a scalar token every lookup
     consumes, so autograd runs this backward once, after every lookup's
-    backward has added into ``block._grad_pyr``."""
+    backward has added into the gradient pyramid."""
 
     @staticmethod
-    def forward(ctx, fmap1, fmap2, block):
-        ctx.block = block
+    def forward(ctx, fmap1, fmap2, gs):
+        ctx.gs = gs
         ctx.save_for_backward(fmap1, fmap2)
         return fmap1.new_zeros(())
 
     @staticmethod
     def backward(ctx, _gtoken):
-        block = ctx.block
-        gp, block._grad_pyr = block._grad_pyr, None
+        gs = ctx.gs
+        gp, gs.grad_pyr = gs.grad_pyr, None
         if gp is None:
             return None, None, None
         f1, f2 = ctx.saved_tensors
-        B, D, H, W = block._geom
+        B, D, H, W = gs.geom
         dv = torch.empty((B, H * W, H * W), dtype=torch.float32, device=f1.device)
         lib = nat.load()
-        with _Launch(block._device):
-            st = lib.dxr_pyramid_backward(gp.data_ptr(), nat.DXR_F32, B, H, W, block.num_levels,
+        with _Launch(gs.device):
+            st = lib.dxr_pyramid_backward(gp.data_ptr(), nat.DXR_F32, B, H, W, gs.num_levels,
                                           _sqrt_dim(D), dv.data_ptr(), nat.stream_of(dv))
         nat.check(st, "CorrBlock backward (dxr_pyramid_backward)")
+        del gp
         df1, df2 = _volume_grads(ctx.needs_input_grad, f1, f2, dv)
         return df1, df2, None
 
@@ -107,25 +123,23 @@ class _LookupGrad(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, token, coords, block):
-        ctx.block = block
+        ctx.gs = block._gs
         ctx.save_for_backward(coords)
         return block._lookup(coords)
 
     @staticmethod
     def backward(ctx, gout):
-        block = ctx.block
+        gs = ctx.gs
         (coords,) = ctx.saved_tensors
-        B, D, H, W = block._geom
-        if block._grad_pyr is None:
-            block._grad_pyr = torch.zeros(block._buf.numel(), dtype=torch.float32,
-                                          device=block._device)
+        B, D, H, W = gs.geom
+        if gs.grad_pyr is None:
+            gs.grad_pyr = torch.zeros(gs.numel, dtype=torch.float32, device=gs.device)
         g = gout.contiguous().float()
         lib = nat.load()
-        with _Launch(block._device):
+        with _Launch(gs.device):
             st = lib.dxr_corr_lookup_backward(coords.data_ptr(), g.data_ptr(), B, H, W,
-                                              block.num_levels, block.radius,
-                                              block._grad_pyr.data_ptr(), nat.DXR_F32,
-                                              nat.stream_of(g))
+                                              gs.num_levels, gs.radius, gs.grad_pyr.data_ptr(),
+                                              nat.DXR_F32, nat.stream_of(g))
         nat.check(st, "CorrBlock lookup backward (dxr_corr_lookup_backward)")
         return gout.new_zeros(()), None, None
 
@@ -308,7 +322,7 @@ class CorrBlock:
         self.radius = radius
         B, D, H, W = _fmap_geometry(fmap1, fmap2)
         self._token = None
-        self._grad_pyr = None
+        self._gs = None
         if not isinstance(num_levels, int) or num_levels < 1:
             raise ValueError(f"num_levels must be a positive int, got {num_levels!r}")
         if not isinstance(radius, int) or radius < 0:
@@ -328,23 +342,33 @@ class CorrBlock:
         lib = nat.load()
         numel = lib.dxr_pyramid_numel(B, H, W, num_levels)
         self._buf = torch.empty(numel, dtype=pyr_torch, device=fmap1.device)
-        if _wants_grad(fmap1, fmap2):
-            f1, f2 = fmap1.contiguous(), fmap2.contiguous()   # tracked by autograd
-        else:
-            f1, f2 = _nchw(fmap1), _nchw(fmap2)
-        # Split-plane workspace (f32 fmaps): a temporary from torch's caching
-        # allocator, released in stream order after the build's kernels.
-        ws_bytes = lib.dxr_build_workspace_bytes(B, D, H, W, in_dt)
-        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=fmap1.device) if ws_bytes else None
-        with _Launch(self._device):
-            st = lib.dxr_corr_pyramid_build(
-                f1.data_ptr(), f2.data_ptr(), in_dt, B, D, H, W, num_levels, _sqrt_dim(D),
-                self._buf.data_ptr(), pyr_dt, nat.ptr(ws), ws_bytes, nat.stream_of(f1))
+        grad = _wants_grad(fmap1, fmap2)
+        st = nat.DXR_EUNSUPPORTED
+        if not grad and _channels_last(fmap1) and _channels_last(fmap2):
+            # channels-last fmaps: read in place by the
+            # build's NHWC operand loads, no layout pass
+            f1, f2 = fmap1, fmap2
+            with _Launch(self._device):
+                st = lib.dxr_corr_pyramid_build(
+                    f1.data_ptr(), f2.data_ptr(), in_dt, nat.DXR_NHWC, B, D, H, W, num_levels,
+                    _sqrt_dim(D), self._buf.data_ptr(), pyr_dt, nat.DXR_BUILD_AUTO,
+                    nat.stream_of(f1))
+        if st == nat.DXR_EUNSUPPORTED:
+            if grad:
+                f1, f2 = fmap1.contiguous(), fmap2.contiguous()   # tracked by autograd
+            else:
+                f1, f2 = _nchw(fmap1), _nchw(fmap2)
+            with _Launch(self._device):
+                st = lib.dxr_corr_pyramid_build(
+                    f1.data_ptr(), f2.data_ptr(), in_dt, nat.DXR_NCHW, B, D, H, W, num_levels,
+                    _sqrt_dim(D), self._buf.data_ptr(), pyr_dt, nat.DXR_BUILD_AUTO,
+                    nat.stream_of(f1))
         nat.check(st, "CorrBlock build (dxr_corr_pyramid_build)")
         self._level_sizes = sizes
         self._ref_pyramid = None
-        if _wants_grad(fmap1, fmap2):
-            self._token = _BuildGrad.apply(f1, f2, self)
+        if grad:
+            self._gs = _GradState(self._geom, num_levels, radius, self._device, numel)
+            self._token = _BuildGrad.apply(f1, f2, self._gs)
 
     @property
     def corr_pyramid(self):
@@ -477,8 +501,14 @@ class AlternateCorrBlock:
         B, D, H, W = _fmap_geometry(fmap1, fmap2)
         _require_no_grad(fmap1, fmap2, what="AlternateCorrBlock (the reference's alt_cuda_corr "
                                             "output carries no autograd graph, core/corr.py:85-88)")
-        if fmap1.dtype != torch.float32:
-            raise RuntimeError(f"AlternateCorrBlock expects float32 fmaps, got {fmap1.dtype}")
+        if fmap1.dtype == torch.bfloat16:
+            # The reference computes in float32 (core/raft.py:139-142 casts the
+            # fmaps; alt_cuda_corr is float-only): bf16 encoder outputs are widened
+            # exactly, keeping their memory format (channels-last stays a free view).
+            fmap1, fmap2 = fmap1.float(), fmap2.float()
+        elif fmap1.dtype != torch.float32:
+            raise RuntimeError(f"AlternateCorrBlock expects float32 or bfloat16 fmaps, got "
+                               f"{fmap1.dtype}")
         if not isinstance(num_levels, int) or num_levels < 1:
             raise ValueError(f"num_levels must be a positive int, got {num_levels!r}")
         if not isinstance(radius, int) or radius < 0:

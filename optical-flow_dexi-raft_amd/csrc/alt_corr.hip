@@ -21,7 +21,6 @@
 // and after one barrier every thread emits outputs for one query with coalesced
 // 256-byte wave stores along the query dimension.
 #include <cstdint>
-#include <cstdlib>
 
 #include "dxr_common.h"
 
@@ -227,8 +226,7 @@ template <int R, int NRB, int CMAX>
 __global__ __launch_bounds__(256, 2) void alt_corr_mfma_kernel(const float* __restrict__ f1,
                                                                const float* __restrict__ coords,
                                                                float* __restrict__ out,
-                                                               AltGeom g, int W1, int tiles_x,
-                                                               int remap) {
+                                                               AltGeom g, int W1, int tiles_x) {
   constexpr int RD = 2 * R + 1, RD1 = RD + 1, NCELL = RD1 * RD1;
   constexpr int CHUNK = 4 * 32 * NRB;                       // box cells per chunk
   constexpr int KB = CMAX / 8;                              // 8-channel blocks
@@ -238,11 +236,12 @@ __global__ __launch_bounds__(256, 2) void alt_corr_mfma_kernel(const float* __re
   __shared__ int box[4];                                    // bx0, by0, bw, bh
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // Workgroups are dealt round-robin to the 8 XCDs; with `remap` XCD k takes the
-  // k-th contiguous band of tiles instead, so neighbouring tiles (whose boxes
-  // overlap) share one L2 (the bijection of csrc/corr_build.hip's page_coord).
+  // Workgroups are dealt round-robin to the 8 XCDs; XCD k takes the k-th
+  // contiguous band of tiles instead, so neighbouring tiles (whose boxes overlap)
+  // share one L2 (the bijection of csrc/corr_build.hip's page_coord; r01 1080p:
+  // FETCH 424 -> 162 MB per lookup).
   int tile = blockIdx.x;
-  if (remap) {
+  {
     const int n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = tile % 8;
     tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + tile / 8;
   }
@@ -407,11 +406,6 @@ __global__ __launch_bounds__(256, 2) void alt_corr_mfma_kernel(const float* __re
   }
 }
 
-int alt_variant() {
-  const char* v = std::getenv("DXR_ALT_VARIANT");
-  return v ? std::atoi(v) : 0;
-}
-
 template <int R, int NRB>
 int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const AltGeom& g,
                       int levels, int Z, int W1, hipStream_t stream) {
@@ -420,7 +414,7 @@ int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const Al
   const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)levels, (unsigned)Z);
   if (g.C > 256) return DXR_EUNSUPPORTED;
   hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256>), grid, dim3(256), 0, stream, f1, coords,
-                     out, g, W1, tiles_x, alt_variant() == 4 ? 0 : 1);
+                     out, g, W1, tiles_x);
   return dxr::launch_status();
 }
 
@@ -437,20 +431,15 @@ int launch_alt_r(const float* f1, const float* coords, float* out, const AltGeom
 
 int launch_alt(const float* f1, const float* coords, float* out, const AltGeom& g, int levels,
                int Z, int radius, bool vec, hipStream_t stream, int W1 = 0) {
-  // MFMA form: C a multiple of 16 (k16 steps) up to 256, 16-byte aligned rows.
-  // DXR_ALT_VARIANT 1 selects the per-query form, 2 / 3 the MFMA form with 2 / 4
-  // row blocks per wave (r = 4), 4 the MFMA form in plain (round-robin XCD) tile order.
-  const int v = alt_variant();
-  if (vec && W1 > 0 && g.C % 16 == 0 && g.C <= 256 && v != 1) {
+  // MFMA form: C a multiple of 16 (k16 steps) up to 256, 16-byte aligned rows;
+  // the per-query VALU form otherwise.
+  if (vec && W1 > 0 && g.C % 16 == 0 && g.C <= 256) {
     switch (radius) {
       case 0: return launch_alt_mfma_r<0, 1>(f1, coords, out, g, levels, Z, W1, stream);
       case 1: return launch_alt_mfma_r<1, 1>(f1, coords, out, g, levels, Z, W1, stream);
       case 2: return launch_alt_mfma_r<2, 1>(f1, coords, out, g, levels, Z, W1, stream);
       case 3: return launch_alt_mfma_r<3, 1>(f1, coords, out, g, levels, Z, W1, stream);
-      case 4:
-        if (v == 2) return launch_alt_mfma_r<4, 2>(f1, coords, out, g, levels, Z, W1, stream);
-        if (v == 3) return launch_alt_mfma_r<4, 4>(f1, coords, out, g, levels, Z, W1, stream);
-        return launch_alt_mfma_r<4, 1>(f1, coords, out, g, levels, Z, W1, stream);
+      case 4: return launch_alt_mfma_r<4, 1>(f1, coords, out, g, levels, Z, W1, stream);
       case 5: return launch_alt_mfma_r<5, 1>(f1, coords, out, g, levels, Z, W1, stream);
       case 6: return launch_alt_mfma_r<6, 1>(f1, coords, out, g, levels, Z, W1, stream);
       default: return DXR_EUNSUPPORTED;

@@ -25,7 +25,6 @@
 // (Scattered per-query row stores — 64 lines per wave store — cost more than the
 // MFMA loop itself: measured 346 vs 220 us at Sintel shape.)
 #include <cmath>
-#include <cstdlib>
 
 #include "dxr_common.h"
 
@@ -227,28 +226,14 @@ __device__ __forceinline__ void store8(OT* dst, const float* src) {
 // or pools of zeros) and never read.  Every pooled value is computed from the
 // f32 values of the level above, in the reference's window order
 // ((v00+v01)+v10)+v11 (F.avg_pool2d), then rounded to OT once.
-typedef float f32x4v __attribute__((ext_vector_type(4)));
-
-// 16-byte global store, optionally nontemporal (streamed past the caches' LRU).
-__device__ __forceinline__ void gst(float4* p, float4 v, bool nt) {
-  if (nt) {
-    const f32x4v w = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(w, reinterpret_cast<f32x4v*>(p));
-  } else {
-    *p = v;
-  }
-}
-
-// `region`: this wave's LDS staging region; `qslot`: which 32 queries of the
-// page the wave holds; `active` = false keeps the barriers but stores nothing
-// (a wave whose page lies past the pyramid's last query page).
-template <typename OT, bool NTS = false>
+// `wave`: which 32 queries of the page this wave holds (and its private LDS
+// staging region).
+template <typename OT>
 __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT* __restrict__ pyr,
-                                               const BuildGeom& g, long long page, int region,
-                                               int qslot, bool active, int lane) {
+                                               const BuildGeom& g, long long page, int wave,
+                                               int lane) {
   const int j = lane & 31, h = lane >> 5;
-  const int wave = qslot;
-  float* wl = lds + region * 16 * P0;   // this wave's private LDS region
+  float* wl = lds + wave * 16 * P0;   // this wave's private LDS region
 
   // Level 0: 16 queries per round staged as [q][8][16] f32 rows, then streamed
   // as 1 KiB wave stores.
@@ -270,16 +255,14 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
       for (int k = 0; k < 8; ++k) {
         const int qq = 2 * k + (lane >> 5);
         const int off = (lane & 31) * 4;
-        if (active)
-          gst(reinterpret_cast<float4*>(pg0 + (r * 16 + qq) * NTGT + off), f4(wl + qq * P0 + off),
-              NTS);
+        *reinterpret_cast<float4*>(pg0 + (r * 16 + qq) * NTGT + off) = f4(wl + qq * P0 + off);
       }
     } else {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int qq = 4 * k + (lane >> 4);
         const int off = (lane & 15) * 8;
-        if (active) store8<OT>(pg0 + (r * 16 + qq) * NTGT + off, wl + qq * P0 + off);
+        store8<OT>(pg0 + (r * 16 + qq) * NTGT + off, wl + qq * P0 + off);
       }
     }
     __syncthreads();
@@ -315,13 +298,12 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
   __syncthreads();
   {
     OT* pg1 = pyr + g.loff[1] + page * (BM * NTGT / 4) + (long long)wave * 32 * (NTGT / 4);
-    if (!active) {
-    } else if constexpr (sizeof(OT) == 4) {
+    if constexpr (sizeof(OT) == 4) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int qq = 8 * k + (lane >> 3);
         const int off = (lane & 7) * 4;
-        gst(reinterpret_cast<float4*>(pg1 + qq * 32 + off), f4(wl + qq * P1 + off), NTS);
+        *reinterpret_cast<float4*>(pg1 + qq * 32 + off) = f4(wl + qq * P1 + off);
       }
     } else {
 #pragma unroll
@@ -332,7 +314,7 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
       }
     }
   }
-  if (g.levels < 3 || !active) return;   // no barriers below this point
+  if (g.levels < 3) return;   // no barriers below this point
 
   // Level 2: [q][2][4] per page; lane (j, h) writes row h (a 1 KiB wave run).
   {
@@ -382,16 +364,7 @@ __device__ __forceinline__ void scale_acc(f32x16 (&acc)[4], const BuildGeom& g) 
     }
 }
 
-// GLDS: stage operands with global_load_lds_dwordx4 (no staging registers).
-// Out-of-range rows/cols/queries read clamped, valid addresses: their values
-// only reach page padding (never read; pooled cells touching them fall outside
-// the floor-mode level bounds).  Requires W % 4 == 0 and D % BK == 0.
-__device__ __forceinline__ void glds16(const float* g, float* l) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g),
-                                   (__attribute__((address_space(3))) void*)(l), 16, 0, 0);
-}
-
-template <bool VEC, int BK, bool PAGED, typename OT, bool NTS, bool GLDS, bool DIV>
+template <bool VEC, int BK, bool PAGED, typename OT, bool DIV>
 __device__ __forceinline__ void build_page_f32(const float* __restrict__ f1,
                                                const float* __restrict__ f2,
                                                OT* __restrict__ pyr, const BuildGeom& g,
@@ -443,34 +416,7 @@ __device__ __forceinline__ void build_page_f32(const float* __restrict__ f1,
                                                       acc[t], 0, 0, 0);
     }
   };
-  if constexpr (GLDS) {
-    static_assert(BK == 16, "glds staging is laid out for BK = 16 (two k-rows per wave load)");
-    // Wave w fills k-row pairs 2w and 2w+1 of both tiles: one 1 KiB wave load
-    // per pair and tile, lane l -> (k = 2p + l/32, 16 B at column (l%32)*4), which
-    // is exactly the [k][128] LDS image (lane-linear destination).
-    const int qa = min(q0 + (lane & 31) * 4, g.N - 4);
-    const int r = (lane >> 2) & 7;
-    const long long tb = (long long)min(th0 + r, g.H - 1) * g.W + min(tw0 + (lane & 3) * 4, g.W - 4);
-    auto issue = [&](int k0, int buf) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int pr = 2 * wave + i;
-        const long long krow = (long long)(k0 + 2 * pr + khalf) * g.N;
-        glds16(f1b + krow + qa, As(buf) + pr * 256);
-        glds16(f2b + krow + tb, Bs(buf) + pr * 256);
-      }
-    };
-    issue(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int ks = 0; ks < nk; ++ks) {
-      const int buf = ks & 1;
-      if (ks + 1 < nk) issue((ks + 1) * BK, buf ^ 1);
-      mfma_stage(buf);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-  } else {
+  {
     Stage<VEC, BK> st;
     st.load(f1b, f2b, 0, q0, th0, tw0, g, tid);
     st.store(As(0), Bs(0), tid);
@@ -508,35 +454,23 @@ __device__ __forceinline__ void build_page_f32(const float* __restrict__ f1,
     }
     return;
   } else {
-    paged_epilogue<OT, NTS>(acc, lds, pyr, g, page, wave, wave, true, lane);
+    paged_epilogue<OT>(acc, lds, pyr, g, page, wave, lane);
   }
 }
 
+// Exact-f32 build (v_mfma_f32_32x32x2_f32): the fallback when the split build's
+// layout conditions fail (D % 16 != 0, odd W), the kernel of CorrBlock.corr, and
+// the f32 reference the split build is tested against (DXR_BUILD_EXACT_F32).
 // One page per workgroup (grid = TX*TY x QT x B).  MINW = waves per SIMD the
 // register allocation must allow (0 = compiler's choice).
-template <bool VEC, int BK, bool PAGED, typename OT, bool NTS, int MINW, bool GLDS, bool DIV>
+template <bool VEC, int BK, bool PAGED, typename OT, int MINW, bool DIV>
 __global__ __launch_bounds__(NT, MINW) void corr_build_f32_kernel(const float* __restrict__ f1,
                                                             const float* __restrict__ f2,
                                                             OT* __restrict__ pyr, BuildGeom g) {
   __shared__ float lds[build_lds_floats<BK>()];
   const long long page =
       ((long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-  build_page_f32<VEC, BK, PAGED, OT, NTS, GLDS, DIV>(f1, f2, pyr, g, lds, page);
-}
-
-// Persistent: gridDim.x resident workgroups walk the pages with stride
-// gridDim.x, so a page's store drain overlaps the next page's MFMA loop instead
-// of every workgroup on a CU storing in lockstep.  With TX*TY a multiple of 8
-// (e.g. 56 at Sintel shape) each XCD keeps one residue class of target tiles.
-template <bool VEC, int BK, typename OT, bool NTS, int MINW, bool GLDS, bool DIV>
-__global__ __launch_bounds__(NT, MINW) void corr_build_f32_persistent(
-    const float* __restrict__ f1, const float* __restrict__ f2, OT* __restrict__ pyr,
-    BuildGeom g, long long pages) {
-  __shared__ float lds[build_lds_floats<BK>()];
-  for (long long page = blockIdx.x; page < pages; page += gridDim.x) {
-    build_page_f32<VEC, BK, true, OT, NTS, GLDS, DIV>(f1, f2, pyr, g, lds, page);
-    __syncthreads();  // the next page's prologue overwrites the epilogue's LDS
-  }
+  build_page_f32<VEC, BK, PAGED, OT, DIV>(f1, f2, pyr, g, lds, page);
 }
 
 // ---------------------------------------------------------------------------
@@ -693,8 +627,7 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_
   }
 
   scale_acc<DIV>(acc, g);
-  const long long page = pc.page;
-  paged_epilogue<OT, false>(acc, reinterpret_cast<float*>(smem), pyr, g, page, wave, wave, true, lane);
+  paged_epilogue<OT>(acc, reinterpret_cast<float*>(smem), pyr, g, pc.page, wave, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -751,11 +684,9 @@ __device__ __forceinline__ Split3 split3(float a, float b) {
   return {h, m, pack_hi(__float_as_uint(la), __float_as_uint(lb))};
 }
 
-// ABL (timing-only ablations, never the default): 1 skips the epilogue stores,
-// 2 skips the MFMAs.
 // BV: target staging width in floats — 4 (float4 units; W % 4 == 0) or 2
 // (float2 units; W even, e.g. Chairs' 62-wide fmaps).
-template <typename OT, bool DIV, int MINW, int ABL = 0, bool REMAP = false, int BV = 4>
+template <typename OT, bool DIV, int MINW, int BV = 4>
 __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float* __restrict__ f1,
                                                                     const float* __restrict__ f2,
                                                                     OT* __restrict__ pyr,
@@ -766,7 +697,7 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
   uint16_t* lh = reinterpret_cast<uint16_t*>(smem);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const PageCoord pc = page_coord<REMAP>(g);
+  const PageCoord pc = page_coord<false>(g);
   const int txi = pc.txi, tyi = pc.tyi;
   const int th0 = tyi * TH, tw0 = txi * TW;
   const int q0 = pc.qblk * BM;
@@ -875,13 +806,6 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     for (int t = 0; t < 4; ++t) {
       const bf8v th = frag(P + t * 32), tm = frag(P + PLANE_S + t * 32),
                  tl = frag(P + 2 * PLANE_S + t * 32);
-      if constexpr (ABL == 2) {
-        const s8v x = __builtin_bit_cast(s8v, th) ^ __builtin_bit_cast(s8v, tm) ^
-                      __builtin_bit_cast(s8v, tl) ^ __builtin_bit_cast(s8v, qh) ^
-                      __builtin_bit_cast(s8v, qm) ^ __builtin_bit_cast(s8v, ql);
-        acc[t][0] += (float)(x[0] + x[3] + x[5] + x[7]);
-        continue;
-      }
       // small terms first
       acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm, acc[t], 0, 0, 0);
       acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh, acc[t], 0, 0, 0);
@@ -898,194 +822,7 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
   }
 
   scale_acc<DIV>(acc, g);
-  if constexpr (ABL == 1 || ABL == 4 || ABL == 5) {
-    float sum = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sum += acc[t][r];
-    if (sum == 1234.5f) pyr[tid] = to_out<OT>(sum);  // keeps the K loop live
-    return;
-  }
-  const long long page = pc.page;
-  paged_epilogue<OT, false>(acc, reinterpret_cast<float*>(smem), pyr, g, page, wave, wave, true, lane);
-}
-
-// ---------------------------------------------------------------------------
-// Pre-split f32 build ("presplit", DXR_BUILD_VARIANT 11-14; not the default).
-// The same exact hi+mid+lo operand split and the same six bf16 MFMA products as
-// the split build above, but the split is done ONCE per fmap element by
-// split_planes_kernel into a workspace, instead of once per workgroup that reads
-// the element (55-56 times at Sintel).  The split build's profile (r01, sintel:
-// 113 us of its 173 us left with the MFMAs removed, ~195 VALU per wave and
-// k-step) was that in-loop split plus its staging; here the K loop issues no
-// VALU work beyond address increments.
-//
-// Workspace layout (16-byte chunks of 8 consecutive k of one pixel, bf16):
-//   chunk(fmap, b, plane, kb, pixel) at (((fmap*B + b)*3 + plane)*(D/8) + kb)*N + pixel
-// An MFMA operand lane (row = pixel, 8 k) is one chunk, so 32 lanes of a wave
-// read 512 contiguous bytes.  Query operands go global -> registers (each wave
-// reads only its own 32 queries); the 8x16 target tile, shared by the four
-// waves, goes global -> LDS by global_load_lds_dwordx4 into a 3-stage ring, in
-// slot order (target, k-half ^ target-row parity): that swizzle makes the
-// per-lane 16-byte fragment reads conflict-free.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void split_planes_kernel(const float* __restrict__ f1,
-                                                           const float* __restrict__ f2,
-                                                           uint4* __restrict__ ws, int B, int D,
-                                                           int N) {
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  const int kb = blockIdx.y;
-  const int fb = blockIdx.z;               // fmap * B + b
-  if (p >= N) return;
-  const float* src = (fb < B ? f1 + (long long)fb * D * N : f2 + (long long)(fb - B) * D * N) +
-                     (long long)kb * 8 * N + p;
-  float x[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) x[e] = src[(long long)e * N];
-  uint32_t h[4], m[4], l[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const Split3 v = split3(x[2 * e], x[2 * e + 1]);
-    h[e] = v.h; m[e] = v.m; l[e] = v.l;
-  }
-  const long long plane = (long long)(D / 8) * N;
-  uint4* dst = ws + (long long)fb * 3 * plane + (long long)kb * N + p;
-  dst[0] = make_uint4(h[0], h[1], h[2], h[3]);
-  dst[plane] = make_uint4(m[0], m[1], m[2], m[3]);
-  dst[2 * plane] = make_uint4(l[0], l[1], l[2], l[3]);
-}
-
-// Stage = one 16-deep k slice: target tile (3 planes x 128 targets x 2 k-halves
-// x 16 B, shared by the four waves) + query panel (4 waves x 3 planes x 2 halves
-// x 32 queries x 16 B; each wave's part is read only by that wave).
-constexpr int PS_B = 3 * NTGT * 2 * 16;      // 12 KiB
-constexpr int PS_AW = 3 * 2 * 32 * 16;       // 3 KiB per wave
-constexpr int PS_STAGE = PS_B + WAVES * PS_AW;
-
-__device__ __forceinline__ void glds_chunk(const uint4* g, unsigned char* l) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g),
-                                   (__attribute__((address_space(3))) void*)(l), 16, 0, 0);
-}
-
-// Both operands arrive by LDS-DMA only (no VGPR-destination loads in the loop,
-// so no compiler-inserted vmcnt(0)), NS stages in flight, a counted
-// s_waitcnt vmcnt and a raw s_barrier per k step (__syncthreads() would drain
-// the in-flight DMA: cdna_hip_programming.md §5 "Pipelining across barriers").
-// ABL (timing-only ablations, never the default): 1 skips the epilogue stores,
-// 2 skips the MFMAs, 3 skips the K loop, 4 = 1 + 2, 5 skips the DMA and the
-// epilogue stores (LDS reads + MFMAs + barriers only).
-template <typename OT, bool DIV, int MINW, int NS, int ABL = 0>
-__global__ __launch_bounds__(NT, MINW) void corr_build_presplit_kernel(const uint4* __restrict__ ws,
-                                                                       OT* __restrict__ pyr,
-                                                                       BuildGeom g, int B) {
-  constexpr int LDS_E = WAVES * 16 * P0 * 4;              // epilogue bytes
-  constexpr int LDS_K = NS * PS_STAGE;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_K > LDS_E ? LDS_K : LDS_E];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int txi = blockIdx.x % g.tiles_w, tyi = blockIdx.x / g.tiles_w;
-  const int th0 = tyi * TH, tw0 = txi * TW;
-  const int q0 = blockIdx.y * BM;
-  const int b = blockIdx.z;
-  const long long plane = (long long)(g.D / 8) * g.N;     // chunks per plane
-  const uint4* wa = ws + (long long)b * 3 * plane;          // fmap1 planes of pair b
-  const uint4* wb = ws + (long long)(B + b) * 3 * plane;    // fmap2 planes of pair b
-
-  f32x16 acc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-
-  // Query DMA: lane -> (k-half lane >> 5, query q0 + 32 wave + (lane & 31)); the
-  // LDS image [plane][half][32] is lane-linear, and so is the fragment read.
-  // Padding queries read a clamped, valid pixel (their outputs are page padding).
-  const int kh = lane >> 5;
-  const uint4* pa = wa + (long long)kh * g.N + min(q0 + wave * 32 + (lane & 31), g.N - 1);
-  // Target DMA: thread tid fills slot tid of each plane: target sp = tid >> 1,
-  // k-half (tid & 1) ^ (target row parity).  Off-image targets read clamped pixels.
-  const int sp = tid >> 1;
-  const int sr = sp >> 4, sc = sp & 15;
-  const int skh = (tid & 1) ^ (sr & 1);
-  const uint4* pb = wb + (long long)skh * g.N + (long long)min(th0 + sr, g.H - 1) * g.W +
-                    min(tw0 + sc, g.W - 1);
-  // Fragment read offset of tile t: target j of MFMA tile t is spatial
-  // (2t + ((j >> 2) & 1), (j & 3) + 4 (j >> 3)).
-  const int j = lane & 31;
-  const int rsp = ((j >> 2) & 1) * 16 + (j & 3) + 4 * (j >> 3);
-  const int rdb = (rsp * 2 + (kh ^ ((j >> 2) & 1))) * 16;
-  const int rda = PS_B + wave * PS_AW + lane * 16;
-
-  const int nk = g.D / 16;
-  auto issue = [&](int ks) {
-    if constexpr (ABL == 5) return;
-    unsigned char* st = smem + (ks % NS) * PS_STAGE;
-    const long long ko = (long long)ks * 2 * g.N;
-#pragma unroll
-    for (int p = 0; p < 3; ++p) glds_chunk(pb + ko + p * plane, st + p * (NTGT * 2 * 16) + wave * 1024);
-#pragma unroll
-    for (int p = 0; p < 3; ++p) glds_chunk(pa + ko + p * plane, st + PS_B + wave * PS_AW + p * 1024);
-  };
-  auto compute = [&](int ks) {
-    const unsigned char* st = smem + (ks % NS) * PS_STAGE;
-    const bf8v qh = *reinterpret_cast<const bf8v*>(st + rda);
-    const bf8v qm = *reinterpret_cast<const bf8v*>(st + rda + 1024);
-    const bf8v ql = *reinterpret_cast<const bf8v*>(st + rda + 2048);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const unsigned char* pt = st + rdb + t * 32 * 2 * 16;
-      const bf8v th = *reinterpret_cast<const bf8v*>(pt);
-      const bf8v tm = *reinterpret_cast<const bf8v*>(pt + NTGT * 2 * 16);
-      const bf8v tl = *reinterpret_cast<const bf8v*>(pt + 2 * NTGT * 2 * 16);
-      if constexpr (ABL == 2 || ABL == 4) {
-        const s8v x = __builtin_bit_cast(s8v, th) ^ __builtin_bit_cast(s8v, tm) ^
-                      __builtin_bit_cast(s8v, tl) ^ __builtin_bit_cast(s8v, qh) ^
-                      __builtin_bit_cast(s8v, qm) ^ __builtin_bit_cast(s8v, ql);
-        acc[t][0] += (float)(x[0] + x[3] + x[5] + x[7]);
-        continue;
-      }
-      // small terms first
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, ql, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qh, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qm, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh, acc[t], 0, 0, 0);
-    }
-  };
-
-  // Iteration ks: wait for stage ks (all but the 6 DMA ops of each younger stage
-  // in flight), raw barrier (the DMA data of every wave is then visible, and
-  // every wave has finished reading stage ks - 1), issue stage ks + NS - 1 into
-  // the slot stage ks - 1 used, compute stage ks.
-#pragma unroll
-  for (int s = 0; s < NS - 1; ++s)
-    if (ABL != 3 && s < nk) issue(s);
-  for (int ks = 0; ks < (ABL == 3 ? 0 : nk); ++ks) {
-    const int younger = min(NS - 2, nk - 1 - ks);   // stages issued after ks
-    if (NS >= 3 && younger >= 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (ks + NS - 1 < nk) issue(ks + NS - 1);
-    compute(ks);
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();   // the epilogue reuses the ring's LDS
-
-  scale_acc<DIV>(acc, g);
-  if constexpr (ABL == 1 || ABL == 4 || ABL == 5) {
-    float sum = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sum += acc[t][r];
-    if (sum == 1234.5f) pyr[tid] = to_out<OT>(sum);  // keeps the K loop live
-    return;
-  }
-  const long long page = ((long long)b * gridDim.y + blockIdx.y) * ((long long)g.tiles_h *
-                         g.tiles_w) + (long long)tyi * g.tiles_w + txi;
-  paged_epilogue<OT, false>(acc, reinterpret_cast<float*>(smem), pyr, g, page, wave, wave, true, lane);
+  paged_epilogue<OT>(acc, reinterpret_cast<float*>(smem), pyr, g, pc.page, wave, lane);
 }
 
 // Floor-mode 2x2 average pool of one pyramid level into the next, for levels
@@ -1209,207 +946,87 @@ dim3 remap_grid(const BuildGeom& g, int B) {
   return dim3((unsigned)((long long)B * g.qt * g.tiles_h * g.tiles_w));
 }
 
-int resident_build_groups(int per_cu) {
-  static int cus = [] {
-    int dev = 0, n = 256;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      n = 256;
-    return n;
-  }();
-  return cus * per_cu;
-}
-
-// One f32 build configuration.  PERSIST: gridDim = resident workgroups
-// (MINW of 4-wave workgroups per CU) walking the pages.
-template <bool VEC, int BK, bool PAGED, typename OT, bool NTS, int MINW, bool GLDS, bool PERSIST>
-int launch_f32(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, int B,
+// Exact-f32 build: VEC = float4 staging (W % 4 == 0, aligned) at 3 waves/SIMD
+// (r01: 247-258 us at Sintel against 278 at the compiler's choice); scalar
+// staging at the compiler's choice.
+template <bool PAGED, typename OT>
+int launch_f32(bool vec, const float* f1, const float* f2, OT* pyr, const BuildGeom& g, int B,
                hipStream_t stream) {
   const dim3 grid = build_grid(g, B);
   if (grid.y > 65535) return DXR_EINVAL;
-  if constexpr (PERSIST) {
-    static_assert(PAGED, "persistent build writes pages");
-    const long long pages = (long long)grid.x * grid.y * grid.z;
-    const long long cap = resident_build_groups(MINW > 0 ? MINW : 2);
-    const unsigned groups = (unsigned)(pages < cap ? pages : cap);
-    if (g.recip != 0.f)
-      hipLaunchKernelGGL((corr_build_f32_persistent<VEC, BK, OT, NTS, MINW, GLDS, false>),
-                         dim3(groups), dim3(NT), 0, stream, f1, f2, pyr, g, pages);
-    else
-      hipLaunchKernelGGL((corr_build_f32_persistent<VEC, BK, OT, NTS, MINW, GLDS, true>),
-                         dim3(groups), dim3(NT), 0, stream, f1, f2, pyr, g, pages);
-  } else {
-    if (g.recip != 0.f)
-      hipLaunchKernelGGL((corr_build_f32_kernel<VEC, BK, PAGED, OT, NTS, MINW, GLDS, false>), grid,
-                         dim3(NT), 0, stream, f1, f2, pyr, g);
-    else
-      hipLaunchKernelGGL((corr_build_f32_kernel<VEC, BK, PAGED, OT, NTS, MINW, GLDS, true>), grid,
-                         dim3(NT), 0, stream, f1, f2, pyr, g);
-  }
-  return dxr::launch_status();
-}
-
-template <bool VEC, int MINW, typename OT, bool REMAP = false>
-int launch_bf16_w(const uint16_t* f1, const uint16_t* f2, OT* pyr, const BuildGeom& g, dim3 grid,
-                  hipStream_t stream) {
-  if (g.recip == 0.f)
-    hipLaunchKernelGGL((corr_build_bf16_kernel<VEC, OT, true, MINW, REMAP>), grid, dim3(NT), 0,
+  const bool div = g.recip == 0.f;
+  if (vec && div)
+    hipLaunchKernelGGL((corr_build_f32_kernel<true, 16, PAGED, OT, 3, true>), grid, dim3(NT), 0,
+                       stream, f1, f2, pyr, g);
+  else if (vec)
+    hipLaunchKernelGGL((corr_build_f32_kernel<true, 16, PAGED, OT, 3, false>), grid, dim3(NT), 0,
+                       stream, f1, f2, pyr, g);
+  else if (div)
+    hipLaunchKernelGGL((corr_build_f32_kernel<false, 16, PAGED, OT, 0, true>), grid, dim3(NT), 0,
                        stream, f1, f2, pyr, g);
   else
-    hipLaunchKernelGGL((corr_build_bf16_kernel<VEC, OT, false, MINW, REMAP>), grid, dim3(NT), 0,
+    hipLaunchKernelGGL((corr_build_f32_kernel<false, 16, PAGED, OT, 0, false>), grid, dim3(NT), 0,
                        stream, f1, f2, pyr, g);
   return dxr::launch_status();
 }
 
-int build_variant();
-
-// bf16 variants: 0 default (launch bound 3 waves/SIMD; compiled at 120 VGPRs = 4,
-// matching the 4 workgroups per CU its 40 KB of LDS allows; XCD-aware page order: r01 KITTI b8
-// 721 us vs 837 in grid order; the scalar-staging path keeps the compiler's
-// choice, it would spill at 3); 1 compiler-chosen occupancy; 3 grid order;
-// 6 = 0 at 2 waves/SIMD.  Tried and removed (r01, KITTI b8): operand stages two
-// ahead from two register sets, with all 20 fragment reads of a stage issued
-// before its MFMAs: 660-704 us vs 645-662 — the K loop is not load- or
-// LDS-latency-bound.  64-deep K stages (half the barriers, 80 KB LDS, 2 workgroups
-// per CU): 862 vs 669 us at KITTI b8, 108 vs 86 us at Sintel — nor barrier-bound.
+// bf16 build: launch bound 3 waves/SIMD (compiled at 120 VGPRs = 4, matching
+// the 4 workgroups per CU its 40 KB of LDS allows) and the XCD-aware page order
+// (r01 KITTI b8: 721 us vs 837 in grid order).  The scalar-staging path keeps
+// the compiler's choice (it would spill at 3) and the grid order.
 template <typename OT>
 int launch_build_bf16(bool vec, const uint16_t* f1, const uint16_t* f2, OT* pyr,
                       const BuildGeom& g, int B, hipStream_t stream) {
   const dim3 grid = build_grid(g, B);
   if (grid.y > 65535) return DXR_EINVAL;
-  if (!vec) return launch_bf16_w<false, 0>(f1, f2, pyr, g, grid, stream);
-  if (build_variant() == 1) return launch_bf16_w<true, 0>(f1, f2, pyr, g, grid, stream);
-  if (build_variant() == 3) return launch_bf16_w<true, 3>(f1, f2, pyr, g, grid, stream);
-  if (build_variant() == 6)  // 2 waves/SIMD: 628-640 vs 645-662 us (KITTI b8, within noise)
-    return launch_bf16_w<true, 2, OT, true>(f1, f2, pyr, g, remap_grid(g, B), stream);
-  return launch_bf16_w<true, 3, OT, true>(f1, f2, pyr, g, remap_grid(g, B), stream);
+  const bool div = g.recip == 0.f;
+  if (vec) {
+    const dim3 rg = remap_grid(g, B);
+    if (div)
+      hipLaunchKernelGGL((corr_build_bf16_kernel<true, OT, true, 3, true>), rg, dim3(NT), 0, stream,
+                         f1, f2, pyr, g);
+    else
+      hipLaunchKernelGGL((corr_build_bf16_kernel<true, OT, false, 3, true>), rg, dim3(NT), 0,
+                         stream, f1, f2, pyr, g);
+  } else if (div) {
+    hipLaunchKernelGGL((corr_build_bf16_kernel<false, OT, true, 0, false>), grid, dim3(NT), 0,
+                       stream, f1, f2, pyr, g);
+  } else {
+    hipLaunchKernelGGL((corr_build_bf16_kernel<false, OT, false, 0, false>), grid, dim3(NT), 0,
+                       stream, f1, f2, pyr, g);
+  }
+  return dxr::launch_status();
 }
 
-template <int MINW, typename OT, int ABL = 0, bool REMAP = false, int BV = 4>
+// Split build (f32 class on bf16 MFMA) at 4 waves/SIMD (r01: 172 us at Sintel
+// against 177 at 3 and 183 at the compiler's choice).
+template <typename OT, int BV>
 int launch_split(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, int B,
                  hipStream_t stream) {
-  const dim3 grid = REMAP ? remap_grid(g, B) : build_grid(g, B);
-  if (!REMAP && grid.y > 65535) return DXR_EINVAL;
-  if ((long long)B * g.qt * g.tiles_h * g.tiles_w > (1LL << 31) - 1) return DXR_EINVAL;
-  if (g.recip == 0.f)
-    hipLaunchKernelGGL((corr_build_split_kernel<OT, true, MINW, ABL, REMAP, BV>), grid, dim3(NT),
-                       0, stream, f1, f2, pyr, g);
-  else
-    hipLaunchKernelGGL((corr_build_split_kernel<OT, false, MINW, ABL, REMAP, BV>), grid, dim3(NT),
-                       0, stream, f1, f2, pyr, g);
-  return dxr::launch_status();
-}
-
-// Workspace of the presplit build: hi/mid/lo bf16 planes of both fmaps.
-long long presplit_ws_bytes(long long B, long long D, long long N) {
-  return 2LL * B * 3 * D * N * 2;
-}
-
-template <int MINW, int NS, typename OT, int ABL = 0>
-int launch_presplit(const float* f1, const float* f2, void* ws, OT* pyr, const BuildGeom& g,
-                    int B, hipStream_t stream) {
   const dim3 grid = build_grid(g, B);
-  if (grid.y > 65535 || 2LL * B > 65535) return DXR_EINVAL;
-  uint4* w = static_cast<uint4*>(ws);
-  hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((g.N + 255) / 256), (unsigned)(g.D / 8),
-                                               (unsigned)(2 * B)),
-                     dim3(256), 0, stream, f1, f2, w, B, g.D, g.N);
-  const int st = dxr::launch_status();
-  if (st != DXR_OK) return st;
+  if (grid.y > 65535) return DXR_EINVAL;
   if (g.recip == 0.f)
-    hipLaunchKernelGGL((corr_build_presplit_kernel<OT, true, MINW, NS, ABL>), grid, dim3(NT), 0,
-                       stream, w, pyr, g, B);
+    hipLaunchKernelGGL((corr_build_split_kernel<OT, true, 4, BV>), grid, dim3(NT), 0, stream, f1,
+                       f2, pyr, g);
   else
-    hipLaunchKernelGGL((corr_build_presplit_kernel<OT, false, MINW, NS, ABL>), grid, dim3(NT), 0,
-                       stream, w, pyr, g, B);
+    hipLaunchKernelGGL((corr_build_split_kernel<OT, false, 4, BV>), grid, dim3(NT), 0, stream, f1,
+                       f2, pyr, g);
   return dxr::launch_status();
 }
 
-// DXR_BUILD_VARIANT selects a tuning variant (same-process A/B timing only).
-int build_variant() {
-  const char* v = std::getenv("DXR_BUILD_VARIANT");
-  return v ? std::atoi(v) : 0;
-}
-
-// Variants: 0 default (= 8, the split build, when D % 16 == 0 and W % 4 == 0;
-// else 2); presplit builds (need the workspace; r01 sintel: 181-190 us vs 178
-// for 8, operand staging L2 -> LDS bound, §DESIGN): 11 = 3-stage ring (72 KiB, 2 WG/CU),
-// 12 = 2 stages at 3 WG/CU, 13 = 2 stages at 2 WG/CU;
-// f32-MFMA builds: 1 register staging,
-// 2 waves/SIMD; 2 register staging, 3 waves/SIMD; 3 glds staging, 3 waves/SIMD;
-// 4 glds staging, 4 waves/SIMD; 5 = 3 persistent; 6 = 2 with nontemporal
-// stores.  Measured (sintel, MI355X, r01i): 257 / 278 / 258 / 247 / 245 / 250 /
-// 257 us for variants 0(old default = 2) .. 6; 10 = 4.  Split builds (bf16x6
-// MFMA, f32-class error): 7 at 3 waves/SIMD, 8 at 4, 9 compiler-chosen —
-// r01k: 177 / 172 / 183 us against 289 us for the f32-MFMA build on that box.
-template <bool PAGED, typename OT = float>
+// f32 fmaps: the split build when its layout conditions hold (D % 16 == 0;
+// float4 target units for W % 4 == 0, float2 units for even W), else — or on
+// request (DXR_BUILD_EXACT_F32) — the exact-f32 MFMA build.
+template <typename OT>
 int launch_build_f32(bool vec, const float* f1, const float* f2, OT* pyr, const BuildGeom& g,
-                     int B, hipStream_t stream, void* ws = nullptr) {
-  if constexpr (PAGED) {
-    // presplit: any W (edge tiles read clamped pixels), needs D % 16 and the workspace
-    const int v = build_variant();
-    if (ws != nullptr && g.D % 16 == 0) {
-      if (v == 11) return launch_presplit<2, 3, OT>(f1, f2, ws, pyr, g, B, stream);
-      if (v == 12) return launch_presplit<3, 2, OT>(f1, f2, ws, pyr, g, B, stream);
-      if (v == 13) return launch_presplit<2, 2, OT>(f1, f2, ws, pyr, g, B, stream);
-      if (v == 111) return launch_presplit<2, 3, OT, 1>(f1, f2, ws, pyr, g, B, stream);  // timing
-      if (v == 112) return launch_presplit<2, 3, OT, 2>(f1, f2, ws, pyr, g, B, stream);  // timing
-      if (v == 113) return launch_presplit<2, 3, OT, 3>(f1, f2, ws, pyr, g, B, stream);  // timing
-      if (v == 114) return launch_presplit<2, 3, OT, 4>(f1, f2, ws, pyr, g, B, stream);  // timing
-      if (v == 115) return launch_presplit<2, 3, OT, 5>(f1, f2, ws, pyr, g, B, stream);  // timing
-      if (v == 125) return launch_presplit<3, 2, OT, 5>(f1, f2, ws, pyr, g, B, stream);  // timing
-    }
+                     int B, int algo, hipStream_t stream) {
+  if (algo == DXR_BUILD_AUTO && g.D % 16 == 0) {
+    if (vec) return launch_split<OT, 4>(f1, f2, pyr, g, B, stream);
+    if (g.W % 2 == 0 && ((uintptr_t)f1 % 8) == 0 && ((uintptr_t)f2 % 8) == 0 &&
+        ((uintptr_t)pyr % 16) == 0)
+      return launch_split<OT, 2>(f1, f2, pyr, g, B, stream);
   }
-  if constexpr (PAGED) {
-    // W even but not a multiple of 4 (Chairs: 62): the split build on float2 target units
-    if (!vec && g.D % 16 == 0 && g.W % 2 == 0 && build_variant() != 2 && ((uintptr_t)f2 % 8) == 0)
-      return launch_split<4, OT, 0, false, 2>(f1, f2, pyr, g, B, stream);
-  }
-  if (!vec) return launch_f32<false, 16, PAGED, OT, false, 0, false, false>(f1, f2, pyr, g, B, stream);
-  if constexpr (PAGED) {
-    const bool glds = g.D % 16 == 0;
-    switch (build_variant()) {
-      case 1: return launch_f32<true, 16, true, OT, false, 0, false, false>(f1, f2, pyr, g, B, stream);
-      case 2: return launch_f32<true, 16, true, OT, false, 3, false, false>(f1, f2, pyr, g, B, stream);
-      case 3:
-        if (glds) return launch_f32<true, 16, true, OT, false, 3, true, false>(f1, f2, pyr, g, B, stream);
-        break;
-      case 4:
-        if (glds) return launch_f32<true, 16, true, OT, false, 4, true, false>(f1, f2, pyr, g, B, stream);
-        break;
-      case 5:
-        if (glds) return launch_f32<true, 16, true, OT, false, 3, true, true>(f1, f2, pyr, g, B, stream);
-        break;
-      case 6: return launch_f32<true, 16, true, OT, true, 3, false, false>(f1, f2, pyr, g, B, stream);
-      case 7:
-        if (glds) return launch_split<3>(f1, f2, pyr, g, B, stream);
-        break;
-      case 8:
-        if (glds) return launch_split<4>(f1, f2, pyr, g, B, stream);
-        break;
-      case 9:
-        if (glds) return launch_split<2>(f1, f2, pyr, g, B, stream);
-        break;
-      case 91:  // timing-only ablations of the split build (outputs invalid)
-        if (glds) return launch_split<4, OT, 1>(f1, f2, pyr, g, B, stream);
-        break;
-      case 92:
-        if (glds) return launch_split<4, OT, 2>(f1, f2, pyr, g, B, stream);
-        break;
-      case 40:  // split build, XCD-aware page order
-        if (glds) return launch_split<4, OT, 0, true>(f1, f2, pyr, g, B, stream);
-        break;
-      case 10:  // f32 MFMA build (glds staging, 4 waves/SIMD)
-        if (glds) return launch_f32<true, 16, true, OT, false, 4, true, false>(f1, f2, pyr, g, B, stream);
-        break;
-      default:
-        if (glds) return launch_split<4>(f1, f2, pyr, g, B, stream);
-        break;
-    }
-    return launch_f32<true, 16, true, OT, false, 3, false, false>(f1, f2, pyr, g, B, stream);
-  } else {
-    return launch_f32<true, 16, false, OT, false, 0, false, false>(f1, f2, pyr, g, B, stream);
-  }
+  return launch_f32<true>(vec, f1, f2, pyr, g, B, stream);
 }
 
 BuildGeom make_geom(int64_t D, int64_t H, int64_t W, float divisor, const dxr::Levels& L) {
@@ -1456,39 +1073,30 @@ extern "C" int dxr_avg_pool2x2(const float* in, float* out, int64_t planes, int6
   return launch_avg_pool(in, out, planes, (int)H, (int)W, stream);
 }
 
-extern "C" int64_t dxr_build_workspace_bytes(int64_t B, int64_t D, int64_t H, int64_t W,
-                                             int in_dtype) {
-  if (B < 1 || D < 1 || H < 1 || W < 1 || H * W > (1LL << 30)) return 0;
-  if (in_dtype != DXR_F32 || D % 16 != 0) return 0;
-  const int v = build_variant();   // only the presplit variants use a workspace
-  if (!((v >= 11 && v <= 13) || (v >= 111 && v <= 115) || v == 125))
-    return 0;
-  return presplit_ws_bytes(B, D, H * W);
-}
-
 extern "C" int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int in_dtype,
-                                      int64_t B, int64_t D, int64_t H, int64_t W,
-                                      int num_levels, float divisor, void* pyramid,
-                                      int pyr_dtype, void* workspace, int64_t workspace_bytes,
-                                      hipStream_t stream) {
+                                      int fmap_layout, int64_t B, int64_t D, int64_t H,
+                                      int64_t W, int num_levels, float divisor, void* pyramid,
+                                      int pyr_dtype, int algo, hipStream_t stream) {
   dxr::Levels L;
   if (!dxr::make_levels(B, H, W, num_levels, &L)) return DXR_EINVAL;
+  if (fmap_layout != DXR_NCHW && fmap_layout != DXR_NHWC) return DXR_EINVAL;
+  if (algo != DXR_BUILD_AUTO && algo != DXR_BUILD_EXACT_F32) return DXR_EINVAL;
   const int chk = check_build_args(fmap1, fmap2, in_dtype, B, D, divisor, pyramid, pyr_dtype);
   if (chk != PROCEED) return chk;
-  if (workspace_bytes < 0 || (workspace != nullptr && !aligned16(workspace))) return DXR_EINVAL;
+  // Levels beyond the fused four are pooled by f32 passes: f32 pyramids only.
+  if (L.n > dxr::TILED_LEVELS && pyr_dtype != DXR_F32) return DXR_EUNSUPPORTED;
+  if (algo == DXR_BUILD_EXACT_F32 && in_dtype != DXR_F32) return DXR_EUNSUPPORTED;
+  if (fmap_layout == DXR_NHWC) return DXR_EUNSUPPORTED;
   const BuildGeom g = make_geom(D, H, W, divisor, L);
   int st;
   if (in_dtype == DXR_F32) {
     const float* f1 = static_cast<const float*>(fmap1);
     const float* f2 = static_cast<const float*>(fmap2);
     const bool vec = (W % 4) == 0 && aligned16(f1) && aligned16(f2) && aligned16(pyramid);
-    const int64_t need = dxr_build_workspace_bytes(B, D, H, W, in_dtype);
-    void* ws = (need > 0 && workspace != nullptr && workspace_bytes >= need) ? workspace : nullptr;
     st = pyr_dtype == DXR_F32
-             ? launch_build_f32<true>(vec, f1, f2, static_cast<float*>(pyramid), g, (int)B, stream,
-                                      ws)
-             : launch_build_f32<true>(vec, f1, f2, static_cast<uint16_t*>(pyramid), g, (int)B,
-                                      stream, ws);
+             ? launch_build_f32(vec, f1, f2, static_cast<float*>(pyramid), g, (int)B, algo, stream)
+             : launch_build_f32(vec, f1, f2, static_cast<uint16_t*>(pyramid), g, (int)B, algo,
+                                stream);
   } else {
     const uint16_t* f1 = static_cast<const uint16_t*>(fmap1);
     const uint16_t* f2 = static_cast<const uint16_t*>(fmap2);
@@ -1499,7 +1107,6 @@ extern "C" int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int 
              : launch_build_bf16(vec, f1, f2, static_cast<uint16_t*>(pyramid), g, (int)B, stream);
   }
   if (st != DXR_OK) return st;
-  if (L.n > dxr::TILED_LEVELS && pyr_dtype != DXR_F32) return DXR_EUNSUPPORTED;
   float* pyr = static_cast<float*>(pyramid);
   // Levels beyond the fused four: plain pooling passes, level l from level l-1.
   for (int l = dxr::TILED_LEVELS; l < L.n; ++l) {
@@ -1524,7 +1131,7 @@ extern "C" int dxr_corr_volume(const void* fmap1, const void* fmap2, int in_dtyp
   const float* f1 = static_cast<const float*>(fmap1);
   const float* f2 = static_cast<const float*>(fmap2);
   const bool vec = (W % 4) == 0 && aligned16(f1) && aligned16(f2) && aligned16(out);
-  return launch_build_f32<false>(vec, f1, f2, out, g, (int)B, stream);
+  return launch_f32<false>(vec, f1, f2, out, g, (int)B, stream);
 }
 
 extern "C" int dxr_pyramid_unpack(const void* pyramid, int pyr_dtype, int64_t B, int64_t H,

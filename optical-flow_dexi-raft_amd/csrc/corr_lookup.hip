@@ -29,8 +29,6 @@
 //            gathers thrash the 32 KiB L1 and become L2-bandwidth bound);
 //   phase 2  thread = (query, x-offset class): taps from LDS, fused sum, and
 //            every output store is a coalesced 256-B wave store along queries.
-#include <cstdlib>
-
 #include "dxr_common.h"
 
 namespace {
@@ -84,156 +82,9 @@ __device__ __forceinline__ float sample_coord(float c, float sm1, float half_sm1
   return __fmul_rn(__fadd_rn(gn, 1.f), half_sm1);
 }
 
-template <int R>
-struct LookupCfg {
-  static constexpr int RD = 2 * R + 1;     // samples per axis
-  static constexpr int WD = RD + 2;        // staged window side
-  static constexpr int NC = WD * WD;       // cells per window (odd: bank-friendly pitch)
-  static constexpr int NTHR = 128;         // two waves
-  static constexpr int QB = R <= 4 ? 32 : 16;  // queries per workgroup
-  static constexpr int NG = NTHR / QB;     // x-offset classes in phase 2
-  static constexpr int QPW = QB / (NTHR / 64);  // queries gathered per wave
-  static constexpr int CPL = (NC + 63) / 64;    // window cells per lane per query
-};
-
-// ABL (timing-only ablations, DXR_LOOKUP_VARIANT; outputs invalid): bit 0 skips
-// the window gathers, bit 1 skips the output stores.
-template <int R, typename PT, int ABL = 0>
-__global__ __launch_bounds__(LookupCfg<R>::NTHR) void corr_lookup_kernel(const PT* __restrict__ pyr,
-                                                           const float* __restrict__ coords,
-                                                           float* __restrict__ out,
-                                                           LookupGeom g) {
-  using C = LookupCfg<R>;
-  constexpr int RD = C::RD, WD = C::WD, NC = C::NC, QB = C::QB, NG = C::NG;
-  constexpr int QPW = C::QPW, CPL = C::CPL;
-  __shared__ float cells[QB * NC];
-  __shared__ float sx[RD * QB];
-  __shared__ float sy[RD * QB];
-  __shared__ int org[2 * QB];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int l = blockIdx.y, b = blockIdx.z;
-  const int q0 = blockIdx.x * QB;
-  const LevelAddr A = g.lv[l];
-  const int Hl = A.h, Wl = A.w;
-
-  // ---- phase 0: sample positions and window origin per query
-  if (tid < QB) {
-    const int q = q0 + tid;
-    float x = 0.f, y = 0.f;
-    if (q < g.N) {
-      const float inv = 1.f / (float)(1 << l);  // exact power of two
-      x = coords[((long long)b * 2 + 0) * g.N + q] * inv;
-      y = coords[((long long)b * 2 + 1) * g.N + q] * inv;
-    }
-    const float wm1 = (float)(Wl - 1), hm1 = (float)(Hl - 1);
-    const float whalf = wm1 / 2.f, hhalf = hm1 / 2.f;
-    bool far = false;
-    int mx = 1 << 30, my = 1 << 30;
-#pragma unroll
-    for (int j = 0; j < RD; ++j) {
-      const float u = sample_coord(__fadd_rn(x, (float)(j - R)), wm1, whalf);
-      const float v = sample_coord(__fadd_rn(y, (float)(j - R)), hm1, hhalf);
-      sx[j * QB + tid] = u;
-      sy[j * QB + tid] = v;
-      const float fu = floorf(u), fv = floorf(v);
-      if (!(fabsf(fu) < 1.0e7f) || !(fabsf(fv) < 1.0e7f)) {
-        far = true;
-      } else {
-        mx = min(mx, (int)fu - j);
-        my = min(my, (int)fv - j);
-      }
-    }
-    // Windows entirely off the level hold only zeros: skip their loads.
-    if (!far && (mx + WD <= 0 || mx >= Wl || my + WD <= 0 || my >= Hl)) far = true;
-    org[tid] = far ? FAR_ORIGIN : mx;
-    org[QB + tid] = far ? FAR_ORIGIN : my;
-  }
-  __syncthreads();
-
-  // ---- phase 1: gather each query's window into LDS (zeros off the level).
-  // All of a wave's loads are issued before its first LDS store, so the
-  // QPW x CPL gathers are in flight together (one memory latency per wave).
-  float cellv[QPW][CPL];
-#pragma unroll
-  for (int i = 0; i < QPW; ++i) {
-    const int qq = wave * QPW + i;
-    const int q = q0 + qq;
-    const int xlo = org[qq], ylo = org[QB + qq];
-    const bool live = q < g.N && xlo != FAR_ORIGIN;
-    const int qs = live ? q : 0;
-    const PT* img = pyr + A.off + ((long long)b * A.qt + (qs >> A.lqb)) * A.qstride +
-                    (long long)(qs & ((1 << A.lqb) - 1)) * A.S;
-#pragma unroll
-    for (int m = 0; m < CPL; ++m) {
-      const int c = m * 64 + lane;
-      const int yy = ylo + c / WD, xx = xlo + c % WD;
-      const bool in = live && c < NC && (unsigned)yy < (unsigned)Hl && (unsigned)xx < (unsigned)Wl;
-      const long long e = ((long long)(yy >> A.lth) * A.tx + (xx >> A.ltw)) * A.pageS +
-                          (yy & A.mh) * A.tw + (xx & A.mw);
-      if constexpr (ABL & 1) cellv[i][m] = in ? (float)(e & 7) : 0.f;
-      else cellv[i][m] = in ? load_cell(img + e) : 0.f;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < QPW; ++i)
-#pragma unroll
-    for (int m = 0; m < CPL; ++m) {
-      const int c = m * 64 + lane;
-      if (c < NC) cells[(wave * QPW + i) * NC + c] = cellv[i][m];
-    }
-  __syncthreads();
-
-  // ---- phase 2: bilinear taps from LDS, coalesced stores along queries
-  const int qq = tid % QB;
-  const int q = q0 + qq;
-  if (q >= g.N) return;
-  const int xlo = org[qq], ylo = org[QB + qq];
-  const bool live = xlo != FAR_ORIGIN;
-  const float* cq = cells + qq * NC;
-  int row[RD];
-  float fn[RD], fs[RD];
-#pragma unroll
-  for (int oy = 0; oy < RD; ++oy) {
-    const float v = sy[oy * QB + qq];
-    const float fl = floorf(v);
-    fn[oy] = __fsub_rn(v, fl);
-    fs[oy] = __fsub_rn(1.f, fn[oy]);
-    row[oy] = live ? ((int)fl - ylo) * WD : 0;
-  }
-  float* ob = out + ((long long)b * g.cout + (long long)l * RD * RD) * g.N + q;
-  for (int ox = tid / QB; ox < RD; ox += NG) {
-    const float u = sx[ox * QB + qq];
-    const float fl = floorf(u);
-    const float fx = __fsub_rn(u, fl);
-    const float ex = __fsub_rn(1.f, fx);
-    const int col = live ? (int)fl - xlo : 0;
-#pragma unroll
-    for (int oy = 0; oy < RD; ++oy) {
-      float v00 = 0.f, v01 = 0.f, v10 = 0.f, v11 = 0.f;
-      if (live) {
-        const float* p = cq + row[oy] + col;
-        v00 = p[0]; v01 = p[1]; v10 = p[WD]; v11 = p[WD + 1];
-      }
-      const float nw = __fmul_rn(fs[oy], ex), ne = __fmul_rn(fs[oy], fx);
-      const float sw = __fmul_rn(fn[oy], ex), se = __fmul_rn(fn[oy], fx);
-      float v = __fmul_rn(nw, v00);
-      v = __builtin_fmaf(ne, v01, v);
-      v = __builtin_fmaf(sw, v10, v);
-      v = __builtin_fmaf(se, v11, v);
-      if constexpr (ABL & 2) {
-        if (v == 1234.5f) ob[(long long)(ox * RD + oy) * g.N] = v;
-      } else {
-        ob[(long long)(ox * RD + oy) * g.N] = v;
-      }
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
-// Lookup, wide form (default).  Same arithmetic, sample by sample, as
-// corr_lookup_kernel above; the work of a workgroup (QB queries x one level) is
-// spread over NT = 512 threads so that no phase is a long per-thread chain:
+// Lookup.  The work of a workgroup (QB queries x one level) is spread over
+// NT = 512 threads so that no phase is a long per-thread chain:
 //   phase 0  one thread per (query, sample index j): both axes' coordinate
 //            round trips, floors and fractions; the window origin
 //            min_j(floor_j - j) and the far test are reduced over the query's
@@ -245,10 +96,9 @@ __global__ __launch_bounds__(LookupCfg<R>::NTHR) void corr_lookup_kernel(const P
 //            base, into LDS rows of RS cells starting at the origin rounded down
 //            to a multiple of 4;
 //   phase 2  thread = (query, output class), stores along queries.
-// The narrow form's profile (r01, sintel: 1,600 VALU instructions per wave,
-// 1.7 waves per SIMD, 8.8 of 11.6 us left with gathers and stores removed) was
-// its per-thread instruction chains: the per-cell address arithmetic of the
-// gather, and phase 0 on a quarter of the threads.
+// A narrow predecessor (128 threads per 32 queries; r01, sintel: 1,600 VALU
+// instructions per wave, 1.7 waves per SIMD, 8.8 of 11.6 us left with gathers
+// and stores removed) was bound by its per-thread instruction chains.
 // ---------------------------------------------------------------------------
 template <int R, int NT_ = 512>
 struct WideCfg {
@@ -405,9 +255,7 @@ __device__ __forceinline__ void wide_phase0(const float* __restrict__ coords, co
   }
 }
 
-// ABL (timing-only ablations, outputs invalid): 4 returns at once, 5 after phase 0,
-// 6 after phase 1, 7 skips the gathers.
-template <int R, typename PT, int ABL = 0, int NT_ = 512>
+template <int R, typename PT, int NT_ = 512>
 __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
     const PT* __restrict__ pyr, const float* __restrict__ coords, float* __restrict__ out,
     LookupGeom g) {
@@ -422,18 +270,13 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
   const int l = blockIdx.y, b = blockIdx.z;
   const int q0 = blockIdx.x * QB;
   const LevelAddr A = g.lv[l];
-  if constexpr (ABL == 4) return;
 
   // ---- phase 0
   wide_phase0<R, NT_>(coords, g, A, b, l, q0, tid, xs, ys, org);
   __syncthreads();
-  if constexpr (ABL == 5) {
-    if (xs[tid % (RD * QB)].y == 1234.5f) out[tid] = 0.f;
-    return;
-  }
 
   // ---- phase 1 (zeros off the level and for far queries)
-  if constexpr (ABL != 7) {
+  {
     const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
     const int qb0 = q0 & ((1 << A.lqb) - 1);
     if (A.lth == 30)
@@ -446,10 +289,6 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
       gather_windows<R, NT_, 1>(base, qb0, A, org, cells, q0, g.N, tid);
   }
   __syncthreads();
-  if constexpr (ABL == 6) {
-    if (cells[tid] == 1234.5f) out[tid] = 0.f;
-    return;
-  }
 
   // ---- phase 2
   const int qq = tid % QB, cls = tid / QB;
@@ -559,64 +398,13 @@ int launch_lookup_backward_r(const float* coords, const float* gout, float* gpyr
   return dxr::launch_status();
 }
 
-int lookup_variant() {
-  const char* v = std::getenv("DXR_LOOKUP_VARIANT");
-  return v ? std::atoi(v) : 0;
-}
-
 template <int R, typename PT>
 int launch_lookup_r(const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
                     hipStream_t stream) {
-  using C = LookupCfg<R>;
-  const dim3 grid((unsigned)((g.N + C::QB - 1) / C::QB), (unsigned)g.levels, (unsigned)B);
-  switch (lookup_variant()) {
-    case 91:
-      hipLaunchKernelGGL((corr_lookup_kernel<R, PT, 1>), grid, dim3(C::NTHR), 0, stream, pyr,
-                         coords, out, g);
-      break;
-    case 92:
-      hipLaunchKernelGGL((corr_lookup_kernel<R, PT, 2>), grid, dim3(C::NTHR), 0, stream, pyr,
-                         coords, out, g);
-      break;
-    case 93:
-      hipLaunchKernelGGL((corr_lookup_kernel<R, PT, 3>), grid, dim3(C::NTHR), 0, stream, pyr,
-                         coords, out, g);
-      break;
-    case 1:  // narrow form
-      hipLaunchKernelGGL((corr_lookup_kernel<R, PT>), grid, dim3(C::NTHR), 0, stream, pyr, coords,
-                         out, g);
-      break;
-    case 2: {  // wide form at 256 threads
-      using W = WideCfg<R, 256>;
-      const dim3 gw((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
-      hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT, 0, 256>), gw, dim3(256), 0, stream, pyr,
-                         coords, out, g);
-      break;
-    }
-    case 3: {  // wide form at 1024 threads
-      using W = WideCfg<R, 1024>;
-      const dim3 gw((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
-      hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT, 0, 1024>), gw, dim3(1024), 0, stream,
-                         pyr, coords, out, g);
-      break;
-    }
-    case 94: case 95: case 96: case 97: {
-      using W = WideCfg<R>;
-      const dim3 gw((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
-      const int v = lookup_variant();
-      if (v == 94) hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT, 4>), gw, dim3(W::NT), 0, stream, pyr, coords, out, g);
-      if (v == 95) hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT, 5>), gw, dim3(W::NT), 0, stream, pyr, coords, out, g);
-      if (v == 96) hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT, 6>), gw, dim3(W::NT), 0, stream, pyr, coords, out, g);
-      if (v == 97) hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT, 7>), gw, dim3(W::NT), 0, stream, pyr, coords, out, g);
-      break;
-    }
-    default: {
-      using W = WideCfg<R>;
-      const dim3 gw((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
-      hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT>), gw, dim3(W::NT), 0, stream, pyr,
-                         coords, out, g);
-    }
-  }
+  using W = WideCfg<R>;
+  const dim3 grid((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
+  hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT>), grid, dim3(W::NT), 0, stream, pyr, coords,
+                     out, g);
   return dxr::launch_status();
 }
 
@@ -707,9 +495,7 @@ __global__ __launch_bounds__(256) void conv1x1_pack_weight_kernel(const float* _
 // are latency-bound at 8 waves per CU).  With 16 waves the GEMM splits K in two
 // halves per output block: waves 8..15 add their partial accumulators through
 // LDS (the lookup's staging area, free by then).
-// ABL (timing-only ablations, outputs invalid): 1 skips the GEMM's MFMAs and
-// weight loads, 2 skips the lookup phases.
-template <int R, typename PT, int NT = 1024, int PF = 4, int ABL = 0>
+template <int R, typename PT, int NT = 1024, int PF = 4>
 __global__ __launch_bounds__(NT) void corr_lookup_conv1x1_kernel(
     const PT* __restrict__ pyr, const float* __restrict__ coords, const float4* __restrict__ wpk,
     const float* __restrict__ bias, float* __restrict__ out, LookupGeom g, int cout, int relu) {
@@ -754,7 +540,7 @@ __global__ __launch_bounds__(NT) void corr_lookup_conv1x1_kernel(
 #pragma unroll
     for (int s = 0; s < PF; ++s) wload(wbuf[s], ob, min(kbeg + s, kend - 1));
   };
-  if (ABL != 1 && wob < nob) preload(wob);
+  if (wob < nob) preload(wob);
 
   // zero the channel padding [cin, kpad) of the three planes
   {
@@ -769,14 +555,14 @@ __global__ __launch_bounds__(NT) void corr_lookup_conv1x1_kernel(
   // phase 0 of every level, then every level's window gathers in flight at
   // once (registers), then per level: windows -> LDS, samples -> operand planes
 #pragma unroll
-  for (int l = 0; l < (ABL == 2 ? 0 : M::LMAX); ++l)
+  for (int l = 0; l < M::LMAX; ++l)
     if (l < g.levels)
       wide_phase0<R, NT>(coords, g, g.lv[l], b, l, q0, tid, xs + l * RD * QB, ys + l * RD * QB,
                          org + l * QB);
   __syncthreads();
   float4 win[M::LMAX][C::VIT];
 #pragma unroll
-  for (int l = 0; l < (ABL == 2 ? 0 : M::LMAX); ++l) {
+  for (int l = 0; l < M::LMAX; ++l) {
     if (l < g.levels) {
       const LevelAddr& A = g.lv[l];
       const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
@@ -789,7 +575,7 @@ __global__ __launch_bounds__(NT) void corr_lookup_conv1x1_kernel(
     }
   }
 #pragma unroll
-  for (int l = 0; l < (ABL == 2 ? 0 : M::LMAX); ++l) {
+  for (int l = 0; l < M::LMAX; ++l) {
     if (l >= g.levels) break;
     gather_store<R, NT>(win[l], cells, tid);
     __syncthreads();
@@ -823,7 +609,6 @@ __global__ __launch_bounds__(NT) void corr_lookup_conv1x1_kernel(
     __syncthreads();   // cells are rewritten by the next level (and the staging
                        // area becomes the reduction area after the last one)
   }
-  if constexpr (ABL == 2) __syncthreads();
 
   // ---- (Cout x 32 queries x Cin) GEMM, f32 class
   const int q = q0 + j;
@@ -833,7 +618,7 @@ __global__ __launch_bounds__(NT) void corr_lookup_conv1x1_kernel(
     mf16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    if (ABL != 1 && act) {
+    if (act) {
       if (ob0 > 0) preload(ob);
       // One k step: split the weight fragment of slot sl in registers, refill the
       // slot PF steps ahead (unconditionally, clamped: a conditional refill makes
@@ -900,14 +685,6 @@ __global__ __launch_bounds__(NT) void corr_lookup_conv1x1_kernel(
   }
 }
 
-template <int R, typename PT, int NT, int PF, int ABL = 0>
-void launch_conv1x1_k(dim3 grid, hipStream_t stream, const PT* pyr, const float* coords,
-                      const float4* wpl, const float* bias, float* out, const LookupGeom& g,
-                      int cout, int relu) {
-  hipLaunchKernelGGL((corr_lookup_conv1x1_kernel<R, PT, NT, PF, ABL>), grid, dim3(NT), 0, stream,
-                     pyr, coords, wpl, bias, out, g, cout, relu);
-}
-
 template <int R, typename PT>
 int launch_lookup_conv1x1_r(const PT* pyr, const float* coords, const float4* wpl,
                             const float* bias, float* out, const LookupGeom& g, int B, int cout,
@@ -915,17 +692,8 @@ int launch_lookup_conv1x1_r(const PT* pyr, const float* coords, const float4* wp
   using C = WideCfg<R, 1024>;
   if (g.cout > MotionCfg<R>::KP) return DXR_EUNSUPPORTED;
   const dim3 grid((unsigned)((g.N + C::QB - 1) / C::QB), (unsigned)B);
-  // DXR_MOTION_VARIANT (A/B only): 1 = 512 threads; 91 / 92 ablations.
-  const char* v = std::getenv("DXR_MOTION_VARIANT");
-  const int var = v ? std::atoi(v) : 0;
-  if (var == 1)
-    launch_conv1x1_k<R, PT, 512, 4>(grid, stream, pyr, coords, wpl, bias, out, g, cout, relu);
-  else if (var == 91)
-    launch_conv1x1_k<R, PT, 1024, 4, 1>(grid, stream, pyr, coords, wpl, bias, out, g, cout, relu);
-  else if (var == 92)
-    launch_conv1x1_k<R, PT, 1024, 4, 2>(grid, stream, pyr, coords, wpl, bias, out, g, cout, relu);
-  else
-    launch_conv1x1_k<R, PT, 1024, 4>(grid, stream, pyr, coords, wpl, bias, out, g, cout, relu);
+  hipLaunchKernelGGL((corr_lookup_conv1x1_kernel<R, PT, 1024, 4>), grid, dim3(1024), 0, stream,
+                     pyr, coords, wpl, bias, out, g, cout, relu);
   return dxr::launch_status();
 }
 

@@ -10,11 +10,14 @@ importing the reference ``core/corr.py`` in the build container
 autograd gradients, ``tests/golden/make_backward_golden.py``); see
 ``tests/test_oracle_golden.py``.
 """
-from .corr_oracle import (motion_conv1x1, alt_corr_backward, alt_corr_block, alt_corr_forward, avg_pool2x2, avg_pool2x2_backward,
-                          bilinear_sample, bilinear_sample_backward, corr_lookup,
-                          corr_lookup_backward, corr_pyramid, corr_pyramid_backward, corr_volume,
-                          sample_coord)
+from .corr_oracle import (alt_corr_backward, alt_corr_block, alt_corr_block_queries,
+                          alt_corr_forward, avg_pool2x2, avg_pool2x2_backward, bilinear_sample,
+                          bilinear_sample_backward, corr_lookup, corr_lookup_backward,
+                          corr_lookup_rows, corr_pyramid, corr_pyramid_backward,
+                          corr_rows_pyramid, corr_volume, motion_conv1x1, sample_coord)
 
-__all__ = ["motion_conv1x1", "alt_corr_backward", "alt_corr_block", "alt_corr_forward", "avg_pool2x2", "avg_pool2x2_backward",
-           "bilinear_sample", "bilinear_sample_backward", "corr_lookup", "corr_lookup_backward",
-           "corr_pyramid", "corr_pyramid_backward", "corr_volume", "sample_coord"]
+__all__ = ["alt_corr_backward", "alt_corr_block", "alt_corr_block_queries", "alt_corr_forward",
+           "avg_pool2x2", "avg_pool2x2_backward", "bilinear_sample", "bilinear_sample_backward",
+           "corr_lookup", "corr_lookup_backward", "corr_lookup_rows", "corr_pyramid",
+           "corr_pyramid_backward", "corr_rows_pyramid", "corr_volume", "motion_conv1x1",
+           "sample_coord"]

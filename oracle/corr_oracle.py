@@ -65,6 +65,61 @@ def corr_pyramid(fmap1, fmap2, num_levels: int = 4, dtype=np.float64) -> list[np
     return pyr
 
 
+def corr_rows_pyramid(fmap1, fmap2, queries, num_levels: int = 4,
+                      dtype=np.float64) -> list[np.ndarray]:
+    """corr_pyramid of ONE pair restricted to some query rows (core/corr.py:13-27,
+    52-60): every level of a query row depends only on that row, since the
+    pooling runs over the image-2 dims.  ``fmap1, fmap2``: [D, H, W];
+    ``queries``: flat query indices.  Level l: [len(queries), H_l, W_l].  Lets
+    full-size configurations (C4 Sintel B=64, C5 1080p) be checked on sampled
+    rows without the O(N^2) volume."""
+    D, H, W = fmap1.shape
+    q = np.asarray(queries, dtype=np.int64)
+    f1 = fmap1.reshape(D, H * W)[:, q].astype(dtype)
+    f2 = fmap2.reshape(D, H * W).astype(dtype)
+    rows = f1.T @ f2
+    rows = rows / rows.dtype.type(np.sqrt(F32(D), dtype=F32))
+    pyr = [rows.reshape(len(q), H, W)]
+    for _ in range(num_levels - 1):
+        pyr.append(avg_pool2x2(pyr[-1]))
+    return pyr
+
+
+def corr_lookup_rows(rows_pyramid: list[np.ndarray], coords_q: np.ndarray,
+                     radius: int) -> np.ndarray:
+    """corr_lookup for the query rows of corr_rows_pyramid: ``coords_q`` [Q, 2]
+    (x, y) of those queries.  Returns [Q, L*(2r+1)^2] in the reference's channel
+    order (core/corr.py:29-50)."""
+    Q = coords_q.shape[0]
+    c = np.asarray(coords_q, dtype=F32).T.reshape(1, 2, 1, Q)
+    return corr_lookup(rows_pyramid, c, radius)[0, :, 0, :].T
+
+
+def alt_corr_block_queries(fmap1: np.ndarray, fmap2: np.ndarray, coords: np.ndarray, queries,
+                           num_levels: int = 4, radius: int = 4,
+                           dtype=np.float64) -> np.ndarray:
+    """alt_corr_block (core/corr.py:63-91) of ONE pair restricted to some query
+    pixels.  ``fmap1, fmap2``: [D, H, W]; ``coords``: [2, H, W]; ``queries``: flat
+    indices.  Returns [len(queries), L*(2r+1)^2] (already / sqrt(D))."""
+    D, H, W = fmap1.shape
+    q = np.asarray(queries, dtype=np.int64)
+    f1q = fmap1.reshape(D, H * W)[:, q].T[:, None, None, :]          # [Q, 1, 1, D]
+    cq = np.asarray(coords, dtype=F32).reshape(2, H * W)[:, q].T      # [Q, 2]
+    f2 = fmap2
+    outs = []
+    for i in range(num_levels):
+        if i:
+            f2 = avg_pool2x2(f2)
+        f2i = f2.transpose(1, 2, 0)                                  # [H_i, W_i, D]
+        ci = (cq / F32(2 ** i)).reshape(len(q), 1, 1, 1, 2)
+        # each query as its own 1x1 "image" with the level's fmap2 (the kernel's
+        # semantics do not depend on the query's own position)
+        o = alt_corr_forward(f1q, np.broadcast_to(f2i, (len(q),) + f2i.shape), ci, radius, dtype)
+        outs.append(o[:, 0, :, 0, 0])
+    out = np.concatenate(outs, axis=1)
+    return out / out.dtype.type(np.sqrt(F32(D), dtype=F32))
+
+
 def sample_coord(c: np.ndarray, size: int) -> np.ndarray:
     """Pixel coordinate -> grid_sample sampling position, all in float32.
 

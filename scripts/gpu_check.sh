@@ -26,11 +26,11 @@ run() {  # name seconds cmd...
 }
 
 run smoke 240 python -u -c "import __graft_entry__ as g; g.smoke()"
-run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider
-run ab 300 python -u scripts/ab_kernels.py --workload sintel --variants 0,7,9 --ablations 10,2,91,92 --rounds 7
-run ab_bf16 300 python -u scripts/ab_kernels.py --workload kitti --batch 8 --dtype bf16 --variants 0,1 --rounds 7
+run pytest_gpu ${PYTEST_SECS:-900} python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider
 run bench 300 python -u bench.py --steps 30 --warmup 3 --cpu-seconds 8 "$@"
 run rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof" -o run -- \
   python -u bench.py --steps 30 --warmup 3 --no-cpu-baseline "$@"
 find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \; 2>/dev/null
+rm -rf "$OUT/prof"
+run e2e 300 python -u scripts/bench_e2e.py --workload chairs
 echo "== done"

@@ -168,3 +168,29 @@ def epe(a, b) -> float:
 
 def torch_weights(W: dict[str, np.ndarray], device) -> dict[str, torch.Tensor]:
     return {k: torch.from_numpy(v).to(device) for k, v in W.items()}
+
+
+class E2EModel:
+    """A ``model(image1, image2, iters=, test_mode=True) -> (flow_low, flow_up)``
+    for ``driver.infer_pairs`` (the reference RAFT.forward signature,
+    core/raft.py:101): the refinement loop above around ``block_cls`` blocks.
+    The encoders are out of scope, so the "images" only select the synthetic
+    encoder outputs: pair p is an image whose pixels all equal p, and its
+    inputs are ``e2e_inputs(E2E['input_seed'] + 97 * p)`` (p = 0: the golden's)."""
+
+    def __init__(self, block_cls, device, weights=None):
+        self.block_cls = block_cls
+        self.device = device
+        self.W = torch_weights(weights or update_weights(), device)
+
+    def inputs(self, p: int) -> dict[str, torch.Tensor]:
+        x = e2e_inputs(E2E["input_seed"] + 97 * p)
+        return {k: torch.from_numpy(v).to(self.device) for k, v in x.items()}
+
+    def __call__(self, image1, image2, iters=E2E["iters"], test_mode=True):
+        p = int(round(float(image1.reshape(-1)[0])))
+        t = self.inputs(p)
+        corr_fn = self.block_cls(t["fmap1"], t["fmap2"])
+        corr_en = self.block_cls(t["fem1"], t["fem2"])
+        flows, up, _ = refine(corr_fn, corr_en, self.W, t, iters)
+        return flows[-1], up

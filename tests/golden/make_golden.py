@@ -55,6 +55,9 @@ LARGE = {
     "chairs": (1, 256, 46, 62, 4, "normal", [("normal", 4.0, 101), ("normal", 4.0, 102)]),
     "sintel": (1, 256, 55, 128, 4, "normal", [("normal", 4.0, 101), ("uniform", 12.0, 112)]),
     "kitti": (1, 256, 47, 156, 4, "fnet", [("normal", 4.0, 101)]),
+    # C5 1080p (1088x1920 padded -> 136x240 fmaps): pins both the full pyramid
+    # and, by linearity, the on-the-fly AlternateCorrBlock at that size
+    "hd": (1, 256, 136, 240, 4, "fnet", [("normal", 4.0, 101), ("uniform", 12.0, 112)]),
 }
 NSAMPLE = 4096
 PYR_FULL_MAX = 200_000   # tiny cases above this many level-0 elements keep PYR_ROWS query rows
@@ -70,11 +73,19 @@ def _reference_corrblock():
 
 
 def main() -> None:
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--large", default=None, help="regenerate only this benchmark-shape case")
+    only = ap.parse_args().large
     warnings.filterwarnings("ignore")
     torch, CorrBlock = _reference_corrblock()
     manifest = {"tiny": {}, "large": {}, "nsample": NSAMPLE}
+    if only is not None:
+        manifest = json.loads((HERE / "manifest.json").read_text())
 
     for i, (name, (B, D, H, W, r, L, dist, sets)) in enumerate(TINY.items()):
+        if only is not None:
+            break
         s1, s2 = 1000 + 10 * i, 1001 + 10 * i
         f1 = dg.fmap(s1, B, D, H, W, dist)
         f2 = dg.fmap(s2, B, D, H, W, dist)
@@ -97,14 +108,16 @@ def main() -> None:
         print("tiny", name, {k: v.shape for k, v in out.items()})
 
     for name, (B, D, H, W, r, dist, sets) in LARGE.items():
+        if only is not None and name != only:
+            continue
         s1, s2 = 7, 8
         f1 = dg.fmap(s1, B, D, H, W, dist)
         f2 = dg.fmap(s2, B, D, H, W, dist)
         cb = CorrBlock(torch.from_numpy(f1), torch.from_numpy(f2), num_levels=4, radius=r)
         out = {"fmap_checksum": np.array([f1.astype(np.float64).sum(), f2.astype(np.float64).sum()])}
         rng = np.random.default_rng(12345)
-        for lvl, p in enumerate(cb.corr_pyramid):
-            a = p[:, 0].numpy()
+        for lvl in range(4):
+            a = cb.corr_pyramid[lvl][:, 0].numpy()
             flat = a.reshape(-1)
             idx = rng.integers(0, flat.size, NSAMPLE)
             out[f"pyr{lvl}_sum"] = np.array([a.astype(np.float64).sum(),

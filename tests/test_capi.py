@@ -38,7 +38,7 @@ def test_header_declares_the_documented_entry_points():
         "dxr_abi_version", "dxr_status_string", "dxr_last_hip_error", "dxr_pyramid_numel",
         "dxr_pyramid_level_offset", "dxr_corr_pyramid_build", "dxr_corr_lookup",
         "dxr_avg_pool2x2", "dxr_alt_corr_forward", "dxr_alt_corr_lookup", "dxr_corr_volume",
-        "dxr_pyramid_unpack", "dxr_pyramid_pack", "dxr_build_workspace_bytes",
+        "dxr_pyramid_unpack", "dxr_pyramid_pack",
         "dxr_corr_lookup_backward", "dxr_pyramid_backward", "dxr_alt_corr_backward",
         "dxr_conv1x1_packed_bytes", "dxr_conv1x1_pack_weight", "dxr_corr_lookup_conv1x1",
         "dxr_transpose", "dxr_avg_pool2x2_nhwc"}
@@ -65,7 +65,7 @@ def test_library_is_gfx950_code(nat):
 
 def test_abi_version_and_status_strings(nat):
     lib = nat.load()
-    assert lib.dxr_abi_version() == nat.ABI_VERSION == 4
+    assert lib.dxr_abi_version() == nat.ABI_VERSION == 5
     assert lib.dxr_status_string(0) == b"ok"
     assert lib.dxr_status_string(1) == b"invalid argument"
     assert lib.dxr_status_string(2) == b"unsupported by this build"
@@ -109,21 +109,20 @@ def test_host_side_validation_needs_no_gpu(nat):
     P = 1 << 12  # a non-null dummy address: never dereferenced on these paths
     EINVAL, EUNSUP, OK = nat.DXR_EINVAL, nat.DXR_EUNSUPPORTED, nat.DXR_OK
     b = lib.dxr_corr_pyramid_build
-    assert b(P, P, 0, -1, 256, 8, 8, 4, 16.0, P, 0, None, 0, None) == EINVAL      # B < 0
-    assert b(P, P, 0, 1, 0, 8, 8, 4, 16.0, P, 0, None, 0, None) == EINVAL        # D = 0
-    assert b(P, P, 0, 1, 256, 7, 30, 4, 16.0, P, 0, None, 0, None) == EINVAL     # empty level
-    assert b(P, P, 0, 1, 256, 8, 8, 4, 0.0, P, 0, None, 0, None) == EINVAL       # divisor 0
-    assert b(P, P, 0, 1, 256, 8, 8, 4, float("nan"), P, 0, None, 0, None) == EINVAL
-    assert b(None, P, 0, 1, 256, 8, 8, 4, 16.0, P, 0, None, 0, None) == EINVAL   # null input
-    assert b(P, P, 0, 0, 256, 8, 8, 4, 16.0, None, 0, None, 0, None) == OK       # empty batch
-    assert b(P, P, 7, 1, 256, 8, 8, 4, 16.0, P, 0, None, 0, None) == EINVAL      # unknown dtype
-    assert b(P, P, 0, 1, 256, 8, 8, 4, 16.0, P, 0, P + 4, 1 << 20, None) == EINVAL  # unaligned ws
-    assert b(P, P, 0, 1, 256, 8, 8, 4, 16.0, P, 0, P, -1, None) == EINVAL          # negative size
-    ws = lib.dxr_build_workspace_bytes
-    assert ws(2, 256, 55, 128, 0) == 0            # the default (split) build needs none
-    assert ws(1, 256, 8, 8, 1) == 0                                   # bf16 fmaps: no split
-    assert ws(1, 24, 8, 8, 0) == 0                                    # D % 16 != 0
-    assert ws(0, 256, 8, 8, 0) == 0
+    # (fmap1, fmap2, in_dtype, layout, B, D, H, W, L, divisor, pyramid, pyr_dtype, algo, stream)
+    assert b(P, P, 0, 0, -1, 256, 8, 8, 4, 16.0, P, 0, 0, None) == EINVAL      # B < 0
+    assert b(P, P, 0, 0, 1, 0, 8, 8, 4, 16.0, P, 0, 0, None) == EINVAL        # D = 0
+    assert b(P, P, 0, 0, 1, 256, 7, 30, 4, 16.0, P, 0, 0, None) == EINVAL     # empty level
+    assert b(P, P, 0, 0, 1, 256, 8, 8, 4, 0.0, P, 0, 0, None) == EINVAL       # divisor 0
+    assert b(P, P, 0, 0, 1, 256, 8, 8, 4, float("nan"), P, 0, 0, None) == EINVAL
+    assert b(None, P, 0, 0, 1, 256, 8, 8, 4, 16.0, P, 0, 0, None) == EINVAL   # null input
+    assert b(P, P, 0, 0, 0, 256, 8, 8, 4, 16.0, None, 0, 0, None) == OK       # empty batch
+    assert b(P, P, 7, 0, 1, 256, 8, 8, 4, 16.0, P, 0, 0, None) == EINVAL      # unknown dtype
+    assert b(P, P, 0, 2, 1, 256, 8, 8, 4, 16.0, P, 0, 0, None) == EINVAL      # unknown layout
+    assert b(P, P, 0, 0, 1, 256, 8, 8, 4, 16.0, P, 0, 9, None) == EINVAL      # unknown algo
+    assert b(P, P, 1, 0, 1, 256, 8, 8, 4, 16.0, P, 1, 1, None) == EUNSUP      # exact-f32 of bf16
+    # bf16 pyramid beyond the four fused levels: refused before any launch
+    assert b(P, P, 1, 0, 1, 256, 64, 64, 5, 16.0, P, 1, 0, None) == EUNSUP
     assert lib.dxr_corr_volume(P, P, 0, 1, 0, 8, 8, 16.0, P, None) == EINVAL
     assert lib.dxr_pyramid_unpack(P, 0, 1, 8, 8, 4, 4, P, None) == EINVAL   # level >= L
     assert lib.dxr_pyramid_pack(P, 1, 8, 8, 4, 0, P, 3, None) == EINVAL     # bad dtype
@@ -185,16 +184,6 @@ def test_host_side_validation_needs_no_gpu(nat):
     assert pb(P, 0, 1, 7, 30, 4, 16.0, P, None) == EINVAL               # empty level
     assert pb(P, 1, 1, 8, 8, 4, 16.0, P, None) == EUNSUP
     assert lib.dxr_last_hip_error() == 0
-
-
-def test_presplit_workspace_size(nat, monkeypatch):
-    """The presplit build variants (DXR_BUILD_VARIANT 11-14) take the hi/mid/lo
-    planes of both fmaps as workspace; the size query reads the variant per call."""
-    lib = nat.load()
-    monkeypatch.setenv("DXR_BUILD_VARIANT", "11")
-    assert lib.dxr_build_workspace_bytes(2, 256, 55, 128, 0) == 2 * 2 * 3 * 256 * 55 * 128 * 2
-    assert lib.dxr_build_workspace_bytes(1, 256, 8, 8, 1) == 0      # bf16 fmaps: no split
-    assert lib.dxr_build_workspace_bytes(1, 24, 8, 8, 0) == 0       # D % 16 != 0
 
 
 def test_check_maps_status_to_reference_exceptions(nat):

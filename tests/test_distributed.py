@@ -74,3 +74,55 @@ def test_single_process_gather_is_identity():
     x = torch.arange(12.0).reshape(3, 4)
     assert gather_pairs(x, 3) is x
     assert max_over_ranks(2.5) == 2.5
+
+
+_RANK_SCRIPT = r'''
+import json, os, sys
+import torch.distributed as dist
+sys.path.insert(0, {repo!r})
+from dexiraft_amd.shard import gather_pairs, pair_range
+import torch
+dist.init_process_group("gloo")
+rank, world = dist.get_rank(), dist.get_world_size()
+total = int(sys.argv[sys.argv.index("--total-pairs") + 1])
+start, stop = pair_range(total, world, rank)
+local = torch.arange(start, stop, dtype=torch.float64) * 10.0
+sums = gather_pairs(local, total)
+with open(os.path.join({out!r}, f"rank{{rank}}.json"), "w") as f:
+    json.dump({{"rank": rank, "world": world, "local_rank": int(os.environ["LOCAL_RANK"]),
+               "span": [start, stop], "sums": sums.tolist()}}, f)
+dist.destroy_process_group()
+'''
+
+
+def test_bench_launcher_builds_n_ranks(tmp_path):
+    """``bench.py --gpus N`` without a launcher starts torch.distributed.run with N
+    ranks as a child (bench.relaunch_distributed); each rank owns its pair_range
+    share and the per-pair checksums come back whole from gather_pairs (gloo here,
+    RCCL in bench.py)."""
+    import json
+    import sys
+    from pathlib import Path
+    repo = Path(__file__).resolve().parents[1]
+    sys.path.insert(0, str(repo))
+    import bench
+    script = tmp_path / "rank.py"
+    script.write_text(_RANK_SCRIPT.format(repo=str(repo), out=str(tmp_path)))
+    rc = bench.relaunch_distributed(2, script=str(script), argv=["--gpus", "2",
+                                                                  "--total-pairs", "5"])
+    assert rc == 0
+    recs = sorted((json.loads((tmp_path / f"rank{r}.json").read_text()) for r in range(2)),
+                  key=lambda d: d["rank"])
+    assert [d["span"] for d in recs] == [[0, 3], [3, 5]]
+    assert all(d["world"] == 2 and d["local_rank"] == d["rank"] for d in recs)
+    assert all(d["sums"] == [0.0, 10.0, 20.0, 30.0, 40.0] for d in recs)
+
+
+def test_bench_refuses_world_size_mismatch(monkeypatch):
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    with pytest.raises(SystemExit, match="must agree"):
+        bench.init_dist(4)

@@ -121,3 +121,36 @@ def test_infer_pairs_world2_gathers_every_flow(tmp_path):
     for k in range(5):                              # every pair written once, by its owner
         np.testing.assert_array_equal(read_flo(tmp_path / f"frame{k:04d}.flo"),
                                       ref[k].transpose(1, 2, 0))
+
+
+@pytest.mark.gpu
+def test_infer_pairs_with_hip_corrblock_on_gpu(tmp_path):
+    """SURVEY §8(f) row 3 on the GPU: driver.infer_pairs runs the Dexi+RAFT
+    refinement loop (tests/e2e_flow.py) with the HIP CorrBlock inside, over three
+    368x496 pairs (config 1; InputPadder is the identity there).  Pair 0 is the
+    e2e golden's input: its full-resolution flow matches the reference loop's
+    (tests/golden/e2e_chairs.npz) within the fp32 criterion (8x the low-res
+    1e-3 px, as test_e2e_flow); pairs 1 and 2 equal direct runs of the loop bit for
+    bit; the .flo written for pair 0 reads back exactly."""
+    import e2e_flow as ef
+    import dexiraft_amd
+    from conftest import GOLDEN
+    dev = "cuda"
+    model = ef.E2EModel(dexiraft_amd.CorrBlock, dev)
+    P, Hi, Wi = 3, 8 * ef.E2E["H"], 8 * ef.E2E["W"]
+    img = torch.arange(P, dtype=torch.float32, device=dev).reshape(P, 1, 1, 1).expand(P, 3, Hi, Wi)
+    paths = [tmp_path / f"pair{k}.flo" for k in range(P)]
+    flows = infer_pairs(model, img.contiguous(), img.contiguous(), iters=ef.E2E["iters"],
+                        flo_paths=paths)
+    assert flows.shape == (P, 2, Hi, Wi) and flows.device.type == "cuda"
+    with np.load(GOLDEN / "e2e_chairs.npz") as z:
+        gold_up = z["flow_up_sub4"]
+    e = ef.epe(flows[0:1, :, ::4, ::4], gold_up)
+    print(f"pair 0 full-res EPE vs reference loop: {e:.3e} px")
+    assert e < 8e-3
+    with torch.no_grad():
+        for p in (1, 2):
+            _, up = model(img[p:p + 1], img[p:p + 1])
+            assert torch.equal(up[0], flows[p])
+    np.testing.assert_array_equal(read_flo(paths[0]),
+                                  flows[0].permute(1, 2, 0).cpu().numpy())

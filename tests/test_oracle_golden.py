@@ -174,6 +174,38 @@ def test_large_chairs_checksums():
     assert np.abs(out.reshape(-1)[d["out0_idx"]] - d["out0_val"]).max() <= 1e-6 * maxabs
 
 
+def test_large_hd_sampled_rows():
+    """C5 1080p (136x240) pin of the sampled-row oracle the GPU tests use at full
+    size: corr_rows_pyramid / corr_lookup_rows / alt_corr_block_queries against
+    the reference CorrBlock's sampled entries (tests/golden/large_hd.npz)."""
+    d = load_large("hd")
+    B, D, H, W, r = d["B"], d["D"], d["H"], d["W"], d["radius"]
+    n = H * W
+    f1 = dg.fmap(d["fmap_seeds"][0], B, D, H, W, d["dist"])[0]
+    f2 = dg.fmap(d["fmap_seeds"][1], B, D, H, W, d["dist"])[0]
+    np.testing.assert_allclose([f1.astype(np.float64).sum(), f2.astype(np.float64).sum()],
+                               d["fmap_checksum"], rtol=0, atol=1e-6)
+    sizes = [(H >> lvl, W >> lvl) for lvl in range(4)]
+    for lvl, (h, w) in enumerate(sizes):
+        idx = d[f"pyr{lvl}_idx"][:512]
+        q, cell = np.divmod(idx, h * w)
+        uq, inv = np.unique(q, return_inverse=True)
+        rows = oracle.corr_rows_pyramid(f1, f2, uq, lvl + 1, np.float64)[lvl].reshape(len(uq), -1)
+        got = rows[inv, cell]
+        assert np.abs(got - d[f"pyr{lvl}_val"][:512]).max() <= 1e-5 * float(d[f"pyr{lvl}_maxabs"])
+    for k, (mode, scale, seed) in enumerate(d["coords"]):
+        c = dg.coords(int(seed), B, H, W, mode, float(scale))[0]
+        idx = d[f"out{k}_idx"][:256]
+        ch, q = np.divmod(idx, n)
+        uq, inv = np.unique(q, return_inverse=True)
+        cq = c.reshape(2, n)[:, uq].T
+        look = oracle.corr_lookup_rows(oracle.corr_rows_pyramid(f1, f2, uq, 4, np.float64), cq, r)
+        alt = oracle.alt_corr_block_queries(f1, f2, c, uq, 4, r, np.float64)
+        maxabs = float(d[f"out{k}_maxabs"])
+        for got in (look[inv, ch], alt[inv, ch]):
+            assert np.abs(got - d[f"out{k}_val"][:256]).max() <= 1e-5 * maxabs
+
+
 # --------------------------------------------------------------------------- backward
 @pytest.mark.parametrize("name", ["bw_basic", "bw_batch2_r3", "bw_d256"])
 def test_oracle_backward_matches_reference_autograd(name):
