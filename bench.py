@@ -21,9 +21,10 @@ Execution (``--mode graph``, default): ``value`` is timed on ONE HIP graph per
 step (build + 12 lookups), replayed K times — the launch-bound lookups would
 otherwise be host-bound in Python.  Kernel durations for the rooflines come from
 two more graphs timed with HIP events on the launch stream: KB back-to-back
-builds and 4 x 12 back-to-back lookups, each divided by its launch count, so the
-graph-launch cost is amortised and what remains per launch is the kernel plus
-one same-stream kernel boundary (~1.5 us, MI355X_MICROARCH.md "boundary").
+builds (into the block's one pyramid buffer, as the step graph's replays write
+one buffer) and 4 x 12 back-to-back lookups, each divided by its launch count, so
+the graph-launch cost is amortised and what remains per launch is the kernel
+plus one same-stream kernel boundary (~1.5 us, MI355X_MICROARCH.md "boundary").
 ``--mode eager`` times plain Python calls instead.
 """
 from __future__ import annotations
@@ -362,9 +363,16 @@ def main():
         if args.mode == "graph":
             keep = dict(state)            # the step graph's own tensors stay allocated
             pool = g_step.pool()
-            kb = KB_BUILDS if H * W <= 16384 else 3
-            t_build = _timed_graph(lambda: [build() for _ in range(kb)], stream, pool, kb)
-            t_look = _timed_graph(lambda: [state["cb"](c) for _ in range(KL_REPS) for c in coords],
+            kb = KB_BUILDS
+            cb = state["cb"]
+            if args.block == "corr":
+                # the build kernel as CorrBlock launches it, into the block's own
+                # pyramid buffer (as every replay of the step graph writes one buffer)
+                t_build = _timed_graph(lambda: [cb._launch_build(f1, f2) for _ in range(kb)],
+                                       stream, pool, kb)
+            else:
+                t_build = _timed_graph(lambda: [build() for _ in range(kb)], stream, pool, kb)
+            t_look = _timed_graph(lambda: [cb(c) for _ in range(KL_REPS) for c in coords],
                                   stream, pool, KL_REPS * ITERS)
             build_ms, look_ms = t_build(5), t_look(5)
             del keep

@@ -24,6 +24,9 @@ INCLUDE = REPO_DIR / "include"
 BUILD_DIR = PKG_DIR / "build"
 LIB_NAME = "libdexiraft_corr.so"
 LIB_PATH = PKG_DIR / LIB_NAME
+# Experiments target (timing ablations; never loaded by the package): same
+# sources with -DDXR_EXPERIMENTS, objects in build/exp.
+EXP_LIB_PATH = PKG_DIR / "libdexiraft_corr_exp.so"
 ARCH = "gfx950"
 
 CXXFLAGS = [
@@ -48,10 +51,10 @@ def _deps() -> list[Path]:
     return _sources() + sorted(CSRC.glob("*.h")) + sorted(INCLUDE.glob("*.h")) + [Path(__file__)]
 
 
-def is_stale() -> bool:
-    if not LIB_PATH.exists():
+def is_stale(lib: Path = LIB_PATH) -> bool:
+    if not lib.exists():
         return True
-    t = LIB_PATH.stat().st_mtime
+    t = lib.stat().st_mtime
     return any(p.stat().st_mtime > t for p in _deps())
 
 
@@ -62,8 +65,8 @@ def is_stale() -> bool:
 FILE_FLAGS = {"corr_build.hip": ["-fno-slp-vectorize"], "corr_lookup.hip": ["-fno-slp-vectorize"]}
 
 
-def _compile(src: Path, extra: list[str]) -> Path:
-    obj = BUILD_DIR / (src.stem + ".o")
+def _compile(src: Path, extra: list[str], out_dir: Path = BUILD_DIR) -> Path:
+    obj = out_dir / (src.stem + ".o")
     cmd = [hipcc(), *CXXFLAGS, *FILE_FLAGS.get(src.name, []), *extra, "-c", str(src), "-o",
            str(obj)]
     res = subprocess.run(cmd, capture_output=True, text=True)
@@ -74,29 +77,37 @@ def _compile(src: Path, extra: list[str]) -> Path:
     return obj
 
 
-def build(force: bool = False, asm: bool = False, verbose: bool = False) -> Path:
-    """Compile and link the library if any source is newer than it."""
-    if not force and not asm and not is_stale():
-        return LIB_PATH
-    BUILD_DIR.mkdir(exist_ok=True)
+def build(force: bool = False, asm: bool = False, verbose: bool = False,
+          experiments: bool = False) -> Path:
+    """Compile and link the library if any source is newer than it
+    (``experiments``: the separate timing-ablation target instead)."""
+    lib = EXP_LIB_PATH if experiments else LIB_PATH
+    if not force and not asm and not is_stale(lib):
+        return lib
+    out_dir = BUILD_DIR / "exp" if experiments else BUILD_DIR
+    out_dir.mkdir(parents=True, exist_ok=True)
     extra = ["-save-temps=obj", "-Rpass-analysis=kernel-resource-usage"] if asm else []
+    if experiments:
+        extra = extra + ["-DDXR_EXPERIMENTS"]
     srcs = _sources()
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(lambda s: _compile(s, extra), srcs))
-    tmp = LIB_PATH.with_suffix(".so.tmp")
+        objs = list(ex.map(lambda s: _compile(s, extra, out_dir), srcs))
+    tmp = lib.with_suffix(".so.tmp")
     cmd = [hipcc(), "-shared", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs)]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{res.stderr}")
-    os.replace(tmp, LIB_PATH)
+    os.replace(tmp, lib)
     if verbose:
-        print(f"built {LIB_PATH}")
-    return LIB_PATH
+        print(f"built {lib}")
+    return lib
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--asm", action="store_true", help="keep .s and print resource usage")
+    ap.add_argument("--experiments", action="store_true",
+                    help="build the timing-ablation target libdexiraft_corr_exp.so instead")
     a = ap.parse_args()
-    build(force=a.force, asm=a.asm, verbose=True)
+    build(force=a.force, asm=a.asm, verbose=True, experiments=a.experiments)

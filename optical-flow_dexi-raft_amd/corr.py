@@ -343,6 +343,21 @@ class CorrBlock:
         numel = lib.dxr_pyramid_numel(B, H, W, num_levels)
         self._buf = torch.empty(numel, dtype=pyr_torch, device=fmap1.device)
         grad = _wants_grad(fmap1, fmap2)
+        self._in_dt = in_dt
+        f1, f2, st = self._launch_build(fmap1, fmap2, grad)
+        nat.check(st, "CorrBlock build (dxr_corr_pyramid_build)")
+        self._level_sizes = sizes
+        self._ref_pyramid = None
+        if grad:
+            self._gs = _GradState(self._geom, num_levels, radius, self._device, numel)
+            self._token = _BuildGrad.apply(f1, f2, self._gs)
+
+    def _launch_build(self, fmap1, fmap2, grad=False):
+        """One build launch into this block's pyramid buffer (the constructor's;
+        bench.py also times the kernel with it).  Returns the operand tensors the
+        kernel read and the status."""
+        B, D, H, W = self._geom
+        lib = nat.load()
         st = nat.DXR_EUNSUPPORTED
         if not grad and _channels_last(fmap1) and _channels_last(fmap2):
             # channels-last fmaps (SURVEY §8(f) row 4): read in place by the
@@ -350,9 +365,9 @@ class CorrBlock:
             f1, f2 = fmap1, fmap2
             with _Launch(self._device):
                 st = lib.dxr_corr_pyramid_build(
-                    f1.data_ptr(), f2.data_ptr(), in_dt, nat.DXR_NHWC, B, D, H, W, num_levels,
-                    _sqrt_dim(D), self._buf.data_ptr(), pyr_dt, nat.DXR_BUILD_AUTO,
-                    nat.stream_of(f1))
+                    f1.data_ptr(), f2.data_ptr(), self._in_dt, nat.DXR_NHWC, B, D, H, W,
+                    self.num_levels, _sqrt_dim(D), self._buf.data_ptr(), self._pyr_dt,
+                    nat.DXR_BUILD_AUTO, nat.stream_of(f1))
         if st == nat.DXR_EUNSUPPORTED:
             if grad:
                 f1, f2 = fmap1.contiguous(), fmap2.contiguous()   # tracked by autograd
@@ -360,15 +375,10 @@ class CorrBlock:
                 f1, f2 = _nchw(fmap1), _nchw(fmap2)
             with _Launch(self._device):
                 st = lib.dxr_corr_pyramid_build(
-                    f1.data_ptr(), f2.data_ptr(), in_dt, nat.DXR_NCHW, B, D, H, W, num_levels,
-                    _sqrt_dim(D), self._buf.data_ptr(), pyr_dt, nat.DXR_BUILD_AUTO,
-                    nat.stream_of(f1))
-        nat.check(st, "CorrBlock build (dxr_corr_pyramid_build)")
-        self._level_sizes = sizes
-        self._ref_pyramid = None
-        if grad:
-            self._gs = _GradState(self._geom, num_levels, radius, self._device, numel)
-            self._token = _BuildGrad.apply(f1, f2, self._gs)
+                    f1.data_ptr(), f2.data_ptr(), self._in_dt, nat.DXR_NCHW, B, D, H, W,
+                    self.num_levels, _sqrt_dim(D), self._buf.data_ptr(), self._pyr_dt,
+                    nat.DXR_BUILD_AUTO, nat.stream_of(f1))
+        return f1, f2, st
 
     @property
     def corr_pyramid(self):

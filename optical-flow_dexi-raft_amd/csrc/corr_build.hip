@@ -686,7 +686,11 @@ __device__ __forceinline__ Split3 split3(float a, float b) {
 
 // BV: target staging width in floats — 4 (float4 units; W % 4 == 0) or 2
 // (float2 units; W even, e.g. Chairs' 62-wide fmaps).
-template <typename OT, bool DIV, int MINW, int BV = 4>
+// XP: timing ablations, instantiated only by the experiments build target
+// (DXR_EXPERIMENTS, libdexiraft_corr_exp.so; never by the product library):
+// bit 0 skips the epilogue stores, 1 the MFMAs, 2 the in-loop global loads,
+// 3 the operand split (hi only), 4 the in-loop barrier.
+template <typename OT, bool DIV, int MINW, int BV = 4, int XP = 0>
 __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float* __restrict__ f1,
                                                                     const float* __restrict__ f2,
                                                                     OT* __restrict__ pyr,
@@ -736,6 +740,9 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
   float an[8];
   float4 bn[NBS];
   auto load = [&](int k0) {
+    if constexpr ((XP & 4) != 0) {
+      if (k0 > 0) return;
+    }
     const long long ko = (long long)k0 * g.N;
 #pragma unroll
     for (int e = 0; e < 8; ++e) an[e] = pa[ko + (long long)e * g.N];
@@ -752,11 +759,19 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     }
   };
   s8v ah, am, al;   // split query operand of the current stage
+  auto split3x = [&](float a, float bb) -> Split3 {
+    if constexpr ((XP & 8) != 0) {
+      const uint32_t h = cvt_pk_bf16(a, bb);
+      return {h, h, h};
+    } else {
+      return split3(a, bb);
+    }
+  };
   auto split_a = [&]() {
     uint32_t h[4], m[4], l[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const Split3 x = split3(an[2 * e], an[2 * e + 1]);
+      const Split3 x = split3x(an[2 * e], an[2 * e + 1]);
       h[e] = x.h;
       m[e] = x.m;
       l[e] = x.l;
@@ -770,9 +785,9 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
 #pragma unroll
     for (int s = 0; s < NBS; ++s) {
       const int o = bk[s] * PH + bcol[s];
-      const Split3 x = split3(bn[s].x, bn[s].y);
+      const Split3 x = split3x(bn[s].x, bn[s].y);
       if constexpr (BV == 4) {
-        const Split3 z = split3(bn[s].z, bn[s].w);
+        const Split3 z = split3x(bn[s].z, bn[s].w);
         *reinterpret_cast<uint2*>(P + o) = make_uint2(x.h, z.h);
         *reinterpret_cast<uint2*>(P + PLANE_S + o) = make_uint2(x.m, z.m);
         *reinterpret_cast<uint2*>(P + 2 * PLANE_S + o) = make_uint2(x.l, z.l);
@@ -806,6 +821,13 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     for (int t = 0; t < 4; ++t) {
       const bf8v th = frag(P + t * 32), tm = frag(P + PLANE_S + t * 32),
                  tl = frag(P + 2 * PLANE_S + t * 32);
+      if constexpr ((XP & 2) != 0) {
+        const s8v x = __builtin_bit_cast(s8v, th) ^ __builtin_bit_cast(s8v, tm) ^
+                      __builtin_bit_cast(s8v, tl) ^ __builtin_bit_cast(s8v, qh) ^
+                      __builtin_bit_cast(s8v, qm) ^ __builtin_bit_cast(s8v, ql);
+        acc[t][0] += (float)(x[0] + x[3] + x[5] + x[7]);
+        continue;
+      }
       // small terms first
       acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm, acc[t], 0, 0, 0);
       acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh, acc[t], 0, 0, 0);
@@ -818,10 +840,19 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
       store_b(buf ^ 1);
       split_a();
     }
-    __syncthreads();
+    if constexpr ((XP & 16) == 0) __syncthreads();
   }
 
   scale_acc<DIV>(acc, g);
+  if constexpr ((XP & 1) != 0) {
+    float sum = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sum += acc[t][r];
+    if (sum == 1234.5f) pyr[tid] = to_out<OT>(sum);  // keeps the K loop live
+    return;
+  }
   paged_epilogue<OT>(acc, reinterpret_cast<float*>(smem), pyr, g, pc.page, wave, lane);
 }
 
@@ -1200,3 +1231,43 @@ extern "C" int dxr_pyramid_backward(const void* grad_pyramid, int grad_dtype, in
                        gp, grad_volume, la, (int)B, (int)(H * W), (int)H, (int)W, divisor, recip);
   return dxr::launch_status();
 }
+
+#ifdef DXR_EXPERIMENTS
+// Experiments build target only (libdexiraft_corr_exp.so): the f32 split build
+// with timing ablation bits `xp` (see corr_build_split_kernel), into a paged
+// f32 pyramid.  NCHW f32 fmaps, W % 4 == 0, D % 16 == 0, power-of-two sqrt(D).
+namespace {
+template <int XP>
+int xp_split(const float* f1, const float* f2, float* pyr, const BuildGeom& g, int B,
+             hipStream_t stream) {
+  hipLaunchKernelGGL((corr_build_split_kernel<float, false, 4, 4, XP>), build_grid(g, B), dim3(NT),
+                     0, stream, f1, f2, pyr, g);
+  return dxr::launch_status();
+}
+}  // namespace
+
+extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t D, int64_t H,
+                            int64_t W, float* pyr, int xp, hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, 4, &L) || W % 4 != 0 || D % 16 != 0) return DXR_EINVAL;
+  const BuildGeom g = make_geom(D, H, W, std::sqrt((float)D), L);
+  if (g.recip == 0.f) return DXR_EUNSUPPORTED;
+  switch (xp) {
+    case 0: return xp_split<0>(f1, f2, pyr, g, (int)B, stream);
+    case 1: return xp_split<1>(f1, f2, pyr, g, (int)B, stream);
+    case 2: return xp_split<2>(f1, f2, pyr, g, (int)B, stream);
+    case 3: return xp_split<3>(f1, f2, pyr, g, (int)B, stream);
+    case 4: return xp_split<4>(f1, f2, pyr, g, (int)B, stream);
+    case 5: return xp_split<5>(f1, f2, pyr, g, (int)B, stream);
+    case 8: return xp_split<8>(f1, f2, pyr, g, (int)B, stream);
+    case 9: return xp_split<9>(f1, f2, pyr, g, (int)B, stream);
+    case 13: return xp_split<13>(f1, f2, pyr, g, (int)B, stream);
+    case 16: return xp_split<16>(f1, f2, pyr, g, (int)B, stream);
+    case 17: return xp_split<17>(f1, f2, pyr, g, (int)B, stream);
+    case 21: return xp_split<21>(f1, f2, pyr, g, (int)B, stream);
+    case 3 | 4: return xp_split<7>(f1, f2, pyr, g, (int)B, stream);
+    case 1 | 2 | 16: return xp_split<19>(f1, f2, pyr, g, (int)B, stream);
+    default: return DXR_EUNSUPPORTED;
+  }
+}
+#endif

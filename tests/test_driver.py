@@ -131,7 +131,9 @@ def test_infer_pairs_with_hip_corrblock_on_gpu(tmp_path):
     e2e golden's input: its full-resolution flow matches the reference loop's
     (tests/golden/e2e_chairs.npz) within the fp32 criterion (8x the low-res
     1e-3 px, as test_e2e_flow); pairs 1 and 2 equal direct runs of the loop bit for
-    bit; the .flo written for pair 0 reads back exactly."""
+    bit in the correlation path (the update block's MIOpen convolutions are not
+    bitwise reproducible across calls: equal within 1e-4 px); the .flo written
+    for pair 0 reads back exactly."""
     import e2e_flow as ef
     import dexiraft_amd
     from conftest import GOLDEN
@@ -151,6 +153,6 @@ def test_infer_pairs_with_hip_corrblock_on_gpu(tmp_path):
     with torch.no_grad():
         for p in (1, 2):
             _, up = model(img[p:p + 1], img[p:p + 1])
-            assert torch.equal(up[0], flows[p])
+            assert ef.epe(up, flows[p:p + 1]) < 1e-4
     np.testing.assert_array_equal(read_flo(paths[0]),
                                   flows[0].permute(1, 2, 0).cpu().numpy())
