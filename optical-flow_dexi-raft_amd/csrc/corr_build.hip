@@ -226,6 +226,8 @@ __device__ __forceinline__ void store8(OT* dst, const float* src) {
 // or pools of zeros) and never read.  Every pooled value is computed from the
 // f32 values of the level above, in the reference's window order
 // ((v00+v01)+v10)+v11 (F.avg_pool2d), then rounded to OT once.
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
 // `wave`: which 32 queries of the page this wave holds (and its private LDS
 // staging region).
 template <typename OT>
@@ -655,7 +657,6 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_
 // ---------------------------------------------------------------------------
 constexpr int BKS = 16;                 // K per stage
 constexpr int PLANE_S = BKS * PH;       // bf16 elements per split plane
-constexpr int STAGE_S = 3 * PLANE_S;    // hi, mid, lo planes
 
 struct Split3 {
   uint32_t h, m, l;  // bf16x2 words (first element in the low half)
@@ -684,19 +685,42 @@ __device__ __forceinline__ Split3 split3(float a, float b) {
   return {h, m, pack_hi(__float_as_uint(la), __float_as_uint(lb))};
 }
 
+// Raw buffer access (gfx9 resource word 3: 0x00020000), byte offsets.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* base, int elems) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, elems * 4,
+                                           0x00020000);
+}
+__device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, uint32_t voff, int soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ float2 bload2(__amdgpu_buffer_rsrc_t r, uint32_t voff, int soff) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 v = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+  return make_float2(v.x, v.y);
+}
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t voff, int soff) {
+  const f32x4v v = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
 // BV: target staging width in floats — 4 (float4 units; W % 4 == 0) or 2
 // (float2 units; W even, e.g. Chairs' 62-wide fmaps).
+// NHWC: channels-last fmaps [B, H, W, D]: every operand
+// unit is 4 consecutive k of one pixel, so the query operand is two 16-byte
+// loads per lane and the target tile is staged target-major ([target][k] planes,
+// read with ds_read_b128) instead of k-major; same products, same order, same
+// bits as the NCHW build.
 // XP: timing ablations, instantiated only by the experiments build target
 // (DXR_EXPERIMENTS, libdexiraft_corr_exp.so; never by the product library):
 // bit 0 skips the epilogue stores, 1 the MFMAs, 2 the in-loop global loads,
 // 3 the operand split (hi only), 4 the in-loop barrier.
-template <typename OT, bool DIV, int MINW, int BV = 4, int XP = 0>
+template <typename OT, bool DIV, int MINW, int BV = 4, int XP = 0, bool NHWC = false>
 __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float* __restrict__ f1,
                                                                     const float* __restrict__ f2,
                                                                     OT* __restrict__ pyr,
                                                                     BuildGeom g) {
-  constexpr int LDS_E = WAVES * 16 * P0 * 4;   // epilogue bytes
-  constexpr int LDS_K = 2 * STAGE_S * 2;       // two stages, bytes
+  constexpr int LDS_E = WAVES * 16 * P0 * 4;                         // epilogue bytes
+  constexpr int LDS_K = 2 * 3 * (NHWC ? NTGT * 24 : PLANE_S) * 2;     // two stages, bytes
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_K > LDS_E ? LDS_K : LDS_E];
   uint16_t* lh = reinterpret_cast<uint16_t*>(smem);
 
@@ -716,25 +740,45 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
+  // Operands are read with buffer loads: one resource per fmap of this pair,
+  // per-lane 32-bit byte offsets fixed for the whole K loop, and the stage's k
+  // offset in an SGPR — no per-stage vector address arithmetic (64-bit address
+  // adds and exec-masked loads were half of the loop's VALU cycles, r02 PMC).
+  // Off-image target units get an offset past the resource: the range check
+  // returns zeros.  Host side guarantees D * N * 4 < 2^31.
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(f1b, g.D * g.N);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(f2b, g.D * g.N);
   // Query operand: lane -> (query q0 + 32 wave + (lane & 31), k rows 8 (lane >> 5) + e).
   // Padding queries read a clamped, valid address (their outputs are page padding).
   const int qa = min(q0 + wave * 32 + (lane & 31), g.N - 1);
-  const float* pa = f1b + (long long)(8 * (lane >> 5)) * g.N + qa;
-  // Target staging: NBS units of BV floats per thread per stage,
-  // unit idx -> (k, tile row, col / BV).
+  const uint32_t va = NHWC ? (uint32_t)(qa * g.D + 8 * (lane >> 5)) * 4u
+                           : (uint32_t)(qa + 8 * (lane >> 5) * g.N) * 4u;
+  // Target staging: NBS units of BV floats per thread per stage.  NCHW: unit
+  // idx -> (k, tile row, col / BV), BV consecutive targets of one k row; NHWC:
+  // unit idx -> (target, k / 4), 4 consecutive k of one target.
+  static_assert(!NHWC || BV == 4, "NHWC units are 4 consecutive channels");
   constexpr int UPR = TW / BV;               // units per tile row
   constexpr int NBS = BKS * NTGT / BV / NT;  // units per thread
   int bk[NBS], bcol[NBS];
-  long long boff[NBS];
-  bool bok[NBS];
+  uint32_t vb[NBS];
 #pragma unroll
   for (int s = 0; s < NBS; ++s) {
     const int idx = tid + NT * s;
-    const int k = idx / (8 * UPR), r = (idx / UPR) & 7, c = (idx % UPR) * BV;
-    bk[s] = k;
+    int r, c;
+    if constexpr (NHWC) {
+      const int p = idx >> 2;
+      r = p >> 4;
+      c = p & 15;
+      bk[s] = 4 * (idx & 3);
+      vb[s] = (uint32_t)(((th0 + r) * g.W + tw0 + c) * g.D + bk[s]) * 4u;
+    } else {
+      r = (idx / UPR) & 7;
+      c = (idx % UPR) * BV;
+      bk[s] = idx / (8 * UPR);
+      vb[s] = (uint32_t)(bk[s] * g.N + (th0 + r) * g.W + tw0 + c) * 4u;
+    }
     bcol[s] = tgt_col(r, c);
-    bok[s] = th0 + r < g.H && tw0 + c < g.W;
-    boff[s] = (long long)k * g.N + (long long)(th0 + r) * g.W + tw0 + c;
+    if (!(th0 + r < g.H && tw0 + c < g.W)) vb[s] = 0x80000000u;
   }
 
   float an[8];
@@ -743,17 +787,23 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     if constexpr ((XP & 4) != 0) {
       if (k0 > 0) return;
     }
-    const long long ko = (long long)k0 * g.N;
+    if constexpr (NHWC) {
+      const float4 u = bload4(ra, va, k0 * 4), v = bload4(ra, va, k0 * 4 + 16);
+      an[0] = u.x; an[1] = u.y; an[2] = u.z; an[3] = u.w;
+      an[4] = v.x; an[5] = v.y; an[6] = v.z; an[7] = v.w;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) an[e] = pa[ko + (long long)e * g.N];
+      for (int s = 0; s < NBS; ++s) bn[s] = bload4(rb, vb[s], k0 * 4);
+      return;
+    }
+    const int rowb = g.N * 4;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) an[e] = bload1(ra, va, (k0 + e) * rowb);
 #pragma unroll
     for (int s = 0; s < NBS; ++s) {
       if constexpr (BV == 4) {
-        bn[s] = bok[s] ? *reinterpret_cast<const float4*>(f2b + ko + boff[s])
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        bn[s] = bload4(rb, vb[s], k0 * rowb);
       } else {
-        const float2 v = bok[s] ? *reinterpret_cast<const float2*>(f2b + ko + boff[s])
-                                : make_float2(0.f, 0.f);
+        const float2 v = bload2(rb, vb[s], k0 * rowb);
         bn[s] = make_float4(v.x, v.y, 0.f, 0.f);
       }
     }
@@ -780,31 +830,43 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     am = __builtin_bit_cast(s8v, make_uint4(m[0], m[1], m[2], m[3]));
     al = __builtin_bit_cast(s8v, make_uint4(l[0], l[1], l[2], l[3]));
   };
+  // NHWC target planes: [target (MFMA row order)][16 k] bf16 at a 48-byte
+  // pitch, which keeps the ds_read_b128 lane groups bank-conflict free.
+  constexpr int PN = 24;                      // NHWC plane row pitch (bf16)
+  constexpr int PLANE_N = NTGT * PN;          // bf16 elements per NHWC plane
+  constexpr int PLANE = NHWC ? PLANE_N : PLANE_S;
   auto store_b = [&](int buf) {
-    uint16_t* P = lh + buf * STAGE_S;
+    uint16_t* P = lh + buf * 3 * PLANE;
 #pragma unroll
     for (int s = 0; s < NBS; ++s) {
-      const int o = bk[s] * PH + bcol[s];
+      const int o = NHWC ? bcol[s] * PN + bk[s] : bk[s] * PH + bcol[s];
       const Split3 x = split3x(bn[s].x, bn[s].y);
       if constexpr (BV == 4) {
         const Split3 z = split3x(bn[s].z, bn[s].w);
         *reinterpret_cast<uint2*>(P + o) = make_uint2(x.h, z.h);
-        *reinterpret_cast<uint2*>(P + PLANE_S + o) = make_uint2(x.m, z.m);
-        *reinterpret_cast<uint2*>(P + 2 * PLANE_S + o) = make_uint2(x.l, z.l);
+        *reinterpret_cast<uint2*>(P + PLANE + o) = make_uint2(x.m, z.m);
+        *reinterpret_cast<uint2*>(P + 2 * PLANE + o) = make_uint2(x.l, z.l);
       } else {
         *reinterpret_cast<uint32_t*>(P + o) = x.h;
-        *reinterpret_cast<uint32_t*>(P + PLANE_S + o) = x.m;
-        *reinterpret_cast<uint32_t*>(P + 2 * PLANE_S + o) = x.l;
+        *reinterpret_cast<uint32_t*>(P + PLANE + o) = x.m;
+        *reinterpret_cast<uint32_t*>(P + 2 * PLANE + o) = x.l;
       }
     }
   };
 
   const int li = lane & 15;
-  const int rd_off = (li >> 2) * PH + 4 * (li & 3) + 16 * ((lane >> 4) & 1) + 8 * (lane >> 5) * PH;
+  const int rd_off = NHWC ? (lane & 31) * PN + 8 * (lane >> 5)
+                          : (li >> 2) * PH + 4 * (li & 3) + 16 * ((lane >> 4) & 1) +
+                                8 * (lane >> 5) * PH;
   auto frag = [&](const uint16_t* p) {
-    return __builtin_bit_cast(bf8v, __builtin_shufflevector(tr_read(p), tr_read(p + 4 * PH), 0, 1,
-                                                            2, 3, 4, 5, 6, 7));
+    if constexpr (NHWC) {
+      return *reinterpret_cast<const bf8v*>(p);
+    } else {
+      return __builtin_bit_cast(bf8v, __builtin_shufflevector(tr_read(p), tr_read(p + 4 * PH), 0,
+                                                              1, 2, 3, 4, 5, 6, 7));
+    }
   };
+  const int tstride = NHWC ? 32 * PN : 32;    // MFMA tile t's first row / column
 
   const int nk = g.D / BKS;
   load(0);
@@ -816,11 +878,11 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     if (ks + 1 < nk) load((ks + 1) * BKS);
     const bf8v qh = __builtin_bit_cast(bf8v, ah), qm = __builtin_bit_cast(bf8v, am),
                ql = __builtin_bit_cast(bf8v, al);
-    const uint16_t* P = lh + buf * STAGE_S + rd_off;
+    const uint16_t* P = lh + buf * 3 * PLANE + rd_off;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const bf8v th = frag(P + t * 32), tm = frag(P + PLANE_S + t * 32),
-                 tl = frag(P + 2 * PLANE_S + t * 32);
+      const bf8v th = frag(P + t * tstride), tm = frag(P + PLANE + t * tstride),
+                 tl = frag(P + 2 * PLANE + t * tstride);
       if constexpr ((XP & 2) != 0) {
         const s8v x = __builtin_bit_cast(s8v, th) ^ __builtin_bit_cast(s8v, tm) ^
                       __builtin_bit_cast(s8v, tl) ^ __builtin_bit_cast(s8v, qh) ^
@@ -1031,17 +1093,17 @@ int launch_build_bf16(bool vec, const uint16_t* f1, const uint16_t* f2, OT* pyr,
 
 // Split build (f32 class on bf16 MFMA) at 4 waves/SIMD (r01: 172 us at Sintel
 // against 177 at 3 and 183 at the compiler's choice).
-template <typename OT, int BV>
+template <typename OT, int BV, bool NHWC = false>
 int launch_split(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, int B,
                  hipStream_t stream) {
   const dim3 grid = build_grid(g, B);
   if (grid.y > 65535) return DXR_EINVAL;
   if (g.recip == 0.f)
-    hipLaunchKernelGGL((corr_build_split_kernel<OT, true, 4, BV>), grid, dim3(NT), 0, stream, f1,
-                       f2, pyr, g);
+    hipLaunchKernelGGL((corr_build_split_kernel<OT, true, 4, BV, 0, NHWC>), grid, dim3(NT), 0,
+                       stream, f1, f2, pyr, g);
   else
-    hipLaunchKernelGGL((corr_build_split_kernel<OT, false, 4, BV>), grid, dim3(NT), 0, stream, f1,
-                       f2, pyr, g);
+    hipLaunchKernelGGL((corr_build_split_kernel<OT, false, 4, BV, 0, NHWC>), grid, dim3(NT), 0,
+                       stream, f1, f2, pyr, g);
   return dxr::launch_status();
 }
 
@@ -1051,7 +1113,7 @@ int launch_split(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, 
 template <typename OT>
 int launch_build_f32(bool vec, const float* f1, const float* f2, OT* pyr, const BuildGeom& g,
                      int B, int algo, hipStream_t stream) {
-  if (algo == DXR_BUILD_AUTO && g.D % 16 == 0) {
+  if (algo == DXR_BUILD_AUTO && g.D % 16 == 0 && (long long)g.D * g.N < (1LL << 29)) {
     if (vec) return launch_split<OT, 4>(f1, f2, pyr, g, B, stream);
     if (g.W % 2 == 0 && ((uintptr_t)f1 % 8) == 0 && ((uintptr_t)f2 % 8) == 0 &&
         ((uintptr_t)pyr % 16) == 0)
@@ -1117,10 +1179,22 @@ extern "C" int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int 
   // Levels beyond the fused four are pooled by f32 passes: f32 pyramids only.
   if (L.n > dxr::TILED_LEVELS && pyr_dtype != DXR_F32) return DXR_EUNSUPPORTED;
   if (algo == DXR_BUILD_EXACT_F32 && in_dtype != DXR_F32) return DXR_EUNSUPPORTED;
-  if (fmap_layout == DXR_NHWC) return DXR_EUNSUPPORTED;
   const BuildGeom g = make_geom(D, H, W, divisor, L);
   int st;
-  if (in_dtype == DXR_F32) {
+  if (fmap_layout == DXR_NHWC) {
+    // channels-last operands: the split build's NHWC form, where the NCHW build
+    // would also be the split build (f32 fmaps, D % 16 == 0, even W: same bits),
+    // with 16-byte aligned rows; other requests are unsupported (callers transpose)
+    if (in_dtype != DXR_F32 || algo != DXR_BUILD_AUTO || D % 16 != 0 || W % 2 != 0 ||
+        D * H * W >= (1LL << 29) || !aligned16(fmap1) || !aligned16(fmap2) || !aligned16(pyramid))
+      return DXR_EUNSUPPORTED;
+    const float* f1 = static_cast<const float*>(fmap1);
+    const float* f2 = static_cast<const float*>(fmap2);
+    st = pyr_dtype == DXR_F32
+             ? launch_split<float, 4, true>(f1, f2, static_cast<float*>(pyramid), g, (int)B, stream)
+             : launch_split<uint16_t, 4, true>(f1, f2, static_cast<uint16_t*>(pyramid), g, (int)B,
+                                               stream);
+  } else if (in_dtype == DXR_F32) {
     const float* f1 = static_cast<const float*>(fmap1);
     const float* f2 = static_cast<const float*>(fmap2);
     const bool vec = (W % 4) == 0 && aligned16(f1) && aligned16(f2) && aligned16(pyramid);
@@ -1249,7 +1323,8 @@ int xp_split(const float* f1, const float* f2, float* pyr, const BuildGeom& g, i
 extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t D, int64_t H,
                             int64_t W, float* pyr, int xp, hipStream_t stream) {
   dxr::Levels L;
-  if (!dxr::make_levels(B, H, W, 4, &L) || W % 4 != 0 || D % 16 != 0) return DXR_EINVAL;
+  if (!dxr::make_levels(B, H, W, 4, &L) || W % 4 != 0 || D % 16 != 0 || D * H * W >= (1LL << 29))
+    return DXR_EINVAL;
   const BuildGeom g = make_geom(D, H, W, std::sqrt((float)D), L);
   if (g.recip == 0.f) return DXR_EUNSUPPORTED;
   switch (xp) {

@@ -104,9 +104,13 @@ def test_alternate_block_channels_last_matches_oracle(dx):
     assert np.abs(got - ref).max() <= 1e-4 * scale
 
 
+@pytest.mark.parametrize("shape", [(2, 256, 23, 31), (2, 256, 23, 32), (1, 256, 46, 62),
+                                   (1, 64, 55, 128)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_corr_block_channels_last_bit_identical(dx, dtype):
-    B, D, H, W = 2, 256, 23, 31
+def test_corr_block_channels_last_bit_identical(dx, dtype, shape):
+    """Channels-last fmaps give the NCHW block's bits: f32 with even W takes the
+    split build's NHWC operand loads (no layout pass), other cases one transpose."""
+    B, D, H, W = shape
     f1 = _t(dg.fmap(51, B, D, H, W, "fnet")).to(dtype)
     f2 = _t(dg.fmap(52, B, D, H, W, "fnet")).to(dtype)
     c = _t(dg.coords(53, B, H, W, "normal", 4.0))
@@ -135,3 +139,29 @@ def test_corr_block_channels_last_under_grad_keeps_autograd(dx):
         out.square().sum().backward()
         grads.append((f1.grad.contiguous(), f2.grad.contiguous()))
     assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
+
+
+def test_nhwc_build_entry_point(dx):
+    """dxr_corr_pyramid_build with DXR_NHWC reads channels-last operands in place
+    (f32, D % 16 == 0, even W) and writes the NCHW build's pyramid bit for bit;
+    other layouts of the request are DXR_EUNSUPPORTED (the shell transposes)."""
+    from dexiraft_amd import _native as nat
+    lib = nat.load()
+    B, D, H, W = 2, 128, 21, 40
+    f1 = _t(dg.fmap(71, B, D, H, W, "fnet"))
+    f2 = _t(dg.fmap(72, B, D, H, W, "fnet"))
+    n = lib.dxr_pyramid_numel(B, H, W, 4)
+    bufs = []
+    for layout, a, b in ((nat.DXR_NCHW, f1, f2), (nat.DXR_NHWC, _cl(f1), _cl(f2))):
+        buf = torch.full((n,), float("nan"), device=DEV)
+        st = lib.dxr_corr_pyramid_build(a.data_ptr(), b.data_ptr(), nat.DXR_F32, layout, B, D, H,
+                                        W, 4, float(np.sqrt(np.float32(D))), buf.data_ptr(),
+                                        nat.DXR_F32, nat.DXR_BUILD_AUTO, nat.stream_of(a))
+        assert st == 0
+        bufs.append(buf)
+    assert torch.equal(bufs[0], bufs[1])          # pages, padding included
+    g1, g2 = _cl(f1[:, :, :, :39].contiguous()), _cl(f2[:, :, :, :39].contiguous())
+    st = lib.dxr_corr_pyramid_build(g1.data_ptr(), g2.data_ptr(), nat.DXR_F32, nat.DXR_NHWC, B, D,
+                                    H, 39, 4, 11.3137, bufs[0].data_ptr(), nat.DXR_F32,
+                                    nat.DXR_BUILD_AUTO, nat.stream_of(g1))
+    assert st == nat.DXR_EUNSUPPORTED             # odd W: the NCHW build is exact-f32 there
