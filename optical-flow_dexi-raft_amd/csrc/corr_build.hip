@@ -1341,7 +1341,10 @@ extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t
     case 17: return xp_split<17>(f1, f2, pyr, g, (int)B, stream);
     case 21: return xp_split<21>(f1, f2, pyr, g, (int)B, stream);
     case 3 | 4: return xp_split<7>(f1, f2, pyr, g, (int)B, stream);
-    case 1 | 2 | 16: return xp_split<19>(f1, f2, pyr, g, (int)B, stream);
+    case 200:
+      hipLaunchKernelGGL((corr_build_split_kernel<float, false, 3, 4, 0>), build_grid(g, (int)B),
+                         dim3(NT), 0, stream, f1, f2, pyr, g);
+      return dxr::launch_status();
     default: return DXR_EUNSUPPORTED;
   }
 }

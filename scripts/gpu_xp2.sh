@@ -16,7 +16,7 @@ run() {  # name seconds cmd...
   if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "== stopping after $name (rc=$rc)"; exit "$rc"; fi
   return 0
 }
-run xp_sintel 240 python -u scripts/xp_build.py --xp ${XPS:-0,1,2,4,5,8}
-run xp_b8 240 python -u scripts/xp_build.py --B 8 --xp 0,1 --launches 4 --rounds 5
-run pytest_build 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_channels_last.py tests/test_gpu_configs.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
+run xp_sintel 240 python -u scripts/xp_build.py --xp ${XPS:-0,1,2,4,5,8} --check ${CHECK:-0}
+run xp_b8 240 python -u scripts/xp_build.py --B 8 --xp ${XPB8:-0,1} --launches 4 --rounds 5
+[ -n "${SKIP_PYTEST:-}" ] || run pytest_build 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_channels_last.py tests/test_gpu_configs.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
 echo "== done"

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--xp", default="0,1,2,3,4,5,8,16,19")
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--check", default="", help="variants whose pyramid must equal xp 0's bit for bit")
     a = ap.parse_args()
     import dexiraft_amd
     nat = dexiraft_amd._native
@@ -57,6 +58,20 @@ def main():
         if st != 0:
             raise RuntimeError(f"xp {xp}: status {st}")
 
+    ref = None
+    if a.check:
+        pyr.fill_(float("nan"))
+        launch(0)
+        torch.cuda.synchronize()
+        ref = pyr.clone()
+        for xp in (int(x) for x in a.check.split(",")):
+            pyr.fill_(float("nan"))
+            launch(xp)
+            torch.cuda.synchronize()
+            same = torch.equal(pyr, ref)
+            diff = (pyr - ref).abs().nan_to_num(nan=float("inf")).max().item()
+            print(json.dumps({"xp": xp, "bit_identical_to_xp0": same, "max_abs_diff": diff}),
+                  flush=True)
     for xp in xps:
         launch(xp)
     torch.cuda.synchronize()
