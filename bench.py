@@ -20,11 +20,11 @@ and reported.  Rank 0 prints ONE JSON line.
 Execution (``--mode graph``, default): ``value`` is timed on ONE HIP graph per
 step (build + 12 lookups), replayed K times — the launch-bound lookups would
 otherwise be host-bound in Python.  Kernel durations for the rooflines come from
-two more graphs timed with HIP events on the launch stream: KB back-to-back
-builds (into the block's one pyramid buffer, as the step graph's replays write
-one buffer) and 4 x 12 back-to-back lookups, each divided by its launch count, so
-the graph-launch cost is amortised and what remains per launch is the kernel
-plus one same-stream kernel boundary (~1.5 us, MI355X_MICROARCH.md "boundary").
+HIP events on the launch stream around alternating replays of the step graph
+and of a graph of its 12 lookups: lookup = that graph / 12, build = step -
+lookups, i.e. each kernel in the step's own conditions, including one
+same-stream kernel boundary (~1.5 us, MI355X_MICROARCH.md "boundary") and the
+graph launch (~10 us per replay, charged to the build).
 ``--mode eager`` times plain Python calls instead.
 """
 from __future__ import annotations
@@ -59,8 +59,6 @@ WORKLOADS = {
     "1080p": ((1088, 1920), (136, 240), 1, "f32"),
 }
 D, RADIUS, LEVELS, ITERS = 256, 4, 4, 12
-KB_BUILDS = 8                # builds per kernel-timing graph
-KL_REPS = 4                  # x 12 lookups per kernel-timing graph
 
 
 def level_sizes(H, W, L=LEVELS):
@@ -244,27 +242,6 @@ def cpu_baseline(H, W, budget_s, impl="torch", reps=5):
                       f"{ITERS} lookups, {sum(times):.1f} s; {what}"}
 
 
-def _timed_graph(fn, stream, pool, count):
-    """Capture ``fn`` (``count`` launches of one kernel) into a graph sharing
-    ``pool``; return a callable giving the mean ms per launch over ``reps``
-    replays, timed with HIP events on ``stream``."""
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=stream, pool=pool):
-        fn()
-
-    def measure(reps):
-        g.replay()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(reps)]
-        for a, b in ev:
-            a.record(stream)
-            g.replay()
-            b.record(stream)
-        torch.cuda.synchronize()
-        return float(np.mean([a.elapsed_time(b) for a, b in ev])) / count
-    return measure
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -325,7 +302,8 @@ def main():
         build()
         lookups()
 
-    timing = "hip events around graphs of back-to-back launches, divided by the launch count"
+    timing = ("hip events around alternating replays of the step graph and of a graph of its "
+              "12 lookups: lookup = lookups graph / 12, build = step - lookups")
     with torch.no_grad(), torch.cuda.stream(stream):
         for _ in range(max(args.warmup, 1)):          # eager warmup (also a JIT-free check)
             step()
@@ -359,22 +337,32 @@ def main():
         sums = gather_pairs(local_sums, total)
         finite = bool(torch.isfinite(sums).all().item())
 
-        # Kernel-timing pass (outside the timed region).
+        # Kernel-timing pass (outside the timed region), in the conditions of the
+        # step: replays of the step graph alternate with replays of a graph of
+        # the same 12 lookups; lookup time = that graph / 12, build (stage a+b,
+        # or the on-the-fly block's pools/layout) = step - lookups.  (Graphs of
+        # back-to-back builds heat the chip into lower clocks: 159 -> 223 us per
+        # build over 48 launches in an r02 kernel trace.)
         if args.mode == "graph":
             keep = dict(state)            # the step graph's own tensors stay allocated
-            pool = g_step.pool()
-            kb = KB_BUILDS
             cb = state["cb"]
-            if args.block == "corr":
-                # the build kernel as CorrBlock launches it, into the block's own
-                # pyramid buffer (as every replay of the step graph writes one buffer)
-                t_build = _timed_graph(lambda: [cb._launch_build(f1, f2) for _ in range(kb)],
-                                       stream, pool, kb)
-            else:
-                t_build = _timed_graph(lambda: [build() for _ in range(kb)], stream, pool, kb)
-            t_look = _timed_graph(lambda: [cb(c) for _ in range(KL_REPS) for c in coords],
-                                  stream, pool, KL_REPS * ITERS)
-            build_ms, look_ms = t_build(5), t_look(5)
+            g_look = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_look, stream=stream, pool=g_step.pool()):
+                [cb(c) for c in coords]
+            g_look.replay()
+            torch.cuda.synchronize()
+            reps = max(10, min(args.steps, 50))
+            ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(reps)]
+            for e in ev:
+                e[0].record(stream)
+                g_step.replay()
+                e[1].record(stream)
+                g_look.replay()
+                e[2].record(stream)
+            torch.cuda.synchronize()
+            t_step = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+            t_look = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+            build_ms, look_ms = t_step - t_look, t_look / ITERS
             del keep
         else:
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]

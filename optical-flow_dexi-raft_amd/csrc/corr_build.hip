@@ -506,7 +506,9 @@ __device__ __forceinline__ int tgt_col(int r, int c) {
   return (r >> 1) * 32 + (c & 3) + 4 * (r & 1) + 8 * (c >> 2);
 }
 
-template <bool VEC, typename OT, bool DIV, int MINW, bool REMAP = false>
+// XP: timing ablations (experiments build target only): bit 0 skips the epilogue
+// stores, 1 the MFMAs, 2 the in-loop global loads.
+template <bool VEC, typename OT, bool DIV, int MINW, bool REMAP = false, int XP = 0>
 __global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_t* __restrict__ f1,
                                                              const uint16_t* __restrict__ f2,
                                                              OT* __restrict__ pyr, BuildGeom g) {
@@ -531,28 +533,40 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
-  // Staging units: VEC = 4 bf16 (8 B) per unit, 4 units per thread per image.
+  // Staging units: VEC = 4 bf16 (8 B) per unit, 4 units per thread per image,
+  // read with buffer loads (per-lane byte offsets fixed over the K loop, the
+  // stage's k offset in an SGPR; units past the query count, off the image or
+  // past D fall outside the resource and read zeros).  Host side guarantees
+  // D * N * 2 < 2^31 for VEC.
   uint2 ra[4], rb[4];
   uint16_t sa[16], sb[16];
+  uint32_t voa[4], vob[4];
+  __amdgpu_buffer_rsrc_t rsa, rsb;
+  if constexpr (VEC) {
+    rsa = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(f1b), (short)0, g.D * g.N * 2,
+                                            0x00020000);
+    rsb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(f2b), (short)0, g.D * g.N * 2,
+                                            0x00020000);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int idx = tid + NT * s;
+      const int k = idx >> 5;
+      const int q = q0 + (idx & 31) * 4;
+      voa[s] = q < g.N ? (uint32_t)(k * g.N + q) * 2u : 0x80000000u;
+      const int r = (idx >> 2) & 7, c = (idx & 3) * 4, hh = th0 + r, ww = tw0 + c;
+      vob[s] = (hh < g.H && ww < g.W) ? (uint32_t)(k * g.N + hh * g.W + ww) * 2u : 0x80000000u;
+    }
+  }
   auto load = [&](int k0) {
+    if constexpr ((XP & 4) != 0) {
+      if (k0 > 0) return;
+    }
     if constexpr (VEC) {
+      const int so = k0 * g.N * 2;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const int idx = tid + NT * s;
-        const int k = idx >> 5;
-        {
-          const int c = (idx & 31) * 4, kk = k0 + k, q = q0 + c;
-          ra[s] = (kk < g.D && q < g.N)
-                      ? *reinterpret_cast<const uint2*>(f1b + (long long)kk * g.N + q)
-                      : make_uint2(0u, 0u);
-        }
-        {
-          const int r = (idx >> 2) & 7, c = (idx & 3) * 4;
-          const int kk = k0 + k, hh = th0 + r, ww = tw0 + c;
-          rb[s] = (kk < g.D && hh < g.H && ww < g.W)
-                      ? *reinterpret_cast<const uint2*>(f2b + (long long)kk * g.N + hh * g.W + ww)
-                      : make_uint2(0u, 0u);
-        }
+        ra[s] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rsa, voa[s], so, 0));
+        rb[s] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rsb, vob[s], so, 0));
       }
     } else {
 #pragma unroll
@@ -620,8 +634,13 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_
         const uint16_t* pb = Bt + kk * PH + rd_off + t * 32;
         const s8v tv = __builtin_shufflevector(tr_read(pb), tr_read(pb + 4 * PH), 0, 1, 2, 3, 4,
                                                5, 6, 7);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8v, tv), qf, acc[t],
-                                                         0, 0, 0);
+        if constexpr ((XP & 2) != 0) {
+          const s8v x = tv ^ qv;
+          acc[t][0] += (float)(x[0] + x[3] + x[5] + x[7]);
+        } else {
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8v, tv), qf, acc[t],
+                                                           0, 0, 0);
+        }
       }
     }
     if (ks + 1 < nk) store(buf ^ 1);
@@ -629,6 +648,15 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_
   }
 
   scale_acc<DIV>(acc, g);
+  if constexpr ((XP & 1) != 0) {
+    float sum = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sum += acc[t][r];
+    if (sum == 1234.5f) pyr[tid] = to_out<OT>(sum);  // keeps the K loop live
+    return;
+  }
   paged_epilogue<OT>(acc, reinterpret_cast<float*>(smem), pyr, g, pc.page, wave, lane);
 }
 
@@ -1206,7 +1234,7 @@ extern "C" int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int 
     const uint16_t* f1 = static_cast<const uint16_t*>(fmap1);
     const uint16_t* f2 = static_cast<const uint16_t*>(fmap2);
     const bool vec = (W % 4) == 0 && ((uintptr_t)f1 % 8) == 0 && ((uintptr_t)f2 % 8) == 0 &&
-                     aligned16(pyramid);
+                     aligned16(pyramid) && D * H * W < (1LL << 30);
     st = pyr_dtype == DXR_F32
              ? launch_build_bf16(vec, f1, f2, static_cast<float*>(pyramid), g, (int)B, stream)
              : launch_build_bf16(vec, f1, f2, static_cast<uint16_t*>(pyramid), g, (int)B, stream);
@@ -1319,6 +1347,34 @@ int xp_split(const float* f1, const float* f2, float* pyr, const BuildGeom& g, i
   return dxr::launch_status();
 }
 }  // namespace
+
+template <int XP>
+int xp_bf16(const uint16_t* f1, const uint16_t* f2, uint16_t* pyr, const BuildGeom& g, int B,
+            hipStream_t stream) {
+  hipLaunchKernelGGL((corr_build_bf16_kernel<true, uint16_t, false, 3, true, XP>), remap_grid(g, B),
+                     dim3(NT), 0, stream, f1, f2, pyr, g);
+  return dxr::launch_status();
+}
+
+// bf16 fmaps and pyramid, W % 4 == 0: the bf16 build with ablation bits.
+extern "C" int dxr_xp_build_bf16(const void* f1, const void* f2, int64_t B, int64_t D, int64_t H,
+                                 int64_t W, void* pyr, int xp, hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, 4, &L) || W % 4 != 0) return DXR_EINVAL;
+  const BuildGeom g = make_geom(D, H, W, std::sqrt((float)D), L);
+  const uint16_t* a = static_cast<const uint16_t*>(f1);
+  const uint16_t* b = static_cast<const uint16_t*>(f2);
+  uint16_t* p = static_cast<uint16_t*>(pyr);
+  switch (xp) {
+    case 0: return xp_bf16<0>(a, b, p, g, (int)B, stream);
+    case 1: return xp_bf16<1>(a, b, p, g, (int)B, stream);
+    case 2: return xp_bf16<2>(a, b, p, g, (int)B, stream);
+    case 3: return xp_bf16<3>(a, b, p, g, (int)B, stream);
+    case 4: return xp_bf16<4>(a, b, p, g, (int)B, stream);
+    case 5: return xp_bf16<5>(a, b, p, g, (int)B, stream);
+    default: return DXR_EUNSUPPORTED;
+  }
+}
 
 extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t D, int64_t H,
                             int64_t W, float* pyr, int xp, hipStream_t stream) {

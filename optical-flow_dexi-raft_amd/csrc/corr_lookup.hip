@@ -255,7 +255,10 @@ __device__ __forceinline__ void wide_phase0(const float* __restrict__ coords, co
   }
 }
 
-template <int R, typename PT, int NT_ = 512>
+// XP: timing ablations, instantiated only by the experiments build target
+// (DXR_EXPERIMENTS): bit 0 skips the window gathers, 1 the output stores,
+// 2 returns after phase 0.
+template <int R, typename PT, int NT_ = 512, int XP = 0>
 __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
     const PT* __restrict__ pyr, const float* __restrict__ coords, float* __restrict__ out,
     LookupGeom g) {
@@ -275,8 +278,13 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
   wide_phase0<R, NT_>(coords, g, A, b, l, q0, tid, xs, ys, org);
   __syncthreads();
 
+  if constexpr ((XP & 4) != 0) {
+    if (xs[tid % (RD * QB)].y == 1234.5f) out[tid] = 0.f;
+    return;
+  }
+
   // ---- phase 1 (zeros off the level and for far queries)
-  {
+  if constexpr ((XP & 1) == 0) {
     const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
     const int qb0 = q0 & ((1 << A.lqb) - 1);
     if (A.lth == 30)
@@ -306,7 +314,11 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
     r = __builtin_fmaf(ne, v01, r);
     r = __builtin_fmaf(sw, v10, r);
     r = __builtin_fmaf(se, v11, r);
-    ob[(unsigned)(k * g.N)] = r;
+    if constexpr ((XP & 2) != 0) {
+      if (r == 1234.5f) ob[(unsigned)(k * g.N)] = r;
+    } else {
+      ob[(unsigned)(k * g.N)] = r;
+    }
   }
 }
 
@@ -808,3 +820,47 @@ extern "C" int dxr_corr_lookup_conv1x1(const void* pyramid, int pyr_dtype, int64
                                  (int)B, radius, (int)cout, relu, stream);
   return DXR_EINVAL;
 }
+
+#ifdef DXR_EXPERIMENTS
+// Experiments build target only: the radius-4 lookup with ablation bits `xp`.
+namespace {
+template <int XP, typename PT>
+int xp_lookup_k(const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
+                hipStream_t stream) {
+  using W = WideCfg<4>;
+  const dim3 grid((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
+  hipLaunchKernelGGL((corr_lookup_wide_kernel<4, PT, 512, XP>), grid, dim3(W::NT), 0, stream, pyr,
+                     coords, out, g);
+  return dxr::launch_status();
+}
+}  // namespace
+
+extern "C" int dxr_xp_lookup(const void* pyramid, int pyr_dtype, int64_t B, int64_t H, int64_t W,
+                             const float* coords, float* out, int xp, hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, 4, &L)) return DXR_EINVAL;
+  LookupGeom g;
+  g.N = (int)(H * W);
+  g.levels = 4;
+  g.cout = 4 * 81;
+  for (int l = 0; l < 4; ++l) g.lv[l] = level_addr(L.lay[l]);
+  if (pyr_dtype == DXR_F32) {
+    const float* p = static_cast<const float*>(pyramid);
+    switch (xp) {
+      case 0: return xp_lookup_k<0>(p, coords, out, g, (int)B, stream);
+      case 1: return xp_lookup_k<1>(p, coords, out, g, (int)B, stream);
+      case 2: return xp_lookup_k<2>(p, coords, out, g, (int)B, stream);
+      case 3: return xp_lookup_k<3>(p, coords, out, g, (int)B, stream);
+      case 4: return xp_lookup_k<4>(p, coords, out, g, (int)B, stream);
+      default: return DXR_EUNSUPPORTED;
+    }
+  }
+  const uint16_t* p = static_cast<const uint16_t*>(pyramid);
+  switch (xp) {
+    case 0: return xp_lookup_k<0>(p, coords, out, g, (int)B, stream);
+    case 1: return xp_lookup_k<1>(p, coords, out, g, (int)B, stream);
+    case 2: return xp_lookup_k<2>(p, coords, out, g, (int)B, stream);
+    default: return DXR_EUNSUPPORTED;
+  }
+}
+#endif

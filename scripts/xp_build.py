@@ -35,11 +35,13 @@ def main():
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--check", default="", help="variants whose pyramid must equal xp 0's bit for bit")
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"],
+                    help="bf16: the bf16 build (dxr_xp_build_bf16) instead of the split build")
     a = ap.parse_args()
     import dexiraft_amd
     nat = dexiraft_amd._native
     lib = ctypes.CDLL(str(nat.LIB_PATH.with_name("libdexiraft_corr_exp.so")))
-    fn = lib.dxr_xp_build
+    fn = lib.dxr_xp_build_bf16 if a.dtype == "bf16" else lib.dxr_xp_build
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                    ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
@@ -49,7 +51,10 @@ def main():
     g.manual_seed(0)
     f1 = torch.randn((B, D, H, W), generator=g, device=dev)
     f2 = torch.randn((B, D, H, W), generator=g, device=dev)
-    pyr = torch.empty(nat.load().dxr_pyramid_numel(B, H, W, 4), device=dev)
+    if a.dtype == "bf16":
+        f1, f2 = f1.bfloat16(), f2.bfloat16()
+    pyr = torch.empty(nat.load().dxr_pyramid_numel(B, H, W, 4), device=dev,
+                      dtype=torch.bfloat16 if a.dtype == "bf16" else torch.float32)
     s = torch.cuda.current_stream().cuda_stream
     xps = [int(x) for x in a.xp.split(",")]
 
