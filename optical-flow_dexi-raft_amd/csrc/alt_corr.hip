@@ -406,6 +406,380 @@ __global__ __launch_bounds__(256, 2) void alt_corr_mfma_kernel(const float* __re
   }
 }
 
+#ifdef DXR_EXPERIMENTS
+// Two alternative forms of alt_corr_mfma_kernel, measured at 1080p (12 coordinate
+// sets, scripts/xp_alt.py) and kept only in the experiments target: both are
+// bit-identical (rq) or f32-class (grouped) but slower than the product kernel
+// (258 us): register queries 368 us, grouped 16x16x32 308 us (NRB 1) / 351 us
+// (NRB 2).  The product kernel is bound by its scattered cell-vector loads, not by
+// MFMA issue (grouped: -30% MFMA work, slower) nor by occupancy (rq: 2x the waves,
+// slower).
+// ---------------------------------------------------------------------------
+// Register-query MFMA form: as alt_corr_mfma_kernel (4 x 8 query tile, union
+// box, v_mfma_f32_32x32x16_bf16, f32-class split), but the query operand is
+// loaded and split per k step in registers (each wave reads its lanes' 32
+// queries x 16 channels from the NHWC fmap1 — L1/L2-resident) instead of
+// staged once as 49 KB of split planes in LDS.  LDS falls to the window dot
+// products (12.8 KB), so 4+ workgroups fit per CU instead of 2.
+// ---------------------------------------------------------------------------
+template <int R, int MINW>
+__global__ __launch_bounds__(256, MINW) void alt_corr_mfma_rq_kernel(const float* __restrict__ f1,
+                                                                     const float* __restrict__ coords,
+                                                                     float* __restrict__ out,
+                                                                     AltGeom g, int W1, int tiles_x) {
+  constexpr int RD = 2 * R + 1, RD1 = RD + 1, NCELL = RD1 * RD1;
+  constexpr int CHUNK = 4 * 32;                             // box cells per chunk
+  __shared__ float S[TQ * NCELL];                           // window dot products
+  __shared__ int4 qinfo[TQ];                                // {x0, y0, live, -}
+  __shared__ int box[4];                                    // bx0, by0, bw, bh
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int tile = blockIdx.x;
+  {
+    const int n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = tile % 8;
+    tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + tile / 8;
+  }
+  const int tx = tile % tiles_x, ty = tile / tiles_x;
+  const AltLevel lv = g.lv[blockIdx.y];
+  const int z = blockIdx.z, bf = z / g.Nc;
+  const float* cz = coords + (long long)z * g.coord_zstride;
+  const float* f1b = f1 + (long long)bf * g.f1_bstride;
+  const float* f2b = lv.f2 + (long long)bf * lv.H2 * lv.W2 * g.C;
+  const int H1 = g.N / W1;
+  const int nks = g.C / 16;
+
+  if (tid < TQ) {
+    const int qy = ty * TQY + tid / TQX, qx = tx * TQX + tid % TQX;
+    int x0 = 0, y0 = 0, live = 0;
+    if (qy < H1 && qx < W1) {
+      const int q = qy * W1 + qx;
+      const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
+      const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
+      const float xf = floorf(x), yf = floorf(y);
+      if (fabsf(xf) < 1.0e8f && fabsf(yf) < 1.0e8f) {
+        x0 = (int)xf - R;
+        y0 = (int)yf - R;
+        live = (x0 + RD1 > 0 && x0 < lv.W2 && y0 + RD1 > 0 && y0 < lv.H2) ? 1 : 0;
+      }
+    }
+    qinfo[tid] = make_int4(x0, y0, live, 0);
+    int lx0 = live ? max(x0, 0) : 0x7fffffff, ly0 = live ? max(y0, 0) : 0x7fffffff;
+    int lx1 = live ? min(x0 + RD1, lv.W2) : -1, ly1 = live ? min(y0 + RD1, lv.H2) : -1;
+#pragma unroll
+    for (int o = 1; o < TQ; o <<= 1) {
+      lx0 = min(lx0, __shfl_xor(lx0, o));
+      ly0 = min(ly0, __shfl_xor(ly0, o));
+      lx1 = max(lx1, __shfl_xor(lx1, o));
+      ly1 = max(ly1, __shfl_xor(ly1, o));
+    }
+    if (tid == 0) {
+      const bool any = lx1 > lx0;
+      box[0] = any ? lx0 : 0;
+      box[1] = any ? ly0 : 0;
+      box[2] = any ? lx1 - lx0 : 0;
+      box[3] = any ? ly1 - ly0 : 0;
+    }
+  }
+  for (int i = tid; i < TQ * NCELL; i += 256) S[i] = 0.f;
+  __syncthreads();
+
+  const int bx0 = box[0], by0 = box[1], bw = box[2], bh = box[3];
+  const int ncells = bw * bh;
+  const int j = lane & 31, kh = lane >> 5;
+  const int4 qi = qinfo[j];
+  // this lane's query operand row: query j of the tile (clamped), channels 8 kh .. + 8 per k16
+  const int qy = min(ty * TQY + j / TQX, H1 - 1), qx = min(tx * TQX + j % TQX, W1 - 1);
+  const float* qsrc = f1b + (long long)(qy * W1 + qx) * g.C + 8 * kh;
+  for (int c0 = 0; c0 < ncells; c0 += CHUNK) {
+    af16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const int c = min(c0 + wave * 32 + j, ncells - 1);
+    const int cy = c / bw, cx = c - cy * bw;
+    const float* src = f2b + ((long long)(by0 + cy) * lv.W2 + bx0 + cx) * g.C + 8 * kh;
+    float4 ca = *reinterpret_cast<const float4*>(src), cb = *reinterpret_cast<const float4*>(src + 4);
+    float4 qa = *reinterpret_cast<const float4*>(qsrc), qb = *reinterpret_cast<const float4*>(qsrc + 4);
+    for (int ks = 0; ks < nks; ++ks) {
+      float4 na, nb, nqa, nqb;
+      if (ks + 1 < nks) {
+        na = *reinterpret_cast<const float4*>(src + (ks + 1) * 16);
+        nb = *reinterpret_cast<const float4*>(src + (ks + 1) * 16 + 4);
+        nqa = *reinterpret_cast<const float4*>(qsrc + (ks + 1) * 16);
+        nqb = *reinterpret_cast<const float4*>(qsrc + (ks + 1) * 16 + 4);
+      }
+      uint4 qh4, qm4, ql4, h, m, l;
+      {
+        const float x[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+        alt_split8(x, qh4, qm4, ql4);
+      }
+      {
+        const float x[8] = {ca.x, ca.y, ca.z, ca.w, cb.x, cb.y, cb.z, cb.w};
+        alt_split8(x, h, m, l);
+      }
+      const abf8 qh = __builtin_bit_cast(abf8, qh4), qm = __builtin_bit_cast(abf8, qm4),
+                 ql = __builtin_bit_cast(abf8, ql4);
+      const abf8 th = __builtin_bit_cast(abf8, h), tm = __builtin_bit_cast(abf8, m),
+                 tl = __builtin_bit_cast(abf8, l);
+      // small terms first
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, ql, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qh, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qm, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh, acc, 0, 0, 0);
+      if (ks + 1 < nks) {
+        ca = na; cb = nb; qa = nqa; qb = nqb;
+      }
+    }
+    if (qi.z) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int cc = c0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+        if (cc < ncells) {
+          const int ccy = cc / bw, ccx = cc - ccy * bw;
+          const int iy = by0 + ccy - qi.y, ix = bx0 + ccx - qi.x;
+          if ((unsigned)iy < (unsigned)RD1 && (unsigned)ix < (unsigned)RD1)
+            S[j * NCELL + iy * RD1 + ix] = acc[r];
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  const int qq = tid & (TQ - 1), cls = tid / TQ;
+  const int oqy = ty * TQY + qq / TQX, oqx = tx * TQX + qq % TQX;
+  if (oqy >= H1 || oqx >= W1) return;
+  const int q = oqy * W1 + oqx;
+  const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
+  const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
+  const float dx = x - floorf(x), dy = y - floorf(y);
+  const float* sq = S + qq * NCELL;
+  float* o = out + (long long)z * g.cout * g.N + (long long)lv.ch_off * g.N + q;
+  for (int ox = cls; ox < RD; ox += 256 / TQ) {
+#pragma unroll
+    for (int oy = 0; oy < RD; ++oy) {
+      const float s00 = sq[oy * RD1 + ox], s01 = sq[oy * RD1 + ox + 1];
+      const float s10 = sq[(oy + 1) * RD1 + ox], s11 = sq[(oy + 1) * RD1 + ox + 1];
+      float v = __fmul_rn(__fmul_rn(s00, 1.f - dy), 1.f - dx);
+      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s01, 1.f - dy), dx));
+      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s10, dy), 1.f - dx));
+      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s11, dy), dx));
+      o[(long long)(oy + RD * ox) * g.N] = v / g.divisor;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Grouped MFMA form (experiment).  As alt_corr_mfma_kernel,
+// but the tile's 32 queries are ranked by window origin x (off-level windows
+// last) and split into two groups of 16, each with the union box of ITS windows,
+// and the box GEMMs run on v_mfma_f32_16x16x32_bf16 (16 cells x 16 queries x
+// 32 channels).  With scattered coordinates (the benchmark's i.i.d. N(0, 4^2)
+// flows) two narrower boxes cover ~0.7x the (cell, query) pairs of the single
+// 4 x 8 box (level 0: 4.4x instead of 7.3x the compulsory window pairs).  Same
+// products, same f32-class split, same bilinear stage and output.
+// ---------------------------------------------------------------------------
+typedef float af4 __attribute__((ext_vector_type(4)));
+
+template <int R, int NRB, int CMAX>
+__global__ __launch_bounds__(256, 2) void alt_corr_mfma16_kernel(const float* __restrict__ f1,
+                                                                 const float* __restrict__ coords,
+                                                                 float* __restrict__ out,
+                                                                 AltGeom g, int W1, int tiles_x) {
+  constexpr int RD = 2 * R + 1, RD1 = RD + 1, NCELL = RD1 * RD1;
+  constexpr int CHUNK = 4 * 16 * NRB;                       // box cells per chunk
+  constexpr int KB = CMAX / 8;                              // 8-channel blocks
+  __shared__ __attribute__((aligned(16))) uint4 qplanes[3 * KB * TQ];   // [plane][kb][q]
+  __shared__ float S[TQ * NCELL];                           // window dot products
+  __shared__ int4 qinfo[TQ];                                // {x0, y0, live, key}
+  __shared__ int gq[2][16];                                 // group -> member query
+  __shared__ int box[2][4];                                 // per group bx0, by0, bw, bh
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int tile = blockIdx.x;
+  {
+    const int n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = tile % 8;
+    tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + tile / 8;
+  }
+  const int tx = tile % tiles_x, ty = tile / tiles_x;
+  const AltLevel lv = g.lv[blockIdx.y];
+  const int z = blockIdx.z, bf = z / g.Nc;
+  const float* cz = coords + (long long)z * g.coord_zstride;
+  const float* f1b = f1 + (long long)bf * g.f1_bstride;
+  const float* f2b = lv.f2 + (long long)bf * lv.H2 * lv.W2 * g.C;
+  const int H1 = g.N / W1;
+  const int nkb = g.C / 8;
+
+  // ---- query coordinates, window origins, sort key (window x origin; off-level last)
+  if (tid < TQ) {
+    const int qy = ty * TQY + tid / TQX, qx = tx * TQX + tid % TQX;
+    int x0 = 0, y0 = 0, live = 0;
+    if (qy < H1 && qx < W1) {
+      const int q = qy * W1 + qx;
+      const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
+      const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
+      const float xf = floorf(x), yf = floorf(y);
+      if (fabsf(xf) < 1.0e8f && fabsf(yf) < 1.0e8f) {
+        x0 = (int)xf - R;
+        y0 = (int)yf - R;
+        live = (x0 + RD1 > 0 && x0 < lv.W2 && y0 + RD1 > 0 && y0 < lv.H2) ? 1 : 0;
+      }
+    }
+    qinfo[tid] = make_int4(x0, y0, live, live ? x0 : 0x7fffffff);
+  }
+  for (int i = tid; i < TQ * NCELL; i += 256) S[i] = 0.f;
+  // query operand planes: unit (kb, q) -> f1[q][8 kb .. 8 kb + 8), split once
+  for (int u = tid; u < nkb * TQ; u += 256) {
+    const int kb = u / TQ, qq = u - kb * TQ;
+    const int qy = min(ty * TQY + qq / TQX, H1 - 1), qx = min(tx * TQX + qq % TQX, W1 - 1);
+    const float* src = f1b + (long long)(qy * W1 + qx) * g.C + kb * 8;
+    const float4 a = *reinterpret_cast<const float4*>(src);
+    const float4 c = *reinterpret_cast<const float4*>(src + 4);
+    const float x[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+    uint4 h, m, l;
+    alt_split8(x, h, m, l);
+    qplanes[(0 * KB + kb) * TQ + qq] = h;
+    qplanes[(1 * KB + kb) * TQ + qq] = m;
+    qplanes[(2 * KB + kb) * TQ + qq] = l;
+  }
+  __syncthreads();
+  if (tid < TQ) {
+    const int4 me = qinfo[tid];
+    int rank = 0;
+    for (int i = 0; i < TQ; ++i) {
+      const int k = qinfo[i].w;
+      rank += (k < me.w || (k == me.w && i < tid)) ? 1 : 0;
+    }
+    gq[rank >> 4][rank & 15] = tid;
+  }
+  __syncthreads();
+  if (tid < TQ) {     // lane (group tid >> 4, slot tid & 15): union box of the group's live windows
+    const int4 qi = qinfo[gq[tid >> 4][tid & 15]];
+    int lx0 = qi.z ? max(qi.x, 0) : 0x7fffffff, ly0 = qi.z ? max(qi.y, 0) : 0x7fffffff;
+    int lx1 = qi.z ? min(qi.x + RD1, lv.W2) : -1, ly1 = qi.z ? min(qi.y + RD1, lv.H2) : -1;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      lx0 = min(lx0, __shfl_xor(lx0, o));
+      ly0 = min(ly0, __shfl_xor(ly0, o));
+      lx1 = max(lx1, __shfl_xor(lx1, o));
+      ly1 = max(ly1, __shfl_xor(ly1, o));
+    }
+    if ((tid & 15) == 0) {
+      const bool any = lx1 > lx0;
+      box[tid >> 4][0] = any ? lx0 : 0;
+      box[tid >> 4][1] = any ? ly0 : 0;
+      box[tid >> 4][2] = any ? lx1 - lx0 : 0;
+      box[tid >> 4][3] = any ? ly1 - ly0 : 0;
+    }
+  }
+  __syncthreads();
+
+  const int j = lane & 15, kq = lane >> 4;
+#pragma unroll 1
+  for (int grp = 0; grp < 2; ++grp) {
+    const int bx0 = box[grp][0], by0 = box[grp][1], bw = box[grp][2], bh = box[grp][3];
+    const int ncells = bw * bh;
+    const int jq = gq[grp][j];                  // this lane's accumulator column (query)
+    const int4 qi = qinfo[jq];
+    for (int c0 = 0; c0 < ncells; c0 += CHUNK) {
+      af4 acc[NRB];
+      const float* src[NRB];
+#pragma unroll
+      for (int rb = 0; rb < NRB; ++rb) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[rb][r] = 0.f;
+        // A operand lane -> cell c0 + 16 (wave NRB + rb) + j, channels 8 kq .. + 8 per k32
+        const int c = min(c0 + (wave * NRB + rb) * 16 + j, ncells - 1);
+        const int cy = c / bw, cx = c - cy * bw;
+        src[rb] = f2b + ((long long)(by0 + cy) * lv.W2 + bx0 + cx) * g.C + 8 * kq;
+      }
+      float4 ca[NRB], cb[NRB];
+#pragma unroll
+      for (int rb = 0; rb < NRB; ++rb) {
+        ca[rb] = *reinterpret_cast<const float4*>(src[rb]);
+        cb[rb] = *reinterpret_cast<const float4*>(src[rb] + 4);
+      }
+      for (int ks = 0; ks < nkb / 4; ++ks) {
+        float4 na[NRB], nb[NRB];
+        if (ks + 1 < nkb / 4) {
+#pragma unroll
+          for (int rb = 0; rb < NRB; ++rb) {
+            na[rb] = *reinterpret_cast<const float4*>(src[rb] + (ks + 1) * 32);
+            nb[rb] = *reinterpret_cast<const float4*>(src[rb] + (ks + 1) * 32 + 4);
+          }
+        }
+        const int kb = 4 * ks + kq;
+        const abf8 qh = __builtin_bit_cast(abf8, qplanes[(0 * KB + kb) * TQ + jq]);
+        const abf8 qm = __builtin_bit_cast(abf8, qplanes[(1 * KB + kb) * TQ + jq]);
+        const abf8 ql = __builtin_bit_cast(abf8, qplanes[(2 * KB + kb) * TQ + jq]);
+#pragma unroll
+        for (int rb = 0; rb < NRB; ++rb) {
+          const float4 a = ca[rb], b = cb[rb];
+          const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+          uint4 h, m, l;
+          alt_split8(x, h, m, l);
+          const abf8 th = __builtin_bit_cast(abf8, h), tm = __builtin_bit_cast(abf8, m),
+                     tl = __builtin_bit_cast(abf8, l);
+          // small terms first
+          acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tm, qm, acc[rb], 0, 0, 0);
+          acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tl, qh, acc[rb], 0, 0, 0);
+          acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(th, ql, acc[rb], 0, 0, 0);
+          acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tm, qh, acc[rb], 0, 0, 0);
+          acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(th, qm, acc[rb], 0, 0, 0);
+          acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(th, qh, acc[rb], 0, 0, 0);
+        }
+        if (ks + 1 < nkb / 4) {
+#pragma unroll
+          for (int rb = 0; rb < NRB; ++rb) {
+            ca[rb] = na[rb];
+            cb[rb] = nb[rb];
+          }
+        }
+      }
+      // keep the entries inside query jq's window: D row = 4 kq + r
+      if (qi.z) {
+#pragma unroll
+        for (int rb = 0; rb < NRB; ++rb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int c = c0 + (wave * NRB + rb) * 16 + 4 * kq + r;
+            if (c < ncells) {
+              const int cy = c / bw, cx = c - cy * bw;
+              const int iy = by0 + cy - qi.y, ix = bx0 + cx - qi.x;
+              if ((unsigned)iy < (unsigned)RD1 && (unsigned)ix < (unsigned)RD1)
+                S[jq * NCELL + iy * RD1 + ix] = acc[rb][r];
+            }
+          }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- bilinear combination, as the per-query form (reference order)
+  const int qq = tid & (TQ - 1), cls = tid / TQ;
+  const int qy = ty * TQY + qq / TQX, qx = tx * TQX + qq % TQX;
+  if (qy >= H1 || qx >= W1) return;
+  const int q = qy * W1 + qx;
+  const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
+  const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
+  const float dx = x - floorf(x), dy = y - floorf(y);
+  const float* s = S + qq * NCELL;
+  float* o = out + (long long)z * g.cout * g.N + (long long)lv.ch_off * g.N + q;
+  for (int ox = cls; ox < RD; ox += 256 / TQ) {
+#pragma unroll
+    for (int oy = 0; oy < RD; ++oy) {
+      const float s00 = s[oy * RD1 + ox], s01 = s[oy * RD1 + ox + 1];
+      const float s10 = s[(oy + 1) * RD1 + ox], s11 = s[(oy + 1) * RD1 + ox + 1];
+      float v = __fmul_rn(__fmul_rn(s00, 1.f - dy), 1.f - dx);
+      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s01, 1.f - dy), dx));
+      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s10, dy), 1.f - dx));
+      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s11, dy), dx));
+      o[(long long)(oy + RD * ox) * g.N] = v / g.divisor;
+    }
+  }
+}
+#endif  // DXR_EXPERIMENTS
+
 template <int R, int NRB>
 int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const AltGeom& g,
                       int levels, int Z, int W1, hipStream_t stream) {
@@ -805,3 +1179,58 @@ extern "C" int dxr_alt_corr_lookup(const float* fmap1, const float* const* fmap2
   }
   return launch_alt(fmap1, coords, out, g, num_levels, (int)B, radius, vec, stream, (int)W);
 }
+
+#ifdef DXR_EXPERIMENTS
+// Experiments build target only: the fused on-the-fly lookup with a chosen kernel
+// (0: 4x8-box 32x32x16 form, 1: grouped 16x16x32 form NRB 2, 2: NRB 1).
+namespace {
+template <int NRB>
+int xp_alt16(const float* f1, const float* coords, float* out, const AltGeom& g, int levels, int Z,
+             int W1, hipStream_t stream) {
+  const int H1 = g.N / W1;
+  const int tiles_x = (W1 + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
+  const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)levels, (unsigned)Z);
+  hipLaunchKernelGGL((alt_corr_mfma16_kernel<4, NRB, 256>), grid, dim3(256), 0, stream, f1, coords,
+                     out, g, W1, tiles_x);
+  return dxr::launch_status();
+}
+}  // namespace
+
+extern "C" int dxr_xp_alt(const float* fmap1, const float* const* fmap2_levels, const float* coords,
+                          float* out, int64_t B, int64_t H, int64_t W, int64_t C, int num_levels,
+                          float divisor, int xp, hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, num_levels, &L) || C != 256) return DXR_EINVAL;
+  AltGeom g;
+  g.N = (int)(H * W);
+  g.C = (int)C;
+  g.Nc = 1;
+  g.cout = num_levels * 81;
+  g.divisor = divisor;
+  g.f1_bstride = H * W * C;
+  g.coord_zstride = 2 * H * W;
+  g.coord_cstride = H * W;
+  g.coord_qstride = 1;
+  for (int l = 0; l < num_levels; ++l)
+    g.lv[l] = AltLevel{fmap2_levels[l], L.h[l], L.w[l], 1.f / (float)(1 << l), l * 81};
+  if (xp == 0) return launch_alt_mfma_r<4, 1>(fmap1, coords, out, g, num_levels, (int)B, (int)W, stream);
+  if (xp == 1) return xp_alt16<2>(fmap1, coords, out, g, num_levels, (int)B, (int)W, stream);
+  if (xp == 2) return xp_alt16<1>(fmap1, coords, out, g, num_levels, (int)B, (int)W, stream);
+  if (xp == 3 || xp == 4 || xp == 5) {
+    const int H1 = g.N / (int)W;
+    const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
+    const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
+    if (xp == 3)
+      hipLaunchKernelGGL((alt_corr_mfma_rq_kernel<4, 2>), grid, dim3(256), 0, stream, fmap1, coords,
+                         out, g, (int)W, tiles_x);
+    else if (xp == 4)
+      hipLaunchKernelGGL((alt_corr_mfma_rq_kernel<4, 4>), grid, dim3(256), 0, stream, fmap1, coords,
+                         out, g, (int)W, tiles_x);
+    else
+      hipLaunchKernelGGL((alt_corr_mfma_rq_kernel<4, 6>), grid, dim3(256), 0, stream, fmap1, coords,
+                         out, g, (int)W, tiles_x);
+    return dxr::launch_status();
+  }
+  return DXR_EUNSUPPORTED;
+}
+#endif

@@ -322,6 +322,81 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
   }
 }
 
+#ifdef DXR_EXPERIMENTS
+// ---------------------------------------------------------------------------
+// Two-level lookup (experiment): a workgroup handles the same 32 queries on
+// levels 2y and 2y+1: phase 0 of both, BOTH levels' window gathers issued into
+// registers before either is staged (twice the loads in flight per thread),
+// then level 2y's windows -> LDS -> outputs, level 2y+1's windows -> the same
+// LDS -> outputs.  Same arithmetic as corr_lookup_wide_kernel; measured slower
+// (xp 100 in scripts/xp_lookup.py), kept in the experiments target only.
+// ---------------------------------------------------------------------------
+template <int R, typename PT, int NT_ = 512>
+__global__ __launch_bounds__(NT_) void corr_lookup_wide2_kernel(
+    const PT* __restrict__ pyr, const float* __restrict__ coords, float* __restrict__ out,
+    LookupGeom g) {
+  using C = WideCfg<R, NT_>;
+  constexpr int RD = C::RD, RS = C::RS, K = C::K, QB = C::QB;
+  __shared__ __attribute__((aligned(16))) float cells[QB * C::QS];
+  __shared__ float4 xs[2][RD * QB];
+  __shared__ float4 ys[2][RD * QB];
+  __shared__ int2 org[2][QB];
+
+  const int tid = threadIdx.x;
+  const int b = blockIdx.z;
+  const int q0 = blockIdx.x * QB;
+  const int l0 = 2 * blockIdx.y;
+  const int nl = min(2, g.levels - l0);
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+    if (u < nl) wide_phase0<R, NT_>(coords, g, g.lv[l0 + u], b, l0 + u, q0, tid, xs[u], ys[u], org[u]);
+  __syncthreads();
+  float4 win[2][C::VIT];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (u >= nl) break;
+    const LevelAddr& A = g.lv[l0 + u];
+    const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
+    const int qb0 = q0 & ((1 << A.lqb) - 1);
+    if (A.lth == 30)
+      gather_load<R, NT_, 1>(base, qb0, A, org[u], q0, g.N, tid, win[u]);
+    else if (A.tw >= 4)
+      gather_load<R, NT_, 4>(base, qb0, A, org[u], q0, g.N, tid, win[u]);
+    else if (A.tw == 2)
+      gather_load<R, NT_, 2>(base, qb0, A, org[u], q0, g.N, tid, win[u]);
+    else
+      gather_load<R, NT_, 1>(base, qb0, A, org[u], q0, g.N, tid, win[u]);
+  }
+  const int qq = tid % QB, cls = tid / QB;
+  const bool live = q0 + qq < g.N;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (u >= nl) break;
+    if (u > 0) __syncthreads();          // level u-1's phase 2 is done with the cells
+    gather_store<R, NT_>(win[u], cells, tid);
+    __syncthreads();
+    if (live) {
+      const float* cq = cells + qq * C::QS;
+      float* ob = out + ((long long)b * g.cout + (long long)(l0 + u) * K) * g.N + q0 + qq;
+      for (int k = cls; k < K; k += C::NCLS) {
+        const int ox = k / RD, oy = k - ox * RD;
+        const float4 xd = xs[u][ox * QB + qq], yd = ys[u][oy * QB + qq];
+        const float* p = cq + __float_as_int(yd.x) + __float_as_int(xd.x);
+        const float v00 = p[0], v01 = p[1], v10 = p[RS], v11 = p[RS + 1];
+        const float nw = __fmul_rn(yd.z, xd.z), ne = __fmul_rn(yd.z, xd.y);
+        const float sw = __fmul_rn(yd.y, xd.z), se = __fmul_rn(yd.y, xd.y);
+        float r = __fmul_rn(nw, v00);
+        r = __builtin_fmaf(ne, v01, r);
+        r = __builtin_fmaf(sw, v10, r);
+        r = __builtin_fmaf(se, v11, r);
+        ob[(unsigned)(k * g.N)] = r;
+      }
+    }
+  }
+}
+
+#endif  // DXR_EXPERIMENTS
+
 // ---------------------------------------------------------------------------
 // Lookup backward (training: train.py:175-178 backpropagates through the
 // grid_sample calls of core/utils/utils.py:65).  The gradient of one query's
@@ -833,6 +908,16 @@ int xp_lookup_k(const PT* pyr, const float* coords, float* out, const LookupGeom
                      coords, out, g);
   return dxr::launch_status();
 }
+template <typename PT>
+int xp_lookup2(const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
+               hipStream_t stream) {
+  using W = WideCfg<4>;
+  const dim3 grid((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)((g.levels + 1) / 2),
+                  (unsigned)B);
+  hipLaunchKernelGGL((corr_lookup_wide2_kernel<4, PT>), grid, dim3(W::NT), 0, stream, pyr, coords,
+                     out, g);
+  return dxr::launch_status();
+}
 }  // namespace
 
 extern "C" int dxr_xp_lookup(const void* pyramid, int pyr_dtype, int64_t B, int64_t H, int64_t W,
@@ -852,11 +937,13 @@ extern "C" int dxr_xp_lookup(const void* pyramid, int pyr_dtype, int64_t B, int6
       case 2: return xp_lookup_k<2>(p, coords, out, g, (int)B, stream);
       case 3: return xp_lookup_k<3>(p, coords, out, g, (int)B, stream);
       case 4: return xp_lookup_k<4>(p, coords, out, g, (int)B, stream);
+      case 100: return xp_lookup2(p, coords, out, g, (int)B, stream);
       default: return DXR_EUNSUPPORTED;
     }
   }
   const uint16_t* p = static_cast<const uint16_t*>(pyramid);
   switch (xp) {
+    case 100: return xp_lookup2(p, coords, out, g, (int)B, stream);
     case 0: return xp_lookup_k<0>(p, coords, out, g, (int)B, stream);
     case 1: return xp_lookup_k<1>(p, coords, out, g, (int)B, stream);
     case 2: return xp_lookup_k<2>(p, coords, out, g, (int)B, stream);
