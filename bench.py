@@ -49,7 +49,7 @@ METRIC = "frame pairs/sec (corr build + 12 lookups) @436x1024, 1–8 GPU; % MFMA
 PEAK_F32_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 PEAK_BF16_TFLOPS = 2500.0    # dense BF16 MFMA
 PEAK_HBM_GBS = 8000.0        # HBM3E spec
-SPLIT_PRODUCTS = 6           # bf16 MFMA products per f32 product in the split build
+SPLIT_PRODUCTS = 3           # f16 MFMA products per f32 product in the split build
 
 # name -> (image H, W after InputPadder, fmap H, W, default pairs per GPU, dtype)
 WORKLOADS = {
@@ -90,15 +90,16 @@ def lookup_bytes(B, H, W, s_pyr=4):
 def build_kernel(dtype, H, W):
     """The build kernel the library runs for this workload (csrc/corr_build.hip
     launch_build_f32 / launch_build_bf16) and the ceiling of the arithmetic it
-    runs: the split f32 build issues six bf16 MFMA products per f32 product
-    (exact hi+mid+lo operand split, f32 accumulation), so its binding ceiling is
-    2.5 PF / 6 = 417 TF f32-equivalent; the f32 peak (157.3 TF) is §8(d)'s."""
+    runs: the split f32 build issues three f16 MFMA products per f32 product
+    (f16 pair split x = hi + 2^-11 lo, products hi*hi and hi*lo + lo*hi into two
+    f32 accumulators), so its binding ceiling is 2.5 PF / 3 = 833 TF
+    f32-equivalent; the f32 peak (157.3 TF) is §8(d)'s."""
     if dtype == "bf16":
         return "corr_build_bf16_kernel", 1, PEAK_BF16_TFLOPS, "bf16"
     if D % 16 == 0 and W % 2 == 0:
-        return ("corr_build_split_kernel (f32 operands split exactly into 3 bf16, "
-                "bf16x6 MFMA, f32 accumulate)", SPLIT_PRODUCTS, PEAK_BF16_TFLOPS,
-                "bf16 MFMA, f32 accumulate")
+        return ("corr_build_split_kernel (f32 operands as f16 pairs hi + 2^-11 lo, "
+                "3 f16 MFMA products, f32 accumulate)", SPLIT_PRODUCTS, PEAK_BF16_TFLOPS,
+                "f16 MFMA, f32 accumulate")
     return "corr_build_f32_kernel", 1, PEAK_F32_TFLOPS, "f32"
 
 
@@ -419,8 +420,8 @@ def main():
             kname, mfma_per_flop, pipe_peak, mfma_dtype = build_kernel(dtype, H, W)
             # achieved = ALGORITHMIC flops (2*B*N^2*D) per launch / launch time.
             # Ceiling = the dense MFMA peak of the arithmetic actually run: bf16 fmaps
-            # 2.5 PF; f32 fmaps on the split build 2.5 PF / 6 = 417 TF f32-equivalent
-            # (its bf16 pipe); the exact-f32 build 157.3 TF.  frac_f32_peak keeps
+            # 2.5 PF; f32 fmaps on the split build 2.5 PF / 3 = 833 TF f32-equivalent
+            # (its f16 pipe, same dense peak as bf16); the exact-f32 build 157.3 TF.  frac_f32_peak keeps
             # SURVEY §8(d)'s f32 pricing beside it.
             achieved = flops / (build_ms * 1e-3) / 1e12
             ceiling = pipe_peak / mfma_per_flop
@@ -431,7 +432,7 @@ def main():
                 "kernel": kname + " (stage a+b)",
                 "bound": "mfma", "achieved": round(achieved, 2), "peak": round(ceiling, 1),
                 "unit": "TFLOP/s", "frac": round(achieved / ceiling, 4),
-                "peak_basis": (f"dense bf16 MFMA 2.5 PF / {mfma_per_flop} products per f32 product"
+                "peak_basis": (f"dense f16 MFMA 2.5 PF / {mfma_per_flop} products per f32 product"
                                if mfma_per_flop > 1 else f"dense {mfma_dtype} MFMA peak"),
                 "frac_f32_peak": None if dtype == "bf16" else round(achieved / PEAK_F32_TFLOPS, 4),
                 "traffic": b_traffic, "traffic_source": b_src,

@@ -25,6 +25,7 @@
 // (Scattered per-query row stores — 64 lines per wave store — cost more than the
 // MFMA loop itself: measured 346 vs 220 us at Sintel shape.)
 #include <cmath>
+#include <type_traits>
 
 #include "dxr_common.h"
 
@@ -713,6 +714,33 @@ __device__ __forceinline__ Split3 split3(float a, float b) {
   return {h, m, pack_hi(__float_as_uint(la), __float_as_uint(lb))};
 }
 
+// f16 pair split (H2 form of the split build): x = hi + 2^-11 lo with
+// hi = RNE_f16(x) and lo = RNE_f16((x - hi) * 2^11).  x - hi is exact in f32 and
+// the scaling is exact, so the representation error is lo's rounding:
+// <= 2^-22 |x| (hi normal) or <= 2^-36 absolute (|x| < 2^-14, lo subnormal).
+// x*y = hi*hi + 2^-11 (hi*lo + lo*hi) + 2^-22 lo*lo; the last term (<= 2^-22 |x y|,
+// sign-symmetric under RNE) is dropped.  f16 x f16 products are exact in f32.
+// Valid while |x| < 65520 (hi finite): the kernel detects the overflow from its
+// own accumulators and re-runs the page on the 3-way bf16 split.
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+
+struct Split2 {
+  uint32_t h, l;  // f16x2 words (first element in the low half)
+};
+
+__device__ __forceinline__ uint32_t cvt_pk_f16(float a, float b) {
+  const f32x2_t v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2_t));
+}
+
+__device__ __forceinline__ Split2 split2h(float a, float b) {
+  const uint32_t h = cvt_pk_f16(a, b);
+  const f16x2_t hv = __builtin_bit_cast(f16x2_t, h);
+  const float ra = (a - (float)hv[0]) * 2048.f, rb = (b - (float)hv[1]) * 2048.f;
+  return {h, cvt_pk_f16(ra, rb)};
+}
+
 // Raw buffer access (gfx9 resource word 3: 0x00020000), byte offsets.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* base, int elems) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, elems * 4,
@@ -742,7 +770,8 @@ __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t voff
 // (DXR_EXPERIMENTS, libdexiraft_corr_exp.so; never by the product library):
 // bit 0 skips the epilogue stores, 1 the MFMAs, 2 the in-loop global loads,
 // 3 the operand split (hi only), 4 the in-loop barrier.
-template <typename OT, bool DIV, int MINW, int BV = 4, int XP = 0, bool NHWC = false>
+template <typename OT, bool DIV, int MINW, int BV = 4, int XP = 0, bool NHWC = false,
+          bool H2 = false, bool REMAP = false>
 __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float* __restrict__ f1,
                                                                     const float* __restrict__ f2,
                                                                     OT* __restrict__ pyr,
@@ -750,10 +779,12 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
   constexpr int LDS_E = WAVES * 16 * P0 * 4;                         // epilogue bytes
   constexpr int LDS_K = 2 * 3 * (NHWC ? NTGT * 24 : PLANE_S) * 2;     // two stages, bytes
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_K > LDS_E ? LDS_K : LDS_E];
+  __shared__ int redo;  // H2: some accumulator of the page is not finite
   uint16_t* lh = reinterpret_cast<uint16_t*>(smem);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const PageCoord pc = page_coord<false>(g);
+  if (H2 && tid == 0) redo = 0;
+  const PageCoord pc = page_coord<REMAP>(g);
   const int txi = pc.txi, tyi = pc.tyi;
   const int th0 = tyi * TH, tw0 = txi * TW;
   const int q0 = pc.qblk * BM;
@@ -762,11 +793,11 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
   const float* f1b = f1 + b * fstride;
   const float* f2b = f2 + b * fstride;
 
-  f32x16 acc[4];
+  f32x16 acc[4], acc2[4];  // acc2: H2 cross terms (hi*lo + lo*hi, scaled 2^11)
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    for (int r = 0; r < 16; ++r) acc[t][r] = acc2[t][r] = 0.f;
 
   // Operands are read with buffer loads: one resource per fmap of this pair,
   // per-lane 32-bit byte offsets fixed for the whole K loop, and the stage's k
@@ -836,7 +867,9 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
       }
     }
   };
-  s8v ah, am, al;   // split query operand of the current stage
+  s8v ah, am, al;   // split query operand of the current stage (H2: ah, al)
+  using S3 = std::integral_constant<bool, false>;
+  using S2 = std::integral_constant<bool, true>;
   auto split3x = [&](float a, float bb) -> Split3 {
     if constexpr ((XP & 8) != 0) {
       const uint32_t h = cvt_pk_bf16(a, bb);
@@ -845,14 +878,21 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
       return split3(a, bb);
     }
   };
-  auto split_a = [&]() {
+  auto split_a = [&](auto mode) {
     uint32_t h[4], m[4], l[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const Split3 x = split3x(an[2 * e], an[2 * e + 1]);
-      h[e] = x.h;
-      m[e] = x.m;
-      l[e] = x.l;
+      if constexpr (decltype(mode)::value) {
+        const Split2 x = split2h(an[2 * e], an[2 * e + 1]);
+        h[e] = x.h;
+        m[e] = 0;
+        l[e] = x.l;
+      } else {
+        const Split3 x = split3x(an[2 * e], an[2 * e + 1]);
+        h[e] = x.h;
+        m[e] = x.m;
+        l[e] = x.l;
+      }
     }
     ah = __builtin_bit_cast(s8v, make_uint4(h[0], h[1], h[2], h[3]));
     am = __builtin_bit_cast(s8v, make_uint4(m[0], m[1], m[2], m[3]));
@@ -863,21 +903,34 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
   constexpr int PN = 24;                      // NHWC plane row pitch (bf16)
   constexpr int PLANE_N = NTGT * PN;          // bf16 elements per NHWC plane
   constexpr int PLANE = NHWC ? PLANE_N : PLANE_S;
-  auto store_b = [&](int buf) {
+  // Target planes of a stage: hi, mid, lo (bf16) or hi, lo (H2: f16).
+  auto store_b = [&](int buf, auto mode) {
     uint16_t* P = lh + buf * 3 * PLANE;
 #pragma unroll
     for (int s = 0; s < NBS; ++s) {
       const int o = NHWC ? bcol[s] * PN + bk[s] : bk[s] * PH + bcol[s];
-      const Split3 x = split3x(bn[s].x, bn[s].y);
-      if constexpr (BV == 4) {
-        const Split3 z = split3x(bn[s].z, bn[s].w);
-        *reinterpret_cast<uint2*>(P + o) = make_uint2(x.h, z.h);
-        *reinterpret_cast<uint2*>(P + PLANE + o) = make_uint2(x.m, z.m);
-        *reinterpret_cast<uint2*>(P + 2 * PLANE + o) = make_uint2(x.l, z.l);
+      if constexpr (decltype(mode)::value) {
+        const Split2 x = split2h(bn[s].x, bn[s].y);
+        if constexpr (BV == 4) {
+          const Split2 z = split2h(bn[s].z, bn[s].w);
+          *reinterpret_cast<uint2*>(P + o) = make_uint2(x.h, z.h);
+          *reinterpret_cast<uint2*>(P + PLANE + o) = make_uint2(x.l, z.l);
+        } else {
+          *reinterpret_cast<uint32_t*>(P + o) = x.h;
+          *reinterpret_cast<uint32_t*>(P + PLANE + o) = x.l;
+        }
       } else {
-        *reinterpret_cast<uint32_t*>(P + o) = x.h;
-        *reinterpret_cast<uint32_t*>(P + PLANE + o) = x.m;
-        *reinterpret_cast<uint32_t*>(P + 2 * PLANE + o) = x.l;
+        const Split3 x = split3x(bn[s].x, bn[s].y);
+        if constexpr (BV == 4) {
+          const Split3 z = split3x(bn[s].z, bn[s].w);
+          *reinterpret_cast<uint2*>(P + o) = make_uint2(x.h, z.h);
+          *reinterpret_cast<uint2*>(P + PLANE + o) = make_uint2(x.m, z.m);
+          *reinterpret_cast<uint2*>(P + 2 * PLANE + o) = make_uint2(x.l, z.l);
+        } else {
+          *reinterpret_cast<uint32_t*>(P + o) = x.h;
+          *reinterpret_cast<uint32_t*>(P + PLANE + o) = x.m;
+          *reinterpret_cast<uint32_t*>(P + 2 * PLANE + o) = x.l;
+        }
       }
     }
   };
@@ -897,40 +950,80 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
   const int tstride = NHWC ? 32 * PN : 32;    // MFMA tile t's first row / column
 
   const int nk = g.D / BKS;
-  load(0);
-  store_b(0);
-  split_a();
-  __syncthreads();
-  for (int ks = 0; ks < nk; ++ks) {
-    const int buf = ks & 1;
-    if (ks + 1 < nk) load((ks + 1) * BKS);
-    const bf8v qh = __builtin_bit_cast(bf8v, ah), qm = __builtin_bit_cast(bf8v, am),
-               ql = __builtin_bit_cast(bf8v, al);
-    const uint16_t* P = lh + buf * 3 * PLANE + rd_off;
+  // The K loop, on the 3-way bf16 split (six products into acc) or on the f16
+  // pair split (hi*hi into acc, the two cross products into acc2).
+  auto kloop = [&](auto mode) {
+    constexpr bool M2 = decltype(mode)::value;
+    load(0);
+    store_b(0, mode);
+    split_a(mode);
+    __syncthreads();
+    for (int ks = 0; ks < nk; ++ks) {
+      const int buf = ks & 1;
+      if (ks + 1 < nk) load((ks + 1) * BKS);
+      const uint16_t* P = lh + buf * 3 * PLANE + rd_off;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const bf8v th = frag(P + t * tstride), tm = frag(P + PLANE + t * tstride),
-                 tl = frag(P + 2 * PLANE + t * tstride);
-      if constexpr ((XP & 2) != 0) {
-        const s8v x = __builtin_bit_cast(s8v, th) ^ __builtin_bit_cast(s8v, tm) ^
-                      __builtin_bit_cast(s8v, tl) ^ __builtin_bit_cast(s8v, qh) ^
-                      __builtin_bit_cast(s8v, qm) ^ __builtin_bit_cast(s8v, ql);
-        acc[t][0] += (float)(x[0] + x[3] + x[5] + x[7]);
-        continue;
+      for (int t = 0; t < 4; ++t) {
+        if constexpr ((XP & 2) != 0) {
+          const s8v x = __builtin_bit_cast(s8v, frag(P + t * tstride)) ^
+                        __builtin_bit_cast(s8v, frag(P + PLANE + t * tstride)) ^ ah ^ am ^ al;
+          acc[t][0] += (float)(x[0] + x[3] + x[5] + x[7]);
+          continue;
+        }
+        if constexpr (M2) {
+          const h8v th = __builtin_bit_cast(h8v, frag(P + t * tstride)),
+                    tl = __builtin_bit_cast(h8v, frag(P + PLANE + t * tstride));
+          const h8v qh = __builtin_bit_cast(h8v, ah), ql = __builtin_bit_cast(h8v, al);
+          acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc2[t], 0, 0, 0);
+          acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc2[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qh, acc[t], 0, 0, 0);
+        } else {
+          const bf8v qh = __builtin_bit_cast(bf8v, ah), qm = __builtin_bit_cast(bf8v, am),
+                     ql = __builtin_bit_cast(bf8v, al);
+          const bf8v th = frag(P + t * tstride), tm = frag(P + PLANE + t * tstride),
+                     tl = frag(P + 2 * PLANE + t * tstride);
+          // small terms first
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, ql, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qh, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qm, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh, acc[t], 0, 0, 0);
+        }
       }
-      // small terms first
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, ql, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qh, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qm, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh, acc[t], 0, 0, 0);
+      if (ks + 1 < nk) {
+        store_b(buf ^ 1, mode);
+        split_a(mode);
+      }
+      if constexpr ((XP & 16) == 0) __syncthreads();
     }
-    if (ks + 1 < nk) {
-      store_b(buf ^ 1);
-      split_a();
+  };
+
+  if constexpr (H2) {
+    kloop(S2{});
+    // Combine (one rounding) and vote: a non-finite sum means an operand of the
+    // page overflowed f16 (|x| >= 65520) or was itself inf/NaN; the page is then
+    // recomputed on the 3-way bf16 split, which covers the whole f32 range and
+    // propagates inf/NaN operands as the f32 product would.
+    bool bad = false;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        acc[t][r] = __builtin_fmaf(acc2[t][r], 0x1p-11f, acc[t][r]);
+        bad |= !(__builtin_fabsf(acc[t][r]) <= 3.40282347e38f);
+      }
+    if (bad) redo = 1;
+    __syncthreads();
+    if (redo) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+      kloop(S3{});
     }
-    if constexpr ((XP & 16) == 0) __syncthreads();
+  } else {
+    kloop(S3{});
   }
 
   scale_acc<DIV>(acc, g);
@@ -1119,19 +1212,21 @@ int launch_build_bf16(bool vec, const uint16_t* f1, const uint16_t* f2, OT* pyr,
   return dxr::launch_status();
 }
 
-// Split build (f32 class on bf16 MFMA) at 4 waves/SIMD (r01: 172 us at Sintel
-// against 177 at 3 and 183 at the compiler's choice).
+// Split build on the f16 pair split (H2; overflowing pages re-run on the 3-way
+// bf16 split) at 3 waves/SIMD: r02 Sintel 134-142 us against 151-154 for the
+// 3-way bf16 split at 4 waves/SIMD, and 0.4-0.8x its max error against f64
+// (scripts/xp_accuracy.py).
 template <typename OT, int BV, bool NHWC = false>
 int launch_split(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, int B,
                  hipStream_t stream) {
   const dim3 grid = build_grid(g, B);
   if (grid.y > 65535) return DXR_EINVAL;
   if (g.recip == 0.f)
-    hipLaunchKernelGGL((corr_build_split_kernel<OT, true, 4, BV, 0, NHWC>), grid, dim3(NT), 0,
-                       stream, f1, f2, pyr, g);
+    hipLaunchKernelGGL((corr_build_split_kernel<OT, true, 3, BV, 0, NHWC, true>), grid, dim3(NT),
+                       0, stream, f1, f2, pyr, g);
   else
-    hipLaunchKernelGGL((corr_build_split_kernel<OT, false, 4, BV, 0, NHWC>), grid, dim3(NT), 0,
-                       stream, f1, f2, pyr, g);
+    hipLaunchKernelGGL((corr_build_split_kernel<OT, false, 3, BV, 0, NHWC, true>), grid, dim3(NT),
+                       0, stream, f1, f2, pyr, g);
   return dxr::launch_status();
 }
 
@@ -1397,6 +1492,30 @@ extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t
     case 17: return xp_split<17>(f1, f2, pyr, g, (int)B, stream);
     case 21: return xp_split<21>(f1, f2, pyr, g, (int)B, stream);
     case 3 | 4: return xp_split<7>(f1, f2, pyr, g, (int)B, stream);
+    case 1002:
+      hipLaunchKernelGGL((corr_build_split_kernel<float, false, 2, 4, 0, false, true>),
+                         build_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);
+      return dxr::launch_status();
+    case 1003:
+      hipLaunchKernelGGL((corr_build_split_kernel<float, false, 3, 4, 0, false, true>),
+                         build_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);
+      return dxr::launch_status();
+    case 1012:
+      hipLaunchKernelGGL((corr_build_split_kernel<float, false, 2, 4, 0, false, true, true>),
+                         remap_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);
+      return dxr::launch_status();
+    case 1013:
+      hipLaunchKernelGGL((corr_build_split_kernel<float, false, 3, 4, 0, false, true, true>),
+                         remap_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);
+      return dxr::launch_status();
+    case 210:
+      hipLaunchKernelGGL((corr_build_split_kernel<float, false, 4, 4, 0, false, false, true>),
+                         remap_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);
+      return dxr::launch_status();
+    case 1001:
+      hipLaunchKernelGGL((corr_build_split_kernel<float, false, 2, 4, 1, false, true>),
+                         build_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);
+      return dxr::launch_status();
     case 200:
       hipLaunchKernelGGL((corr_build_split_kernel<float, false, 3, 4, 0>), build_grid(g, (int)B),
                          dim3(NT), 0, stream, f1, f2, pyr, g);
