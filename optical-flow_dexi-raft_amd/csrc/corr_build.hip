@@ -68,17 +68,20 @@ struct PageCoord {
 
 constexpr int STRIP = 8;
 
-template <bool REMAP>
+// QB: query blocks per workgroup (the grid walks groups of QB blocks; qblk is
+// the group's first block, page its first page).
+template <bool REMAP, int QB = 1>
 __device__ __forceinline__ PageCoord page_coord(const BuildGeom& g) {
   PageCoord c;
   const int T = g.tiles_w * g.tiles_h;
+  const int qtq = (g.qt + QB - 1) / QB;
   if constexpr (!REMAP) {
     c.txi = blockIdx.x % g.tiles_w;
     c.tyi = blockIdx.x / g.tiles_w;
-    c.qblk = blockIdx.y;
+    c.qblk = blockIdx.y * QB;
     c.b = blockIdx.z;
   } else {
-    const long long per_pair = (long long)g.qt * T;
+    const long long per_pair = (long long)qtq * T;
     const long long nwg = (long long)gridDim.x;
     const long long w = blockIdx.x;
     const long long q8 = nwg / 8, r8 = nwg % 8, xcd = w % 8;
@@ -87,15 +90,15 @@ __device__ __forceinline__ PageCoord page_coord(const BuildGeom& g) {
     long long rem = wl - c.b * per_pair;
     const int nfull = T / STRIP;
     int tile;
-    if (rem < (long long)nfull * g.qt * STRIP) {
-      const int st = (int)(rem / ((long long)g.qt * STRIP));
-      const int in = (int)(rem - (long long)st * g.qt * STRIP);
-      c.qblk = in / STRIP;
+    if (rem < (long long)nfull * qtq * STRIP) {
+      const int st = (int)(rem / ((long long)qtq * STRIP));
+      const int in = (int)(rem - (long long)st * qtq * STRIP);
+      c.qblk = in / STRIP * QB;
       tile = st * STRIP + in % STRIP;
     } else {
       const int nl = T - nfull * STRIP;
-      const int in = (int)(rem - (long long)nfull * g.qt * STRIP);
-      c.qblk = in / nl;
+      const int in = (int)(rem - (long long)nfull * qtq * STRIP);
+      c.qblk = in / nl * QB;
       tile = nfull * STRIP + in % nl;
     }
     c.txi = tile % g.tiles_w;
@@ -204,16 +207,20 @@ __device__ __forceinline__ OT to_out(float v) {
 
 // Store 8 consecutive values (two float4 read from LDS) as OT: 16 B of bf16 or
 // 2 x 16 B of f32.
-template <typename OT>
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+
+template <typename OT, int EX = 0>
 __device__ __forceinline__ void store8(OT* dst, const float* src) {
   const float4 a = f4(src), c = f4(src + 4);
   if constexpr (sizeof(OT) == 2) {
-    uint4 u;
+    u32x4v u;
     u.x = (uint32_t)to_out<OT>(a.x) | ((uint32_t)to_out<OT>(a.y) << 16);
     u.y = (uint32_t)to_out<OT>(a.z) | ((uint32_t)to_out<OT>(a.w) << 16);
     u.z = (uint32_t)to_out<OT>(c.x) | ((uint32_t)to_out<OT>(c.y) << 16);
     u.w = (uint32_t)to_out<OT>(c.z) | ((uint32_t)to_out<OT>(c.w) << 16);
-    *reinterpret_cast<uint4*>(dst) = u;
+    if constexpr ((EX & 2) != 0) __builtin_nontemporal_store(u, reinterpret_cast<u32x4v*>(dst));
+    else *reinterpret_cast<u32x4v*>(dst) = u;
   } else {
     *reinterpret_cast<float4*>(dst) = a;
     *reinterpret_cast<float4*>(dst + 4) = c;
@@ -231,7 +238,35 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 // `wave`: which 32 queries of the page this wave holds (and its private LDS
 // staging region).
-template <typename OT>
+// EX (experiments): bit 0 syncs only the wave around its private staging
+// region instead of the workgroup; bit 1 streams the pyramid with non-temporal
+// stores.
+template <int EX>
+__device__ __forceinline__ void epi_sync() {
+  if constexpr ((EX & 1) != 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
+}
+template <int EX>
+__device__ __forceinline__ void epi_st4(float* p, const float4 v) {
+  if constexpr ((EX & 2) != 0) {
+    const f32x4v w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<f32x4v*>(p));
+  } else {
+    *reinterpret_cast<float4*>(p) = v;
+  }
+}
+template <int EX, typename V>
+__device__ __forceinline__ void epi_stv(void* p, const V v) {
+  if constexpr ((EX & 2) != 0) __builtin_nontemporal_store(v, reinterpret_cast<V*>(p));
+  else *reinterpret_cast<V*>(p) = v;
+}
+
+template <typename OT, int EX = 0>
 __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT* __restrict__ pyr,
                                                const BuildGeom& g, long long page, int wave,
                                                int lane) {
@@ -252,23 +287,23 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
           st4(row + 2 * t * TW + 4 * c4, acc[t][4 * c4], acc[t][4 * c4 + 1],
               acc[t][4 * c4 + 2], acc[t][4 * c4 + 3]);
     }
-    __syncthreads();
+    epi_sync<EX>();
     if constexpr (sizeof(OT) == 4) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int qq = 2 * k + (lane >> 5);
         const int off = (lane & 31) * 4;
-        *reinterpret_cast<float4*>(pg0 + (r * 16 + qq) * NTGT + off) = f4(wl + qq * P0 + off);
+        epi_st4<EX>(pg0 + (r * 16 + qq) * NTGT + off, f4(wl + qq * P0 + off));
       }
     } else {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int qq = 4 * k + (lane >> 4);
         const int off = (lane & 15) * 8;
-        store8<OT>(pg0 + (r * 16 + qq) * NTGT + off, wl + qq * P0 + off);
+        store8<OT, EX>(pg0 + (r * 16 + qq) * NTGT + off, wl + qq * P0 + off);
       }
     }
-    __syncthreads();
+    epi_sync<EX>();
   }
   if (g.levels < 2) return;
 
@@ -298,7 +333,7 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
     for (int n = 0; n < 4; ++n)
       l2[u][n] = (((l1[0][2 * n] + l1[0][2 * n + 1]) + l1[1][2 * n]) + l1[1][2 * n + 1]) * 0.25f;
   }
-  __syncthreads();
+  epi_sync<EX>();
   {
     OT* pg1 = pyr + g.loff[1] + page * (BM * NTGT / 4) + (long long)wave * 32 * (NTGT / 4);
     if constexpr (sizeof(OT) == 4) {
@@ -306,14 +341,14 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
       for (int k = 0; k < 4; ++k) {
         const int qq = 8 * k + (lane >> 3);
         const int off = (lane & 7) * 4;
-        *reinterpret_cast<float4*>(pg1 + qq * 32 + off) = f4(wl + qq * P1 + off);
+        epi_st4<EX>(pg1 + qq * 32 + off, f4(wl + qq * P1 + off));
       }
     } else {
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         const int qq = 16 * k + (lane >> 2);
         const int off = (lane & 3) * 8;
-        store8<OT>(pg1 + qq * 32 + off, wl + qq * P1 + off);
+        store8<OT, EX>(pg1 + qq * 32 + off, wl + qq * P1 + off);
       }
     }
   }
@@ -323,12 +358,12 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
   {
     OT* pg2 = pyr + g.loff[2] + page * (BM * NTGT / 16) + (long long)wave * 32 * 8 + j * 8 + 4 * h;
     if constexpr (sizeof(OT) == 4) {
-      st4(pg2, l2[h][0], l2[h][1], l2[h][2], l2[h][3]);
+      epi_st4<EX>(pg2, make_float4(l2[h][0], l2[h][1], l2[h][2], l2[h][3]));
     } else {
-      uint2 w;
+      u32x2v w;
       w.x = (uint32_t)to_out<OT>(l2[h][0]) | ((uint32_t)to_out<OT>(l2[h][1]) << 16);
       w.y = (uint32_t)to_out<OT>(l2[h][2]) | ((uint32_t)to_out<OT>(l2[h][3]) << 16);
-      *reinterpret_cast<uint2*>(pg2) = w;
+      epi_stv<EX>(pg2, w);
     }
   }
   if (g.levels < 4) return;
@@ -658,7 +693,136 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_
     if (sum == 1234.5f) pyr[tid] = to_out<OT>(sum);  // keeps the K loop live
     return;
   }
-  paged_epilogue<OT>(acc, reinterpret_cast<float*>(smem), pyr, g, pc.page, wave, lane);
+  paged_epilogue<OT, (XP >> 5) & 3>(acc, reinterpret_cast<float*>(smem), pyr, g, pc.page, wave,
+                                    lane);
+}
+
+// ---------------------------------------------------------------------------
+// bf16 build, two query blocks per workgroup (8 waves: waves 0-3 hold queries
+// q0..q0+127, waves 4-7 the next 128, all of them the same 8x16 target tile).
+// The target tile is staged once for 256 queries, so a page costs 96 KB of
+// operand reads from L2 instead of 128 KB (KITTI B=8: the r02 ablations put the
+// 3.65 GB of operand re-reads at ~196 of 625 us).  Same MFMA tile per wave,
+// same products in the same order, same epilogue: bit-identical pages.
+// The epilogue syncs per wave (each wave stages through its own LDS region),
+// so a half whose query block is past the end (odd block count) just returns.
+// ---------------------------------------------------------------------------
+constexpr int STAGE_Q2 = 3 * BKH * PH;  // A0, A1, target images (bf16 elements)
+
+template <typename OT, bool DIV, int MINW, int XP = 0>
+__global__ __launch_bounds__(2 * NT, MINW) void corr_build_bf16_q2_kernel(
+    const uint16_t* __restrict__ f1, const uint16_t* __restrict__ f2, OT* __restrict__ pyr,
+    BuildGeom g) {
+  constexpr int LDS_E = 2 * WAVES * 16 * P0 * 4;   // epilogue bytes (8 waves)
+  constexpr int LDS_K = 2 * STAGE_Q2 * 2;          // two stages, bytes
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_K > LDS_E ? LDS_K : LDS_E];
+  uint16_t* lh = reinterpret_cast<uint16_t*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int half = wave >> 2, w4 = wave & 3;
+  const PageCoord pc = page_coord<true, 2>(g);
+  const int th0 = pc.tyi * TH, tw0 = pc.txi * TW;
+  const int q0 = pc.qblk * BM;                      // first of the two blocks
+  const long long fstride = (long long)g.D * g.N;
+  const uint16_t* f1b = f1 + pc.b * fstride;
+  const uint16_t* f2b = f2 + pc.b * fstride;
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  // Staging units of 4 bf16 (8 B): thread unit s covers idx = tid + 512 s;
+  // s = 0,1 -> image A0, 2,3 -> A1, 4,5 -> targets; u = idx & 1023 within the
+  // image: k = u >> 5, 4 consecutive queries / target cols (buffer loads,
+  // out-of-range units read zeros).  Host side guarantees D * N * 2 < 2^31.
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(f1b), (short)0, g.D * g.N * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(f2b), (short)0, g.D * g.N * 2, 0x00020000);
+  uint32_t vo[6];
+  int lo[6];
+#pragma unroll
+  for (int s = 0; s < 6; ++s) {
+    const int u = (tid + 2 * NT * s) & 1023, img = s >> 1;
+    const int k = u >> 5;
+    if (img < 2) {
+      const int q = q0 + img * BM + (u & 31) * 4;
+      vo[s] = q < g.N ? (uint32_t)(k * g.N + q) * 2u : 0x80000000u;
+      lo[s] = img * BKH * PH + k * PH + (u & 31) * 4;
+    } else {
+      const int r = (u >> 2) & 7, c = (u & 3) * 4, hh = th0 + r, ww = tw0 + c;
+      vo[s] = (hh < g.H && ww < g.W) ? (uint32_t)(k * g.N + hh * g.W + ww) * 2u : 0x80000000u;
+      lo[s] = 2 * BKH * PH + k * PH + tgt_col(r, c);
+    }
+  }
+  uint2 rr[6];
+  auto load = [&](int k0) {
+    if constexpr ((XP & 4) != 0) {
+      if (k0 > 0) return;
+    }
+    const int so = k0 * g.N * 2;
+#pragma unroll
+    for (int s = 0; s < 6; ++s)
+      rr[s] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(s < 4 ? rsa : rsb,
+                                                                              vo[s], so, 0));
+  };
+  auto store = [&](int buf) {
+    uint16_t* S = lh + buf * STAGE_Q2;
+#pragma unroll
+    for (int s = 0; s < 6; ++s) *reinterpret_cast<uint2*>(S + lo[s]) = rr[s];
+  };
+
+  const int li = lane & 15;
+  const int rd_off = (li >> 2) * PH + 4 * (li & 3) + 16 * ((lane >> 4) & 1) + 8 * (lane >> 5) * PH;
+  const int nk = (g.D + BKH - 1) / BKH;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) load((ks + 1) * BKH);
+    const uint16_t* A = lh + buf * STAGE_Q2 + half * BKH * PH;
+    const uint16_t* Bt = lh + buf * STAGE_Q2 + 2 * BKH * PH;
+#pragma unroll
+    for (int kk = 0; kk < BKH; kk += 16) {
+      const uint16_t* pa = A + kk * PH + rd_off + w4 * 32;
+      const s8v qv = __builtin_shufflevector(tr_read(pa), tr_read(pa + 4 * PH), 0, 1, 2, 3, 4, 5,
+                                             6, 7);
+      const bf8v qf = __builtin_bit_cast(bf8v, qv);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint16_t* pb = Bt + kk * PH + rd_off + t * 32;
+        const s8v tv = __builtin_shufflevector(tr_read(pb), tr_read(pb + 4 * PH), 0, 1, 2, 3, 4,
+                                               5, 6, 7);
+        if constexpr ((XP & 2) != 0) {
+          const s8v x = tv ^ qv;
+          acc[t][0] += (float)(x[0] + x[3] + x[5] + x[7]);
+        } else {
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8v, tv), qf, acc[t],
+                                                           0, 0, 0);
+        }
+      }
+    }
+    if (ks + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  if (pc.qblk + half >= g.qt) return;   // past the last query block: no page
+  scale_acc<DIV>(acc, g);
+  if constexpr ((XP & 1) != 0) {
+    float sum = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sum += acc[t][r];
+    if (sum == 1234.5f) pyr[tid] = to_out<OT>(sum);  // keeps the K loop live
+    return;
+  }
+  const long long page = pc.page + (long long)half * g.tiles_h * g.tiles_w;
+  paged_epilogue<OT, 1 | ((XP >> 5) & 2)>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0,
+                                          pyr, g, page, w4, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -1036,7 +1200,8 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     if (sum == 1234.5f) pyr[tid] = to_out<OT>(sum);  // keeps the K loop live
     return;
   }
-  paged_epilogue<OT>(acc, reinterpret_cast<float*>(smem), pyr, g, pc.page, wave, lane);
+  paged_epilogue<OT, (XP >> 5) & 3>(acc, reinterpret_cast<float*>(smem), pyr, g, pc.page, wave,
+                                    lane);
 }
 
 // Floor-mode 2x2 average pool of one pyramid level into the next, for levels
@@ -1155,9 +1320,10 @@ dim3 build_grid(const BuildGeom& g, int B) {
   return dim3((unsigned)(g.tiles_h * g.tiles_w), (unsigned)((g.N + BM - 1) / BM), (unsigned)B);
 }
 
-// 1-D grid of every page (REMAP launches).
-dim3 remap_grid(const BuildGeom& g, int B) {
-  return dim3((unsigned)((long long)B * g.qt * g.tiles_h * g.tiles_w));
+// 1-D grid of every page (REMAP launches), or of every group of QB pages along
+// queries.
+dim3 remap_grid(const BuildGeom& g, int B, int QB = 1) {
+  return dim3((unsigned)((long long)B * ((g.qt + QB - 1) / QB) * g.tiles_h * g.tiles_w));
 }
 
 // Exact-f32 build: VEC = float4 staging (W % 4 == 0, aligned) at 3 waves/SIMD
@@ -1441,6 +1607,13 @@ int xp_split(const float* f1, const float* f2, float* pyr, const BuildGeom& g, i
                      0, stream, f1, f2, pyr, g);
   return dxr::launch_status();
 }
+template <int XP>
+int xp_h2(const float* f1, const float* f2, float* pyr, const BuildGeom& g, int B,
+          hipStream_t stream) {
+  hipLaunchKernelGGL((corr_build_split_kernel<float, false, 3, 4, XP, false, true>),
+                     build_grid(g, B), dim3(NT), 0, stream, f1, f2, pyr, g);
+  return dxr::launch_status();
+}
 }  // namespace
 
 template <int XP>
@@ -1448,6 +1621,14 @@ int xp_bf16(const uint16_t* f1, const uint16_t* f2, uint16_t* pyr, const BuildGe
             hipStream_t stream) {
   hipLaunchKernelGGL((corr_build_bf16_kernel<true, uint16_t, false, 3, true, XP>), remap_grid(g, B),
                      dim3(NT), 0, stream, f1, f2, pyr, g);
+  return dxr::launch_status();
+}
+
+template <int XP, int MINW>
+int xp_bf16q2(const uint16_t* f1, const uint16_t* f2, uint16_t* pyr, const BuildGeom& g, int B,
+              hipStream_t stream) {
+  hipLaunchKernelGGL((corr_build_bf16_q2_kernel<uint16_t, false, MINW, XP>), remap_grid(g, B, 2),
+                     dim3(2 * NT), 0, stream, f1, f2, pyr, g);
   return dxr::launch_status();
 }
 
@@ -1467,6 +1648,15 @@ extern "C" int dxr_xp_build_bf16(const void* f1, const void* f2, int64_t B, int6
     case 3: return xp_bf16<3>(a, b, p, g, (int)B, stream);
     case 4: return xp_bf16<4>(a, b, p, g, (int)B, stream);
     case 5: return xp_bf16<5>(a, b, p, g, (int)B, stream);
+    case 100: return xp_bf16q2<0, 4>(a, b, p, g, (int)B, stream);
+    case 101: return xp_bf16q2<1, 4>(a, b, p, g, (int)B, stream);
+    case 104: return xp_bf16q2<4, 4>(a, b, p, g, (int)B, stream);
+    case 105: return xp_bf16q2<5, 4>(a, b, p, g, (int)B, stream);
+    case 130: return xp_bf16q2<0, 3>(a, b, p, g, (int)B, stream);
+    case 132: return xp_bf16<32>(a, b, p, g, (int)B, stream);
+    case 164: return xp_bf16<64>(a, b, p, g, (int)B, stream);
+    case 196: return xp_bf16<96>(a, b, p, g, (int)B, stream);
+    case 264: return xp_bf16q2<64, 4>(a, b, p, g, (int)B, stream);
     default: return DXR_EUNSUPPORTED;
   }
 }
@@ -1500,6 +1690,15 @@ extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t
       hipLaunchKernelGGL((corr_build_split_kernel<float, false, 3, 4, 0, false, true>),
                          build_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);
       return dxr::launch_status();
+    case 2001: return xp_h2<1>(f1, f2, pyr, g, (int)B, stream);
+    case 2032: return xp_h2<32>(f1, f2, pyr, g, (int)B, stream);
+    case 2064: return xp_h2<64>(f1, f2, pyr, g, (int)B, stream);
+    case 2096: return xp_h2<96>(f1, f2, pyr, g, (int)B, stream);
+    case 2003: return xp_h2<3>(f1, f2, pyr, g, (int)B, stream);
+    case 2005: return xp_h2<5>(f1, f2, pyr, g, (int)B, stream);
+    case 2017: return xp_h2<17>(f1, f2, pyr, g, (int)B, stream);
+    case 2002: return xp_h2<2>(f1, f2, pyr, g, (int)B, stream);
+    case 2004: return xp_h2<4>(f1, f2, pyr, g, (int)B, stream);
     case 1012:
       hipLaunchKernelGGL((corr_build_split_kernel<float, false, 2, 4, 0, false, true, true>),
                          remap_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);

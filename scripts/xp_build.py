@@ -34,7 +34,8 @@ def main():
     ap.add_argument("--xp", default="0,1,2,3,4,5,8,16,19")
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=7)
-    ap.add_argument("--check", default="", help="variants whose pyramid must equal xp 0's bit for bit")
+    ap.add_argument("--check", default="", help="variants whose pyramid must equal --ref's bit for bit")
+    ap.add_argument("--ref", type=int, default=0, help="reference variant of --check")
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"],
                     help="bf16: the bf16 build (dxr_xp_build_bf16) instead of the split build")
     a = ap.parse_args()
@@ -66,7 +67,7 @@ def main():
     ref = None
     if a.check:
         pyr.fill_(float("nan"))
-        launch(0)
+        launch(a.ref)
         torch.cuda.synchronize()
         ref = pyr.clone()
         for xp in (int(x) for x in a.check.split(",")):
@@ -75,7 +76,7 @@ def main():
             torch.cuda.synchronize()
             same = torch.equal(pyr, ref)
             diff = (pyr - ref).abs().nan_to_num(nan=float("inf")).max().item()
-            print(json.dumps({"xp": xp, "bit_identical_to_xp0": same, "max_abs_diff": diff}),
+            print(json.dumps({"xp": xp, "ref": a.ref, "bit_identical_to_ref": same, "max_abs_diff": diff}),
                   flush=True)
     for xp in xps:
         launch(xp)
