@@ -706,6 +706,8 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_
 // same products in the same order, same epilogue: bit-identical pages.
 // The epilogue syncs per wave (each wave stages through its own LDS region),
 // so a half whose query block is past the end (odd block count) just returns.
+// r02, KITTI B=8: 556 us per build against 619 for one query block per
+// workgroup (both with their r02 epilogues; K loop alone 295 vs 391 us).
 // ---------------------------------------------------------------------------
 constexpr int STAGE_Q2 = 3 * BKH * PH;  // A0, A1, target images (bf16 elements)
 
@@ -821,8 +823,11 @@ __global__ __launch_bounds__(2 * NT, MINW) void corr_build_bf16_q2_kernel(
     return;
   }
   const long long page = pc.page + (long long)half * g.tiles_h * g.tiles_w;
-  paged_epilogue<OT, 1 | ((XP >> 5) & 2)>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0,
-                                          pyr, g, page, w4, lane);
+  // non-temporal pyramid stores (KITTI B=8: 556 vs 606 us; the 1.13 GB pyramid
+  // outgrows the caches anyway); XP bit 6 turns them off
+  constexpr int EX = (XP & 64) ? 1 : 3;
+  paged_epilogue<OT, EX>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0, pyr, g, page,
+                         w4, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -1200,8 +1205,12 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     if (sum == 1234.5f) pyr[tid] = to_out<OT>(sum);  // keeps the K loop live
     return;
   }
-  paged_epilogue<OT, (XP >> 5) & 3>(acc, reinterpret_cast<float*>(smem), pyr, g, pc.page, wave,
-                                    lane);
+  // Wave-local syncs around the per-wave staging (r02: -2 % per Sintel step);
+  // XP bit 5 restores workgroup barriers, bit 6 adds non-temporal stores
+  // (faster build alone, no faster step: the lookups then read the pyramid
+  // from HBM instead of the caches).
+  constexpr int EX = ((XP & 32) ? 0 : 1) | ((XP & 64) ? 2 : 0);
+  paged_epilogue<OT, EX>(acc, reinterpret_cast<float*>(smem), pyr, g, pc.page, wave, lane);
 }
 
 // Floor-mode 2x2 average pool of one pyramid level into the next, for levels
@@ -1361,13 +1370,14 @@ int launch_build_bf16(bool vec, const uint16_t* f1, const uint16_t* f2, OT* pyr,
   if (grid.y > 65535) return DXR_EINVAL;
   const bool div = g.recip == 0.f;
   if (vec) {
-    const dim3 rg = remap_grid(g, B);
+    // two query blocks per workgroup, XCD-banded group order
+    const dim3 rg = remap_grid(g, B, 2);
     if (div)
-      hipLaunchKernelGGL((corr_build_bf16_kernel<true, OT, true, 3, true>), rg, dim3(NT), 0, stream,
-                         f1, f2, pyr, g);
+      hipLaunchKernelGGL((corr_build_bf16_q2_kernel<OT, true, 4>), rg, dim3(2 * NT), 0, stream, f1,
+                         f2, pyr, g);
     else
-      hipLaunchKernelGGL((corr_build_bf16_kernel<true, OT, false, 3, true>), rg, dim3(NT), 0,
-                         stream, f1, f2, pyr, g);
+      hipLaunchKernelGGL((corr_build_bf16_q2_kernel<OT, false, 4>), rg, dim3(2 * NT), 0, stream, f1,
+                         f2, pyr, g);
   } else if (div) {
     hipLaunchKernelGGL((corr_build_bf16_kernel<false, OT, true, 0, false>), grid, dim3(NT), 0,
                        stream, f1, f2, pyr, g);

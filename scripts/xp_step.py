@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--xp", default="1003,2032,2096")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"],
+                    help="bf16: dxr_xp_build_bf16 variants, bf16 fmaps and pyramid")
     a = ap.parse_args()
     import dexiraft_amd
     nat = dexiraft_amd._native
@@ -40,6 +42,10 @@ def main():
     vp, i64 = ctypes.c_void_p, ctypes.c_int64
     lib.dxr_xp_build.restype = ctypes.c_int
     lib.dxr_xp_build.argtypes = [vp, vp, i64, i64, i64, i64, vp, ctypes.c_int, vp]
+    lib.dxr_xp_build_bf16.restype = ctypes.c_int
+    lib.dxr_xp_build_bf16.argtypes = [vp, vp, i64, i64, i64, i64, vp, ctypes.c_int, vp]
+    bf = a.dtype == "bf16"
+    xbuild = lib.dxr_xp_build_bf16 if bf else lib.dxr_xp_build
     lib.dxr_corr_lookup.restype = ctypes.c_int
     lib.dxr_corr_lookup.argtypes = [vp, ctypes.c_int, i64, i64, i64, ctypes.c_int, ctypes.c_int, vp,
                                     vp, vp]
@@ -49,23 +55,26 @@ def main():
     g.manual_seed(0)
     f1 = torch.randn((B, D, H, W), generator=g, device=dev)
     f2 = torch.randn((B, D, H, W), generator=g, device=dev)
+    if bf:
+        f1, f2 = f1.bfloat16(), f2.bfloat16()
     ys, xs = torch.meshgrid(torch.arange(H, device=dev, dtype=torch.float32),
                             torch.arange(W, device=dev, dtype=torch.float32), indexing="ij")
     grid = torch.stack([xs, ys])[None].repeat(B, 1, 1, 1)
     coords = [grid + 4.0 * torch.randn(grid.shape, generator=g, device=dev) for _ in range(12)]
-    pyr = torch.empty(nat.load().dxr_pyramid_numel(B, H, W, 4), device=dev)
+    pyr = torch.empty(nat.load().dxr_pyramid_numel(B, H, W, 4), device=dev,
+                      dtype=torch.bfloat16 if bf else torch.float32)
     out = torch.empty((B, 324, H, W), device=dev)
     xps = [int(x) for x in a.xp.split(",")]
     side = torch.cuda.Stream()
 
     def build(xp, s):
-        st = lib.dxr_xp_build(f1.data_ptr(), f2.data_ptr(), B, D, H, W, pyr.data_ptr(), xp, s)
+        st = xbuild(f1.data_ptr(), f2.data_ptr(), B, D, H, W, pyr.data_ptr(), xp, s)
         assert st == 0, (xp, st)
 
     def lookups(s):
         for c in coords:
-            st = lib.dxr_corr_lookup(pyr.data_ptr(), 0, B, H, W, 4, 4, c.data_ptr(), out.data_ptr(),
-                                     s)
+            st = lib.dxr_corr_lookup(pyr.data_ptr(), 1 if bf else 0, B, H, W, 4, 4, c.data_ptr(),
+                                     out.data_ptr(), s)
             assert st == 0, st
 
     graphs = {}
