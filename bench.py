@@ -95,6 +95,8 @@ def build_kernel(dtype, H, W):
     f32 accumulators), so its binding ceiling is 2.5 PF / 3 = 833 TF
     f32-equivalent; the f32 peak (157.3 TF) is §8(d)'s."""
     if dtype == "bf16":
+        if W % 4 == 0:   # the two-query-block form (float4-aligned rows)
+            return "corr_build_bf16_q2_kernel", 1, PEAK_BF16_TFLOPS, "bf16"
         return "corr_build_bf16_kernel", 1, PEAK_BF16_TFLOPS, "bf16"
     if D % 16 == 0 and W % 2 == 0:
         return ("corr_build_split_kernel (f32 operands as f16 pairs hi + 2^-11 lo, "

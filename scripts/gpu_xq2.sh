@@ -1,6 +1,8 @@
-# Full-step A/B: bf16 KITTI B=8 build variants (q2 with / without non-temporal stores, one-block kernel).
+# Lookup tap-span staging A/B (xp 0 = product, xp 8 = full 11x16 staging), bit-checked; then parity.
 set -o pipefail
-O=gpurun_out/xq4.log
+O=gpurun_out/xq5.log
 : > $O
-timeout -k 10 200 python -u scripts/xp_step.py --dtype bf16 --B 8 --H 47 --W 156 --steps 5 --xp 0,100,264 >> $O 2>&1 || exit $?
-timeout -k 10 150 python -u scripts/xp_step.py --xp 1003,2032,2064 >> $O 2>&1 || exit $?
+timeout -k 10 120 python -u scripts/xp_lookup.py --xp 0,8 --check 8 >> $O 2>&1 || exit $?
+timeout -k 10 120 python -u scripts/xp_lookup.py --B 8 --xp 0,8 --check 8 >> $O 2>&1 || exit $?
+timeout -k 10 120 python -u scripts/xp_lookup.py --B 8 --H 47 --W 156 --dtype bf16 --xp 0,8 --check 8 >> $O 2>&1 || exit $?
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider >> $O 2>&1 || exit $?
