@@ -22,6 +22,8 @@
 // 256-byte wave stores along the query dimension.
 #include <cstdint>
 
+#include <type_traits>
+
 #include "dxr_common.h"
 
 namespace {
@@ -222,15 +224,41 @@ __device__ __forceinline__ void alt_split8(const float (&x)[8], uint4& h, uint4&
   l = make_uint4(ll[0], ll[1], ll[2], ll[3]);
 }
 
-template <int R, int NRB, int CMAX>
-__global__ __launch_bounds__(256, 2) void alt_corr_mfma_kernel(const float* __restrict__ f1,
+// f16 pair split of 8 floats (csrc/corr_build.hip split2h): x = hi + 2^-11 lo,
+// hi = RNE_f16(x), lo = RNE_f16((x - hi) * 2^11); valid while |x| < 65520.
+typedef _Float16 ah2 __attribute__((ext_vector_type(2)));
+typedef _Float16 ah8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ uint32_t alt_cvt_pk_h(float a, float b) {
+  const af2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, ah2));
+}
+__device__ __forceinline__ void alt_split8h(const float (&x)[8], uint4& h, uint4& l) {
+  uint32_t hh[4], ll[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float a = x[2 * e], b = x[2 * e + 1];
+    hh[e] = alt_cvt_pk_h(a, b);
+    const ah2 hv = __builtin_bit_cast(ah2, hh[e]);
+    ll[e] = alt_cvt_pk_h((a - (float)hv[0]) * 2048.f, (b - (float)hv[1]) * 2048.f);
+  }
+  h = make_uint4(hh[0], hh[1], hh[2], hh[3]);
+  l = make_uint4(ll[0], ll[1], ll[2], ll[3]);
+}
+
+// H2: the f16 pair split (3 f16 products, cross terms in a second accumulator),
+// as the split build; a chunk whose sums are not finite (an operand beyond f16
+// range, or inf/NaN) is recomputed by its wave on the 3-way bf16 split, with
+// the query operand split from fmap1 in registers.
+template <int R, int NRB, int CMAX, bool H2 = false, int MINW = 2>
+__global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* __restrict__ f1,
                                                                const float* __restrict__ coords,
                                                                float* __restrict__ out,
                                                                AltGeom g, int W1, int tiles_x) {
   constexpr int RD = 2 * R + 1, RD1 = RD + 1, NCELL = RD1 * RD1;
   constexpr int CHUNK = 4 * 32 * NRB;                       // box cells per chunk
   constexpr int KB = CMAX / 8;                              // 8-channel blocks
-  __shared__ __attribute__((aligned(16))) uint4 qplanes[3 * KB * TQ];   // [plane][kb][q]
+  constexpr int NPL = H2 ? 2 : 3;                           // query operand planes
+  __shared__ __attribute__((aligned(16))) uint4 qplanes[NPL * KB * TQ]; // [plane][kb][q]
   __shared__ float S[TQ * NCELL];                           // window dot products
   __shared__ int4 qinfo[TQ];                                // {x0, y0, live, -}
   __shared__ int box[4];                                    // bx0, by0, bw, bh
@@ -297,11 +325,18 @@ __global__ __launch_bounds__(256, 2) void alt_corr_mfma_kernel(const float* __re
     const float4 a = *reinterpret_cast<const float4*>(src);
     const float4 c = *reinterpret_cast<const float4*>(src + 4);
     const float x[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
-    uint4 h, m, l;
-    alt_split8(x, h, m, l);
-    qplanes[(0 * KB + kb) * TQ + qq] = h;
-    qplanes[(1 * KB + kb) * TQ + qq] = m;
-    qplanes[(2 * KB + kb) * TQ + qq] = l;
+    if constexpr (H2) {
+      uint4 h, l;
+      alt_split8h(x, h, l);
+      qplanes[(0 * KB + kb) * TQ + qq] = h;
+      qplanes[(1 * KB + kb) * TQ + qq] = l;
+    } else {
+      uint4 h, m, l;
+      alt_split8(x, h, m, l);
+      qplanes[(0 * KB + kb) * TQ + qq] = h;
+      qplanes[(1 * KB + kb) * TQ + qq] = m;
+      qplanes[(2 * KB + kb) * TQ + qq] = l;
+    }
   }
   __syncthreads();
 
@@ -314,55 +349,109 @@ __global__ __launch_bounds__(256, 2) void alt_corr_mfma_kernel(const float* __re
     const float* src[NRB];
 #pragma unroll
     for (int rb = 0; rb < NRB; ++rb) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[rb][r] = 0.f;
       // A operand lane -> cell c0 + 32 (wave NRB + rb) + j, channels 8 kh .. + 8 per k16
       const int c = min(c0 + (wave * NRB + rb) * 32 + j, ncells - 1);
       const int cy = c / bw, cx = c - cy * bw;
       src[rb] = f2b + ((long long)(by0 + cy) * lv.W2 + bx0 + cx) * g.C + 8 * kh;
     }
     // cell vectors one k step ahead in registers
-    float4 ca[NRB], cb[NRB];
+    auto kloop = [&](auto h2tag) {
+      constexpr bool M2 = decltype(h2tag)::value;
+      af16 acc2[NRB];
 #pragma unroll
-    for (int rb = 0; rb < NRB; ++rb) {
-      ca[rb] = *reinterpret_cast<const float4*>(src[rb]);
-      cb[rb] = *reinterpret_cast<const float4*>(src[rb] + 4);
-    }
-    for (int ks = 0; ks < nkb / 2; ++ks) {
-      float4 na[NRB], nb[NRB];
-      if (ks + 1 < nkb / 2) {
+      for (int rb = 0; rb < NRB; ++rb)
 #pragma unroll
-        for (int rb = 0; rb < NRB; ++rb) {
-          na[rb] = *reinterpret_cast<const float4*>(src[rb] + (ks + 1) * 16);
-          nb[rb] = *reinterpret_cast<const float4*>(src[rb] + (ks + 1) * 16 + 4);
-        }
-      }
-      const abf8 qh = __builtin_bit_cast(abf8, qplanes[(0 * KB + 2 * ks + kh) * TQ + j]);
-      const abf8 qm = __builtin_bit_cast(abf8, qplanes[(1 * KB + 2 * ks + kh) * TQ + j]);
-      const abf8 ql = __builtin_bit_cast(abf8, qplanes[(2 * KB + 2 * ks + kh) * TQ + j]);
+        for (int r = 0; r < 16; ++r) acc[rb][r] = acc2[rb][r] = 0.f;
+      float4 ca[NRB], cb[NRB];
 #pragma unroll
       for (int rb = 0; rb < NRB; ++rb) {
-        const float4 a = ca[rb], b = cb[rb];
-        const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-        uint4 h, m, l;
-        alt_split8(x, h, m, l);
-        const abf8 th = __builtin_bit_cast(abf8, h), tm = __builtin_bit_cast(abf8, m),
-                   tl = __builtin_bit_cast(abf8, l);
-        // small terms first
-        acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm, acc[rb], 0, 0, 0);
-        acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh, acc[rb], 0, 0, 0);
-        acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, ql, acc[rb], 0, 0, 0);
-        acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qh, acc[rb], 0, 0, 0);
-        acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qm, acc[rb], 0, 0, 0);
-        acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh, acc[rb], 0, 0, 0);
+        ca[rb] = *reinterpret_cast<const float4*>(src[rb]);
+        cb[rb] = *reinterpret_cast<const float4*>(src[rb] + 4);
       }
-      if (ks + 1 < nkb / 2) {
+      // fallback form: this lane's query operand straight from fmap1
+      const int fqy = min(ty * TQY + j / TQX, H1 - 1), fqx = min(tx * TQX + j % TQX, W1 - 1);
+      const float* qsrc = f1b + (long long)(fqy * W1 + fqx) * g.C + 8 * kh;
+      for (int ks = 0; ks < nkb / 2; ++ks) {
+        float4 na[NRB], nb[NRB];
+        if (ks + 1 < nkb / 2) {
 #pragma unroll
-        for (int rb = 0; rb < NRB; ++rb) {
-          ca[rb] = na[rb];
-          cb[rb] = nb[rb];
+          for (int rb = 0; rb < NRB; ++rb) {
+            na[rb] = *reinterpret_cast<const float4*>(src[rb] + (ks + 1) * 16);
+            nb[rb] = *reinterpret_cast<const float4*>(src[rb] + (ks + 1) * 16 + 4);
+          }
+        }
+        if constexpr (M2) {
+          const ah8 qh = __builtin_bit_cast(ah8, qplanes[(0 * KB + 2 * ks + kh) * TQ + j]);
+          const ah8 ql = __builtin_bit_cast(ah8, qplanes[(1 * KB + 2 * ks + kh) * TQ + j]);
+#pragma unroll
+          for (int rb = 0; rb < NRB; ++rb) {
+            const float4 a = ca[rb], b = cb[rb];
+            const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+            uint4 h, l;
+            alt_split8h(x, h, l);
+            const ah8 th = __builtin_bit_cast(ah8, h), tl = __builtin_bit_cast(ah8, l);
+            acc2[rb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc2[rb], 0, 0, 0);
+            acc2[rb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc2[rb], 0, 0, 0);
+            acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qh, acc[rb], 0, 0, 0);
+          }
+        } else {
+          abf8 qh, qm, ql;
+          if constexpr (H2) {     // fallback: split the query operand here
+            const float4 u = *reinterpret_cast<const float4*>(qsrc + ks * 16);
+            const float4 w = *reinterpret_cast<const float4*>(qsrc + ks * 16 + 4);
+            const float x[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
+            uint4 h, m, l;
+            alt_split8(x, h, m, l);
+            qh = __builtin_bit_cast(abf8, h);
+            qm = __builtin_bit_cast(abf8, m);
+            ql = __builtin_bit_cast(abf8, l);
+          } else {
+            qh = __builtin_bit_cast(abf8, qplanes[(0 * KB + 2 * ks + kh) * TQ + j]);
+            qm = __builtin_bit_cast(abf8, qplanes[(1 * KB + 2 * ks + kh) * TQ + j]);
+            ql = __builtin_bit_cast(abf8, qplanes[(2 * KB + 2 * ks + kh) * TQ + j]);
+          }
+#pragma unroll
+          for (int rb = 0; rb < NRB; ++rb) {
+            const float4 a = ca[rb], b = cb[rb];
+            const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+            uint4 h, m, l;
+            alt_split8(x, h, m, l);
+            const abf8 th = __builtin_bit_cast(abf8, h), tm = __builtin_bit_cast(abf8, m),
+                       tl = __builtin_bit_cast(abf8, l);
+            // small terms first
+            acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm, acc[rb], 0, 0, 0);
+            acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh, acc[rb], 0, 0, 0);
+            acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, ql, acc[rb], 0, 0, 0);
+            acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qh, acc[rb], 0, 0, 0);
+            acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qm, acc[rb], 0, 0, 0);
+            acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh, acc[rb], 0, 0, 0);
+          }
+        }
+        if (ks + 1 < nkb / 2) {
+#pragma unroll
+          for (int rb = 0; rb < NRB; ++rb) {
+            ca[rb] = na[rb];
+            cb[rb] = nb[rb];
+          }
         }
       }
+      if constexpr (M2) {
+#pragma unroll
+        for (int rb = 0; rb < NRB; ++rb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[rb][r] = __builtin_fmaf(acc2[rb][r], 0x1p-11f, acc[rb][r]);
+      }
+    };
+    if constexpr (H2) {
+      kloop(std::integral_constant<bool, true>{});
+      bool bad = false;
+#pragma unroll
+      for (int rb = 0; rb < NRB; ++rb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bad |= !(__builtin_fabsf(acc[rb][r]) <= 3.40282347e38f);
+      if (__ballot(bad) != 0) kloop(std::integral_constant<bool, false>{});   // wave-uniform
+    } else {
+      kloop(std::integral_constant<bool, false>{});
     }
     // keep the entries inside query j's window: D row = (r & 3) + 8 (r >> 2) + 4 kh
     if (qi.z) {
@@ -1216,6 +1305,18 @@ extern "C" int dxr_xp_alt(const float* fmap1, const float* const* fmap2_levels, 
   if (xp == 0) return launch_alt_mfma_r<4, 1>(fmap1, coords, out, g, num_levels, (int)B, (int)W, stream);
   if (xp == 1) return xp_alt16<2>(fmap1, coords, out, g, num_levels, (int)B, (int)W, stream);
   if (xp == 2) return xp_alt16<1>(fmap1, coords, out, g, num_levels, (int)B, (int)W, stream);
+  if (xp == 6 || xp == 7) {
+    const int H1 = g.N / (int)W;
+    const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
+    const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
+    if (xp == 6)
+      hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3>), grid, dim3(256), 0, stream,
+                         fmap1, coords, out, g, (int)W, tiles_x);
+    else
+      hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 2>), grid, dim3(256), 0, stream,
+                         fmap1, coords, out, g, (int)W, tiles_x);
+    return dxr::launch_status();
+  }
   if (xp == 3 || xp == 4 || xp == 5) {
     const int H1 = g.N / (int)W;
     const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
