@@ -187,9 +187,10 @@ __global__ __launch_bounds__(256) void alt_corr_kernel(const float* __restrict__
 // query's own window.  Every fmap2 cell vector is then read once per workgroup
 // instead of once per query (the per-query form above re-reads 100 cell vectors
 // per query: 6.7 GB per 1080p lookup, 1.37 ms).  f32 class: both operands are
-// split exactly into hi/mid/lo bf16 (as the split build, csrc/corr_build.hip)
-// and six bf16 products are accumulated in f32; the query planes are split once
-// into LDS, cell vectors in registers as they arrive (one k step ahead).  Box
+// split into f16 pairs (H2, as the split build, csrc/corr_build.hip; r01: a 3-way
+// bf16 split with six products, still the overflow fallback) and accumulated in
+// f32; the query planes are split once into LDS, cell vectors in registers as
+// they arrive (one k step ahead).  Box
 // cells are walked in chunks of 4 waves x 32*NRB.  The bilinear combination and
 // the output follow the per-query form exactly.
 // ---------------------------------------------------------------------------
@@ -876,8 +877,9 @@ int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const Al
   const int tiles_x = (W1 + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
   const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)levels, (unsigned)Z);
   if (g.C > 256) return DXR_EUNSUPPORTED;
-  hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256>), grid, dim3(256), 0, stream, f1, coords,
-                     out, g, W1, tiles_x);
+  // f16 pair split (r02, 1080p: 227 vs 275 us for the 3-way bf16 split), 3 workgroups/CU
+  hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 3>), grid, dim3(256), 0, stream, f1,
+                     coords, out, g, W1, tiles_x);
   return dxr::launch_status();
 }
 
@@ -1305,6 +1307,22 @@ extern "C" int dxr_xp_alt(const float* fmap1, const float* const* fmap2_levels, 
   if (xp == 0) return launch_alt_mfma_r<4, 1>(fmap1, coords, out, g, num_levels, (int)B, (int)W, stream);
   if (xp == 1) return xp_alt16<2>(fmap1, coords, out, g, num_levels, (int)B, (int)W, stream);
   if (xp == 2) return xp_alt16<1>(fmap1, coords, out, g, num_levels, (int)B, (int)W, stream);
+  if (xp == 8) {
+    const int H1 = g.N / (int)W;
+    const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
+    const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
+    hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 2, 256, true, 3>), grid, dim3(256), 0, stream,
+                       fmap1, coords, out, g, (int)W, tiles_x);
+    return dxr::launch_status();
+  }
+  if (xp == 9) {   // the r01 form: 3-way bf16 split, 2 workgroups/CU
+    const int H1 = g.N / (int)W;
+    const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
+    const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
+    hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, false, 2>), grid, dim3(256), 0, stream,
+                       fmap1, coords, out, g, (int)W, tiles_x);
+    return dxr::launch_status();
+  }
   if (xp == 6 || xp == 7) {
     const int H1 = g.N / (int)W;
     const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;

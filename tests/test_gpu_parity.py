@@ -270,6 +270,34 @@ def test_alternate_block_matches_oracle(dx, shape):
     tolerance_check(got, ref, RTOL)
 
 
+def test_alternate_block_overflow_fallback(dx):
+    """The on-the-fly kernel's f16 pair split covers |x| < 65520; a chunk whose sums
+    are not finite is recomputed on the 3-way bf16 split.  Operands of 1e5 (a whole
+    query pixel) and 3e6 (one target channel) stay f32-class per query, and a NaN
+    query yields NaN outputs for that query only, as the reference's f32 kernel."""
+    B, D, H, W = 1, 64, 24, 32
+    f1 = dg.fmap(65, B, D, H, W)
+    f2 = dg.fmap(66, B, D, H, W)
+    f1[0, :, 5, 7] *= 1.0e5
+    f2[0, 3, 10, 12] = 3.0e6
+    c = dg.coords(67, B, H, W, "normal", 3.0)
+    ref = oracle.alt_corr_block(f1, f2, c, 4, 4, np.float64)
+    got = dx.AlternateCorrBlock(_t(f1), _t(f2), radius=4)(_t(c)).cpu().numpy()
+    assert np.isfinite(got).all()
+    scale = np.abs(ref).max(axis=1, keepdims=True) + 1e-30      # per query pixel
+    assert (np.abs(got - ref) <= 1e-4 * scale).all()
+    assert np.abs(got[0, :, 5, 7]).max() > 1.0e4                 # the scaled query itself
+    f1[0, 0, 2, 3] = np.nan
+    ref = oracle.alt_corr_block(f1, f2, c, 4, 4, np.float64)
+    got = dx.AlternateCorrBlock(_t(f1), _t(f2), radius=4)(_t(c)).cpu().numpy()
+    nan_ref = np.isnan(ref)
+    assert np.isnan(got[0, :, 2, 3]).any()
+    fin = ~nan_ref
+    assert np.isfinite(got[fin]).all()
+    scale = np.broadcast_to(np.nanmax(np.abs(ref), axis=1, keepdims=True), ref.shape)
+    assert (np.abs(got[fin] - ref[fin]) <= 1e-4 * scale[fin] + 1e-30).all()
+
+
 def test_alt_cuda_corr_forward_ffi(dx):
     """Reference FFI form: NHWC fmaps, [B, N, H, W, 2] coords, H2 != H1."""
     B, H1, W1, H2, W2, C, N, r = 2, 9, 13, 7, 11, 64, 2, 3
