@@ -1,0 +1,21 @@
+#!/bin/bash
+# PMC passes on the on-the-fly kernel (experiments lib via scripts/xp_alt.py), one counter group per run.
+set -u
+TAG=${1:-pmc_alt}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+i=0
+for P in "SQ_WAIT_INST_LDS SQ_INSTS_MFMA SQ_VALU_MFMA_COEXEC_CYCLES SQ_LDS_IDX_ACTIVE SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU GRBM_GUI_ACTIVE" \
+         "TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCR_TCP_STALL_CYCLES_sum TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum GRBM_GUI_ACTIVE GRBM_TA_BUSY" \
+         "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  N=p${i}
+  timeout -s KILL 90 rocprofv3 --pmc $P --kernel-include-regex "alt_corr_mfma" --output-format csv \
+    -d "$PWD/$OUT/$N" -o run -- python -u scripts/xp_alt.py --xp 0 --rounds 1 > "$OUT/$N.log" 2>&1
+  rc=$?; echo "== pmc $N rc=$rc"; tail -n 2 "$OUT/$N.log"
+  find "$OUT/$N" -name '*counter_collection.csv' -exec cp {} "$OUT/$N.csv" \;
+  rm -rf "$OUT/$N"
+  [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+done
+echo "== done"
