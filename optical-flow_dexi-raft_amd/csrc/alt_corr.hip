@@ -497,6 +497,266 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
 }
 
 #ifdef DXR_EXPERIMENTS
+// ---------------------------------------------------------------------------
+// Large-tile on-the-fly form (experiment): an 8 x 16 query tile (128 queries) per
+// workgroup.  Bit-identical to alt_corr_mfma_kernel but slower at 1080p (253 vs
+// 228 us at 2 waves/SIMD, 256 VGPRs; 482 us at 1): each level-0 workgroup walks
+// ~23 chunks x 16 barrier-separated k steps with one step of prefetch, a longer
+// latency chain than the ~2.8x fewer cell loads save.
+// The union box of 128 windows is ~2.8x fewer cells per query than the 4 x 8
+// form's (level 0, N(0, 4^2) flows: ~1,430 cells for 128 queries against ~1,000
+// for 32), and its cells are loaded once for all four waves: per k step the
+// workgroup stages a 64-cell chunk slab (64 cells x 16 channels, 4 lanes per
+// 64-byte slab: whole segments) split into f16 pairs in LDS, and each wave
+// multiplies it with its own 32 queries, whose f16-pair operands (all C <= 256
+// channels) stay in registers for the workgroup's life.  Same products in the
+// same order as alt_corr_mfma_kernel (H2): bit-identical window sums; same
+// per-wave 3-way bf16 fallback for non-finite chunks (from global memory).
+// ---------------------------------------------------------------------------
+constexpr int T2Y = 8, T2X = 16, T2Q = T2Y * T2X;    // query tile (128 pixels)
+
+// f16 pair split of 4 floats into two f16x2 words each (hi, lo)
+__device__ __forceinline__ void alt_split4h(const float4 a, uint2& h, uint2& l) {
+  const float x[4] = {a.x, a.y, a.z, a.w};
+  uint32_t hh[2], ll[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    hh[e] = alt_cvt_pk_h(x[2 * e], x[2 * e + 1]);
+    const ah2 hv = __builtin_bit_cast(ah2, hh[e]);
+    ll[e] = alt_cvt_pk_h((x[2 * e] - (float)hv[0]) * 2048.f, (x[2 * e + 1] - (float)hv[1]) * 2048.f);
+  }
+  h = make_uint2(hh[0], hh[1]);
+  l = make_uint2(ll[0], ll[1]);
+}
+
+template <int R, int MINW = 2>
+__global__ __launch_bounds__(256, MINW) void alt_corr_tile_kernel(const float* __restrict__ f1,
+                                                                  const float* __restrict__ coords,
+                                                                  float* __restrict__ out,
+                                                                  AltGeom g, int W1, int tiles_x) {
+  constexpr int RD = 2 * R + 1, RD1 = RD + 1, NCELL = RD1 * RD1;
+  constexpr int CH = 64;                       // box cells per chunk (two 32-row MFMA tiles)
+  constexpr int PN = 24;                       // LDS pitch (f16) of a staged cell slab
+  constexpr int PLANE = CH * PN;
+  __shared__ float S[T2Q * NCELL];             // window dot products
+  __shared__ __attribute__((aligned(16))) uint16_t cst[2][2][PLANE];   // [buf][hi, lo][cell][k]
+  __shared__ int4 qinfo[T2Q];                  // {x0, y0, live, -}
+  __shared__ int boxp[2][4];                   // per-wave partial boxes (waves 0, 1)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int tile = blockIdx.x;
+  {
+    const int n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = tile % 8;
+    tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + tile / 8;
+  }
+  const int tx = tile % tiles_x, ty = tile / tiles_x;
+  const AltLevel lv = g.lv[blockIdx.y];
+  const int z = blockIdx.z, bf = z / g.Nc;
+  const float* cz = coords + (long long)z * g.coord_zstride;
+  const float* f1b = f1 + (long long)bf * g.f1_bstride;
+  const float* f2b = lv.f2 + (long long)bf * lv.H2 * lv.W2 * g.C;
+  const int H1 = g.N / W1;
+  const int nks = g.C / 16;
+
+  // query index qi = 32 w + j: wave w holds the 4 x 8 sub-tile (w >> 1, w & 1)
+  auto qpos = [&](int qi, int& qy, int& qx) {
+    const int w = qi >> 5, jj = qi & 31;
+    qy = ty * T2Y + (w >> 1) * 4 + (jj >> 3);
+    qx = tx * T2X + (w & 1) * 8 + (jj & 7);
+  };
+
+  // ---- query coordinates, window origins, the windows' union box
+  if (tid < T2Q) {
+    int qy, qx;
+    qpos(tid, qy, qx);
+    int x0 = 0, y0 = 0, live = 0;
+    if (qy < H1 && qx < W1) {
+      const int q = qy * W1 + qx;
+      const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
+      const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
+      const float xf = floorf(x), yf = floorf(y);
+      if (fabsf(xf) < 1.0e8f && fabsf(yf) < 1.0e8f) {
+        x0 = (int)xf - R;
+        y0 = (int)yf - R;
+        live = (x0 + RD1 > 0 && x0 < lv.W2 && y0 + RD1 > 0 && y0 < lv.H2) ? 1 : 0;
+      }
+    }
+    qinfo[tid] = make_int4(x0, y0, live, 0);
+    int lx0 = live ? max(x0, 0) : 0x7fffffff, ly0 = live ? max(y0, 0) : 0x7fffffff;
+    int lx1 = live ? min(x0 + RD1, lv.W2) : -1, ly1 = live ? min(y0 + RD1, lv.H2) : -1;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      lx0 = min(lx0, __shfl_xor(lx0, o));
+      ly0 = min(ly0, __shfl_xor(ly0, o));
+      lx1 = max(lx1, __shfl_xor(lx1, o));
+      ly1 = max(ly1, __shfl_xor(ly1, o));
+    }
+    if (lane == 0) {
+      boxp[wave][0] = lx0;
+      boxp[wave][1] = ly0;
+      boxp[wave][2] = lx1;
+      boxp[wave][3] = ly1;
+    }
+  }
+  for (int i = tid; i < T2Q * NCELL; i += 256) S[i] = 0.f;
+
+  // this wave's queries as f16 pairs, all k steps, in registers (B operand:
+  // lane -> query j = lane & 31, channels 16 ks + 8 kh .. + 8)
+  const int j = lane & 31, kh = lane >> 5, qi = wave * 32 + j;
+  int mqy, mqx;
+  qpos(qi, mqy, mqx);
+  const float* qsrc = f1b + (long long)(min(mqy, H1 - 1) * W1 + min(mqx, W1 - 1)) * g.C + 8 * kh;
+  uint4 qh[16], ql[16];
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) {
+    if (ks < nks) {
+      const float4 u = *reinterpret_cast<const float4*>(qsrc + ks * 16);
+      const float4 w = *reinterpret_cast<const float4*>(qsrc + ks * 16 + 4);
+      const float x[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
+      alt_split8h(x, qh[ks], ql[ks]);
+    }
+  }
+  __syncthreads();
+
+  int bx0, by0, bw, bh;
+  {
+    const int lx0 = min(boxp[0][0], boxp[1][0]), ly0 = min(boxp[0][1], boxp[1][1]);
+    const int lx1 = max(boxp[0][2], boxp[1][2]), ly1 = max(boxp[0][3], boxp[1][3]);
+    const bool any = lx1 > lx0;
+    bx0 = any ? lx0 : 0;
+    by0 = any ? ly0 : 0;
+    bw = any ? lx1 - lx0 : 0;
+    bh = any ? ly1 - ly0 : 0;
+  }
+  const int ncells = bw * bh;
+  const int4 qinf = qinfo[qi];
+  const int sc = tid >> 2, sp = tid & 3;       // staging: chunk cell, 4-channel part
+  for (int c0 = 0; c0 < ncells; c0 += CH) {
+    const float* tsrc;
+    {
+      const int c = min(c0 + sc, ncells - 1);
+      const int cy = c / bw, cx = c - cy * bw;
+      tsrc = f2b + ((long long)(by0 + cy) * lv.W2 + bx0 + cx) * g.C + 4 * sp;
+    }
+    auto stage = [&](const float4 v, int buf) {
+      uint2 h, l;
+      alt_split4h(v, h, l);
+      *reinterpret_cast<uint2*>(&cst[buf][0][sc * PN + 4 * sp]) = h;
+      *reinterpret_cast<uint2*>(&cst[buf][1][sc * PN + 4 * sp]) = l;
+    };
+    af16 acc[2], acc2[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = acc2[t][r] = 0.f;
+    stage(*reinterpret_cast<const float4*>(tsrc), 0);
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      if (ks < nks) {
+        float4 nv;
+        if (ks + 1 < nks) nv = *reinterpret_cast<const float4*>(tsrc + (ks + 1) * 16);
+        const int buf = ks & 1;
+        const ah8 qhv = __builtin_bit_cast(ah8, qh[ks]), qlv = __builtin_bit_cast(ah8, ql[ks]);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int o = (t * 32 + j) * PN + 8 * kh;
+          const ah8 th = *reinterpret_cast<const ah8*>(&cst[buf][0][o]);
+          const ah8 tl = *reinterpret_cast<const ah8*>(&cst[buf][1][o]);
+          acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qhv, acc2[t], 0, 0, 0);
+          acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qlv, acc2[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qhv, acc[t], 0, 0, 0);
+        }
+        if (ks + 1 < nks) stage(nv, buf ^ 1);
+        __syncthreads();
+      }
+    }
+    bool bad = false;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        acc[t][r] = __builtin_fmaf(acc2[t][r], 0x1p-11f, acc[t][r]);
+        bad |= !(__builtin_fabsf(acc[t][r]) <= 3.40282347e38f);
+      }
+    if (__ballot(bad) != 0) {
+      // 3-way bf16 split from global memory, this wave only (no barriers)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int c = min(c0 + t * 32 + j, ncells - 1);
+        const int cy = c / bw, cx = c - cy * bw;
+        const float* csrc = f2b + ((long long)(by0 + cy) * lv.W2 + bx0 + cx) * g.C + 8 * kh;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+        for (int ks = 0; ks < nks; ++ks) {
+          const float4 u = *reinterpret_cast<const float4*>(qsrc + ks * 16);
+          const float4 w = *reinterpret_cast<const float4*>(qsrc + ks * 16 + 4);
+          const float4 a = *reinterpret_cast<const float4*>(csrc + ks * 16);
+          const float4 bq = *reinterpret_cast<const float4*>(csrc + ks * 16 + 4);
+          const float xq[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
+          const float xc[8] = {a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w};
+          uint4 h, m, l, ch, cm, cl;
+          alt_split8(xq, h, m, l);
+          alt_split8(xc, ch, cm, cl);
+          const abf8 qh3 = __builtin_bit_cast(abf8, h), qm3 = __builtin_bit_cast(abf8, m),
+                     ql3 = __builtin_bit_cast(abf8, l);
+          const abf8 th3 = __builtin_bit_cast(abf8, ch), tm3 = __builtin_bit_cast(abf8, cm),
+                     tl3 = __builtin_bit_cast(abf8, cl);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm3, qm3, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl3, qh3, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th3, ql3, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm3, qh3, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th3, qm3, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th3, qh3, acc[t], 0, 0, 0);
+        }
+      }
+    }
+    // keep the entries inside query qi's window: D row = (r & 3) + 8 (r >> 2) + 4 kh
+    if (qinf.z) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int c = c0 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+          if (c < ncells) {
+            const int cy = c / bw, cx = c - cy * bw;
+            const int iy = by0 + cy - qinf.y, ix = bx0 + cx - qinf.x;
+            if ((unsigned)iy < (unsigned)RD1 && (unsigned)ix < (unsigned)RD1)
+              S[qi * NCELL + iy * RD1 + ix] = acc[t][r];
+          }
+        }
+    }
+  }
+  __syncthreads();
+
+  // ---- bilinear combination, as alt_corr_mfma_kernel
+  const int oq = tid & (T2Q - 1), cls = tid / T2Q;
+  int oqy, oqx;
+  qpos(oq, oqy, oqx);
+  if (oqy >= H1 || oqx >= W1) return;
+  const int q = oqy * W1 + oqx;
+  const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
+  const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
+  const float dx = x - floorf(x), dy = y - floorf(y);
+  const float* s = S + oq * NCELL;
+  float* o = out + (long long)z * g.cout * g.N + (long long)lv.ch_off * g.N + q;
+  for (int ox = cls; ox < RD; ox += 256 / T2Q) {
+#pragma unroll
+    for (int oy = 0; oy < RD; ++oy) {
+      const float s00 = s[oy * RD1 + ox], s01 = s[oy * RD1 + ox + 1];
+      const float s10 = s[(oy + 1) * RD1 + ox], s11 = s[(oy + 1) * RD1 + ox + 1];
+      float v = __fmul_rn(__fmul_rn(s00, 1.f - dy), 1.f - dx);
+      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s01, 1.f - dy), dx));
+      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s10, dy), 1.f - dx));
+      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s11, dy), dx));
+      o[(long long)(oy + RD * ox) * g.N] = v / g.divisor;
+    }
+  }
+}
+
+#endif  // DXR_EXPERIMENTS
+
+#ifdef DXR_EXPERIMENTS
 // Two alternative forms of alt_corr_mfma_kernel, measured at 1080p (12 coordinate
 // sets, scripts/xp_alt.py) and kept only in the experiments target: both are
 // bit-identical (rq) or f32-class (grouped) but slower than the product kernel
@@ -1321,6 +1581,18 @@ extern "C" int dxr_xp_alt(const float* fmap1, const float* const* fmap2_levels, 
     const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
     hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, false, 2>), grid, dim3(256), 0, stream,
                        fmap1, coords, out, g, (int)W, tiles_x);
+    return dxr::launch_status();
+  }
+  if (xp == 20 || xp == 21) {   // 8 x 16 query tiles, cells shared through LDS
+    const int H1 = g.N / (int)W;
+    const int tiles_x = ((int)W + T2X - 1) / T2X, tiles_y = (H1 + T2Y - 1) / T2Y;
+    const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
+    if (xp == 20)
+      hipLaunchKernelGGL((alt_corr_tile_kernel<4, 2>), grid, dim3(256), 0, stream, fmap1, coords,
+                         out, g, (int)W, tiles_x);
+    else
+      hipLaunchKernelGGL((alt_corr_tile_kernel<4, 1>), grid, dim3(256), 0, stream, fmap1, coords,
+                         out, g, (int)W, tiles_x);
     return dxr::launch_status();
   }
   if (xp == 6 || xp == 7) {

@@ -1,6 +1,7 @@
-# On-the-fly kernel with pre-split operands (-1) vs the product's in-kernel split (-2) and the exp kernel (0); tests.
+# Early-gather lookup (xp 200) vs the product lookup (0), bit-checked, three shapes.
 set -o pipefail
-O=gpurun_out/xq7.log
+O=gpurun_out/xq8.log
 : > $O
-timeout -k 10 200 python -u scripts/xp_alt.py --xp 0,-1,-2 >> $O 2>&1 || exit $?
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_channels_last.py tests/test_e2e_flow.py tests/test_gpu_graph.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider >> $O 2>&1 || exit $?
+timeout -k 10 120 python -u scripts/xp_lookup.py --xp 0,200,201 --check 200 >> $O 2>&1 || exit $?
+timeout -k 10 120 python -u scripts/xp_lookup.py --B 8 --xp 0,200 --check 200 >> $O 2>&1 || exit $?
+timeout -k 10 120 python -u scripts/xp_lookup.py --B 8 --H 47 --W 156 --dtype bf16 --xp 0,200 --check 200 >> $O 2>&1 || exit $?
