@@ -603,6 +603,39 @@ def _loss_backward(block_cls, f1, f2, coord_sets, weights, **kw):
     return f1.grad, f2.grad
 
 
+def test_training_step_frees_memory_without_gc(dx):
+    """A differentiable block (pyramid + gradient pyramid, hundreds of MB at
+    benchmark sizes) is freed by refcount when the step's tensors go: the
+    autograd nodes hold only the block's _GradState, never the block, so no
+    reference cycle waits for Python's cyclic collector."""
+    import gc
+    f1, f2 = _pair(H=30, W=44, seed=41)
+    c = [_t(dg.coords(42 + k, 1, 30, 44, "normal", 3.0)) for k in range(3)]
+
+    def one_step():
+        a1, a2 = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
+        cb = dx.CorrBlock(a1, a2)
+        sum(cb(ci).sum() for ci in c).backward()
+
+    one_step()          # first GEMM: torch's persistent BLAS workspace comes from the allocator
+    torch.cuda.synchronize()
+    gc.collect()
+    base = torch.cuda.memory_allocated()
+    gc.disable()
+    try:
+        for _ in range(3):
+            a1, a2 = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
+            cb = dx.CorrBlock(a1, a2)
+            loss = sum(cb(ci).sum() for ci in c)
+            loss.backward()
+            assert a1.grad is not None and a2.grad is not None
+            del a1, a2, cb, loss
+            torch.cuda.synchronize()
+            assert torch.cuda.memory_allocated() == base
+    finally:
+        gc.enable()
+
+
 @pytest.mark.parametrize("name", ["bw_basic", "bw_batch2_r3", "bw_d256"])
 def test_backward_matches_reference_autograd_golden(dx, name):
     """d loss / d fmaps through CorrBlock (build + 3 lookups) against the
