@@ -457,6 +457,9 @@ __global__ __launch_bounds__(512) void corr_lookup_backward_kernel(const float* 
     const int cy = rem / RS, cx = rem - cy * RS;
     const int2 o = org[qq];
     if (q0 + qq >= g.N || o.x == FAR_ORIGIN) continue;
+    // only the WD window columns from o.x can receive gradient (the LDS row starts
+    // at o.x & ~3): the rest would add zero
+    if (cx < (o.x & 3) || cx >= (o.x & 3) + WD) continue;
     const int yy = o.y + cy, xx = (o.x & ~3) + cx;
     if ((unsigned)yy >= (unsigned)A.h || (unsigned)xx >= (unsigned)A.w) continue;
     float acc = 0.f;

@@ -31,6 +31,10 @@ def main():
     ap.add_argument("--W", type=int, default=240)
     ap.add_argument("--xp", default="0,1,2")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--smooth", type=int, default=0,
+                    help="flow correlation length in pixels (0: i.i.d. N(0, 4^2) per pixel, the "
+                         "bench's model; S > 0: a N(0, 4^2) field on an S-pixel grid, bilinearly "
+                         "upsampled — spatially smooth like real optical flow)")
     a = ap.parse_args()
     import dexiraft_amd
     nat = dexiraft_amd._native
@@ -51,8 +55,15 @@ def main():
     ys, xs = torch.meshgrid(torch.arange(H, device=dev, dtype=torch.float32),
                             torch.arange(W, device=dev, dtype=torch.float32), indexing="ij")
     grid = torch.stack((xs, ys))[None].expand(B, 2, H, W)
-    cs = [(grid + 4.0 * torch.randn((B, 2, H, W), generator=g, device=dev)).contiguous()
-          for _ in range(12)]
+    def flow():
+        if a.smooth <= 0:
+            return 4.0 * torch.randn((B, 2, H, W), generator=g, device=dev)
+        hs, ws = max(2, H // a.smooth + 1), max(2, W // a.smooth + 1)
+        coarse = 4.0 * torch.randn((B, 2, hs, ws), generator=g, device=dev)
+        return torch.nn.functional.interpolate(coarse, size=(H, W), mode="bilinear",
+                                               align_corners=True)
+
+    cs = [(grid + flow()).contiguous() for _ in range(12)]
     outs = [torch.empty((B, 324, H, W), device=dev) for _ in range(12)]
     s = torch.cuda.current_stream().cuda_stream
     xps = [int(x) for x in a.xp.split(",")]
