@@ -185,10 +185,13 @@ int dxr_corr_lookup_backward(const float* coords, const float* grad_out,
  * row 2; inference):
  *   out[b,o,h,w] = act(bias[o] + sum_c weight[o,c] * lookup(coords)[b,c,h,w])
  * lookup() is dxr_corr_lookup (bit-identical samples), the contraction runs in
- * f32 class (exact three-way bf16 split of both operands, f32 accumulation).
+ * f32 class (f16 pair split of both operands, x = hi + 2^-11 lo, three MFMA
+ * products, f32 accumulation; workgroups whose sums are not finite re-run it on
+ * the exact three-way bf16 split).
  *   weight_packed : dxr_conv1x1_pack_weight of the [cout, cin] float32 weight,
  *                   cin = num_levels*(2r+1)^2 (dxr_conv1x1_packed_bytes bytes:
- *                   float32 [ceil(cin/16)*2][cout][8], zero padded)
+ *                   float32 [ceil(cin/16)*2][cout][8], zero padded, followed by
+ *                   the same layout as f16 pairs, 8 hi then 8 lo per 32 bytes)
  *   bias          : [cout] float32 or NULL;  relu: 1 = F.relu, 0 = none
  *   out           : [B, cout, H, W] float32
  * Supported: radius 3 or 4, num_levels <= 4, cout a multiple of 32 (<= 4096);

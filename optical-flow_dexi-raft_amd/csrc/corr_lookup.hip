@@ -29,6 +29,8 @@
 //            gathers thrash the 32 KiB L1 and become L2-bandwidth bound);
 //   phase 2  thread = (query, x-offset class): taps from LDS, fused sum, and
 //            every output store is a coalesced 256-B wave store along queries.
+#include <type_traits>
+
 #include "dxr_common.h"
 
 namespace {
@@ -565,6 +567,25 @@ __device__ __forceinline__ void split3(float x, uint16_t& h, uint16_t& m, uint16
 // f32 and split in registers by the fused kernel: 4 bytes per weight streamed
 // from L2 instead of 6 for pre-split planes (the stream is the GEMM's bound:
 // ~70 GB/s of L2 reads per CU, MI355X_MICROARCH.md "gather into LDS").
+// Round 2: the same [Cin_pad/8][Cout][8] layout twice — f32 (the 3-way bf16
+// fallback's operand) and then f16 pairs (8 x f16 hi, 8 x f16 lo in the same 32
+// bytes: the f16-pair GEMM's operand, split once here instead of per k step).
+__device__ __forceinline__ void lk_split8h(const float (&x)[8], uint4& h, uint4& l) {
+  typedef _Float16 h2t __attribute__((ext_vector_type(2)));
+  typedef float f2t __attribute__((ext_vector_type(2)));
+  uint32_t hh[4], ll[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const f2t v = {x[2 * e], x[2 * e + 1]};
+    hh[e] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, h2t));
+    const h2t hv = __builtin_bit_cast(h2t, hh[e]);
+    const f2t r = {(x[2 * e] - (float)hv[0]) * 2048.f, (x[2 * e + 1] - (float)hv[1]) * 2048.f};
+    ll[e] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, h2t));
+  }
+  h = make_uint4(hh[0], hh[1], hh[2], hh[3]);
+  l = make_uint4(ll[0], ll[1], ll[2], ll[3]);
+}
+
 __global__ __launch_bounds__(256) void conv1x1_pack_weight_kernel(const float* __restrict__ w,
                                                                   int cout, int cin, int kbw,
                                                                   float4* __restrict__ packed) {
@@ -579,8 +600,15 @@ __global__ __launch_bounds__(256) void conv1x1_pack_weight_kernel(const float* _
   }
   packed[2LL * u] = make_float4(x[0], x[1], x[2], x[3]);
   packed[2LL * u + 1] = make_float4(x[4], x[5], x[6], x[7]);
+  uint4 h, l;
+  lk_split8h(x, h, l);
+  uint4* pairs = reinterpret_cast<uint4*>(packed + 2LL * kbw * cout);
+  pairs[2LL * u] = h;
+  pairs[2LL * u + 1] = l;
 }
 
+#ifdef DXR_EXPERIMENTS
+// r01 form (experiments target only since r02; see corr_lookup_conv1x1_h2_kernel).
 // NT threads per workgroup (1024 by default: the four levels' lookup phases
 // are latency-bound at 8 waves per CU).  With 16 waves the GEMM splits K in two
 // halves per output block: waves 8..15 add their partial accumulators through
@@ -775,6 +803,209 @@ __global__ __launch_bounds__(NT) void corr_lookup_conv1x1_kernel(
   }
 }
 
+#endif  // DXR_EXPERIMENTS
+
+// ---------------------------------------------------------------------------
+// Round-2 form: two workgroups per CU.  The r01 kernel staged all four levels'
+// tap data and kept three bf16 sample planes (125 KB of LDS: one workgroup per
+// CU, both halves latency-bound).  Here phase 0 runs per level just before its
+// gather (one level's tap data), the samples stay f32 in LDS (43 KB, split into
+// f16 pairs per k step in registers) and the weights arrive pre-split as f16
+// pairs (dxr_conv1x1_pack_weight): ~76 KB, so one workgroup's GEMM overlaps the
+// other's gathers.  The GEMM runs on the f16 pair split (3 products, cross terms
+// in a second accumulator, as the split build); a workgroup whose sums are not
+// finite re-runs the GEMM on the 3-way bf16 split from the f32 samples and the
+// f32 weight copy.  Samples are the lookup's, bit for bit.
+// ---------------------------------------------------------------------------
+typedef _Float16 mh8 __attribute__((ext_vector_type(8)));
+
+template <int R, typename PT, int NT = 512, int PF = 4>
+__global__ __launch_bounds__(NT, 4) void corr_lookup_conv1x1_h2_kernel(
+    const PT* __restrict__ pyr, const float* __restrict__ coords, const float4* __restrict__ wpk,
+    const float* __restrict__ bias, float* __restrict__ out, LookupGeom g, int cout, int relu) {
+  using C = WideCfg<R, NT>;
+  using M = MotionCfg<R>;
+  constexpr int RD = C::RD, RS = C::RS, K = C::K, QB = C::QB, KB = M::KB;
+  constexpr int NW = NT / 64, KSPLIT = NW >= 16 ? 2 : 1;
+  static_assert(NW == 8 || NW == 16, "8 output blocks of 32 per pass");
+  constexpr int CELLS_B = QB * C::QS * 4, XS_B = RD * QB * 16, ORG_B = QB * 8;
+  constexpr int STAGE_B = CELLS_B + 2 * XS_B + ORG_B, RED_B = KSPLIT > 1 ? 8 * 16 * 64 * 4 : 0;
+  __shared__ __attribute__((aligned(16))) char stage[STAGE_B > RED_B ? STAGE_B : RED_B];
+  __shared__ __attribute__((aligned(16))) float spl[KB * QB * 8];   // samples [k/8][q][8], f32
+  __shared__ int nonfinite;
+  float* cells = reinterpret_cast<float*>(stage);
+  float4* xs = reinterpret_cast<float4*>(stage + CELLS_B);
+  float4* ys = reinterpret_cast<float4*>(stage + CELLS_B + XS_B);
+  int2* org = reinterpret_cast<int2*>(stage + CELLS_B + 2 * XS_B);
+  float* red = reinterpret_cast<float*>(stage);
+
+  const int tid = threadIdx.x;
+  const int b = blockIdx.y;
+  const int q0 = blockIdx.x * QB;
+  const int cin = g.cout;
+  const int kpad = (cin + 15) & ~15;
+  const int lane = tid & 63, wave = tid >> 6, j = lane & 31, kh = lane >> 5;
+  const int wob = wave & 7, khalf = wave >> 3;
+  const int nks = kpad / 16;
+  const int kbeg = khalf * nks / KSPLIT, kend = (khalf + 1) * nks / KSPLIT;
+  const int nob = cout / 32;
+  const int kbw = nks * 2;
+  const uint4* wpair = reinterpret_cast<const uint4*>(wpk + 2LL * kbw * cout);
+
+  if (tid == 0) nonfinite = 0;
+  for (int i = tid; i < QB * (kpad - cin); i += NT) {      // channel padding: zeros
+    const int np = kpad - cin, qq = i / np, c = cin + i - qq * np;
+    spl[((c >> 3) * QB + qq) * 8 + (c & 7)] = 0.f;
+  }
+  // ---- per level: phase 0, gather, samples -> spl
+  for (int l = 0; l < g.levels; ++l) {
+    const LevelAddr& A = g.lv[l];
+    wide_phase0<R, NT>(coords, g, A, b, l, q0, tid, xs, ys, org);
+    __syncthreads();
+    {
+      float4 win[C::VIT];
+      const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
+      const int qb0 = q0 & ((1 << A.lqb) - 1);
+      if (l < 3)
+        gather_load<R, NT, 4>(base, qb0, A, org, q0, g.N, tid, win);
+      else
+        gather_load<R, NT, 2>(base, qb0, A, org, q0, g.N, tid, win);
+      gather_store<R, NT>(win, cells, tid);
+    }
+    __syncthreads();
+    {
+      const int qq = tid % QB, cls = tid / QB;
+      const bool live = q0 + qq < g.N;
+      const float* cq = cells + qq * C::QS;
+      for (int k = cls; k < K; k += C::NCLS) {
+        const int ox = k / RD, oy = k - ox * RD;
+        const float4 xd = xs[ox * QB + qq], yd = ys[oy * QB + qq];
+        const float* p = cq + __float_as_int(yd.x) + __float_as_int(xd.x);
+        const float v00 = p[0], v01 = p[1], v10 = p[RS], v11 = p[RS + 1];
+        const float nw = __fmul_rn(yd.z, xd.z), ne = __fmul_rn(yd.z, xd.y);
+        const float sw = __fmul_rn(yd.y, xd.z), se = __fmul_rn(yd.y, xd.y);
+        float r = __fmul_rn(nw, v00);
+        r = __builtin_fmaf(ne, v01, r);
+        r = __builtin_fmaf(sw, v10, r);
+        r = __builtin_fmaf(se, v11, r);
+        if (!live) r = 0.f;                // queries past N: finite zeros
+        const int c = l * K + k;
+        spl[((c >> 3) * QB + qq) * 8 + (c & 7)] = r;
+      }
+    }
+    __syncthreads();   // the next level rewrites xs / ys / org / cells
+  }
+
+  // ---- (Cout x 32 queries x Cin) GEMM: f16 pairs, then (rarely) the 3-way bf16 split
+  const int q = q0 + j;
+  auto gemm = [&](auto mode) {
+    constexpr bool M2 = decltype(mode)::value;
+    for (int ob0 = 0; ob0 < nob; ob0 += 8) {   // uniform trip count: barriers inside
+      const int ob = ob0 + wob;
+      const bool act = ob < nob;
+      mf16 acc, acc2;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = acc2[r] = 0.f;
+      if (act) {
+        uint4 wb[PF][2];
+        auto wload = [&](uint4* dst, int ks) {
+          const long long u = 2 * ((long long)(2 * ks + kh) * cout + ob * 32 + j);
+          if constexpr (M2) {
+            dst[0] = wpair[u];
+            dst[1] = wpair[u + 1];
+          } else {
+            dst[0] = __builtin_bit_cast(uint4, wpk[u]);
+            dst[1] = __builtin_bit_cast(uint4, wpk[u + 1]);
+          }
+        };
+#pragma unroll
+        for (int sl = 0; sl < PF; ++sl) wload(wb[sl], min(kbeg + sl, kend - 1));
+        auto kstep = [&](int ks, int sl, bool refill) {
+          __builtin_amdgcn_sched_barrier(0);
+          const int kb = 2 * ks + kh;
+          const float4* sp = reinterpret_cast<const float4*>(spl + ((long long)kb * QB + j) * 8);
+          const float4 sa = sp[0], sb = sp[1];
+          const float xq[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+          if constexpr (M2) {
+            uint4 qh4, ql4;
+            lk_split8h(xq, qh4, ql4);
+            const mh8 th = __builtin_bit_cast(mh8, wb[sl][0]), tl = __builtin_bit_cast(mh8, wb[sl][1]);
+            if (refill) wload(wb[sl], min(ks + PF, kend - 1));
+            const mh8 qh = __builtin_bit_cast(mh8, qh4), ql = __builtin_bit_cast(mh8, ql4);
+            acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc2, 0, 0, 0);
+            acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc2, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qh, acc, 0, 0, 0);
+          } else {
+            uint4 wh, wm, wl, qh4, qm4, ql4;
+            {
+              const float4 a = __builtin_bit_cast(float4, wb[sl][0]);
+              const float4 c = __builtin_bit_cast(float4, wb[sl][1]);
+              const float x[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+              dxr::split8(x, wh, wm, wl);
+            }
+            dxr::split8(xq, qh4, qm4, ql4);
+            if (refill) wload(wb[sl], min(ks + PF, kend - 1));
+            const mbf8 th = __builtin_bit_cast(mbf8, wh), tm = __builtin_bit_cast(mbf8, wm),
+                       tl = __builtin_bit_cast(mbf8, wl);
+            const mbf8 qh = __builtin_bit_cast(mbf8, qh4), qm = __builtin_bit_cast(mbf8, qm4),
+                       ql = __builtin_bit_cast(mbf8, ql4);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, ql, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qh, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qm, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh, acc, 0, 0, 0);
+          }
+        };
+        const int nfull = kbeg + (kend - kbeg) / PF * PF;
+#pragma unroll 1
+        for (int k0 = kbeg; k0 < nfull; k0 += PF) {
+#pragma unroll
+          for (int sl = 0; sl < PF; ++sl) kstep(k0 + sl, sl, true);
+        }
+#pragma unroll
+        for (int sl = 0; sl < PF; ++sl)
+          if (nfull + sl < kend) kstep(nfull + sl, sl, false);
+        if constexpr (M2) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[r] = __builtin_fmaf(acc2[r], 0x1p-11f, acc[r]);
+        }
+      }
+      if constexpr (KSPLIT > 1) {
+        if (khalf == 1 && act) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) red[(wob * 16 + r) * 64 + lane] = acc[r];
+        }
+        __syncthreads();
+        if (khalf == 0 && act) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[r] += red[(wob * 16 + r) * 64 + lane];
+        }
+        __syncthreads();
+      }
+      if (khalf == 0 && act && q < g.N) {
+        if constexpr (M2) {
+          bool bad = false;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) bad |= !(__builtin_fabsf(acc[r]) <= 3.40282347e38f);
+          if (bad) nonfinite = 1;
+        }
+        float* ob_out = out + (long long)b * cout * g.N + q;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int orow = ob * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+          float v = acc[r] + (bias ? bias[orow] : 0.f);
+          if (relu && v < 0.f) v = 0.f;      // NaN stays NaN, as torch.relu
+          ob_out[(long long)orow * g.N] = v;
+        }
+      }
+    }
+  };
+  gemm(std::integral_constant<bool, true>{});
+  __syncthreads();
+  if (nonfinite) gemm(std::integral_constant<bool, false>{});   // workgroup-uniform
+}
+
 template <int R, typename PT>
 int launch_lookup_conv1x1_r(const PT* pyr, const float* coords, const float4* wpl,
                             const float* bias, float* out, const LookupGeom& g, int B, int cout,
@@ -782,8 +1013,16 @@ int launch_lookup_conv1x1_r(const PT* pyr, const float* coords, const float4* wp
   using C = WideCfg<R, 1024>;
   if (g.cout > MotionCfg<R>::KP) return DXR_EUNSUPPORTED;
   const dim3 grid((unsigned)((g.N + C::QB - 1) / C::QB), (unsigned)B);
-  hipLaunchKernelGGL((corr_lookup_conv1x1_kernel<R, PT, 1024, 4>), grid, dim3(1024), 0, stream,
-                     pyr, coords, wpl, bias, out, g, cout, relu);
+  // Grids up to one workgroup per CU (Sintel B=1: 220) run the 1024-thread form
+  // (more waves per workgroup: 24 vs 26 us); larger grids the 512-thread form,
+  // ~76 KB LDS and 128 VGPRs, two workgroups per CU (Sintel B=2: 35 vs 47 us,
+  // KITTI-shape B=8: 136 vs 190 us; r01 kernel 52 / 214 us).
+  if ((long long)grid.x * grid.y <= 256)
+    hipLaunchKernelGGL((corr_lookup_conv1x1_h2_kernel<R, PT, 1024, 4>), grid, dim3(1024), 0,
+                       stream, pyr, coords, wpl, bias, out, g, cout, relu);
+  else
+    hipLaunchKernelGGL((corr_lookup_conv1x1_h2_kernel<R, PT, 512, 4>), grid, dim3(512), 0, stream,
+                       pyr, coords, wpl, bias, out, g, cout, relu);
   return dxr::launch_status();
 }
 
@@ -857,7 +1096,7 @@ extern "C" int dxr_corr_lookup_backward(const float* coords, const float* grad_o
 
 extern "C" int64_t dxr_conv1x1_packed_bytes(int64_t cout, int64_t cin) {
   if (cout < 1 || cin < 1) return -1;
-  return ((cin + 15) / 16 * 16) * cout * 4;
+  return ((cin + 15) / 16 * 16) * cout * 4 * 2;   // f32 copy + f16-pair copy
 }
 
 extern "C" int dxr_conv1x1_pack_weight(const float* weight, int64_t cout, int64_t cin,
@@ -952,5 +1191,36 @@ extern "C" int dxr_xp_lookup(const void* pyramid, int pyr_dtype, int64_t B, int6
     case 2: return xp_lookup_k<2>(p, coords, out, g, (int)B, stream);
     default: return DXR_EUNSUPPORTED;
   }
+}
+#endif
+
+#ifdef DXR_EXPERIMENTS
+// Experiments target only: the fused lookup + 1x1 conv with a chosen kernel —
+// xp 0: the r01 form (three bf16 sample planes, all levels staged, one
+// workgroup per CU; reads the f32 half of the packed weight), 1: the product's
+// (512 threads, two workgroups per CU), 2: the product's form at 1024 threads.
+extern "C" int dxr_xp_lookup_conv1x1(const float* pyramid, int64_t B, int64_t H, int64_t W,
+                                     const float* coords, const void* weight_packed,
+                                     const float* bias, int64_t cout, float* out, int xp,
+                                     hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, 4, &L) || cout % 32 != 0) return DXR_EINVAL;
+  LookupGeom g;
+  g.N = (int)(H * W);
+  g.levels = 4;
+  g.cout = 4 * 81;
+  for (int l = 0; l < L.n; ++l) g.lv[l] = level_addr(L.lay[l]);
+  const float4* wpl = static_cast<const float4*>(weight_packed);
+  const dim3 grid((unsigned)((g.N + 31) / 32), (unsigned)B);
+  if (xp == 0)
+    hipLaunchKernelGGL((corr_lookup_conv1x1_kernel<4, float, 1024, 4>), grid, dim3(1024), 0, stream,
+                       pyramid, coords, wpl, bias, out, g, (int)cout, 1);
+  else if (xp == 1)
+    hipLaunchKernelGGL((corr_lookup_conv1x1_h2_kernel<4, float, 512, 4>), grid, dim3(512), 0,
+                       stream, pyramid, coords, wpl, bias, out, g, (int)cout, 1);
+  else
+    hipLaunchKernelGGL((corr_lookup_conv1x1_h2_kernel<4, float, 1024, 4>), grid, dim3(1024), 0,
+                       stream, pyramid, coords, wpl, bias, out, g, (int)cout, 1);
+  return dxr::launch_status();
 }
 #endif

@@ -167,7 +167,7 @@ def test_host_side_validation_needs_no_gpu(nat):
     assert ab(P, P, None, P, P, P, 1, 8, 8, 8, 8, 64, 1, 4, None) == EINVAL  # null coords
     assert ab(P, P, P, P, None, P, 1, 8, 8, 8, 8, 64, 1, 4, None) == EINVAL  # null fmap1_grad
     assert ab(None, None, None, None, None, None, 0, 8, 8, 8, 8, 64, 1, 4, None) == OK
-    assert lib.dxr_conv1x1_packed_bytes(256, 324) == 336 * 256 * 4
+    assert lib.dxr_conv1x1_packed_bytes(256, 324) == 336 * 256 * 4 * 2   # f32 + f16-pair copies
     assert lib.dxr_conv1x1_packed_bytes(0, 324) == -1
     assert lib.dxr_conv1x1_pack_weight(P, 0, 324, P, None) == EINVAL
     assert lib.dxr_conv1x1_pack_weight(None, 256, 324, P, None) == EINVAL
