@@ -194,8 +194,9 @@ def _cpu_model() -> str:
 
 
 def cpu_baseline(H, W, budget_s, impl="torch", reps=5):
-    """Time the reference's op sequence on host cores: warm-up 1, then the median
-    of at least ``reps`` single-pair repetitions (more while within ``budget_s``).
+    """Time the reference's op sequence on host cores: warm-up 1,
+    then the median of ``reps`` repetitions, each timing as many single pairs as
+    fit in budget_s / reps (at least one).
 
     impl "torch" (default; SURVEY.md §8(d) "CPU reference timing"): the plain-PyTorch
     restatement tests/torch_ref.py (bmm, / sqrt(D), 3x F.avg_pool2d, 12 x 4
@@ -229,20 +230,24 @@ def cpu_baseline(H, W, budget_s, impl="torch", reps=5):
             for c in cs:
                 oracle.corr_lookup(pyr, c, RADIUS)
         what = f"numpy float32 oracle; matmul on {threads} BLAS threads, lookups single-threaded"
-    times = []
+    rates, pairs, total = [], 0, 0.0
     with torch.no_grad():
         one_pair()                                   # warm-up (allocator, thread pool)
-        t_start = time.perf_counter()
-        while len(times) < reps or (time.perf_counter() - t_start < budget_s and len(times) < 50):
-            t0 = time.perf_counter()
-            one_pair()
-            times.append(time.perf_counter() - t0)
-    med = float(np.median(times))
-    return {"value": round(1.0 / med, 4), "unit": "pairs/s", "cores": threads,
+        for _ in range(reps):
+            n, t0 = 0, time.perf_counter()
+            while n == 0 or time.perf_counter() - t0 < budget_s / reps:
+                one_pair()
+                n += 1
+            dt = time.perf_counter() - t0
+            rates.append(n / dt)
+            pairs += n
+            total += dt
+    med = float(np.median(rates))
+    return {"value": round(med, 4), "unit": "pairs/s", "cores": threads,
             "nproc": os.cpu_count(), "cpu_model": _cpu_model(), "kind": "port",
-            "median_of": len(times), "median_s_per_pair": round(med, 4),
-            "sample": f"{len(times)} single-pair reps (median) of fmap {H}x{W}, D={D}: build + "
-                      f"{ITERS} lookups, {sum(times):.1f} s; {what}"}
+            "median_of": reps, "median_s_per_pair": round(1.0 / med, 4),
+            "sample": f"median of {reps} reps ({pairs} single pairs in {total:.1f} s) of fmap "
+                      f"{H}x{W}, D={D}: build + {ITERS} lookups each; {what}"}
 
 
 def main():
