@@ -1150,6 +1150,15 @@ int xp_lookup_k(const PT* pyr, const float* coords, float* out, const LookupGeom
                      coords, out, g);
   return dxr::launch_status();
 }
+template <int NT2, typename PT>
+int xp_lookup_nt(const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
+                 hipStream_t stream) {
+  using W = WideCfg<4, NT2>;
+  const dim3 grid((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
+  hipLaunchKernelGGL((corr_lookup_wide_kernel<4, PT, NT2, 0>), grid, dim3(W::NT), 0, stream, pyr,
+                     coords, out, g);
+  return dxr::launch_status();
+}
 template <typename PT>
 int xp_lookup2(const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
                hipStream_t stream) {
@@ -1180,12 +1189,15 @@ extern "C" int dxr_xp_lookup(const void* pyramid, int pyr_dtype, int64_t B, int6
       case 3: return xp_lookup_k<3>(p, coords, out, g, (int)B, stream);
       case 4: return xp_lookup_k<4>(p, coords, out, g, (int)B, stream);
       case 100: return xp_lookup2(p, coords, out, g, (int)B, stream);
+      case 256: return xp_lookup_nt<256>(p, coords, out, g, (int)B, stream);
+      case 1024: return xp_lookup_nt<1024>(p, coords, out, g, (int)B, stream);
       default: return DXR_EUNSUPPORTED;
     }
   }
   const uint16_t* p = static_cast<const uint16_t*>(pyramid);
   switch (xp) {
     case 100: return xp_lookup2(p, coords, out, g, (int)B, stream);
+    case 256: return xp_lookup_nt<256>(p, coords, out, g, (int)B, stream);
     case 0: return xp_lookup_k<0>(p, coords, out, g, (int)B, stream);
     case 1: return xp_lookup_k<1>(p, coords, out, g, (int)B, stream);
     case 2: return xp_lookup_k<2>(p, coords, out, g, (int)B, stream);
