@@ -928,6 +928,14 @@ __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t voff
   return make_float4(v.x, v.y, v.z, v.w);
 }
 
+#ifdef DXR_EXPERIMENTS
+// XP bit 10 (experiments): per-workgroup timeline of wave 0 — CU identity and
+// shader-clock stamps at start, after the K loop, after the epilogue's stores
+// are issued and after they complete; read back with dxr_xp_trace_read.
+constexpr int XP_TRACE_WG = 32768;
+__device__ unsigned long long xp_trace[XP_TRACE_WG * 5];
+#endif
+
 // BV: target staging width in floats — 4 (float4 units; W % 4 == 0) or 2
 // (float2 units; W even, e.g. Chairs' 62-wide fmaps).
 // NHWC: channels-last fmaps [B, H, W, D]: every operand
@@ -953,6 +961,19 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (H2 && tid == 0) redo = 0;
+#ifdef DXR_EXPERIMENTS
+  const unsigned long long xt0 = (XP & 1024) ? __builtin_amdgcn_s_memtime() : 0ull;
+#endif
+  if constexpr ((XP & 768) != 0) {
+    // XP bits 8-9 (experiments): stagger the first wave of workgroups — the one
+    // in CU slot s (linear id / 256, breadth-first dispatch) sleeps s * k * 8K
+    // cycles, k = (XP >> 8) & 3, so the slots' epilogues fall at different times.
+    const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    if (L < 768) {
+      const int n = (L >> 8) * ((XP >> 8) & 3);
+      for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+    }
+  }
   const PageCoord pc = page_coord<REMAP>(g);
   const int txi = pc.txi, tyi = pc.tyi;
   const int th0 = tyi * TH, tw0 = txi * TW;
@@ -1195,6 +1216,9 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     kloop(S3{});
   }
 
+#ifdef DXR_EXPERIMENTS
+  const unsigned long long xt1 = (XP & 1024) ? __builtin_amdgcn_s_memtime() : 0ull;
+#endif
   scale_acc<DIV>(acc, g);
   if constexpr ((XP & 1) != 0) {
     float sum = 0.f;
@@ -1210,7 +1234,26 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
   // (faster build alone, no faster step: the lookups then read the pyramid
   // from HBM instead of the caches).
   constexpr int EX = ((XP & 32) ? 0 : 1) | ((XP & 64) ? 2 : 0);
-  paged_epilogue<OT, EX>(acc, reinterpret_cast<float*>(smem), pyr, g, pc.page, wave, lane);
+  // XP bit 7 (experiments): workgroups write a 32-page ring — the epilogue's
+  // instructions, LDS transposes and stores, with the writes L2-resident
+  paged_epilogue<OT, EX>(acc, reinterpret_cast<float*>(smem), pyr, g, (XP & 128) ? (pc.page & 31) : pc.page,
+                         wave, lane);
+#ifdef DXR_EXPERIMENTS
+  if constexpr ((XP & 1024) != 0) {
+    const unsigned long long xt2 = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long xt3 = __builtin_amdgcn_s_memtime();
+    const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    if (wave == 0 && lane < 5 && L < XP_TRACE_WG) {
+      const unsigned long long id =
+          (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+          ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(20 | (15 << 11)) << 32);
+      const unsigned long long v = lane == 0 ? id : lane == 1 ? xt0 : lane == 2 ? xt1
+                                 : lane == 3 ? xt2 : xt3;
+      xp_trace[L * 5 + lane] = v;
+    }
+  }
+#endif
 }
 
 // Floor-mode 2x2 average pool of one pyramid level into the next, for levels
@@ -1691,6 +1734,15 @@ int xp_bf16q2(const uint16_t* f1, const uint16_t* f2, uint16_t* pyr, const Build
   return dxr::launch_status();
 }
 
+// Copies the XP-bit-10 timeline (5 x u64 per workgroup) to host memory.
+extern "C" int dxr_xp_trace_read(void* host, int64_t bytes) {
+  if (bytes > (int64_t)sizeof(unsigned long long) * XP_TRACE_WG * 5) return DXR_EINVAL;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(xp_trace), (size_t)bytes, 0, hipMemcpyDeviceToHost) ==
+                 hipSuccess
+             ? DXR_OK
+             : DXR_EINVAL;
+}
+
 // bf16 fmaps and pyramid, W % 4 == 0: the bf16 build with ablation bits.
 extern "C" int dxr_xp_build_bf16(const void* f1, const void* f2, int64_t B, int64_t D, int64_t H,
                                  int64_t W, void* pyr, int xp, hipStream_t stream) {
@@ -1750,6 +1802,12 @@ extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t
                          build_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);
       return dxr::launch_status();
     case 2001: return xp_h2<1>(f1, f2, pyr, g, (int)B, stream);
+    case 2128: return xp_h2<128>(f1, f2, pyr, g, (int)B, stream);
+    case 3024: return xp_h2<1024>(f1, f2, pyr, g, (int)B, stream);
+    case 3025: return xp_h2<1025>(f1, f2, pyr, g, (int)B, stream);
+    case 2256: return xp_h2<256>(f1, f2, pyr, g, (int)B, stream);
+    case 2512: return xp_h2<512>(f1, f2, pyr, g, (int)B, stream);
+    case 2768: return xp_h2<768>(f1, f2, pyr, g, (int)B, stream);
     case 2032: return xp_h2<32>(f1, f2, pyr, g, (int)B, stream);
     case 2064: return xp_h2<64>(f1, f2, pyr, g, (int)B, stream);
     case 2096: return xp_h2<96>(f1, f2, pyr, g, (int)B, stream);
