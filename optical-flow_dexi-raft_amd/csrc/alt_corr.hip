@@ -250,7 +250,8 @@ __device__ __forceinline__ void alt_split8h(const float (&x)[8], uint4& h, uint4
 // as the split build; a chunk whose sums are not finite (an operand beyond f16
 // range, or inf/NaN) is recomputed by its wave on the 3-way bf16 split, with
 // the query operand split from fmap1 in registers.
-template <int R, int NRB, int CMAX, bool H2 = false, int MINW = 2>
+// ST (experiments): 1 stores the outputs write-through (sc1).
+template <int R, int NRB, int CMAX, bool H2 = false, int MINW = 2, int ST = 0>
 __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* __restrict__ f1,
                                                                const float* __restrict__ coords,
                                                                float* __restrict__ out,
@@ -491,7 +492,11 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
       v = __fadd_rn(v, __fmul_rn(__fmul_rn(s01, 1.f - dy), dx));
       v = __fadd_rn(v, __fmul_rn(__fmul_rn(s10, dy), 1.f - dx));
       v = __fadd_rn(v, __fmul_rn(__fmul_rn(s11, dy), dx));
-      o[(long long)(oy + RD * ox) * g.N] = v / g.divisor;
+      if constexpr (ST == 1)
+        __hip_atomic_store(o + (long long)(oy + RD * ox) * g.N, v / g.divisor, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      else
+        o[(long long)(oy + RD * ox) * g.N] = v / g.divisor;
     }
   }
 }
@@ -1572,6 +1577,14 @@ extern "C" int dxr_xp_alt(const float* fmap1, const float* const* fmap2_levels, 
     const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
     const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
     hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 2, 256, true, 3>), grid, dim3(256), 0, stream,
+                       fmap1, coords, out, g, (int)W, tiles_x);
+    return dxr::launch_status();
+  }
+  if (xp == 30) {   // sc1 (write-through) output stores
+    const int H1 = g.N / (int)W;
+    const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
+    const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
+    hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3, 1>), grid, dim3(256), 0, stream,
                        fmap1, coords, out, g, (int)W, tiles_x);
     return dxr::launch_status();
   }

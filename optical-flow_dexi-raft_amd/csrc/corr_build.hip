@@ -205,27 +205,9 @@ __device__ __forceinline__ OT to_out(float v) {
   else return v;
 }
 
-// Store 8 consecutive values (two float4 read from LDS) as OT: 16 B of bf16 or
-// 2 x 16 B of f32.
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
-
-template <typename OT, int EX = 0>
-__device__ __forceinline__ void store8(OT* dst, const float* src) {
-  const float4 a = f4(src), c = f4(src + 4);
-  if constexpr (sizeof(OT) == 2) {
-    u32x4v u;
-    u.x = (uint32_t)to_out<OT>(a.x) | ((uint32_t)to_out<OT>(a.y) << 16);
-    u.y = (uint32_t)to_out<OT>(a.z) | ((uint32_t)to_out<OT>(a.w) << 16);
-    u.z = (uint32_t)to_out<OT>(c.x) | ((uint32_t)to_out<OT>(c.y) << 16);
-    u.w = (uint32_t)to_out<OT>(c.z) | ((uint32_t)to_out<OT>(c.w) << 16);
-    if constexpr ((EX & 2) != 0) __builtin_nontemporal_store(u, reinterpret_cast<u32x4v*>(dst));
-    else *reinterpret_cast<u32x4v*>(dst) = u;
-  } else {
-    *reinterpret_cast<float4*>(dst) = a;
-    *reinterpret_cast<float4*>(dst + 4) = c;
-  }
-}
+typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 // Paged epilogue (levels 0..3 of one page), shared by the f32 and bf16 builds.
 // acc holds this wave's 32 queries x 8x16 targets, already divided by sqrt(D).
@@ -234,8 +216,6 @@ __device__ __forceinline__ void store8(OT* dst, const float* src) {
 // or pools of zeros) and never read.  Every pooled value is computed from the
 // f32 values of the level above, in the reference's window order
 // ((v00+v01)+v10)+v11 (F.avg_pool2d), then rounded to OT once.
-typedef float f32x4v __attribute__((ext_vector_type(4)));
-
 // `wave`: which 32 queries of the page this wave holds (and its private LDS
 // staging region).
 // EX (experiments): bit 0 syncs only the wave around its private staging
@@ -251,19 +231,46 @@ __device__ __forceinline__ void epi_sync() {
     __syncthreads();
   }
 }
-template <int EX>
-__device__ __forceinline__ void epi_st4(float* p, const float4 v) {
-  if constexpr ((EX & 2) != 0) {
-    const f32x4v w = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(w, reinterpret_cast<f32x4v*>(p));
+// EX bit 2: buffer stores from a workgroup-uniform base `ub` (a level's page)
+// with cache-policy bits AUX = EX >> 8 (16 = sc1, write-through; 18 = sc1 nt;
+// 17 = sc0 sc1; 2 = nt), 16 when EX >> 8 is 0.
+template <int EX, typename V, typename T>
+__device__ __forceinline__ void epi_put(T* ub, T* p, const V v) {
+  constexpr int AUX = (EX >> 8) ? (EX >> 8) : 16;
+  if constexpr ((EX & 4) != 0) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(ub, (short)0, 0x7fffffff, 0x00020000);
+    const unsigned off = (unsigned)((p - ub) * (long long)sizeof(T));
+    if constexpr (sizeof(V) == 16)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), r, off, 0, AUX);
+    else if constexpr (sizeof(V) == 8)
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, v), r, off, 0, AUX);
+    else if constexpr (sizeof(V) == 4)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, AUX);
+    else
+      __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, v), r, off, 0, AUX);
+  } else if constexpr ((EX & 2) != 0 && sizeof(V) >= 8) {
+    __builtin_nontemporal_store(v, reinterpret_cast<V*>(p));
   } else {
-    *reinterpret_cast<float4*>(p) = v;
+    *reinterpret_cast<V*>(p) = v;
   }
 }
-template <int EX, typename V>
-__device__ __forceinline__ void epi_stv(void* p, const V v) {
-  if constexpr ((EX & 2) != 0) __builtin_nontemporal_store(v, reinterpret_cast<V*>(p));
-  else *reinterpret_cast<V*>(p) = v;
+// Store 8 consecutive values (two float4 read from LDS) as OT: 16 B of bf16 or
+// 2 x 16 B of f32.
+template <typename OT, int EX = 0>
+__device__ __forceinline__ void store8(OT* ub, OT* dst, const float* src) {
+  const float4 a = f4(src), c = f4(src + 4);
+  if constexpr (sizeof(OT) == 2) {
+    u32x4v u;
+    u.x = (uint32_t)to_out<OT>(a.x) | ((uint32_t)to_out<OT>(a.y) << 16);
+    u.y = (uint32_t)to_out<OT>(a.z) | ((uint32_t)to_out<OT>(a.w) << 16);
+    u.z = (uint32_t)to_out<OT>(c.x) | ((uint32_t)to_out<OT>(c.y) << 16);
+    u.w = (uint32_t)to_out<OT>(c.z) | ((uint32_t)to_out<OT>(c.w) << 16);
+    epi_put<EX>(ub, dst, u);
+  } else {
+    epi_put<EX>(ub, dst, f32x4v{a.x, a.y, a.z, a.w});
+    epi_put<EX>(ub, dst + 4, f32x4v{c.x, c.y, c.z, c.w});
+  }
 }
 
 template <typename OT, int EX = 0>
@@ -275,7 +282,8 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
 
   // Level 0: 16 queries per round staged as [q][8][16] f32 rows, then streamed
   // as 1 KiB wave stores.
-  OT* pg0 = pyr + g.loff[0] + page * (BM * NTGT) + (long long)wave * 32 * NTGT;
+  OT* const pb0 = pyr + g.loff[0] + page * (BM * NTGT);   // page bases (workgroup-uniform)
+  OT* pg0 = pb0 + (long long)wave * 32 * NTGT;
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     if ((j >> 4) == r) {
@@ -293,14 +301,15 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
       for (int k = 0; k < 8; ++k) {
         const int qq = 2 * k + (lane >> 5);
         const int off = (lane & 31) * 4;
-        epi_st4<EX>(pg0 + (r * 16 + qq) * NTGT + off, f4(wl + qq * P0 + off));
+        { const float4 x = f4(wl + qq * P0 + off);
+          epi_put<EX>(pb0, pg0 + (r * 16 + qq) * NTGT + off, f32x4v{x.x, x.y, x.z, x.w}); }
       }
     } else {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int qq = 4 * k + (lane >> 4);
         const int off = (lane & 15) * 8;
-        store8<OT, EX>(pg0 + (r * 16 + qq) * NTGT + off, wl + qq * P0 + off);
+        store8<OT, EX>(pb0, pg0 + (r * 16 + qq) * NTGT + off, wl + qq * P0 + off);
       }
     }
     epi_sync<EX>();
@@ -335,20 +344,22 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
   }
   epi_sync<EX>();
   {
-    OT* pg1 = pyr + g.loff[1] + page * (BM * NTGT / 4) + (long long)wave * 32 * (NTGT / 4);
+    OT* const pb1 = pyr + g.loff[1] + page * (BM * NTGT / 4);
+    OT* pg1 = pb1 + (long long)wave * 32 * (NTGT / 4);
     if constexpr (sizeof(OT) == 4) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int qq = 8 * k + (lane >> 3);
         const int off = (lane & 7) * 4;
-        epi_st4<EX>(pg1 + qq * 32 + off, f4(wl + qq * P1 + off));
+        { const float4 x = f4(wl + qq * P1 + off);
+        epi_put<EX>(pb1, pg1 + qq * 32 + off, f32x4v{x.x, x.y, x.z, x.w}); }
       }
     } else {
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         const int qq = 16 * k + (lane >> 2);
         const int off = (lane & 3) * 8;
-        store8<OT, EX>(pg1 + qq * 32 + off, wl + qq * P1 + off);
+        store8<OT, EX>(pb1, pg1 + qq * 32 + off, wl + qq * P1 + off);
       }
     }
   }
@@ -356,14 +367,15 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
 
   // Level 2: [q][2][4] per page; lane (j, h) writes row h (a 1 KiB wave run).
   {
-    OT* pg2 = pyr + g.loff[2] + page * (BM * NTGT / 16) + (long long)wave * 32 * 8 + j * 8 + 4 * h;
+    OT* const pb2 = pyr + g.loff[2] + page * (BM * NTGT / 16);
+    OT* pg2 = pb2 + (long long)wave * 32 * 8 + j * 8 + 4 * h;
     if constexpr (sizeof(OT) == 4) {
-      epi_st4<EX>(pg2, make_float4(l2[h][0], l2[h][1], l2[h][2], l2[h][3]));
+      epi_put<EX>(pb2, pg2, f32x4v{l2[h][0], l2[h][1], l2[h][2], l2[h][3]});
     } else {
       u32x2v w;
       w.x = (uint32_t)to_out<OT>(l2[h][0]) | ((uint32_t)to_out<OT>(l2[h][1]) << 16);
       w.y = (uint32_t)to_out<OT>(l2[h][2]) | ((uint32_t)to_out<OT>(l2[h][3]) << 16);
-      epi_stv<EX>(pg2, w);
+      epi_put<EX>(pb2, pg2, w);
     }
   }
   if (g.levels < 4) return;
@@ -373,8 +385,9 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
 #pragma unroll
   for (int v = 0; v < 2; ++v)
     l3[v] = (((l2[0][2 * v] + l2[0][2 * v + 1]) + l2[1][2 * v]) + l2[1][2 * v + 1]) * 0.25f;
-  OT* pg3 = pyr + g.loff[3] + page * (BM * 2) + (long long)wave * 32 * 2;
-  pg3[j * 2 + h] = to_out<OT>(l3[h]);
+  OT* const pb3 = pyr + g.loff[3] + page * (BM * 2);
+  OT* pg3 = pb3 + (long long)wave * 32 * 2;
+  epi_put<EX>(pb3, pg3 + j * 2 + h, to_out<OT>(l3[h]));
 }
 
 // PAGED: write the paged pyramid (levels 1..4 fused).  !PAGED: write level 0
@@ -825,7 +838,9 @@ __global__ __launch_bounds__(2 * NT, MINW) void corr_build_bf16_q2_kernel(
   const long long page = pc.page + (long long)half * g.tiles_h * g.tiles_w;
   // non-temporal pyramid stores (KITTI B=8: 556 vs 606 us; the 1.13 GB pyramid
   // outgrows the caches anyway); XP bit 6 turns them off
-  constexpr int EX = (XP & 64) ? 1 : 3;
+  // XP bit 11 (experiments): buffer stores with cache policy bits 12-16 (default
+  // sc1) instead of nt; write-through is slower here (KITTI B=8 step 1,258 -> 1,345 us)
+  constexpr int EX = (XP & 2048) ? (5 | (((XP >> 12) & 31) << 8)) : (XP & 64) ? 1 : 3;
   paged_epilogue<OT, EX>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0, pyr, g, page,
                          w4, lane);
 }
@@ -1230,10 +1245,16 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     return;
   }
   // Wave-local syncs around the per-wave staging (r02: -2 % per Sintel step);
-  // XP bit 5 restores workgroup barriers, bit 6 adds non-temporal stores
-  // (faster build alone, no faster step: the lookups then read the pyramid
-  // from HBM instead of the caches).
-  constexpr int EX = ((XP & 32) ? 0 : 1) | ((XP & 64) ? 2 : 0);
+  // XP bit 5 restores workgroup barriers, bit 6 selects non-temporal stores
+  // (faster build alone than plain stores, no faster step).
+  // Pyramid stores are write-through (sc1, round 2): no dirty lines pile up in
+  // the XCDs' L2s for the K loops' operand reads to evict around, and none are
+  // left for the kernel boundary to write back (Sintel B=1 step 232 -> 211 us
+  // with the lookups' sc1 stores, scripts/xp_step.py; build alone 125 -> 115).
+  // XP (experiments): bit 6 non-temporal stores instead, bit 11 plain stores,
+  // bits 12-16 another buffer-store cache policy.
+  constexpr int EX = ((XP & 32) ? 0 : 1) | ((XP & 64) ? 2 : (XP & 2048) ? 0 : 4) |
+                     (((XP >> 12) & 31) << 8);
   // XP bit 7 (experiments): workgroups write a 32-page ring — the epilogue's
   // instructions, LDS transposes and stores, with the writes L2-resident
   paged_epilogue<OT, EX>(acc, reinterpret_cast<float*>(smem), pyr, g, (XP & 128) ? (pc.page & 31) : pc.page,
@@ -1768,6 +1789,9 @@ extern "C" int dxr_xp_build_bf16(const void* f1, const void* f2, int64_t B, int6
     case 164: return xp_bf16<64>(a, b, p, g, (int)B, stream);
     case 196: return xp_bf16<96>(a, b, p, g, (int)B, stream);
     case 264: return xp_bf16q2<64, 4>(a, b, p, g, (int)B, stream);
+    case 2148: return xp_bf16q2<2048, 4>(a, b, p, g, (int)B, stream);   // sc1 stores
+    case 2150: return xp_bf16q2<2048 | (18 << 12), 4>(a, b, p, g, (int)B, stream);   // sc1 nt
+    case 2151: return xp_bf16q2<2048 | (17 << 12), 4>(a, b, p, g, (int)B, stream);   // sc0 sc1
     default: return DXR_EUNSUPPORTED;
   }
 }
@@ -1816,6 +1840,10 @@ extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t
     case 2017: return xp_h2<17>(f1, f2, pyr, g, (int)B, stream);
     case 2002: return xp_h2<2>(f1, f2, pyr, g, (int)B, stream);
     case 2004: return xp_h2<4>(f1, f2, pyr, g, (int)B, stream);
+    case 4048: return xp_h2<2048>(f1, f2, pyr, g, (int)B, stream);    // plain pyramid stores
+    case 4050: return xp_h2<18 << 12>(f1, f2, pyr, g, (int)B, stream);   // sc1 nt
+    case 4051: return xp_h2<17 << 12>(f1, f2, pyr, g, (int)B, stream);   // sc0 sc1
+    case 4052: return xp_h2<2 << 12>(f1, f2, pyr, g, (int)B, stream);    // nt (buffer)
     case 1012:
       hipLaunchKernelGGL((corr_build_split_kernel<float, false, 2, 4, 0, false, true, true>),
                          remap_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);

@@ -257,9 +257,11 @@ __device__ __forceinline__ void wide_phase0(const float* __restrict__ coords, co
   }
 }
 
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
 // XP: timing ablations, instantiated only by the experiments build target
 // (DXR_EXPERIMENTS): bit 0 skips the window gathers, 1 the output stores,
-// 2 returns after phase 0.
+// 2 returns after phase 0; bits 12-14 select another output store form (4: plain).
 template <int R, typename PT, int NT_ = 512, int XP = 0>
 __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
     const PT* __restrict__ pyr, const float* __restrict__ coords, float* __restrict__ out,
@@ -301,6 +303,47 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
   __syncthreads();
 
   // ---- phase 2
+  constexpr int STM = (XP >> 12) & 7;
+  if constexpr (STM >= 1 && STM <= 3) {
+    // XP bits 12-14 = 1..3 (experiments): thread = (4 consecutive queries, output
+    // class), one 16-byte store along queries per class — plain (1), nt (2) or
+    // sc1 write-through (3, a buffer store with the sc1 cache-policy bit).
+    // Needs N % 4 == 0 (checked by the host).
+    constexpr int QG = QB / 4, NC4 = C::NT / QG;
+    const int qa = 4 * (tid % QG), cls4 = tid / QG;
+    if (q0 + qa >= g.N) return;
+    float* ob4 = out + ((long long)b * g.cout + (long long)l * K) * g.N + q0;
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(ob4, (short)0, 0x7fffffff,
+                                                                        0x00020000);
+    for (int k = cls4; k < K; k += NC4) {
+      const int ox = k / RD, oy = k - ox * RD;
+      float r4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int qi = qa + i;
+        const float4 xd = xs[ox * QB + qi], yd = ys[oy * QB + qi];
+        const float* p = cells + qi * C::QS + __float_as_int(yd.x) + __float_as_int(xd.x);
+        const float v00 = p[0], v01 = p[1], v10 = p[RS], v11 = p[RS + 1];
+        const float nw = __fmul_rn(yd.z, xd.z), ne = __fmul_rn(yd.z, xd.y);
+        const float sw = __fmul_rn(yd.y, xd.z), se = __fmul_rn(yd.y, xd.y);
+        float r = __fmul_rn(nw, v00);
+        r = __builtin_fmaf(ne, v01, r);
+        r = __builtin_fmaf(sw, v10, r);
+        r4[i] = __builtin_fmaf(se, v11, r);
+      }
+      typedef float f4v __attribute__((ext_vector_type(4)));
+      const f4v w = {r4[0], r4[1], r4[2], r4[3]};
+      const unsigned eo = (unsigned)(k * g.N + qa);
+      if constexpr (STM == 1) {
+        *reinterpret_cast<f4v*>(ob4 + eo) = w;
+      } else if constexpr (STM == 2) {
+        __builtin_nontemporal_store(w, reinterpret_cast<f4v*>(ob4 + eo));
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, w), ro, eo * 4u, 0, 16);
+      }
+    }
+    return;
+  }
   const int qq = tid % QB, cls = tid / QB;
   if (q0 + qq >= g.N) return;
   const float* cq = cells + qq * C::QS;
@@ -318,6 +361,18 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
     r = __builtin_fmaf(se, v11, r);
     if constexpr ((XP & 2) != 0) {
       if (r == 1234.5f) ob[(unsigned)(k * g.N)] = r;
+    } else if constexpr (STM == 0) {
+      // write-through (sc1) output stores (round 2): the outputs leave the XCD's
+      // L2 while the kernel runs instead of as dirty lines the next kernel
+      // boundary writes back (Sintel B=1 9.5 -> 8.5 us, B=8 58.0 -> 54.6 us)
+      __hip_atomic_store(ob + (unsigned)(k * g.N), r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if constexpr (STM >= 5) {   // experiments: buffer stores, policy sc1 nt / sc0 sc1 / nt
+      constexpr int AUX = STM == 5 ? 18 : STM == 6 ? 17 : 2;
+      float* ob0 = out + ((long long)b * g.cout + (long long)l * K) * g.N + q0;
+      const __amdgpu_buffer_rsrc_t ro =
+          __builtin_amdgcn_make_buffer_rsrc(ob0, (short)0, 0x7fffffff, 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r), ro, (unsigned)(k * g.N + qq) * 4u, 0,
+                                            AUX);
     } else {
       ob[(unsigned)(k * g.N)] = r;
     }
@@ -1191,6 +1246,15 @@ extern "C" int dxr_xp_lookup(const void* pyramid, int pyr_dtype, int64_t B, int6
       case 100: return xp_lookup2(p, coords, out, g, (int)B, stream);
       case 256: return xp_lookup_nt<256>(p, coords, out, g, (int)B, stream);
       case 1024: return xp_lookup_nt<1024>(p, coords, out, g, (int)B, stream);
+      // store forms (bits 12-14): 16-byte plain / nt / sc1, scalar plain (r02 before sc1),
+      // scalar buffer stores sc1 nt / sc0 sc1 / nt
+      case 0x1000: return g.N % 4 ? DXR_EUNSUPPORTED : xp_lookup_k<0x1000>(p, coords, out, g, (int)B, stream);
+      case 0x2000: return g.N % 4 ? DXR_EUNSUPPORTED : xp_lookup_k<0x2000>(p, coords, out, g, (int)B, stream);
+      case 0x3000: return g.N % 4 ? DXR_EUNSUPPORTED : xp_lookup_k<0x3000>(p, coords, out, g, (int)B, stream);
+      case 0x4000: return xp_lookup_k<0x4000>(p, coords, out, g, (int)B, stream);
+      case 0x5000: return xp_lookup_k<0x5000>(p, coords, out, g, (int)B, stream);
+      case 0x6000: return xp_lookup_k<0x6000>(p, coords, out, g, (int)B, stream);
+      case 0x7000: return xp_lookup_k<0x7000>(p, coords, out, g, (int)B, stream);
       default: return DXR_EUNSUPPORTED;
     }
   }
@@ -1201,6 +1265,9 @@ extern "C" int dxr_xp_lookup(const void* pyramid, int pyr_dtype, int64_t B, int6
     case 0: return xp_lookup_k<0>(p, coords, out, g, (int)B, stream);
     case 1: return xp_lookup_k<1>(p, coords, out, g, (int)B, stream);
     case 2: return xp_lookup_k<2>(p, coords, out, g, (int)B, stream);
+    case 0x1000: return g.N % 4 ? DXR_EUNSUPPORTED : xp_lookup_k<0x1000>(p, coords, out, g, (int)B, stream);
+    case 0x3000: return g.N % 4 ? DXR_EUNSUPPORTED : xp_lookup_k<0x3000>(p, coords, out, g, (int)B, stream);
+    case 0x4000: return xp_lookup_k<0x4000>(p, coords, out, g, (int)B, stream);
     default: return DXR_EUNSUPPORTED;
   }
 }

@@ -9,6 +9,8 @@ after a build replay, so the lookup time includes whatever the build left in
 the caches (e.g. non-temporal pyramid stores that bypass them).
 
 Usage: python scripts/xp_step.py [--xp 1003,2032,2096] [--B 1 --H 55 --W 128]
+A variant "X:Y" runs build variant X with ``dxr_xp_lookup`` variant Y instead of
+the product lookup (e.g. 1003:16384, sc1 lookup stores).
 """
 from __future__ import annotations
 
@@ -49,6 +51,8 @@ def main():
     lib.dxr_corr_lookup.restype = ctypes.c_int
     lib.dxr_corr_lookup.argtypes = [vp, ctypes.c_int, i64, i64, i64, ctypes.c_int, ctypes.c_int, vp,
                                     vp, vp]
+    lib.dxr_xp_lookup.restype = ctypes.c_int
+    lib.dxr_xp_lookup.argtypes = [vp, ctypes.c_int, i64, i64, i64, vp, vp, ctypes.c_int, vp]
     dev = torch.device("cuda", 0)
     B, D, H, W = a.B, 256, a.H, a.W
     g = torch.Generator(device=dev)
@@ -64,17 +68,22 @@ def main():
     pyr = torch.empty(nat.load().dxr_pyramid_numel(B, H, W, 4), device=dev,
                       dtype=torch.bfloat16 if bf else torch.float32)
     out = torch.empty((B, 324, H, W), device=dev)
-    xps = [int(x) for x in a.xp.split(",")]
+    xps = a.xp.split(",")
     side = torch.cuda.Stream()
 
     def build(xp, s):
-        st = xbuild(f1.data_ptr(), f2.data_ptr(), B, D, H, W, pyr.data_ptr(), xp, s)
+        st = xbuild(f1.data_ptr(), f2.data_ptr(), B, D, H, W, pyr.data_ptr(), int(xp.split(":")[0]), s)
         assert st == 0, (xp, st)
 
-    def lookups(s):
+    def lookups(s, xp="0"):
+        lx = int(xp.split(":")[1]) if ":" in xp else None
         for c in coords:
-            st = lib.dxr_corr_lookup(pyr.data_ptr(), 1 if bf else 0, B, H, W, 4, 4, c.data_ptr(),
-                                     out.data_ptr(), s)
+            if lx is None:
+                st = lib.dxr_corr_lookup(pyr.data_ptr(), 1 if bf else 0, B, H, W, 4, 4, c.data_ptr(),
+                                         out.data_ptr(), s)
+            else:
+                st = lib.dxr_xp_lookup(pyr.data_ptr(), 1 if bf else 0, B, H, W, c.data_ptr(),
+                                       out.data_ptr(), lx, s)
             assert st == 0, st
 
     graphs = {}
@@ -82,14 +91,14 @@ def main():
         for xp in xps:
             s = side.cuda_stream
             build(xp, s)
-            lookups(s)
+            lookups(s, xp)
             side.synchronize()
             gs, gl = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(gs, stream=side):
                 build(xp, torch.cuda.current_stream().cuda_stream)
-                lookups(torch.cuda.current_stream().cuda_stream)
+                lookups(torch.cuda.current_stream().cuda_stream, xp)
             with torch.cuda.graph(gl, stream=side):
-                lookups(torch.cuda.current_stream().cuda_stream)
+                lookups(torch.cuda.current_stream().cuda_stream, xp)
             graphs[xp] = (gs, gl)
     torch.cuda.synchronize()
     step = {xp: [] for xp in xps}
