@@ -19,7 +19,10 @@ and reported.  Rank 0 prints ONE JSON line.
 
 Execution (``--mode graph``, default): ``value`` is timed on ONE HIP graph per
 step (build + 12 lookups), replayed K times — the launch-bound lookups would
-otherwise be host-bound in Python.  Kernel durations for the rooflines come from
+otherwise be host-bound in Python.  Before the W warmup steps the step is
+replayed untimed for ``--clock-warmup-s`` (0.5 s): MI355X raises its clocks only
+after some milliseconds of load, and 30 timed steps behind 3 warmups read 11 %
+below the steady rate (round 2: 3,936 vs 4,414-4,454 pairs/s at 300-2,000 steps).  Kernel durations for the rooflines come from
 HIP events on the launch stream around alternating replays of the step graph
 and of a graph of its 12 lookups: lookup = that graph / 12, build = step -
 lookups, i.e. each kernel in the step's own conditions, including one
@@ -253,8 +256,8 @@ def cpu_baseline(H, W, budget_s, impl="torch", reps=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="sintel", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=None, help="pairs per GPU per step (weak scaling)")
     ap.add_argument("--total-pairs", type=int, default=None,
@@ -266,6 +269,10 @@ def main():
     ap.add_argument("--layout", default="nchw", choices=["nchw", "nhwc"],
                     help="fmap memory format: nchw (the reference's) or nhwc (channels-last "
                          "encoders, SURVEY §8(f) row 4)")
+    ap.add_argument("--clock-warmup-s", type=float, default=0.5,
+                    help="untimed replays of the step for this long before the W warmup steps: "
+                         "the GPU raises its clocks only after ~ms of load (30 timed steps after "
+                         "3 warmups read 11 %% low on MI355X)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-impl", default="torch", choices=["torch", "numpy"],
@@ -313,7 +320,7 @@ def main():
     timing = ("hip events around alternating replays of the step graph and of a graph of its "
               "12 lookups: lookup = lookups graph / 12, build = step - lookups")
     with torch.no_grad(), torch.cuda.stream(stream):
-        for _ in range(max(args.warmup, 1)):          # eager warmup (also a JIT-free check)
+        for _ in range(max(min(args.warmup, 3), 1)):  # eager warmup (also a JIT-free check)
             step()
         torch.cuda.synchronize()
         if args.mode == "graph":
@@ -322,12 +329,22 @@ def main():
             g_step = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_step, stream=stream):
                 step()
-            for _ in range(max(args.warmup, 1)):
-                g_step.replay()
             run_step = g_step.replay
         else:
             run_step = step
             timing = "hip events around eager launches"
+        torch.cuda.synchronize()
+        # clock warm-up: replay the full step (same work, same outputs) until the
+        # chip has been under load for --clock-warmup-s, then the W warmup steps
+        t_w = time.perf_counter()
+        n_clock = 0
+        while time.perf_counter() - t_w < args.clock_warmup_s:
+            for _ in range(20):
+                run_step()
+            n_clock += 20
+            torch.cuda.synchronize()
+        for _ in range(args.warmup):
+            run_step()
         torch.cuda.synchronize()
 
         barrier(world)
@@ -415,6 +432,8 @@ def main():
                 "step_timing": "one HIP graph per step (build + 12 lookups)"
                                if args.mode == "graph" else "eager launches",
                 "kernel_timing": timing,
+                "clock_warmup": f"{n_clock} untimed step replays ({args.clock_warmup_s} s) before "
+                                f"the {args.warmup} warmup steps",
             },
             "pair_checksums": {
                 "what": "float64 sum of each pair's 12th lookup output, all-gathered over "
