@@ -371,6 +371,17 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
     OT* pg2 = pb2 + (long long)wave * 32 * 8 + j * 8 + 4 * h;
     if constexpr (sizeof(OT) == 4) {
       epi_put<EX>(pb2, pg2, f32x4v{l2[h][0], l2[h][1], l2[h][2], l2[h][3]});
+    } else if constexpr ((EX & 8) != 0) {
+      // wide form: lane j (both rows of query j live in every lane) writes the
+      // query's 8 bf16 as one 16-byte store
+      if (h == 0) {
+        u32x4v w;
+        w.x = (uint32_t)to_out<OT>(l2[0][0]) | ((uint32_t)to_out<OT>(l2[0][1]) << 16);
+        w.y = (uint32_t)to_out<OT>(l2[0][2]) | ((uint32_t)to_out<OT>(l2[0][3]) << 16);
+        w.z = (uint32_t)to_out<OT>(l2[1][0]) | ((uint32_t)to_out<OT>(l2[1][1]) << 16);
+        w.w = (uint32_t)to_out<OT>(l2[1][2]) | ((uint32_t)to_out<OT>(l2[1][3]) << 16);
+        epi_put<EX>(pb2, pg2, w);
+      }
     } else {
       u32x2v w;
       w.x = (uint32_t)to_out<OT>(l2[h][0]) | ((uint32_t)to_out<OT>(l2[h][1]) << 16);
@@ -387,7 +398,22 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
     l3[v] = (((l2[0][2 * v] + l2[0][2 * v + 1]) + l2[1][2 * v]) + l2[1][2 * v + 1]) * 0.25f;
   OT* const pb3 = pyr + g.loff[3] + page * (BM * 2);
   OT* pg3 = pb3 + (long long)wave * 32 * 2;
-  epi_put<EX>(pb3, pg3 + j * 2 + h, to_out<OT>(l3[h]));
+  if constexpr ((EX & 8) != 0 && sizeof(OT) == 4) {
+    // wide form: lane L < 16 writes queries 2L, 2L+1 (both cells each) as one
+    // 16-byte store; every lane holds both cells of its query
+    const float a0 = __shfl(l3[0], (2 * lane) & 63), a1 = __shfl(l3[1], (2 * lane) & 63);
+    const float n0 = __shfl(l3[0], (2 * lane + 1) & 63), n1 = __shfl(l3[1], (2 * lane + 1) & 63);
+    if (lane < 16) epi_put<EX>(pb3, pg3 + lane * 4, f32x4v{a0, a1, n0, n1});
+  } else if constexpr ((EX & 8) != 0) {
+    // wide form (bf16): lane L < 8 writes queries 4L .. 4L+3 as one 16-byte store
+    const uint32_t pr = (uint32_t)to_out<OT>(l3[0]) | ((uint32_t)to_out<OT>(l3[1]) << 16);
+    const uint32_t p1 = __shfl(pr, (4 * lane + 1) & 63), p2 = __shfl(pr, (4 * lane + 2) & 63),
+                   p3 = __shfl(pr, (4 * lane + 3) & 63);
+    const uint32_t p0 = __shfl(pr, (4 * lane) & 63);
+    if (lane < 8) epi_put<EX>(pb3, pg3 + lane * 8, u32x4v{p0, p1, p2, p3});
+  } else {
+    epi_put<EX>(pb3, pg3 + j * 2 + h, to_out<OT>(l3[h]));
+  }
 }
 
 // PAGED: write the paged pyramid (levels 1..4 fused).  !PAGED: write level 0
@@ -840,7 +866,8 @@ __global__ __launch_bounds__(2 * NT, MINW) void corr_build_bf16_q2_kernel(
   // outgrows the caches anyway); XP bit 6 turns them off
   // XP bit 11 (experiments): buffer stores with cache policy bits 12-16 (default
   // sc1) instead of nt; write-through is slower here (KITTI B=8 step 1,258 -> 1,345 us)
-  constexpr int EX = (XP & 2048) ? (5 | (((XP >> 12) & 31) << 8)) : (XP & 64) ? 1 : 3;
+  constexpr int EX = ((XP & 2048) ? (5 | (((XP >> 12) & 31) << 8)) : (XP & 64) ? 1 : 3) |
+                     ((XP & (1 << 17)) ? 8 : 0);   // bit 17: 16-byte level-2/3 stores
   paged_epilogue<OT, EX>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0, pyr, g, page,
                          w4, lane);
 }
@@ -1254,7 +1281,7 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
   // XP (experiments): bit 6 non-temporal stores instead, bit 11 plain stores,
   // bits 12-16 another buffer-store cache policy.
   constexpr int EX = ((XP & 32) ? 0 : 1) | ((XP & 64) ? 2 : (XP & 2048) ? 0 : 4) |
-                     (((XP >> 12) & 31) << 8);
+                     (((XP >> 12) & 31) << 8) | ((XP & (1 << 17)) ? 8 : 0);
   // XP bit 7 (experiments): workgroups write a 32-page ring — the epilogue's
   // instructions, LDS transposes and stores, with the writes L2-resident
   paged_epilogue<OT, EX>(acc, reinterpret_cast<float*>(smem), pyr, g, (XP & 128) ? (pc.page & 31) : pc.page,
@@ -1792,6 +1819,8 @@ extern "C" int dxr_xp_build_bf16(const void* f1, const void* f2, int64_t B, int6
     case 2148: return xp_bf16q2<2048, 4>(a, b, p, g, (int)B, stream);   // sc1 stores
     case 2150: return xp_bf16q2<2048 | (18 << 12), 4>(a, b, p, g, (int)B, stream);   // sc1 nt
     case 2151: return xp_bf16q2<2048 | (17 << 12), 4>(a, b, p, g, (int)B, stream);   // sc0 sc1
+    case 2200: return xp_bf16q2<1 << 17, 4>(a, b, p, g, (int)B, stream);   // nt, wide levels 2/3 (no gain)
+    case 2201: return xp_bf16q2<2048 | (1 << 17), 4>(a, b, p, g, (int)B, stream);   // sc1, wide
     default: return DXR_EUNSUPPORTED;
   }
 }
@@ -1844,6 +1873,7 @@ extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t
     case 4050: return xp_h2<18 << 12>(f1, f2, pyr, g, (int)B, stream);   // sc1 nt
     case 4051: return xp_h2<17 << 12>(f1, f2, pyr, g, (int)B, stream);   // sc0 sc1
     case 4052: return xp_h2<2 << 12>(f1, f2, pyr, g, (int)B, stream);    // nt (buffer)
+    case 4200: return xp_h2<1 << 17>(f1, f2, pyr, g, (int)B, stream);    // sc1, wide level 3 (no gain)
     case 1012:
       hipLaunchKernelGGL((corr_build_split_kernel<float, false, 2, 4, 0, false, true, true>),
                          remap_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);

@@ -124,9 +124,13 @@ struct WideCfg {
 };
 
 // V consecutive cells of one tile row (or of a row-major level), widened to f32.
-template <int V, typename PT>
+template <int V, typename PT, bool NTL = false>
 __device__ __forceinline__ void load_vec(const PT* p, float* v) {
-  if constexpr (sizeof(PT) == 4 && V == 4) {
+  if constexpr (sizeof(PT) == 4 && V == 4 && NTL) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v x = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  } else if constexpr (sizeof(PT) == 4 && V == 4) {
     const float4 x = *reinterpret_cast<const float4*>(p);
     v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
   } else if constexpr (sizeof(PT) == 4 && V == 2) {
@@ -148,7 +152,7 @@ __device__ __forceinline__ void load_vec(const PT* p, float* v) {
 // Phase 1 for one level type: V-cell vectors, 4 per LDS vector slot.  Split in
 // a load half (registers) and a store half (LDS) so a caller can keep several
 // levels' gathers in flight at once (the fused motion kernel).
-template <int R, int NT_, int V, typename PT>
+template <int R, int NT_, int V, typename PT, bool NTL = false>
 __device__ __forceinline__ void gather_load(const PT* __restrict__ base, int qb0, const LevelAddr& A,
                                             const int2* org, int q0, int N, int tid,
                                             float4 (&v)[WideCfg<R, NT_>::VIT]) {
@@ -171,7 +175,7 @@ __device__ __forceinline__ void gather_load(const PT* __restrict__ base, int qb0
           const int x = x0 + h;
           const unsigned e = qoff + (yoff + (unsigned)(x >> A.ltw)) * (unsigned)A.pageS + yin +
                              (unsigned)(x & A.mw);
-          if (V == 4 || x < A.w) load_vec<V>(base + e, c + h);
+          if (V == 4 || x < A.w) load_vec<V, PT, NTL>(base + e, c + h);
         }
 #pragma unroll
         for (int h = 1; h < 4; ++h)
@@ -196,12 +200,12 @@ __device__ __forceinline__ void gather_store(const float4 (&v)[WideCfg<R, NT_>::
   }
 }
 
-template <int R, int NT_, int V, typename PT>
+template <int R, int NT_, int V, typename PT, bool NTL = false>
 __device__ __forceinline__ void gather_windows(const PT* __restrict__ base, int qb0, const LevelAddr& A,
                                                const int2* org, float* cells, int q0, int N,
                                                int tid) {
   float4 v[WideCfg<R, NT_>::VIT];
-  gather_load<R, NT_, V>(base, qb0, A, org, q0, N, tid, v);
+  gather_load<R, NT_, V, PT, NTL>(base, qb0, A, org, q0, N, tid, v);
   gather_store<R, NT_>(v, cells, tid);
 }
 
@@ -293,8 +297,8 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
     const int qb0 = q0 & ((1 << A.lqb) - 1);
     if (A.lth == 30)
       gather_windows<R, NT_, 1>(base, qb0, A, org, cells, q0, g.N, tid);
-    else if (A.tw >= 4)
-      gather_windows<R, NT_, 4>(base, qb0, A, org, cells, q0, g.N, tid);
+    else if (A.tw >= 4)   // XP bit 3 (experiments): non-temporal gather loads
+      gather_windows<R, NT_, 4, PT, (XP & 8) != 0>(base, qb0, A, org, cells, q0, g.N, tid);
     else if (A.tw == 2)
       gather_windows<R, NT_, 2>(base, qb0, A, org, cells, q0, g.N, tid);
     else
@@ -1243,6 +1247,7 @@ extern "C" int dxr_xp_lookup(const void* pyramid, int pyr_dtype, int64_t B, int6
       case 2: return xp_lookup_k<2>(p, coords, out, g, (int)B, stream);
       case 3: return xp_lookup_k<3>(p, coords, out, g, (int)B, stream);
       case 4: return xp_lookup_k<4>(p, coords, out, g, (int)B, stream);
+      case 8: return xp_lookup_k<8>(p, coords, out, g, (int)B, stream);
       case 100: return xp_lookup2(p, coords, out, g, (int)B, stream);
       case 256: return xp_lookup_nt<256>(p, coords, out, g, (int)B, stream);
       case 1024: return xp_lookup_nt<1024>(p, coords, out, g, (int)B, stream);
