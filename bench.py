@@ -22,12 +22,11 @@ step (build + 12 lookups), replayed K times — the launch-bound lookups would
 otherwise be host-bound in Python.  Before the W warmup steps the step is
 replayed untimed for ``--clock-warmup-s`` (0.5 s): MI355X raises its clocks only
 after some milliseconds of load, and 30 timed steps behind 3 warmups read 11 %
-below the steady rate (round 2: 3,936 vs 4,414-4,454 pairs/s at 300-2,000 steps).  Kernel durations for the rooflines come from
-HIP events on the launch stream around alternating replays of the step graph
-and of a graph of its 12 lookups: lookup = that graph / 12, build = step -
-lookups, i.e. each kernel in the step's own conditions, including one
-same-stream kernel boundary (~1.5 us, MI355X_MICROARCH.md "boundary") and the
-graph launch (~10 us per replay, charged to the build).
+below the steady rate (round 2: 3,936 vs 4,414-4,454 pairs/s at 300-2,000 steps).
+Kernel durations for the rooflines: lookup = HIP events on the launch stream
+around back-to-back replays of a graph of the step's 12 lookups, / 12 (one
+lookup plus its same-stream kernel boundary); build = the timed step time minus
+12 lookups (the build plus its boundary and the graph launch).
 ``--mode eager`` times plain Python calls instead.
 """
 from __future__ import annotations
@@ -317,8 +316,8 @@ def main():
         build()
         lookups()
 
-    timing = ("hip events around alternating replays of the step graph and of a graph of its "
-              "12 lookups: lookup = lookups graph / 12, build = step - lookups")
+    timing = ("lookup = hip events around back-to-back replays of a graph of the step's 12 "
+              "lookups / 12 (kernel + its same-stream boundary); build = timed step - 12 lookups")
     with torch.no_grad(), torch.cuda.stream(stream):
         for _ in range(max(min(args.warmup, 3), 1)):  # eager warmup (also a JIT-free check)
             step()
@@ -362,32 +361,31 @@ def main():
         sums = gather_pairs(local_sums, total)
         finite = bool(torch.isfinite(sums).all().item())
 
-        # Kernel-timing pass (outside the timed region), in the conditions of the
-        # step: replays of the step graph alternate with replays of a graph of
-        # the same 12 lookups; lookup time = that graph / 12, build (stage a+b,
-        # or the on-the-fly block's pools/layout) = step - lookups.  (Graphs of
-        # back-to-back builds heat the chip into lower clocks: 159 -> 223 us per
-        # build over 48 launches in an r02 kernel trace.)
+        # Kernel-timing pass (outside the timed region): the 12 lookups as one graph,
+        # replayed back to back after the timed steps (steady clocks): lookup = that
+        # time / 12, i.e. one lookup plus its same-stream kernel boundary; build
+        # (stage a+b, or the on-the-fly block's pools/layout) = the timed step time
+        # - 12 lookups, i.e. the build plus its boundary and the graph launch.
+        # Compare with the rocprofv3 kernel durations and the idle time per step of
+        # the same command's kernel trace (scripts/trace_gaps.py, profiles/).
         if args.mode == "graph":
             keep = dict(state)            # the step graph's own tensors stay allocated
             cb = state["cb"]
             g_look = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_look, stream=stream, pool=g_step.pool()):
                 [cb(c) for c in coords]
-            g_look.replay()
-            torch.cuda.synchronize()
-            reps = max(10, min(args.steps, 50))
-            ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(reps)]
-            for e in ev:
-                e[0].record(stream)
-                g_step.replay()
-                e[1].record(stream)
+            for _ in range(5):
                 g_look.replay()
-                e[2].record(stream)
             torch.cuda.synchronize()
-            t_step = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
-            t_look = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
-            build_ms, look_ms = t_step - t_look, t_look / ITERS
+            reps = max(20, min(args.steps, 100))
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                g_look.replay()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            look_ms = e0.elapsed_time(e1) / reps / ITERS
+            build_ms = elapsed / args.steps * 1e3 - ITERS * look_ms
             del keep
         else:
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Step timeline from a rocprofv3 kernel trace of bench.py (profiles only).
+
+A step of the bench is one build (or, for the on-the-fly block, its pools /
+layout kernels) followed by 12 lookups.  For every step whose build kernels are
+followed by exactly 12 lookup kernels and then the next step's build (the back-to-back
+replays of the clock warm-up, the warmup steps and the timed steps), this
+reports medians of: the build kernels' duration, the lookup kernels' durations,
+the step span (build start to next build start), and the idle time of the span
+(span minus the kernels' durations: kernel boundaries and graph launches).
+
+Usage: python scripts/trace_gaps.py <run_kernel_trace.csv>
+"""
+from __future__ import annotations
+
+import csv
+import json
+import sys
+
+import numpy as np
+
+
+def main(path: str) -> None:
+    rows = []
+    with open(path, newline="") as f:
+        for r in csv.DictReader(f):
+            name = r.get("Kernel_Name", "")
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
+    rows.sort()
+    prod = ("corr_build", "pool", "transpose")
+    is_look = [("corr_lookup_wide_kernel" in n or "alt_corr_mfma_kernel" in n) for _, _, n in rows]
+    is_prep = [any(p in n for p in prod) and not is_look[i] for i, (_, _, n) in enumerate(rows)]
+    # step starts: a build-side kernel right after a lookup (or first in the trace)
+    starts = [i for i in range(len(rows)) if is_prep[i] and (i == 0 or is_look[i - 1])]
+    b_us, l_us, span_us, idle_us = [], [], [], []
+    for a, b in zip(starts, starts[1:]):
+        looks = [i for i in range(a, b) if is_look[i]]
+        prep = [i for i in range(a, b) if is_prep[i]]
+        if len(looks) != 12 or len(looks) + len(prep) != b - a:
+            continue
+        b_us.append(sum(rows[i][1] - rows[i][0] for i in prep) / 1e3)
+        l_us.extend((rows[i][1] - rows[i][0]) / 1e3 for i in looks)
+        span = (rows[b][0] - rows[a][0]) / 1e3
+        busy = sum((rows[i][1] - rows[i][0]) for i in range(a, b)) / 1e3
+        span_us.append(span)
+        idle_us.append(span - busy)
+    if not b_us:
+        print(json.dumps({"steps": 0, "note": "no build + 12 lookup steps found"}))
+        return
+    med = lambda v: round(float(np.median(v)), 2)  # noqa: E731
+    print(json.dumps({
+        "steps": len(b_us),
+        "build_us_median": med(b_us), "lookup_us_median": med(l_us),
+        "step_span_us_median": med(span_us), "idle_us_per_step_median": med(idle_us),
+        "what": "back-to-back steps of the bench's step graph: build + 12 lookups, from the "
+                "rocprofv3 kernel trace of the same command (durations are kernel begin-end)",
+    }))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
