@@ -761,6 +761,15 @@ __global__ __launch_bounds__(2 * NT, MINW) void corr_build_bf16_q2_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int half = wave >> 2, w4 = wave & 3;
+  if constexpr ((XP & 768) != 0) {
+    // XP bits 8-9 (experiments): the workgroups of the first dispatch wave in CU
+    // slot 1 (linear id 256..511, breadth-first dispatch) sleep k * 8K cycles,
+    // k = (XP >> 8) & 3, so the two slots' epilogues fall at different times.
+    const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    if (L >= 256 && L < 512) {
+      for (int i = 0; i < ((XP >> 8) & 3); ++i) __builtin_amdgcn_s_sleep(127);
+    }
+  }
   const PageCoord pc = page_coord<true, 2>(g);
   const int th0 = pc.tyi * TH, tw0 = pc.txi * TW;
   const int q0 = pc.qblk * BM;                      // first of the two blocks
@@ -1820,6 +1829,9 @@ extern "C" int dxr_xp_build_bf16(const void* f1, const void* f2, int64_t B, int6
     case 2150: return xp_bf16q2<2048 | (18 << 12), 4>(a, b, p, g, (int)B, stream);   // sc1 nt
     case 2151: return xp_bf16q2<2048 | (17 << 12), 4>(a, b, p, g, (int)B, stream);   // sc0 sc1
     case 2200: return xp_bf16q2<1 << 17, 4>(a, b, p, g, (int)B, stream);   // nt, wide levels 2/3 (no gain)
+    case 2300: return xp_bf16q2<256, 4>(a, b, p, g, (int)B, stream);    // slot-1 stagger k = 1
+    case 2301: return xp_bf16q2<512, 4>(a, b, p, g, (int)B, stream);    // k = 2
+    case 2302: return xp_bf16q2<768, 4>(a, b, p, g, (int)B, stream);    // k = 3
     case 2201: return xp_bf16q2<2048 | (1 << 17), 4>(a, b, p, g, (int)B, stream);   // sc1, wide
     default: return DXR_EUNSUPPORTED;
   }
