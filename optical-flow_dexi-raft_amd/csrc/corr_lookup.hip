@@ -878,7 +878,8 @@ __global__ __launch_bounds__(NT) void corr_lookup_conv1x1_kernel(
 // ---------------------------------------------------------------------------
 typedef _Float16 mh8 __attribute__((ext_vector_type(8)));
 
-template <int R, typename PT, int NT = 512, int PF = 4>
+// ST (experiments): 1 = write-through (sc1) output stores.
+template <int R, typename PT, int NT = 512, int PF = 4, int ST = 0>
 __global__ __launch_bounds__(NT, 4) void corr_lookup_conv1x1_h2_kernel(
     const PT* __restrict__ pyr, const float* __restrict__ coords, const float4* __restrict__ wpk,
     const float* __restrict__ bias, float* __restrict__ out, LookupGeom g, int cout, int relu) {
@@ -1055,7 +1056,11 @@ __global__ __launch_bounds__(NT, 4) void corr_lookup_conv1x1_h2_kernel(
           const int orow = ob * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
           float v = acc[r] + (bias ? bias[orow] : 0.f);
           if (relu && v < 0.f) v = 0.f;      // NaN stays NaN, as torch.relu
-          ob_out[(long long)orow * g.N] = v;
+          if constexpr (ST == 1)
+            __hip_atomic_store(ob_out + (long long)orow * g.N, v, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          else
+            ob_out[(long long)orow * g.N] = v;
         }
       }
     }
@@ -1302,8 +1307,14 @@ extern "C" int dxr_xp_lookup_conv1x1(const float* pyramid, int64_t B, int64_t H,
   else if (xp == 1)
     hipLaunchKernelGGL((corr_lookup_conv1x1_h2_kernel<4, float, 512, 4>), grid, dim3(512), 0,
                        stream, pyramid, coords, wpl, bias, out, g, (int)cout, 1);
-  else
+  else if (xp == 2)
     hipLaunchKernelGGL((corr_lookup_conv1x1_h2_kernel<4, float, 1024, 4>), grid, dim3(1024), 0,
+                       stream, pyramid, coords, wpl, bias, out, g, (int)cout, 1);
+  else if (xp == 3)   // sc1 output stores, 512 threads
+    hipLaunchKernelGGL((corr_lookup_conv1x1_h2_kernel<4, float, 512, 4, 1>), grid, dim3(512), 0,
+                       stream, pyramid, coords, wpl, bias, out, g, (int)cout, 1);
+  else   // sc1 output stores, 1024 threads
+    hipLaunchKernelGGL((corr_lookup_conv1x1_h2_kernel<4, float, 1024, 4, 1>), grid, dim3(1024), 0,
                        stream, pyramid, coords, wpl, bias, out, g, (int)cout, 1);
   return dxr::launch_status();
 }
