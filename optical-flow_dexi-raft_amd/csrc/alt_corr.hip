@@ -251,11 +251,18 @@ __device__ __forceinline__ void alt_split8h(const float (&x)[8], uint4& h, uint4
 // range, or inf/NaN) is recomputed by its wave on the 3-way bf16 split, with
 // the query operand split from fmap1 in registers.
 // ST (experiments): 1 stores the outputs write-through (sc1).
-template <int R, int NRB, int CMAX, bool H2 = false, int MINW = 2, int ST = 0>
+// BIN: the workgroup's 32 queries are not a 4 x 8 pixel tile but 32 consecutive
+// entries of perm (this coordinate set's and level's query list sorted by window
+// position, alt_bin_kernel), so their windows — and the union box — are compact
+// whatever the flow field; `tile` is then the index of that chunk of 32.
+// PF: k steps of cell-vector loads kept in flight (a ring of PF register stages).
+template <int R, int NRB, int CMAX, bool H2 = false, int MINW = 2, int ST = 0, bool BIN = false,
+          int PF = 1>
 __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* __restrict__ f1,
                                                                const float* __restrict__ coords,
                                                                float* __restrict__ out,
-                                                               AltGeom g, int W1, int tiles_x) {
+                                                               AltGeom g, int W1, int tiles_x,
+                                                               const int* __restrict__ perm) {
   constexpr int RD = 2 * R + 1, RD1 = RD + 1, NCELL = RD1 * RD1;
   constexpr int CHUNK = 4 * 32 * NRB;                       // box cells per chunk
   constexpr int KB = CMAX / 8;                              // 8-channel blocks
@@ -264,6 +271,7 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
   __shared__ float S[TQ * NCELL];                           // window dot products
   __shared__ int4 qinfo[TQ];                                // {x0, y0, live, -}
   __shared__ int box[4];                                    // bx0, by0, bw, bh
+  __shared__ int qlist[TQ];                                 // BIN: query index or -1
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // Workgroups are dealt round-robin to the 8 XCDs; XCD k takes the k-th
@@ -283,13 +291,31 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
   const float* f2b = lv.f2 + (long long)bf * lv.H2 * lv.W2 * g.C;
   const int H1 = g.N / W1;
   const int nkb = g.C / 8;
+  // query of lane/slot qq: a pixel of the 4 x 8 tile, or (BIN) entry tile*32 + qq of
+  // the sorted list; -1 past the image / the list
+  auto query_of = [&](int qq) -> int {
+    if constexpr (BIN) {
+      return qlist[qq];
+    } else {
+      const int qy = ty * TQY + qq / TQX, qx = tx * TQX + qq % TQX;
+      return (qy < H1 && qx < W1) ? qy * W1 + qx : -1;
+    }
+  };
+  if constexpr (BIN) {
+    if (tid < TQ) {
+      // perm: per (coordinate set, level) gridDim.x * 32 entries, -1 = padding
+      qlist[tid] = perm[((long long)z * gridDim.y + blockIdx.y) * ((long long)gridDim.x * TQ) +
+                        tile * TQ + tid];
+    }
+    __syncthreads();
+  }
 
   // ---- query coordinates, window origins, the windows' union box
   if (tid < TQ) {
-    const int qy = ty * TQY + tid / TQX, qx = tx * TQX + tid % TQX;
+    const int qsel = query_of(tid);
     int x0 = 0, y0 = 0, live = 0;
-    if (qy < H1 && qx < W1) {
-      const int q = qy * W1 + qx;
+    if (qsel >= 0) {
+      const int q = qsel;
       const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
       const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
       const float xf = floorf(x), yf = floorf(y);
@@ -322,8 +348,14 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
   // query operand planes: unit (kb, q) -> f1[q][8 kb .. 8 kb + 8), split once
   for (int u = tid; u < nkb * TQ; u += 256) {
     const int kb = u / TQ, qq = u - kb * TQ;
-    const int qy = min(ty * TQY + qq / TQX, H1 - 1), qx = min(tx * TQX + qq % TQX, W1 - 1);
-    const float* src = f1b + (long long)(qy * W1 + qx) * g.C + kb * 8;
+    int qsrc0;   // padding slots read a valid query (their outputs are not stored)
+    if constexpr (BIN) {
+      qsrc0 = max(query_of(qq), 0);
+    } else {
+      const int qy = min(ty * TQY + qq / TQX, H1 - 1), qx = min(tx * TQX + qq % TQX, W1 - 1);
+      qsrc0 = qy * W1 + qx;
+    }
+    const float* src = f1b + (long long)qsrc0 * g.C + kb * 8;
     const float4 a = *reinterpret_cast<const float4*>(src);
     const float4 c = *reinterpret_cast<const float4*>(src + 4);
     const float x[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
@@ -364,22 +396,42 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
       for (int rb = 0; rb < NRB; ++rb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[rb][r] = acc2[rb][r] = 0.f;
-      float4 ca[NRB], cb[NRB];
+      const int nst = nkb / 2;
+      float4 ra[PF][NRB], rv[PF][NRB];   // ring of in-flight k steps
 #pragma unroll
-      for (int rb = 0; rb < NRB; ++rb) {
-        ca[rb] = *reinterpret_cast<const float4*>(src[rb]);
-        cb[rb] = *reinterpret_cast<const float4*>(src[rb] + 4);
-      }
-      // fallback form: this lane's query operand straight from fmap1
-      const int fqy = min(ty * TQY + j / TQX, H1 - 1), fqx = min(tx * TQX + j % TQX, W1 - 1);
-      const float* qsrc = f1b + (long long)(fqy * W1 + fqx) * g.C + 8 * kh;
-      for (int ks = 0; ks < nkb / 2; ++ks) {
-        float4 na[NRB], nb[NRB];
-        if (ks + 1 < nkb / 2) {
+      for (int u = 0; u < PF; ++u)
+        if (u < nst) {
 #pragma unroll
           for (int rb = 0; rb < NRB; ++rb) {
-            na[rb] = *reinterpret_cast<const float4*>(src[rb] + (ks + 1) * 16);
-            nb[rb] = *reinterpret_cast<const float4*>(src[rb] + (ks + 1) * 16 + 4);
+            ra[u][rb] = *reinterpret_cast<const float4*>(src[rb] + u * 16);
+            rv[u][rb] = *reinterpret_cast<const float4*>(src[rb] + u * 16 + 4);
+          }
+        }
+      // fallback form: this lane's query operand straight from fmap1
+      int fq;
+      if constexpr (BIN) {
+        fq = max(query_of(j), 0);
+      } else {
+        const int fqy = min(ty * TQY + j / TQX, H1 - 1), fqx = min(tx * TQX + j % TQX, W1 - 1);
+        fq = fqy * W1 + fqx;
+      }
+      const float* qsrc = f1b + (long long)fq * g.C + 8 * kh;
+      for (int ks0 = 0; ks0 < nst; ks0 += PF)
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const int ks = ks0 + u;
+        if (ks >= nst) break;
+        float4 ca[NRB], cb[NRB];
+#pragma unroll
+        for (int rb = 0; rb < NRB; ++rb) {
+          ca[rb] = ra[u][rb];
+          cb[rb] = rv[u][rb];
+        }
+        if (ks + PF < nst) {
+#pragma unroll
+          for (int rb = 0; rb < NRB; ++rb) {
+            ra[u][rb] = *reinterpret_cast<const float4*>(src[rb] + (ks + PF) * 16);
+            rv[u][rb] = *reinterpret_cast<const float4*>(src[rb] + (ks + PF) * 16 + 4);
           }
         }
         if constexpr (M2) {
@@ -429,13 +481,6 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
             acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh, acc[rb], 0, 0, 0);
           }
         }
-        if (ks + 1 < nkb / 2) {
-#pragma unroll
-          for (int rb = 0; rb < NRB; ++rb) {
-            ca[rb] = na[rb];
-            cb[rb] = nb[rb];
-          }
-        }
       }
       if constexpr (M2) {
 #pragma unroll
@@ -475,9 +520,8 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
 
   // ---- bilinear combination, as the per-query form (reference order)
   const int qq = tid & (TQ - 1), cls = tid / TQ;
-  const int qy = ty * TQY + qq / TQX, qx = tx * TQX + qq % TQX;
-  if (qy >= H1 || qx >= W1) return;
-  const int q = qy * W1 + qx;
+  const int q = query_of(qq);
+  if (q < 0) return;
   const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
   const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
   const float dx = x - floorf(x), dy = y - floorf(y);
@@ -1135,6 +1179,275 @@ __global__ __launch_bounds__(256, 2) void alt_corr_mfma16_kernel(const float* __
 }
 #endif  // DXR_EXPERIMENTS
 
+// ---------------------------------------------------------------------------
+// Query binning for the on-the-fly block (BIN form of alt_corr_mfma_kernel).
+// One workgroup per (level, coordinate set): a counting sort of the N queries by
+// the bin of their window position — floor of the level coordinate, clamped to
+// the level, in bins of 2^bsx x 2^bsy cells (about 32 queries per bin at the
+// level's query density) walked in snake order, so consecutive bins are
+// neighbours; non-finite coordinates go last.  perm[(z * levels + l) * N + i].
+// The order inside a bin follows the LDS atomics (not fixed); every query's
+// outputs are computed on their own, so they do not depend on it.
+// ---------------------------------------------------------------------------
+constexpr int BIN_MAX = 8192;
+struct BinGeom {
+  int bsx[8], bsy[8], nbx[8], nby[8];
+};
+
+BinGeom make_bins(const AltGeom& g, int levels) {
+  BinGeom b;
+  for (int l = 0; l < levels; ++l) {
+    const int h2 = g.lv[l].H2, w2 = g.lv[l].W2;
+    const double dens = (double)g.N / ((double)h2 * w2);
+    int lg = 0;
+    while ((1 << lg) * dens < 32.0 && lg < 12) ++lg;   // bin area 2^lg ~ 32 queries
+    int by = lg / 2, bx = lg - by;
+    while (((w2 + (1 << bx) - 1) >> bx) * ((h2 + (1 << by) - 1) >> by) > BIN_MAX) {
+      if (bx <= by) ++bx; else ++by;
+    }
+    b.bsx[l] = bx;
+    b.bsy[l] = by;
+    b.nbx[l] = (w2 + (1 << bx) - 1) >> bx;
+    b.nby[l] = (h2 + (1 << by) - 1) >> by;
+  }
+  return b;
+}
+
+__global__ __launch_bounds__(1024) void alt_bin_kernel(const float* __restrict__ coords,
+                                                       int* __restrict__ perm, AltGeom g,
+                                                       BinGeom bg, int NP) {
+  __shared__ int cnt[BIN_MAX + 1];
+  __shared__ int wsum[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l = blockIdx.x, z = blockIdx.y;
+  const AltLevel lv = g.lv[l];
+  const int nbx = bg.nbx[l], nb = nbx * bg.nby[l], bsx = bg.bsx[l], bsy = bg.bsy[l];
+  const float* cz = coords + (long long)z * g.coord_zstride;
+  for (int i = tid; i <= nb; i += 1024) cnt[i] = 0;
+  __syncthreads();
+  auto bin_of = [&](int q) -> int {
+    const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
+    const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
+    const float xf = floorf(x), yf = floorf(y);
+    if (!(fabsf(xf) < 1.0e8f && fabsf(yf) < 1.0e8f)) return nb;
+    const int cx = min(max((int)xf, 0), lv.W2 - 1), cy = min(max((int)yf, 0), lv.H2 - 1);
+    const int byi = cy >> bsy;
+    int bxi = cx >> bsx;
+    if (byi & 1) bxi = nbx - 1 - bxi;
+    return byi * nbx + bxi;
+  };
+  for (int q = tid; q < g.N; q += 1024) atomicAdd(&cnt[bin_of(q)], 1);
+  __syncthreads();
+  // exclusive scan of cnt[0..nb]: thread t owns a run of `per` bins
+  const int per = (nb + 1 + 1023) / 1024;
+  int loc = 0;
+  for (int k = 0; k < per; ++k) {
+    const int b = tid * per + k;
+    if (b <= nb) loc += cnt[b];
+  }
+  int v = loc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(v, o);
+    if (lane >= o) v += t;
+  }
+  if (lane == 63) wsum[wave] = v;
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int w = 0; w < 16; ++w) {
+      const int t = wsum[w];
+      wsum[w] = acc;
+      acc += t;
+    }
+  }
+  __syncthreads();
+  int run = wsum[wave] + v - loc;
+  for (int k = 0; k < per; ++k) {
+    const int b = tid * per + k;
+    if (b <= nb) {
+      const int c = cnt[b];
+      cnt[b] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  int* pz = perm + ((long long)z * gridDim.x + l) * NP;
+  for (int q = tid; q < g.N; q += 1024) pz[atomicAdd(&cnt[bin_of(q)], 1)] = q;
+  for (int i = g.N + tid; i < NP; i += 1024) pz[i] = -1;
+}
+
+// Parallel form of the binning (three launches per call) with a per-list choice
+// of the order: K1 (alt_bin_count_kernel) walks the queries in 4 x 8-tile order,
+// counts them per bin and sums the union-box area of every spatial tile (the
+// cells the spatial order would multiply); K2 (alt_bin_scan_kernel) scans the
+// counts and keeps the binned order only where its estimated box area is smaller;
+// K3 (alt_bin_scatter_kernel) writes the list: bin order, or the tile order
+// itself (then the main kernel is the spatial form, bit for bit).
+// Workspace (ints): cnt [Z][L][CNT_STRIDE] (bins and the far bin, then the
+// spatial cost and the decision), binid [Z][L][NP], perm [Z][L][NP];
+// NP = whole 4 x 8 tiles x 32.  cnt must be zero before K1.
+constexpr int CNT_STRIDE = BIN_MAX + 4;
+constexpr int CNT_COST = BIN_MAX + 2, CNT_FLAG = BIN_MAX + 3;
+
+__device__ __forceinline__ int bin_of_xy(float xf, float yf, const AltLevel& lv, int nbx, int nb,
+                                         int bsx, int bsy) {
+  if (!(fabsf(xf) < 1.0e8f && fabsf(yf) < 1.0e8f)) return nb;
+  const int cx = min(max((int)xf, 0), lv.W2 - 1), cy = min(max((int)yf, 0), lv.H2 - 1);
+  const int byi = cy >> bsy;
+  int bxi = cx >> bsx;
+  if (byi & 1) bxi = nbx - 1 - bxi;
+  return byi * nbx + bxi;
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void alt_bin_count_kernel(const float* __restrict__ coords,
+                                                            AltGeom g, BinGeom bg, int W1,
+                                                            int tiles_x, int* __restrict__ cnt,
+                                                            int* __restrict__ binid, int NP) {
+  constexpr int RD1 = 2 * R + 2;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int l = blockIdx.y, z = blockIdx.z;
+  const long long zl = (long long)z * gridDim.y + l;
+  const AltLevel lv = g.lv[l];
+  const int H1 = g.N / W1;
+  const int tile = i / TQ, slot = i % TQ;
+  const int qy = (tile / tiles_x) * TQY + slot / TQX, qx = (tile % tiles_x) * TQX + slot % TQX;
+  int* c = cnt + zl * CNT_STRIDE;
+  int lx0 = 0x7fffffff, ly0 = 0x7fffffff, lx1 = -1, ly1 = -1;
+  if (i < NP && qy < H1 && qx < W1) {
+    const int q = qy * W1 + qx;
+    const float* cz = coords + (long long)z * g.coord_zstride;
+    const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
+    const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
+    const float xf = floorf(x), yf = floorf(y);
+    const int nbx = bg.nbx[l], nb = nbx * bg.nby[l];
+    const int bin = bin_of_xy(xf, yf, lv, nbx, nb, bg.bsx[l], bg.bsy[l]);
+    binid[zl * NP + q] = bin;
+    atomicAdd(&c[bin], 1);
+    if (bin < nb) {   // the main kernel's live window, clipped to the level
+      const int x0 = (int)xf - R, y0 = (int)yf - R;
+      if (x0 + RD1 > 0 && x0 < lv.W2 && y0 + RD1 > 0 && y0 < lv.H2) {
+        lx0 = max(x0, 0);
+        ly0 = max(y0, 0);
+        lx1 = min(x0 + RD1, lv.W2);
+        ly1 = min(y0 + RD1, lv.H2);
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < TQ; o <<= 1) {   // union box of this tile (32 lanes)
+    lx0 = min(lx0, __shfl_xor(lx0, o));
+    ly0 = min(ly0, __shfl_xor(ly0, o));
+    lx1 = max(lx1, __shfl_xor(lx1, o));
+    ly1 = max(ly1, __shfl_xor(ly1, o));
+  }
+  if (slot == 0 && lx1 > lx0) atomicAdd(&c[CNT_COST], (lx1 - lx0) * (ly1 - ly0));
+}
+
+template <int R>
+__global__ __launch_bounds__(1024) void alt_bin_scan_kernel(int* __restrict__ cnt, AltGeom g,
+                                                            BinGeom bg) {
+  __shared__ int wsum[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l = blockIdx.x, z = blockIdx.y;
+  int* c = cnt + ((long long)z * gridDim.x + l) * CNT_STRIDE;
+  const int nb = bg.nbx[l] * bg.nby[l];
+  const int per = (nb + 1 + 1023) / 1024;
+  int loc = 0;
+  for (int k = 0; k < per; ++k) {
+    const int b = tid * per + k;
+    if (b <= nb) loc += c[b];
+  }
+  int v = loc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(v, o);
+    if (lane >= o) v += t;
+  }
+  if (lane == 63) wsum[wave] = v;
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int w = 0; w < 16; ++w) {
+      const int t = wsum[w];
+      wsum[w] = acc;
+      acc += t;
+    }
+    // binned estimate: every chunk of 32 spans about one and a half bins along x
+    const int bw = 1 << bg.bsx[l], bh = 1 << bg.bsy[l];
+    const long long est = (long long)((g.N + TQ - 1) / TQ) *
+                          min(bw + bw / 2 + 2 * R + 1, g.lv[l].W2) * min(bh + 2 * R + 1, g.lv[l].H2);
+    c[CNT_FLAG] = est < (long long)c[CNT_COST] ? 1 : 0;
+  }
+  __syncthreads();
+  int run = wsum[wave] + v - loc;
+  for (int k = 0; k < per; ++k) {
+    const int b = tid * per + k;
+    if (b <= nb) {
+      const int t = c[b];
+      c[b] = run;
+      run += t;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void alt_bin_scatter_kernel(AltGeom g, int W1, int tiles_x,
+                                                              int* __restrict__ cnt,
+                                                              const int* __restrict__ binid,
+                                                              int* __restrict__ perm, int NP) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= NP) return;
+  const int l = blockIdx.y, z = blockIdx.z;
+  const long long zl = (long long)z * gridDim.y + l;
+  int* c = cnt + zl * CNT_STRIDE;
+  int* pz = perm + zl * NP;
+  if (c[CNT_FLAG]) {   // bin order: thread i places query i
+    if (i < g.N) pz[atomicAdd(&c[binid[zl * NP + i]], 1)] = i;
+    else pz[i] = -1;
+  } else {             // tile order
+    const int H1 = g.N / W1;
+    const int tile = i / TQ, slot = i % TQ;
+    const int qy = (tile / tiles_x) * TQY + slot / TQX, qx = (tile % tiles_x) * TQX + slot % TQX;
+    pz[i] = (qy < H1 && qx < W1) ? qy * W1 + qx : -1;
+  }
+}
+
+// Binned on-the-fly lookup (K1-K3 + the BIN form).  ws: workspace of
+// alt_ws_ints(...) ints.
+long long alt_ws_ints(long long Z, int levels, int NP) {
+  return Z * levels * ((long long)CNT_STRIDE + 2LL * NP);
+}
+
+template <int R>
+int launch_alt_binned_r(const float* f1, const float* coords, float* out, const AltGeom& g,
+                        int levels, int Z, int W1, int* ws, hipStream_t stream, int upto = 4) {
+  const int H1 = g.N / W1;
+  const int tiles_x = (W1 + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
+  const int NP = tiles_x * tiles_y * TQ;
+  int* cnt = ws;
+  int* binid = cnt + (long long)Z * levels * CNT_STRIDE;
+  int* perm = binid + (long long)Z * levels * NP;
+  const BinGeom bg = make_bins(g, levels);
+  if (hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)Z * levels * CNT_STRIDE, stream) != hipSuccess)
+    return DXR_EHIP;
+  const dim3 gq((unsigned)((NP + 255) / 256), (unsigned)levels, (unsigned)Z);
+  if (upto < 1) return dxr::launch_status();
+  hipLaunchKernelGGL((alt_bin_count_kernel<R>), gq, dim3(256), 0, stream, coords, g, bg, W1, tiles_x,
+                     cnt, binid, NP);
+  if (upto < 2) return dxr::launch_status();
+  hipLaunchKernelGGL((alt_bin_scan_kernel<R>), dim3((unsigned)levels, (unsigned)Z), dim3(1024), 0,
+                     stream, cnt, g, bg);
+  if (upto < 3) return dxr::launch_status();
+  hipLaunchKernelGGL(alt_bin_scatter_kernel, gq, dim3(256), 0, stream, g, W1, tiles_x, cnt, binid,
+                     perm, NP);
+  if (upto < 4) return dxr::launch_status();
+  const dim3 grid((unsigned)(NP / TQ), (unsigned)levels, (unsigned)Z);
+  hipLaunchKernelGGL((alt_corr_mfma_kernel<R, 1, 256, true, 3, 0, true>), grid, dim3(256), 0, stream,
+                     f1, coords, out, g, W1, NP / TQ, perm);
+  return dxr::launch_status();
+}
+
 template <int R, int NRB>
 int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const AltGeom& g,
                       int levels, int Z, int W1, hipStream_t stream) {
@@ -1144,7 +1457,7 @@ int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const Al
   if (g.C > 256) return DXR_EUNSUPPORTED;
   // f16 pair split (r02, 1080p: 227 vs 275 us for the 3-way bf16 split), 3 workgroups/CU
   hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 3>), grid, dim3(256), 0, stream, f1,
-                     coords, out, g, W1, tiles_x);
+                     coords, out, g, W1, tiles_x, nullptr);
   return dxr::launch_status();
 }
 
@@ -1552,6 +1865,13 @@ int xp_alt16(const float* f1, const float* coords, float* out, const AltGeom& g,
 }
 }  // namespace
 
+constexpr long long XP_PERM_MAX = 1LL << 22;
+int xp_np(const AltGeom& g, int W1) {   // perm entries per list: whole 4 x 8 tiles
+  const int H1 = g.N / W1;
+  return ((W1 + TQX - 1) / TQX) * ((H1 + TQY - 1) / TQY) * TQ;
+}
+__device__ int xp_perm[XP_PERM_MAX];   // experiments: binned-form query lists
+
 extern "C" int dxr_xp_alt(const float* fmap1, const float* const* fmap2_levels, const float* coords,
                           float* out, int64_t B, int64_t H, int64_t W, int64_t C, int num_levels,
                           float divisor, int xp, hipStream_t stream) {
@@ -1577,7 +1897,83 @@ extern "C" int dxr_xp_alt(const float* fmap1, const float* const* fmap2_levels, 
     const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
     const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
     hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 2, 256, true, 3>), grid, dim3(256), 0, stream,
-                       fmap1, coords, out, g, (int)W, tiles_x);
+                       fmap1, coords, out, g, (int)W, tiles_x, nullptr);
+    return dxr::launch_status();
+  }
+  if (xp >= 40 && xp <= 42) {
+    // binned form: 40 = binning + binned kernel, 41 = binning only, 42 = binned
+    // kernel only (the perm of the previous call)
+    if ((long long)B * num_levels * xp_np(g, (int)W) > XP_PERM_MAX) return DXR_EUNSUPPORTED;
+    int* perm = nullptr;
+    if (hipGetSymbolAddress(reinterpret_cast<void**>(&perm), HIP_SYMBOL(xp_perm)) != hipSuccess)
+      return DXR_EINVAL;
+    if (xp != 42) {
+      hipLaunchKernelGGL(alt_bin_kernel, dim3((unsigned)num_levels, (unsigned)B), dim3(1024), 0,
+                         stream, coords, perm, g, make_bins(g, num_levels), xp_np(g, (int)W));
+      if (xp == 41) return dxr::launch_status();
+    }
+    const int nchunk = xp_np(g, (int)W) / TQ;
+    const dim3 grid((unsigned)nchunk, (unsigned)num_levels, (unsigned)B);
+    hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3, 0, true>), grid, dim3(256), 0,
+                       stream, fmap1, coords, out, g, (int)W, nchunk, perm);
+    return dxr::launch_status();
+  }
+  if (xp >= 50 && xp <= 54) {   // parallel binning with the per-list order choice (51-54: phases)
+    const int NP = xp_np(g, (int)W);
+    if (alt_ws_ints(B, num_levels, NP) > XP_PERM_MAX) return DXR_EUNSUPPORTED;
+    int* ws = nullptr;
+    if (hipGetSymbolAddress(reinterpret_cast<void**>(&ws), HIP_SYMBOL(xp_perm)) != hipSuccess)
+      return DXR_EINVAL;
+    return launch_alt_binned_r<4>(fmap1, coords, out, g, num_levels, (int)B, (int)W, ws, stream,
+                                  xp == 50 ? 4 : xp - 51);
+  }
+  if (xp == 55) {   // the per-level order decisions of the last xp 50 call -> out[0..levels)
+    int* ws = nullptr;
+    if (hipGetSymbolAddress(reinterpret_cast<void**>(&ws), HIP_SYMBOL(xp_perm)) != hipSuccess)
+      return DXR_EINVAL;
+    for (int l = 0; l < num_levels; ++l) {
+      int v[2];
+      hipMemcpy(v, ws + l * CNT_STRIDE + CNT_COST, 8, hipMemcpyDeviceToHost);
+      const float f[2] = {(float)v[0], (float)v[1]};
+      hipMemcpy(out + 2 * l, f, 8, hipMemcpyHostToDevice);
+    }
+    return DXR_OK;
+  }
+  if (xp >= 43 && xp <= 46) {
+    // binned form with PF k steps of cell loads in flight: 43 PF 4, 44 PF 6, 45 PF 8,
+    // 46 PF 4 at two workgroups per CU
+    if ((long long)B * num_levels * xp_np(g, (int)W) > XP_PERM_MAX) return DXR_EUNSUPPORTED;
+    int* perm = nullptr;
+    if (hipGetSymbolAddress(reinterpret_cast<void**>(&perm), HIP_SYMBOL(xp_perm)) != hipSuccess)
+      return DXR_EINVAL;
+    hipLaunchKernelGGL(alt_bin_kernel, dim3((unsigned)num_levels, (unsigned)B), dim3(1024), 0,
+                       stream, coords, perm, g, make_bins(g, num_levels), xp_np(g, (int)W));
+    const int nchunk = xp_np(g, (int)W) / TQ;
+    const dim3 grid((unsigned)nchunk, (unsigned)num_levels, (unsigned)B);
+    if (xp == 43)
+      hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3, 0, true, 4>), grid, dim3(256), 0,
+                         stream, fmap1, coords, out, g, (int)W, nchunk, perm);
+    else if (xp == 44)
+      hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3, 0, true, 6>), grid, dim3(256), 0,
+                         stream, fmap1, coords, out, g, (int)W, nchunk, perm);
+    else if (xp == 45)
+      hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3, 0, true, 8>), grid, dim3(256), 0,
+                         stream, fmap1, coords, out, g, (int)W, nchunk, perm);
+    else
+      hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 2, 0, true, 4>), grid, dim3(256), 0,
+                         stream, fmap1, coords, out, g, (int)W, nchunk, perm);
+    return dxr::launch_status();
+  }
+  if (xp == 47 || xp == 48) {   // spatial tiles with PF 4 / 8
+    const int H1 = g.N / (int)W;
+    const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
+    const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
+    if (xp == 47)
+      hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3, 0, false, 4>), grid, dim3(256),
+                         0, stream, fmap1, coords, out, g, (int)W, tiles_x, nullptr);
+    else
+      hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3, 0, false, 8>), grid, dim3(256),
+                         0, stream, fmap1, coords, out, g, (int)W, tiles_x, nullptr);
     return dxr::launch_status();
   }
   if (xp == 30) {   // sc1 (write-through) output stores
@@ -1585,7 +1981,7 @@ extern "C" int dxr_xp_alt(const float* fmap1, const float* const* fmap2_levels, 
     const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
     const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
     hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3, 1>), grid, dim3(256), 0, stream,
-                       fmap1, coords, out, g, (int)W, tiles_x);
+                       fmap1, coords, out, g, (int)W, tiles_x, nullptr);
     return dxr::launch_status();
   }
   if (xp == 9) {   // the r01 form: 3-way bf16 split, 2 workgroups/CU
@@ -1593,7 +1989,7 @@ extern "C" int dxr_xp_alt(const float* fmap1, const float* const* fmap2_levels, 
     const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
     const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
     hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, false, 2>), grid, dim3(256), 0, stream,
-                       fmap1, coords, out, g, (int)W, tiles_x);
+                       fmap1, coords, out, g, (int)W, tiles_x, nullptr);
     return dxr::launch_status();
   }
   if (xp == 20 || xp == 21) {   // 8 x 16 query tiles, cells shared through LDS
@@ -1614,10 +2010,10 @@ extern "C" int dxr_xp_alt(const float* fmap1, const float* const* fmap2_levels, 
     const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
     if (xp == 6)
       hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3>), grid, dim3(256), 0, stream,
-                         fmap1, coords, out, g, (int)W, tiles_x);
+                         fmap1, coords, out, g, (int)W, tiles_x, nullptr);
     else
       hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 2>), grid, dim3(256), 0, stream,
-                         fmap1, coords, out, g, (int)W, tiles_x);
+                         fmap1, coords, out, g, (int)W, tiles_x, nullptr);
     return dxr::launch_status();
   }
   if (xp == 3 || xp == 4 || xp == 5) {

@@ -86,6 +86,11 @@ def main():
         torch.cuda.synchronize()
         dev_rel = ((outs[0] - ref).abs().max() / ref.abs().max()).item()
         print(json.dumps({"xp": xp, "max_rel_dev_vs_xp0": dev_rel}), flush=True)
+    if 50 in xps:   # the binned form's per-level order choice (spatial box cost, flag)
+        run(50, 0)
+        run(55, 0)
+        torch.cuda.synchronize()
+        print(json.dumps({"bin_decisions": outs[0].flatten()[:8].tolist()}), flush=True)
     times = {xp: [] for xp in xps}
     for _ in range(a.rounds):
         for xp in xps:
