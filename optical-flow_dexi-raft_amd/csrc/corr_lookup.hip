@@ -385,6 +385,157 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
 
 #ifdef DXR_EXPERIMENTS
 // ---------------------------------------------------------------------------
+// Pipelined persistent lookup (experiment).  A workgroup walks items (32
+// queries x one level of one pair) item = blockIdx.x + k * gridDim.x; while item
+// k's taps are combined and stored (phase 2), item k+1's windows are already in
+// flight (its phase 0 ran before, its coordinates one item earlier still).
+// Same per-sample arithmetic and fused sum as corr_lookup_wide_kernel.
+// One cells buffer (written only after the top barrier, when the previous
+// item's phase 2 is done), double tap data (phase 0 of item k+1 runs while
+// item k's taps are still to be read).
+// ---------------------------------------------------------------------------
+template <int R, int NT_>
+__device__ __forceinline__ void wide_phase0_xy(float cx, float cy, const LevelAddr& A, int l,
+                                               int tid, float4* xs, float4* ys, int2* org) {
+  using C = WideCfg<R, NT_>;
+  constexpr int RD = C::RD, WD = C::WD, RS = C::RS, QB = C::QB, G = C::G;
+  static_assert(C::SIT == 1, "one phase-0 slot per thread");
+  const int Hl = A.h, Wl = A.w;
+  const int slot = tid;
+  if (slot >= QB * G) return;   // whole waves
+  const int j = slot & (G - 1), qq = slot >> C::LG;
+  const float inv = 1.f / (float)(1 << l);
+  const float wm1 = (float)(Wl - 1), hm1 = (float)(Hl - 1);
+  const float ux = sample_coord(__fadd_rn(cx * inv, (float)(j - R)), wm1, wm1 / 2.f);
+  const float uy = sample_coord(__fadd_rn(cy * inv, (float)(j - R)), hm1, hm1 / 2.f);
+  const float flx = floorf(ux), fly = floorf(uy);
+  const bool act = j < RD;
+  int mx = 0x7fffffff, my = 0x7fffffff;
+  if (act) {
+    const bool bad = !(fabsf(flx) < 1.0e7f) || !(fabsf(fly) < 1.0e7f);
+    mx = bad ? FAR_ORIGIN : (int)flx - j;
+    my = bad ? FAR_ORIGIN : (int)fly - j;
+  }
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) {
+    mx = min(mx, __shfl_xor(mx, o));
+    my = min(my, __shfl_xor(my, o));
+  }
+  const bool far = mx + WD <= 0 || mx >= Wl || my + WD <= 0 || my >= Hl;
+  if (j == 0) org[qq] = far ? make_int2(FAR_ORIGIN, FAR_ORIGIN) : make_int2(mx, my);
+  if (act) {
+    const float fx = __fsub_rn(ux, flx), fy = __fsub_rn(uy, fly);
+    const int col = far ? 0 : (int)flx - (mx & ~3);
+    const int row = far ? 0 : ((int)fly - my) * RS;
+    xs[j * QB + qq] = make_float4(__int_as_float(col), fx, __fsub_rn(1.f, fx), 0.f);
+    ys[j * QB + qq] = make_float4(__int_as_float(row), fy, __fsub_rn(1.f, fy), 0.f);
+  }
+}
+
+template <int R, typename PT, int NT_ = 512>
+__global__ __launch_bounds__(NT_) void corr_lookup_pipe_kernel(const PT* __restrict__ pyr,
+                                                               const float* __restrict__ coords,
+                                                               float* __restrict__ out,
+                                                               LookupGeom g, int B) {
+  using C = WideCfg<R, NT_>;
+  constexpr int RD = C::RD, RS = C::RS, K = C::K, QB = C::QB;
+  __shared__ __attribute__((aligned(16))) float cells[QB * C::QS];
+  __shared__ float4 xs[2][RD * QB];
+  __shared__ float4 ys[2][RD * QB];
+  __shared__ int2 org[2][QB];
+  const int tid = threadIdx.x;
+  const int nqb = (g.N + QB - 1) / QB;
+  const int nitems = nqb * g.levels * B;
+  const int stride = gridDim.x;
+  int it = blockIdx.x;
+  if (it >= nitems) return;
+  auto decode = [&](int i, int& b, int& l, int& q0) {
+    const int qb = i % nqb, r = i / nqb;
+    l = r % g.levels;
+    b = r / g.levels;
+    q0 = qb * QB;
+  };
+  auto load_xy = [&](int i, float& cx, float& cy) {
+    cx = 0.f;
+    cy = 0.f;
+    if (i >= nitems) return;
+    int b, l, q0;
+    decode(i, b, l, q0);
+    const int q = q0 + (tid >> C::LG);
+    if (q < g.N && (tid >> C::LG) < QB) {
+      cx = coords[((long long)b * 2 + 0) * g.N + q];
+      cy = coords[((long long)b * 2 + 1) * g.N + q];
+    }
+  };
+  auto gather = [&](int i, const int2* o, float4 (&v)[C::VIT]) {
+    int b, l, q0;
+    decode(i, b, l, q0);
+    const LevelAddr& A = g.lv[l];
+    const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
+    const int qb0 = q0 & ((1 << A.lqb) - 1);
+    if (A.lth == 30)
+      gather_load<R, NT_, 1>(base, qb0, A, o, q0, g.N, tid, v);
+    else if (A.tw >= 4)
+      gather_load<R, NT_, 4>(base, qb0, A, o, q0, g.N, tid, v);
+    else if (A.tw == 2)
+      gather_load<R, NT_, 2>(base, qb0, A, o, q0, g.N, tid, v);
+    else
+      gather_load<R, NT_, 1>(base, qb0, A, o, q0, g.N, tid, v);
+  };
+
+  float cx, cy, ncx, ncy;
+  load_xy(it, cx, cy);
+  {
+    int b, l, q0;
+    decode(it, b, l, q0);
+    wide_phase0_xy<R, NT_>(cx, cy, g.lv[l], l, tid, xs[0], ys[0], org[0]);
+  }
+  load_xy(it + stride, ncx, ncy);
+  __syncthreads();
+  float4 v[C::VIT];
+  gather(it, org[0], v);
+  for (int k = 0;; ++k) {
+    const int buf = k & 1;
+    __syncthreads();                       // phase 2 of the previous item is done
+    gather_store<R, NT_>(v, cells, tid);
+    const int nx = it + stride;
+    if (nx < nitems) {
+      int b, l, q0;
+      decode(nx, b, l, q0);
+      wide_phase0_xy<R, NT_>(ncx, ncy, g.lv[l], l, tid, xs[buf ^ 1], ys[buf ^ 1], org[buf ^ 1]);
+      load_xy(nx + stride, ncx, ncy);
+    }
+    __syncthreads();                       // cells of `it`, taps of `nx` ready
+    if (nx < nitems) gather(nx, org[buf ^ 1], v);
+    // phase 2 of `it`
+    {
+      int b, l, q0;
+      decode(it, b, l, q0);
+      const int qq = tid % QB, cls = tid / QB;
+      if (q0 + qq < g.N) {
+        const float* cq = cells + qq * C::QS;
+        float* ob = out + ((long long)b * g.cout + (long long)l * K) * g.N + q0 + qq;
+        for (int kk = cls; kk < K; kk += C::NCLS) {
+          const int ox = kk / RD, oy = kk - ox * RD;
+          const float4 xd = xs[buf][ox * QB + qq], yd = ys[buf][oy * QB + qq];
+          const float* p = cq + __float_as_int(yd.x) + __float_as_int(xd.x);
+          const float v00 = p[0], v01 = p[1], v10 = p[RS], v11 = p[RS + 1];
+          const float nw = __fmul_rn(yd.z, xd.z), ne = __fmul_rn(yd.z, xd.y);
+          const float sw = __fmul_rn(yd.y, xd.z), se = __fmul_rn(yd.y, xd.y);
+          float r = __fmul_rn(nw, v00);
+          r = __builtin_fmaf(ne, v01, r);
+          r = __builtin_fmaf(sw, v10, r);
+          r = __builtin_fmaf(se, v11, r);
+          __hip_atomic_store(ob + (unsigned)(kk * g.N), r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    it = nx;
+    if (it >= nitems) break;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Two-level lookup (experiment): a workgroup handles the same 32 queries on
 // levels 2y and 2y+1: phase 0 of both, BOTH levels' window gathers issued into
 // registers before either is staged (twice the loads in flight per thread),
@@ -1224,6 +1375,16 @@ int xp_lookup_nt(const PT* pyr, const float* coords, float* out, const LookupGeo
   return dxr::launch_status();
 }
 template <typename PT>
+int xp_lookup_pipe(const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
+                   int per_cu, hipStream_t stream) {
+  using W = WideCfg<4>;
+  const int nitems = ((g.N + W::QB - 1) / W::QB) * g.levels * B;
+  const int grid = nitems < 256 * per_cu ? nitems : 256 * per_cu;
+  hipLaunchKernelGGL((corr_lookup_pipe_kernel<4, PT>), dim3((unsigned)grid), dim3(W::NT), 0, stream,
+                     pyr, coords, out, g, B);
+  return dxr::launch_status();
+}
+template <typename PT>
 int xp_lookup2(const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
                hipStream_t stream) {
   using W = WideCfg<4>;
@@ -1262,6 +1423,8 @@ extern "C" int dxr_xp_lookup(const void* pyramid, int pyr_dtype, int64_t B, int6
       case 0x2000: return g.N % 4 ? DXR_EUNSUPPORTED : xp_lookup_k<0x2000>(p, coords, out, g, (int)B, stream);
       case 0x3000: return g.N % 4 ? DXR_EUNSUPPORTED : xp_lookup_k<0x3000>(p, coords, out, g, (int)B, stream);
       case 0x4000: return xp_lookup_k<0x4000>(p, coords, out, g, (int)B, stream);
+      case 201: case 202: case 203: case 204: case 206: case 208:
+        return xp_lookup_pipe(p, coords, out, g, (int)B, xp - 200, stream);
       case 0x5000: return xp_lookup_k<0x5000>(p, coords, out, g, (int)B, stream);
       case 0x6000: return xp_lookup_k<0x6000>(p, coords, out, g, (int)B, stream);
       case 0x7000: return xp_lookup_k<0x7000>(p, coords, out, g, (int)B, stream);
@@ -1278,6 +1441,8 @@ extern "C" int dxr_xp_lookup(const void* pyramid, int pyr_dtype, int64_t B, int6
     case 0x1000: return g.N % 4 ? DXR_EUNSUPPORTED : xp_lookup_k<0x1000>(p, coords, out, g, (int)B, stream);
     case 0x3000: return g.N % 4 ? DXR_EUNSUPPORTED : xp_lookup_k<0x3000>(p, coords, out, g, (int)B, stream);
     case 0x4000: return xp_lookup_k<0x4000>(p, coords, out, g, (int)B, stream);
+    case 201: case 202: case 203: case 204: case 206: case 208:
+      return xp_lookup_pipe(p, coords, out, g, (int)B, xp - 200, stream);
     default: return DXR_EUNSUPPORTED;
   }
 }
