@@ -1,0 +1,58 @@
+"""CPU tests of the profile tooling: scripts/trace_gaps.py's step timeline."""
+import csv
+import json
+import subprocess
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+
+
+def _trace(path, steps, build_ns=100_000, look_ns=8_000, gap_ns=700, prep=("corr_build_split_kernel<f>",)):
+    t, rows = 0, []
+    for _ in range(steps):
+        for name in prep:
+            rows.append((name, t, t + build_ns))
+            t += build_ns + gap_ns
+        for _ in range(12):
+            rows.append(("corr_lookup_wide_kernel<4, float, 512, 0>", t, t + look_ns))
+            t += look_ns + gap_ns
+    rows.append(("at::native::reduce_kernel<...>", t, t + 1000))   # a non-step kernel at the end
+    with open(path, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        w.writerows(rows)
+
+
+def _run(path):
+    out = subprocess.run([sys.executable, str(REPO / "scripts" / "trace_gaps.py"), str(path)],
+                         capture_output=True, text=True, check=True).stdout
+    return json.loads(out)
+
+
+def test_trace_gaps_step_timeline(tmp_path):
+    p = tmp_path / "run_kernel_trace.csv"
+    _trace(p, steps=6)
+    r = _run(p)
+    assert r["steps"] == 5                       # the last step has no successor
+    assert r["build_us_median"] == 100.0
+    assert r["lookup_us_median"] == 8.0
+    assert r["step_span_us_median"] == round((100_000 + 12 * 8_000 + 13 * 700) / 1e3, 2)
+    assert r["idle_us_per_step_median"] == round(13 * 700 / 1e3, 2)
+
+
+def test_trace_gaps_on_the_fly_block_prep_kernels(tmp_path):
+    p = tmp_path / "run_kernel_trace.csv"
+    _trace(p, steps=4, prep=("transpose_tile_v4_kernel", "avg_pool2x2_nhwc_kernel"),
+           build_ns=10_000)
+    r = _run(p)
+    assert r["steps"] == 3 and r["build_us_median"] == 20.0
+
+
+def test_trace_gaps_without_steps(tmp_path):
+    p = tmp_path / "run_kernel_trace.csv"
+    with open(p, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        w.writerow(["corr_lookup_wide_kernel<4>", 0, 10])
+    assert _run(p)["steps"] == 0
