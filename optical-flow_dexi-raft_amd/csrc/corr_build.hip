@@ -1081,9 +1081,9 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     if (!(th0 + r < g.H && tw0 + c < g.W)) vb[s] = 0x80000000u;
   }
 
-  float an[8];
-  float4 bn[NBS];
-  auto load = [&](int k0) {
+  float an[8], an2[8];
+  float4 bn[NBS], bn2[NBS];
+  auto load_to = [&](int k0, auto& an, auto& bn) {
     if constexpr ((XP & 4) != 0) {
       if (k0 > 0) return;
     }
@@ -1108,6 +1108,7 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
       }
     }
   };
+  auto load = [&](int k0) { load_to(k0, an, bn); };
   s8v ah, am, al;   // split query operand of the current stage (H2: ah, al)
   using S3 = std::integral_constant<bool, false>;
   using S2 = std::integral_constant<bool, true>;
@@ -1119,7 +1120,7 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
       return split3(a, bb);
     }
   };
-  auto split_a = [&](auto mode) {
+  auto split_a_from = [&](auto mode, auto& an) {
     uint32_t h[4], m[4], l[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -1139,13 +1140,14 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     am = __builtin_bit_cast(s8v, make_uint4(m[0], m[1], m[2], m[3]));
     al = __builtin_bit_cast(s8v, make_uint4(l[0], l[1], l[2], l[3]));
   };
+  auto split_a = [&](auto mode) { split_a_from(mode, an); };
   // NHWC target planes: [target (MFMA row order)][16 k] bf16 at a 48-byte
   // pitch, which keeps the ds_read_b128 lane groups bank-conflict free.
   constexpr int PN = 24;                      // NHWC plane row pitch (bf16)
   constexpr int PLANE_N = NTGT * PN;          // bf16 elements per NHWC plane
   constexpr int PLANE = NHWC ? PLANE_N : PLANE_S;
   // Target planes of a stage: hi, mid, lo (bf16) or hi, lo (H2: f16).
-  auto store_b = [&](int buf, auto mode) {
+  auto store_b_from = [&](int buf, auto mode, auto& bn) {
     uint16_t* P = lh + buf * 3 * PLANE;
 #pragma unroll
     for (int s = 0; s < NBS; ++s) {
@@ -1176,6 +1178,7 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     }
   };
 
+  auto store_b = [&](int buf, auto mode) { store_b_from(buf, mode, bn); };
   const int li = lane & 15;
   const int rd_off = NHWC ? (lane & 31) * PN + 8 * (lane >> 5)
                           : (li >> 2) * PH + 4 * (li & 3) + 16 * ((lane >> 4) & 1) +
@@ -1240,7 +1243,44 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     }
   };
 
+  // XP bit 18 (experiments): the f16-pair K loop with loads two k steps ahead
+  // (a second register stage, the loop unrolled by two; nk even).
+  auto mfma2 = [&](int buf) {
+    const uint16_t* P = lh + buf * 3 * PLANE + rd_off;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const h8v th = __builtin_bit_cast(h8v, frag(P + t * tstride)),
+                tl = __builtin_bit_cast(h8v, frag(P + PLANE + t * tstride));
+      const h8v qh = __builtin_bit_cast(h8v, ah), ql = __builtin_bit_cast(h8v, al);
+      acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc2[t], 0, 0, 0);
+      acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc2[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qh, acc[t], 0, 0, 0);
+    }
+  };
+  auto kloop_pd2 = [&]() {
+    load_to(0, an, bn);
+    load_to(BKS, an2, bn2);
+    store_b_from(0, S2{}, bn);
+    split_a_from(S2{}, an);
+    __syncthreads();
+    for (int ks = 0; ks < nk; ks += 2) {
+      if (ks + 2 < nk) load_to((ks + 2) * BKS, an, bn);
+      mfma2(0);
+      store_b_from(1, S2{}, bn2);
+      split_a_from(S2{}, an2);
+      __syncthreads();
+      if (ks + 3 < nk) load_to((ks + 3) * BKS, an2, bn2);
+      mfma2(1);
+      if (ks + 2 < nk) {
+        store_b_from(0, S2{}, bn);
+        split_a_from(S2{}, an);
+      }
+      __syncthreads();
+    }
+  };
+  constexpr bool PD2 = (XP & (1 << 18)) != 0;
   if constexpr (H2) {
+    if constexpr (PD2) kloop_pd2(); else
     kloop(S2{});
     // Combine (one rounding) and vote: a non-finite sum means an operand of the
     // page overflowed f16 (|x| >= 65520) or was itself inf/NaN; the page is then
@@ -1886,6 +1926,14 @@ extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t
     case 4051: return xp_h2<17 << 12>(f1, f2, pyr, g, (int)B, stream);   // sc0 sc1
     case 4052: return xp_h2<2 << 12>(f1, f2, pyr, g, (int)B, stream);    // nt (buffer)
     case 4200: return xp_h2<1 << 17>(f1, f2, pyr, g, (int)B, stream);    // sc1, wide level 3 (no gain)
+    case 4300:   // loads two k steps ahead, 3 waves/SIMD
+      if (D % 32) return DXR_EUNSUPPORTED;
+      return xp_h2<1 << 18>(f1, f2, pyr, g, (int)B, stream);
+    case 4301:   // loads two k steps ahead, 2 waves/SIMD
+      if (D % 32) return DXR_EUNSUPPORTED;
+      hipLaunchKernelGGL((corr_build_split_kernel<float, false, 2, 4, 1 << 18, false, true>),
+                         build_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);
+      return dxr::launch_status();
     case 1012:
       hipLaunchKernelGGL((corr_build_split_kernel<float, false, 2, 4, 0, false, true, true>),
                          remap_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);
