@@ -20,6 +20,7 @@
 // butterfly transpose (each lane ends with one cell's sum), cell sums go to LDS,
 // and after one barrier every thread emits outputs for one query with coalesced
 // 256-byte wave stores along the query dimension.
+#include <cmath>
 #include <cstdint>
 
 #include <type_traits>
@@ -41,6 +42,7 @@ struct AltGeom {
   int Nc;                 // coordinate sets per pair (reference FFI); 1 for the fused form
   int cout;               // channels per output image
   float divisor;
+  float div_recip = 0.f;  // 1 / divisor when divisor is a power of two (exact), else 0
   long long f1_bstride;   // H1 * W1 * C
   long long coord_zstride, coord_cstride, coord_qstride;
   AltLevel lv[8];
@@ -256,8 +258,10 @@ __device__ __forceinline__ void alt_split8h(const float (&x)[8], uint4& h, uint4
 // position, alt_bin_kernel), so their windows — and the union box — are compact
 // whatever the flow field; `tile` is then the index of that chunk of 32.
 // PF: k steps of cell-vector loads kept in flight (a ring of PF register stages).
+// SLOWIDX (experiments): the r02 index arithmetic (integer division by the box
+// width, IEEE division by the divisor) instead of the exact reciprocal forms.
 template <int R, int NRB, int CMAX, bool H2 = false, int MINW = 2, int ST = 0, bool BIN = false,
-          int PF = 1>
+          int PF = 1, bool SLOWIDX = false>
 __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* __restrict__ f1,
                                                                const float* __restrict__ coords,
                                                                float* __restrict__ out,
@@ -375,6 +379,18 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
   __syncthreads();
 
   const int bx0 = box[0], by0 = box[1], bw = box[2], bh = box[3];
+  // c / bw for box cells (c < 2^24): a float estimate corrected to the exact quotient
+  const float rbw = 1.f / (float)max(bw, 1);
+  auto divbw = [&](int c) -> int {
+    if constexpr (SLOWIDX) {
+      return c / bw;
+    } else {
+      int q = (int)((float)c * rbw);
+      q -= (q * bw > c) ? 1 : 0;
+      q += ((q + 1) * bw <= c) ? 1 : 0;
+      return q;
+    }
+  };
   const int ncells = bw * bh;
   const int j = lane & 31, kh = lane >> 5;
   const int4 qi = qinfo[j];                   // this lane's accumulator column (query j)
@@ -385,7 +401,7 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
     for (int rb = 0; rb < NRB; ++rb) {
       // A operand lane -> cell c0 + 32 (wave NRB + rb) + j, channels 8 kh .. + 8 per k16
       const int c = min(c0 + (wave * NRB + rb) * 32 + j, ncells - 1);
-      const int cy = c / bw, cx = c - cy * bw;
+      const int cy = divbw(c), cx = c - cy * bw;
       src[rb] = f2b + ((long long)(by0 + cy) * lv.W2 + bx0 + cx) * g.C + 8 * kh;
     }
     // cell vectors one k step ahead in registers
@@ -508,7 +524,7 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
         for (int r = 0; r < 16; ++r) {
           const int c = c0 + (wave * NRB + rb) * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
           if (c < ncells) {
-            const int cy = c / bw, cx = c - cy * bw;
+            const int cy = divbw(c), cx = c - cy * bw;
             const int iy = by0 + cy - qi.y, ix = bx0 + cx - qi.x;
             if ((unsigned)iy < (unsigned)RD1 && (unsigned)ix < (unsigned)RD1)
               S[j * NCELL + iy * RD1 + ix] = acc[rb][r];
@@ -536,11 +552,13 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
       v = __fadd_rn(v, __fmul_rn(__fmul_rn(s01, 1.f - dy), dx));
       v = __fadd_rn(v, __fmul_rn(__fmul_rn(s10, dy), 1.f - dx));
       v = __fadd_rn(v, __fmul_rn(__fmul_rn(s11, dy), dx));
+      // v / divisor; a power-of-two divisor (sqrt(256) = 16) scales exactly by its reciprocal
+      const float vd = (!SLOWIDX && g.div_recip != 0.f) ? v * g.div_recip : v / g.divisor;
       if constexpr (ST == 1)
-        __hip_atomic_store(o + (long long)(oy + RD * ox) * g.N, v / g.divisor, __ATOMIC_RELAXED,
+        __hip_atomic_store(o + (long long)(oy + RD * ox) * g.N, vd, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
       else
-        o[(long long)(oy + RD * ox) * g.N] = v / g.divisor;
+        o[(long long)(oy + RD * ox) * g.N] = vd;
     }
   }
 }
@@ -1502,6 +1520,13 @@ int launch_alt(const float* f1, const float* coords, float* out, const AltGeom& 
 
 bool aligned16(const void* p) { return ((uintptr_t)p % 16) == 0; }
 
+// 1 / d when d is a (normal) power of two — then x * (1 / d) == x / d exactly — else 0.
+float pow2_recip(float d) {
+  int e;
+  const float m = std::frexp(d, &e);
+  return (m == 0.5f && e > -125 && e < 126) ? 1.f / d : 0.f;
+}
+
 // ---------------------------------------------------------------------------
 // alt_cuda_corr.backward, reference-FFI form (correlation_kernel.cu:122-256,
 // launched by :288-320).  For query q of pair b and coordinate set n, cell
@@ -1733,6 +1758,7 @@ extern "C" int dxr_alt_corr_forward(const float* fmap1, const float* fmap2, cons
   g.Nc = (int)Nc;
   g.cout = rd * rd;
   g.divisor = 1.f;
+  g.div_recip = 1.f;
   g.f1_bstride = H1 * W1 * C;
   g.coord_zstride = H1 * W1 * 2;
   g.coord_cstride = 1;
@@ -1836,6 +1862,7 @@ extern "C" int dxr_alt_corr_lookup(const float* fmap1, const float* const* fmap2
   g.Nc = 1;
   g.cout = num_levels * rd * rd;
   g.divisor = divisor;
+  g.div_recip = pow2_recip(divisor);
   g.f1_bstride = H * W * C;
   g.coord_zstride = 2 * H * W;
   g.coord_cstride = H * W;
@@ -1883,6 +1910,7 @@ extern "C" int dxr_xp_alt(const float* fmap1, const float* const* fmap2_levels, 
   g.Nc = 1;
   g.cout = num_levels * 81;
   g.divisor = divisor;
+  g.div_recip = pow2_recip(divisor);
   g.f1_bstride = H * W * C;
   g.coord_zstride = 2 * H * W;
   g.coord_cstride = H * W;
@@ -1974,6 +2002,14 @@ extern "C" int dxr_xp_alt(const float* fmap1, const float* const* fmap2_levels, 
     else
       hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3, 0, false, 8>), grid, dim3(256),
                          0, stream, fmap1, coords, out, g, (int)W, tiles_x, nullptr);
+    return dxr::launch_status();
+  }
+  if (xp == 60) {   // r02 index arithmetic (integer / IEEE divisions)
+    const int H1 = g.N / (int)W;
+    const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
+    const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
+    hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3, 0, false, 1, true>), grid, dim3(256),
+                       0, stream, fmap1, coords, out, g, (int)W, tiles_x, nullptr);
     return dxr::launch_status();
   }
   if (xp == 30) {   // sc1 (write-through) output stores
