@@ -1197,6 +1197,7 @@ __global__ __launch_bounds__(256, 2) void alt_corr_mfma16_kernel(const float* __
 }
 #endif  // DXR_EXPERIMENTS
 
+#ifdef DXR_EXPERIMENTS   // query binning: experiments target only
 // ---------------------------------------------------------------------------
 // Query binning for the on-the-fly block (BIN form of alt_corr_mfma_kernel).
 // One workgroup per (level, coordinate set): a counting sort of the N queries by
@@ -1465,6 +1466,8 @@ int launch_alt_binned_r(const float* f1, const float* coords, float* out, const 
                      f1, coords, out, g, W1, NP / TQ, perm);
   return dxr::launch_status();
 }
+
+#endif  // DXR_EXPERIMENTS
 
 template <int R, int NRB>
 int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const AltGeom& g,
