@@ -478,13 +478,13 @@ def main():
         else:
             # on-the-fly lookups: (2r+2)^2 window dot products of length D per query
             # and level, f32-class arithmetic (SURVEY.md §8(d) stage d), priced at
-            # the f32 peak; the default kernel runs them as split-bf16 MFMA GEMMs.
+            # the f32 peak; the default kernel runs them as f16-pair split MFMA GEMMs.
             aflops = alt_lookup_flops(B, H, W)
             achieved = aflops / (look_ms * 1e-3) / 1e12
             akern = "alt_corr_mfma_kernel"
             a_traffic, a_src = pmc_traffic(wl_key, akern + "<")
             res["roofline"] = {
-                "kernel": akern + " (split-bf16 MFMA over query-tile window boxes, f32 "
+                "kernel": akern + " (f16-pair split MFMA over query-tile window boxes, f32 "
                                   "accumulate; stage d, per lookup)",
                 "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F32_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_TFLOPS, 4),
