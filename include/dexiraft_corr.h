@@ -122,10 +122,13 @@ int64_t dxr_pyramid_level_offset(int64_t B, int64_t H, int64_t W, int level);
  *                  (levels beyond 4 need pyr_dtype DXR_F32)
  *   num_levels   : >= 1; every level must be at least 1 x 1
  *   algo         : DXR_BUILD_AUTO, or DXR_BUILD_EXACT_F32 (f32 fmaps only)
- * DXR_F32 inputs compute in f32 class: every f32 operand is split exactly into
- * three bf16 parts and six bf16 x bf16 MFMA products per f32 product are
- * accumulated in f32 (terms below 2^-25 |x y| dropped); with D % 16 != 0, odd W
- * or DXR_BUILD_EXACT_F32 the exact-f32 MFMA v_mfma_f32_32x32x2_f32 is used.
+ * DXR_F32 inputs compute in f32 class: every f32 operand is split into an f16
+ * pair x = hi + 2^-11 lo and three f16 x f16 MFMA products per f32 product are
+ * accumulated in two f32 accumulators (the lo*lo term, <= 2^-22 |x y|, dropped);
+ * a page whose sums are not finite (an operand beyond the f16 range, or inf/NaN)
+ * is recomputed on an exact three-way bf16 split (six products).  With
+ * D % 16 != 0, odd W or DXR_BUILD_EXACT_F32 the exact-f32 MFMA
+ * v_mfma_f32_32x32x2_f32 is used.  Pyramid stores are write-through (sc1).
  * DXR_BF16 inputs use bf16 MFMA with f32 accumulation.  NHWC and NCHW inputs
  * of the same values give bit-identical pyramids.
  */

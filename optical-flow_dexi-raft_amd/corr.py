@@ -312,9 +312,12 @@ class CorrBlock:
     ``[B, num_levels*(2r+1)^2, H, W]`` tensor in the reference's channel order.
 
     fp32 fmaps (the reference's dtype, core/raft.py:139-142) compute in f32
-    class (exact three-way bf16 split of every operand, six bf16 MFMA products
-    per f32 product, f32 accumulation) and store an f32 pyramid.  The pyramid lives in one paged buffer
-    (``_buf``); ``corr_pyramid`` gives the reference-layout levels on demand.
+    class (every operand split into an f16 pair hi + 2^-11 lo, three f16 MFMA
+    products per f32 product into two f32 accumulators, with an in-kernel
+    fallback to an exact three-way bf16 split for operands beyond the f16 range)
+    and store an f32 pyramid; bf16 fmaps build a bf16 pyramid on bf16 MFMA.  The
+    pyramid lives in one paged buffer (``_buf``); ``corr_pyramid`` gives the
+    reference-layout levels on demand.
     """
 
     def __init__(self, fmap1, fmap2, num_levels=4, radius=4):

@@ -110,7 +110,7 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
 
 // Exact hi/mid/lo split of 8 floats into three 8 x bf16 MFMA operands
 // (x = hi + mid + lo; hi and mid round to nearest, lo keeps the residual's top
-// 16 bits).  Used by the split-bf16 f32-class MFMA kernels.
+// 16 bits).  Used by the bf16 kernels and the three-way bf16 fallback of the f32-class kernels.
 __device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
   typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
   typedef float f2_t __attribute__((ext_vector_type(2)));

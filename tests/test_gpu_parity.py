@@ -470,8 +470,8 @@ def test_split_build_agrees_with_exact_f32_build(dx, shape):
 
 
 def test_split_build_f32_accuracy(dx):
-    """The split build (f32 operands as exact hi+mid+lo bf16 triples, six bf16
-    MFMA products, f32 accumulation) has f32-class error: within RTOL of the
+    """The split build (f32 operands as f16 pairs hi + 2^-11 lo, three f16 MFMA
+    products into two f32 accumulators) has f32-class error: within RTOL of the
     float64 oracle everywhere, and no worse than 2x the f32-MFMA build's own error."""
     H, W = 55, 128
     f1 = dg.fmap(51, 1, 256, H, W, "fnet")
