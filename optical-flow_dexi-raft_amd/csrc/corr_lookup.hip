@@ -647,16 +647,23 @@ __global__ __launch_bounds__(512) void corr_lookup_backward_kernel(const float* 
   }
   __syncthreads();
 
+  // Sample oy's taps sit on window rows row(oy) and row(oy)+1 with row(oy) in
+  // {oy, oy+1} (row = floor_oy - min_j(floor_j - j)), so row cy hears only from
+  // oy in {cy-2, cy-1, cy}: three candidates instead of all RD, in the same
+  // ascending order (the skipped terms had weight 0, and 0 * inf/NaN gradients
+  // no longer leak into untapped cells, as in grid_sample's backward).
   for (int e = tid; e < QB * WD * RD; e += NT) {
     const int qq = e / (WD * RD), rem = e - qq * (WD * RD);
     const int cy = rem / RD, ox = rem - cy * RD;
     float acc = 0.f;
 #pragma unroll
-    for (int oy = 0; oy < RD; ++oy) {
+    for (int d = 2; d >= 0; --d) {
+      const int oy = cy - d;
+      if (oy < 0 || oy >= RD) continue;
       const float4 yd = ys[oy * QB + qq];
       const int row = __float_as_int(yd.x) / RS;
-      const float w = row == cy ? yd.z : (row + 1 == cy ? yd.y : 0.f);
-      acc = __builtin_fmaf(G[(ox * RD + oy) * QB + qq], w, acc);
+      if (row == cy || row + 1 == cy)
+        acc = __builtin_fmaf(G[(ox * RD + oy) * QB + qq], row == cy ? yd.z : yd.y, acc);
     }
     T[e] = acc;
   }
@@ -664,7 +671,21 @@ __global__ __launch_bounds__(512) void corr_lookup_backward_kernel(const float* 
 
   float* base = gpyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
   const int qb0 = q0 & ((1 << A.lqb) - 1);
-  for (int e = tid; e < QB * WD * RS; e += NT) {
+  // Every (query, cell) of the workgroup is a distinct gradient-pyramid element
+  // (each query owns its images), so the read-modify-writes are independent:
+  // all sums first, then all reads in flight together, then all writes
+  // (round 2; one dependent round trip per element before).
+  constexpr int NE = QB * WD * RS, ITER = (NE + NT - 1) / NT;
+  float accv[ITER];
+  unsigned offv[ITER];
+  bool okv[ITER];
+#pragma unroll
+  for (int i = 0; i < ITER; ++i) {
+    const int e = tid + i * NT;
+    okv[i] = false;
+    accv[i] = 0.f;
+    offv[i] = 0u;
+    if (e >= NE) continue;
     const int qq = e / (WD * RS), rem = e - qq * (WD * RS);
     const int cy = rem / RS, cx = rem - cy * RS;
     const int2 o = org[qq];
@@ -676,18 +697,28 @@ __global__ __launch_bounds__(512) void corr_lookup_backward_kernel(const float* 
     if ((unsigned)yy >= (unsigned)A.h || (unsigned)xx >= (unsigned)A.w) continue;
     float acc = 0.f;
     const float* t = T + (qq * WD + cy) * RD;
+    // col(ox) - (o.x & 3) is ox or ox+1: column cx hears from ox in {c-2, c-1, c}
+    const int c = cx - (o.x & 3);
 #pragma unroll
-    for (int ox = 0; ox < RD; ++ox) {
+    for (int d = 2; d >= 0; --d) {
+      const int ox = c - d;
+      if (ox < 0 || ox >= RD) continue;
       const float4 xd = xs[ox * QB + qq];
       const int col = __float_as_int(xd.x);
-      const float w = col == cx ? xd.z : (col + 1 == cx ? xd.y : 0.f);
-      acc = __builtin_fmaf(t[ox], w, acc);
+      if (col == cx || col + 1 == cx) acc = __builtin_fmaf(t[ox], col == cx ? xd.z : xd.y, acc);
     }
-    const unsigned off = (unsigned)(qb0 + qq) * (unsigned)A.S +
-                         ((unsigned)((yy >> A.lth) * A.tx + (xx >> A.ltw))) * (unsigned)A.pageS +
-                         (unsigned)((yy & A.mh) * A.tw + (xx & A.mw));
-    base[off] += acc;
+    okv[i] = true;
+    accv[i] = acc;
+    offv[i] = (unsigned)(qb0 + qq) * (unsigned)A.S +
+              ((unsigned)((yy >> A.lth) * A.tx + (xx >> A.ltw))) * (unsigned)A.pageS +
+              (unsigned)((yy & A.mh) * A.tw + (xx & A.mw));
   }
+  float old[ITER];
+#pragma unroll
+  for (int i = 0; i < ITER; ++i) old[i] = okv[i] ? base[offv[i]] : 0.f;
+#pragma unroll
+  for (int i = 0; i < ITER; ++i)
+    if (okv[i]) base[offv[i]] = old[i] + accv[i];
 }
 
 template <int R>
