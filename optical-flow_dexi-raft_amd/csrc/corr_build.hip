@@ -961,6 +961,19 @@ __device__ __forceinline__ Split2 split2h(float a, float b) {
   return {h, cvt_pk_f16(ra, rb)};
 }
 
+// The same split with the residual formed and rounded by mixed-precision FMAs:
+// lo = RNE_f16(fma(hi, -2048, 2048 x)).  2048 x and 2048 hi are exact and so is
+// their difference (= 2048 (x - hi)), so the single rounding is the same RNE as
+// split2h's; hi stays an f16 operand (v_fma_mix*_f16), no conversion back.
+__device__ __forceinline__ Split2 split2h_mix(float a, float b) {
+  const uint32_t h = cvt_pk_f16(a, b);
+  const f16x2_t hv = __builtin_bit_cast(f16x2_t, h);
+  f16x2_t lv;
+  lv[0] = (_Float16)__builtin_fmaf((float)hv[0], -2048.f, a * 2048.f);
+  lv[1] = (_Float16)__builtin_fmaf((float)hv[1], -2048.f, b * 2048.f);
+  return {h, __builtin_bit_cast(uint32_t, lv)};
+}
+
 // Raw buffer access (gfx9 resource word 3: 0x00020000), byte offsets.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* base, int elems) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, elems * 4,
@@ -1081,6 +1094,9 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     if (!(th0 + r < g.H && tw0 + c < g.W)) vb[s] = 0x80000000u;
   }
 
+  // Operand split by mixed-precision FMAs (split2h_mix: 44 instead of 68 VALU per
+  // k step, bit-identical; Sintel step 225.4 -> 223.6 us); XP bit 21 restores split2h.
+  constexpr bool MIXS = (XP & (1 << 21)) == 0;
   float an[8], an2[8];
   float4 bn[NBS], bn2[NBS];
   auto load_to = [&](int k0, auto& an, auto& bn) {
@@ -1125,7 +1141,7 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       if constexpr (decltype(mode)::value) {
-        const Split2 x = split2h(an[2 * e], an[2 * e + 1]);
+        const Split2 x = MIXS ? split2h_mix(an[2 * e], an[2 * e + 1]) : split2h(an[2 * e], an[2 * e + 1]);
         h[e] = x.h;
         m[e] = 0;
         l[e] = x.l;
@@ -1153,9 +1169,9 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     for (int s = 0; s < NBS; ++s) {
       const int o = NHWC ? bcol[s] * PN + bk[s] : bk[s] * PH + bcol[s];
       if constexpr (decltype(mode)::value) {
-        const Split2 x = split2h(bn[s].x, bn[s].y);
+        const Split2 x = MIXS ? split2h_mix(bn[s].x, bn[s].y) : split2h(bn[s].x, bn[s].y);
         if constexpr (BV == 4) {
-          const Split2 z = split2h(bn[s].z, bn[s].w);
+          const Split2 z = MIXS ? split2h_mix(bn[s].z, bn[s].w) : split2h(bn[s].z, bn[s].w);
           *reinterpret_cast<uint2*>(P + o) = make_uint2(x.h, z.h);
           *reinterpret_cast<uint2*>(P + PLANE + o) = make_uint2(x.l, z.l);
         } else {
@@ -1278,8 +1294,110 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
       __syncthreads();
     }
   };
+  // XP bit 19 (experiments; H2, NCHW, float4 units, nk even): the target tile
+  // travels by LDS-DMA (buffer_load ... lds) into a two-stage raw f32 ring and the
+  // query operand through a two-stage register ring, both two k steps ahead.
+  // Every wave DMAs exactly the 16-byte units its own lanes split afterwards, so
+  // a wave-local vmcnt wait publishes them (no extra barrier), and the DMA stages
+  // hold no VGPRs while in flight.
+  // XP bit 20: the target tile by LDS-DMA two k steps ahead, the query operand
+  // in registers one step ahead (as the product), so no second register stage.
+  constexpr bool DMA1 = (XP & (1 << 20)) != 0;
+  constexpr bool DMA = (XP & (1 << 19)) != 0 || DMA1;
+  __shared__ __attribute__((aligned(16))) float raw[DMA ? 2 * BKS * NTGT : 4];
+  auto kloop_dma = [&]() {
+    if constexpr (DMA && !NHWC && BV == 4) {
+      uint32_t vdma[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int k = 2 * wave + 8 * i + (lane >> 5), u = lane & 31;
+        const int r = u >> 2, c = 4 * (u & 3);
+        vdma[i] = (th0 + r < g.H && tw0 + c < g.W)
+                      ? (uint32_t)(k * g.N + (th0 + r) * g.W + tw0 + c) * 4u : 0x80000000u;
+      }
+      auto dma = [&](int k0, int st) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rb, (__attribute__((address_space(3))) void*)(raw + st * BKS * NTGT + (2 * wave + 8 * i) * NTGT),
+              16, vdma[i], k0 * g.N * 4, 0, 0);
+      };
+      auto loadq = [&](int k0, float (&A)[8]) {
+        const int rowb = g.N * 4;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) A[e] = bload1(ra, va, (k0 + e) * rowb);
+      };
+      auto split_raw = [&](int st, int buf) {
+        float4 v[NBS];
+#pragma unroll
+        for (int s2 = 0; s2 < NBS; ++s2) {
+          const int idx = tid + NT * s2;
+          v[s2] = *reinterpret_cast<const float4*>(raw + st * BKS * NTGT + (idx >> 5) * NTGT + (idx & 31) * 4);
+        }
+        store_b_from(buf, S2{}, v);
+      };
+      if constexpr (DMA1) {
+        // per step: query loads for ks+1 first, then the DMA for ks+2, so a
+        // vmcnt(2) wait completes the former and leaves the latter in flight
+        dma(0, 0);
+        loadq(0, an);
+        dma(BKS, 1);
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        split_raw(0, 0);
+        split_a_from(S2{}, an);
+        __syncthreads();
+        for (int ks = 0; ks < nk; ++ks) {
+          const int buf = ks & 1;
+          if (ks + 1 < nk) loadq((ks + 1) * BKS, an);
+          if (ks + 2 < nk) dma((ks + 2) * BKS, buf);
+          mfma2(buf);
+          if (ks + 1 < nk) {
+            if (ks + 2 < nk) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            split_raw(buf ^ 1, buf ^ 1);
+            split_a_from(S2{}, an);
+          }
+          __syncthreads();
+        }
+        return;
+      }
+      dma(0, 0);
+      loadq(0, an);
+      dma(BKS, 1);
+      loadq(BKS, an2);
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      split_raw(0, 0);
+      split_a_from(S2{}, an);
+      __syncthreads();
+      for (int ks = 0; ks < nk; ks += 2) {
+        if (ks + 2 < nk) {
+          dma((ks + 2) * BKS, 0);
+          loadq((ks + 2) * BKS, an);
+        }
+        mfma2(0);
+        if (ks + 2 < nk) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        split_raw(1, 1);
+        split_a_from(S2{}, an2);
+        __syncthreads();
+        if (ks + 3 < nk) {
+          dma((ks + 3) * BKS, 1);
+          loadq((ks + 3) * BKS, an2);
+        }
+        mfma2(1);
+        if (ks + 2 < nk) {
+          if (ks + 3 < nk) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          split_raw(0, 0);
+          split_a_from(S2{}, an);
+        }
+        __syncthreads();
+      }
+    }
+  };
   constexpr bool PD2 = (XP & (1 << 18)) != 0;
   if constexpr (H2) {
+    if constexpr (DMA) kloop_dma(); else
     if constexpr (PD2) kloop_pd2(); else
     kloop(S2{});
     // Combine (one rounding) and vote: a non-finite sum means an operand of the
@@ -1929,6 +2047,18 @@ extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t
     case 4300:   // loads two k steps ahead, 3 waves/SIMD
       if (D % 32) return DXR_EUNSUPPORTED;
       return xp_h2<1 << 18>(f1, f2, pyr, g, (int)B, stream);
+    case 4400:   // target tile by LDS-DMA + query registers, both two k steps ahead
+      if (D % 32) return DXR_EUNSUPPORTED;
+      return xp_h2<1 << 19>(f1, f2, pyr, g, (int)B, stream);
+    case 4401:   // the same at 2 waves/SIMD
+      if (D % 32) return DXR_EUNSUPPORTED;
+      hipLaunchKernelGGL((corr_build_split_kernel<float, false, 2, 4, 1 << 19, false, true>),
+                         build_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);
+      return dxr::launch_status();
+    case 4500:   // operand split by split2h (cvt back, sub, mul) instead of the FMA-mix form
+      return xp_h2<1 << 21>(f1, f2, pyr, g, (int)B, stream);
+    case 4402:   // target tile by LDS-DMA two steps ahead, queries one step ahead
+      return xp_h2<1 << 20>(f1, f2, pyr, g, (int)B, stream);
     case 4301:   // loads two k steps ahead, 2 waves/SIMD
       if (D % 32) return DXR_EUNSUPPORTED;
       hipLaunchKernelGGL((corr_build_split_kernel<float, false, 2, 4, 1 << 18, false, true>),
