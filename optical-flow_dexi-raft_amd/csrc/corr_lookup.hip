@@ -186,27 +186,35 @@ __device__ __forceinline__ void gather_load(const PT* __restrict__ base, int qb0
   }
 }
 
-template <int R, int NT_>
+// QST: LDS floats per query (default WideCfg::QS, 16-byte aligned rows); a
+// stride of 2 mod 4 (experiments) writes each vector as two 8-byte halves.
+template <int R, int NT_, int QST = -1>
 __device__ __forceinline__ void gather_store(const float4 (&v)[WideCfg<R, NT_>::VIT], float* cells,
                                              int tid) {
   using C = WideCfg<R, NT_>;
+  constexpr int QSv = QST < 0 ? C::QS : QST;
 #pragma unroll
   for (int i = 0; i < C::VIT; ++i) {
     const int s = tid + i * C::NT;
     if (s < C::VSLOTS) {
       const int qq = s / (C::WD * C::NQ), rem = s - qq * (C::WD * C::NQ);
-      *reinterpret_cast<float4*>(cells + qq * C::QS + rem * 4) = v[i];
+      if constexpr (QSv % 4 == 0) {
+        *reinterpret_cast<float4*>(cells + qq * QSv + rem * 4) = v[i];
+      } else {
+        *reinterpret_cast<float2*>(cells + qq * QSv + rem * 4) = make_float2(v[i].x, v[i].y);
+        *reinterpret_cast<float2*>(cells + qq * QSv + rem * 4 + 2) = make_float2(v[i].z, v[i].w);
+      }
     }
   }
 }
 
-template <int R, int NT_, int V, typename PT, bool NTL = false>
+template <int R, int NT_, int V, typename PT, bool NTL = false, int QST = -1>
 __device__ __forceinline__ void gather_windows(const PT* __restrict__ base, int qb0, const LevelAddr& A,
                                                const int2* org, float* cells, int q0, int N,
                                                int tid) {
   float4 v[WideCfg<R, NT_>::VIT];
   gather_load<R, NT_, V, PT, NTL>(base, qb0, A, org, q0, N, tid, v);
-  gather_store<R, NT_>(v, cells, tid);
+  gather_store<R, NT_, QST>(v, cells, tid);
 }
 
 // Phase 0 of the wide lookup (forward and backward): per (query, sample) the
@@ -272,7 +280,10 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
     LookupGeom g) {
   using C = WideCfg<R, NT_>;
   constexpr int RD = C::RD, RS = C::RS, K = C::K, QB = C::QB;
-  __shared__ __attribute__((aligned(16))) float cells[QB * C::QS];
+  // XP bit 5 (experiments): query stride 2 mod 4 floats (178 at r = 4), so the 32
+  // queries of a phase-2 read spread over 16 bank pairs instead of 8 bank quads
+  constexpr int QSW = (XP & 32) ? C::WD * C::RS + 2 : C::QS;
+  __shared__ __attribute__((aligned(16))) float cells[QB * QSW];
   __shared__ float4 xs[RD * QB];   // {column in the LDS row (int bits), fx, 1-fx, -}
   __shared__ float4 ys[RD * QB];   // {row offset in LDS (int bits), fy, 1-fy, -}
   __shared__ int2 org[QB];         // window origin (x, y) or FAR_ORIGIN
@@ -296,13 +307,13 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
     const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
     const int qb0 = q0 & ((1 << A.lqb) - 1);
     if (A.lth == 30)
-      gather_windows<R, NT_, 1>(base, qb0, A, org, cells, q0, g.N, tid);
+      gather_windows<R, NT_, 1, PT, false, QSW>(base, qb0, A, org, cells, q0, g.N, tid);
     else if (A.tw >= 4)   // XP bit 3 (experiments): non-temporal gather loads
-      gather_windows<R, NT_, 4, PT, (XP & 8) != 0>(base, qb0, A, org, cells, q0, g.N, tid);
+      gather_windows<R, NT_, 4, PT, (XP & 8) != 0, QSW>(base, qb0, A, org, cells, q0, g.N, tid);
     else if (A.tw == 2)
-      gather_windows<R, NT_, 2>(base, qb0, A, org, cells, q0, g.N, tid);
+      gather_windows<R, NT_, 2, PT, false, QSW>(base, qb0, A, org, cells, q0, g.N, tid);
     else
-      gather_windows<R, NT_, 1>(base, qb0, A, org, cells, q0, g.N, tid);
+      gather_windows<R, NT_, 1, PT, false, QSW>(base, qb0, A, org, cells, q0, g.N, tid);
   }
   __syncthreads();
 
@@ -326,7 +337,7 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
       for (int i = 0; i < 4; ++i) {
         const int qi = qa + i;
         const float4 xd = xs[ox * QB + qi], yd = ys[oy * QB + qi];
-        const float* p = cells + qi * C::QS + __float_as_int(yd.x) + __float_as_int(xd.x);
+        const float* p = cells + qi * QSW + __float_as_int(yd.x) + __float_as_int(xd.x);
         const float v00 = p[0], v01 = p[1], v10 = p[RS], v11 = p[RS + 1];
         const float nw = __fmul_rn(yd.z, xd.z), ne = __fmul_rn(yd.z, xd.y);
         const float sw = __fmul_rn(yd.y, xd.z), se = __fmul_rn(yd.y, xd.y);
@@ -350,7 +361,7 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
   }
   const int qq = tid % QB, cls = tid / QB;
   if (q0 + qq >= g.N) return;
-  const float* cq = cells + qq * C::QS;
+  const float* cq = cells + qq * QSW;
   float* ob = out + ((long long)b * g.cout + (long long)l * K) * g.N + q0 + qq;
   for (int k = cls; k < K; k += C::NCLS) {
     const int ox = k / RD, oy = k - ox * RD;
@@ -1445,6 +1456,7 @@ extern "C" int dxr_xp_lookup(const void* pyramid, int pyr_dtype, int64_t B, int6
       case 3: return xp_lookup_k<3>(p, coords, out, g, (int)B, stream);
       case 4: return xp_lookup_k<4>(p, coords, out, g, (int)B, stream);
       case 8: return xp_lookup_k<8>(p, coords, out, g, (int)B, stream);
+      case 32: return xp_lookup_k<32>(p, coords, out, g, (int)B, stream);
       case 100: return xp_lookup2(p, coords, out, g, (int)B, stream);
       case 256: return xp_lookup_nt<256>(p, coords, out, g, (int)B, stream);
       case 1024: return xp_lookup_nt<1024>(p, coords, out, g, (int)B, stream);
@@ -1469,6 +1481,7 @@ extern "C" int dxr_xp_lookup(const void* pyramid, int pyr_dtype, int64_t B, int6
     case 0: return xp_lookup_k<0>(p, coords, out, g, (int)B, stream);
     case 1: return xp_lookup_k<1>(p, coords, out, g, (int)B, stream);
     case 2: return xp_lookup_k<2>(p, coords, out, g, (int)B, stream);
+    case 32: return xp_lookup_k<32>(p, coords, out, g, (int)B, stream);
     case 0x1000: return g.N % 4 ? DXR_EUNSUPPORTED : xp_lookup_k<0x1000>(p, coords, out, g, (int)B, stream);
     case 0x3000: return g.N % 4 ? DXR_EUNSUPPORTED : xp_lookup_k<0x3000>(p, coords, out, g, (int)B, stream);
     case 0x4000: return xp_lookup_k<0x4000>(p, coords, out, g, (int)B, stream);
