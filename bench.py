@@ -195,10 +195,22 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def _nproc() -> int:
+    """What coreutils ``nproc`` reports: the processing units this process may
+    use (its CPU affinity, capped by OMP_NUM_THREADS / OMP_THREAD_LIMIT) — on
+    the GPU box the harness's per-GPU CPU share, not the whole host."""
+    try:
+        return int(subprocess.run(["nproc"], capture_output=True, text=True,
+                                  check=True).stdout.strip())
+    except (OSError, ValueError, subprocess.CalledProcessError):
+        return len(os.sched_getaffinity(0))
+
+
 def cpu_baseline(H, W, budget_s, impl="torch", reps=5):
     """Time the reference's op sequence on host cores: warm-up 1,
     then the median of ``reps`` repetitions, each timing as many single pairs as
-    fit in budget_s / reps (at least one).
+    fit in budget_s / reps (at least one), on ``torch.set_num_threads(nproc)``
+    threads (nproc as coreutils reports it, see _nproc).
 
     impl "torch" (default; SURVEY.md §8(d) "CPU reference timing"): the plain-PyTorch
     restatement tests/torch_ref.py (bmm, / sqrt(D), 3x F.avg_pool2d, 12 x 4
@@ -211,8 +223,11 @@ def cpu_baseline(H, W, budget_s, impl="torch", reps=5):
     f1 = dg.fmap(0, 1, D, H, W)
     f2 = dg.fmap(1, 1, D, H, W)
     cs = [dg.coords(100 + k, 1, H, W, "normal", 4.0) for k in range(ITERS)]
+    nproc = _nproc()
+    prev_threads = torch.get_num_threads()
     if impl == "torch":
         import torch_ref
+        torch.set_num_threads(nproc)
         threads = torch.get_num_threads()
         t1, t2 = torch.from_numpy(f1), torch.from_numpy(f2)
         tc = [torch.from_numpy(c) for c in cs]
@@ -244,9 +259,11 @@ def cpu_baseline(H, W, budget_s, impl="torch", reps=5):
             rates.append(n / dt)
             pairs += n
             total += dt
+    torch.set_num_threads(prev_threads)
     med = float(np.median(rates))
     return {"value": round(med, 4), "unit": "pairs/s", "cores": threads,
-            "nproc": os.cpu_count(), "cpu_model": _cpu_model(), "kind": "port",
+            "nproc": nproc, "host_cpus": os.cpu_count(), "cpu_model": _cpu_model(),
+            "kind": "port",
             "median_of": reps, "median_s_per_pair": round(1.0 / med, 4),
             "sample": f"median of {reps} reps ({pairs} single pairs in {total:.1f} s) of fmap "
                       f"{H}x{W}, D={D}: build + {ITERS} lookups each; {what}"}

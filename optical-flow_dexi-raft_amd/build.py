@@ -24,8 +24,10 @@ INCLUDE = REPO_DIR / "include"
 BUILD_DIR = PKG_DIR / "build"
 LIB_NAME = "libdexiraft_corr.so"
 LIB_PATH = PKG_DIR / LIB_NAME
-# Experiments target (timing ablations; never loaded by the package): same
-# sources with -DDXR_EXPERIMENTS, objects in build/exp.
+# Experiments target (timing ablations; never loaded by the package): the
+# csrc/experiments/*.hip files, each of which includes the product source it
+# varies, objects in build/exp.
+EXP_DIR = CSRC / "experiments"
 EXP_LIB_PATH = PKG_DIR / "libdexiraft_corr_exp.so"
 ARCH = "gfx950"
 
@@ -43,19 +45,20 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found: the HIP toolchain (/opt/rocm) is required to build")
 
 
-def _sources() -> list[Path]:
-    return sorted(CSRC.glob("*.hip"))
+def _sources(experiments: bool = False) -> list[Path]:
+    return sorted((EXP_DIR if experiments else CSRC).glob("*.hip"))
 
 
-def _deps() -> list[Path]:
-    return _sources() + sorted(CSRC.glob("*.h")) + sorted(INCLUDE.glob("*.h")) + [Path(__file__)]
+def _deps(experiments: bool = False) -> list[Path]:
+    deps = _sources() + sorted(CSRC.glob("*.h")) + sorted(INCLUDE.glob("*.h")) + [Path(__file__)]
+    return deps + (_sources(True) if experiments else [])
 
 
 def is_stale(lib: Path = LIB_PATH) -> bool:
     if not lib.exists():
         return True
     t = lib.stat().st_mtime
-    return any(p.stat().st_mtime > t for p in _deps())
+    return any(p.stat().st_mtime > t for p in _deps(lib == EXP_LIB_PATH))
 
 
 # Per-file flags.  corr_build.hip: no SLP vectorisation — packed f32 VALU
@@ -87,9 +90,9 @@ def build(force: bool = False, asm: bool = False, verbose: bool = False,
     out_dir = BUILD_DIR / "exp" if experiments else BUILD_DIR
     out_dir.mkdir(parents=True, exist_ok=True)
     extra = ["-save-temps=obj", "-Rpass-analysis=kernel-resource-usage"] if asm else []
-    if experiments:
-        extra = extra + ["-DDXR_EXPERIMENTS"]
-    srcs = _sources()
+    srcs = _sources(experiments)
+    if not srcs:
+        raise RuntimeError(f"no sources in {EXP_DIR if experiments else CSRC}")
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(lambda s: _compile(s, extra, out_dir), srcs))
     tmp = lib.with_suffix(".so.tmp")

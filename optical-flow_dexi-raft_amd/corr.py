@@ -356,15 +356,15 @@ class CorrBlock:
             self._token = _BuildGrad.apply(f1, f2, self._gs)
 
     def _launch_build(self, fmap1, fmap2, grad=False):
-        """One build launch into this block's pyramid buffer (the constructor's;
-        bench.py also times the kernel with it).  Returns the operand tensors the
-        kernel read and the status."""
+        """One build launch into this block's pyramid buffer.  Returns the operand
+        tensors the kernel read and the status."""
         B, D, H, W = self._geom
         lib = nat.load()
         st = nat.DXR_EUNSUPPORTED
         if not grad and _channels_last(fmap1) and _channels_last(fmap2):
             # channels-last fmaps (SURVEY §8(f) row 4): read in place by the
-            # build's NHWC operand loads, no layout pass
+            # build's NHWC operand loads (f32: the split build, bf16: the two-block
+            # bf16 build), no layout pass
             f1, f2 = fmap1, fmap2
             with _Launch(self._device):
                 st = lib.dxr_corr_pyramid_build(
@@ -528,7 +528,6 @@ class AlternateCorrBlock:
             raise ValueError(f"radius must be a non-negative int, got {radius!r}")
         _level_sizes(H, W, num_levels + 1)  # the reference pools num_levels times
         self._geom = (B, D, H, W)
-        self._token = None   # never differentiable (see the check above)
         self._device = fmap1.device
         # NHWC operands (core/corr.py:82-83 permutes on every call; here once per
         # block): a free view of channels-last fmaps, one tiled transpose otherwise.
@@ -567,8 +566,6 @@ class AlternateCorrBlock:
         B, D, H, W = self._geom
         _require_no_grad(coords, what="coords (the reference detaches them, core/raft.py:170)")
         c = _check_coords(coords, B, H, W, self._device)
-        if self._token is not None and torch.is_grad_enabled():
-            return _LookupGrad.apply(self._token, c, self)
         return self._lookup(c)
 
     def _lookup(self, c):

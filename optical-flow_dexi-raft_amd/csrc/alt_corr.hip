@@ -252,16 +252,12 @@ __device__ __forceinline__ void alt_split8h(const float (&x)[8], uint4& h, uint4
 // as the split build; a chunk whose sums are not finite (an operand beyond f16
 // range, or inf/NaN) is recomputed by its wave on the 3-way bf16 split, with
 // the query operand split from fmap1 in registers.
-// ST (experiments): 1 stores the outputs write-through (sc1).
 // BIN: the workgroup's 32 queries are not a 4 x 8 pixel tile but 32 consecutive
 // entries of perm (this coordinate set's and level's query list sorted by window
 // position, alt_bin_kernel), so their windows — and the union box — are compact
 // whatever the flow field; `tile` is then the index of that chunk of 32.
 // PF: k steps of cell-vector loads kept in flight (a ring of PF register stages).
-// SLOWIDX (experiments): the r02 index arithmetic (integer division by the box
-// width, IEEE division by the divisor) instead of the exact reciprocal forms.
-template <int R, int NRB, int CMAX, bool H2 = false, int MINW = 2, int ST = 0, bool BIN = false,
-          int PF = 1, bool SLOWIDX = false>
+template <int R, int NRB, int CMAX, bool H2 = false, int MINW = 2, bool BIN = false, int PF = 1>
 __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* __restrict__ f1,
                                                                const float* __restrict__ coords,
                                                                float* __restrict__ out,
@@ -382,14 +378,10 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
   // c / bw for box cells (c < 2^24): a float estimate corrected to the exact quotient
   const float rbw = 1.f / (float)max(bw, 1);
   auto divbw = [&](int c) -> int {
-    if constexpr (SLOWIDX) {
-      return c / bw;
-    } else {
-      int q = (int)((float)c * rbw);
-      q -= (q * bw > c) ? 1 : 0;
-      q += ((q + 1) * bw <= c) ? 1 : 0;
-      return q;
-    }
+    int q = (int)((float)c * rbw);
+    q -= (q * bw > c) ? 1 : 0;
+    q += ((q + 1) * bw <= c) ? 1 : 0;
+    return q;
   };
   const int ncells = bw * bh;
   const int j = lane & 31, kh = lane >> 5;
@@ -553,921 +545,10 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
       v = __fadd_rn(v, __fmul_rn(__fmul_rn(s10, dy), 1.f - dx));
       v = __fadd_rn(v, __fmul_rn(__fmul_rn(s11, dy), dx));
       // v / divisor; a power-of-two divisor (sqrt(256) = 16) scales exactly by its reciprocal
-      const float vd = (!SLOWIDX && g.div_recip != 0.f) ? v * g.div_recip : v / g.divisor;
-      if constexpr (ST == 1)
-        __hip_atomic_store(o + (long long)(oy + RD * ox) * g.N, vd, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      else
-        o[(long long)(oy + RD * ox) * g.N] = vd;
+      o[(long long)(oy + RD * ox) * g.N] = g.div_recip != 0.f ? v * g.div_recip : v / g.divisor;
     }
   }
 }
-
-#ifdef DXR_EXPERIMENTS
-// ---------------------------------------------------------------------------
-// Large-tile on-the-fly form (experiment): an 8 x 16 query tile (128 queries) per
-// workgroup.  Bit-identical to alt_corr_mfma_kernel but slower at 1080p (253 vs
-// 228 us at 2 waves/SIMD, 256 VGPRs; 482 us at 1): each level-0 workgroup walks
-// ~23 chunks x 16 barrier-separated k steps with one step of prefetch, a longer
-// latency chain than the ~2.8x fewer cell loads save.
-// The union box of 128 windows is ~2.8x fewer cells per query than the 4 x 8
-// form's (level 0, N(0, 4^2) flows: ~1,430 cells for 128 queries against ~1,000
-// for 32), and its cells are loaded once for all four waves: per k step the
-// workgroup stages a 64-cell chunk slab (64 cells x 16 channels, 4 lanes per
-// 64-byte slab: whole segments) split into f16 pairs in LDS, and each wave
-// multiplies it with its own 32 queries, whose f16-pair operands (all C <= 256
-// channels) stay in registers for the workgroup's life.  Same products in the
-// same order as alt_corr_mfma_kernel (H2): bit-identical window sums; same
-// per-wave 3-way bf16 fallback for non-finite chunks (from global memory).
-// ---------------------------------------------------------------------------
-constexpr int T2Y = 8, T2X = 16, T2Q = T2Y * T2X;    // query tile (128 pixels)
-
-// f16 pair split of 4 floats into two f16x2 words each (hi, lo)
-__device__ __forceinline__ void alt_split4h(const float4 a, uint2& h, uint2& l) {
-  const float x[4] = {a.x, a.y, a.z, a.w};
-  uint32_t hh[2], ll[2];
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    hh[e] = alt_cvt_pk_h(x[2 * e], x[2 * e + 1]);
-    const ah2 hv = __builtin_bit_cast(ah2, hh[e]);
-    ll[e] = alt_cvt_pk_h((x[2 * e] - (float)hv[0]) * 2048.f, (x[2 * e + 1] - (float)hv[1]) * 2048.f);
-  }
-  h = make_uint2(hh[0], hh[1]);
-  l = make_uint2(ll[0], ll[1]);
-}
-
-template <int R, int MINW = 2>
-__global__ __launch_bounds__(256, MINW) void alt_corr_tile_kernel(const float* __restrict__ f1,
-                                                                  const float* __restrict__ coords,
-                                                                  float* __restrict__ out,
-                                                                  AltGeom g, int W1, int tiles_x) {
-  constexpr int RD = 2 * R + 1, RD1 = RD + 1, NCELL = RD1 * RD1;
-  constexpr int CH = 64;                       // box cells per chunk (two 32-row MFMA tiles)
-  constexpr int PN = 24;                       // LDS pitch (f16) of a staged cell slab
-  constexpr int PLANE = CH * PN;
-  __shared__ float S[T2Q * NCELL];             // window dot products
-  __shared__ __attribute__((aligned(16))) uint16_t cst[2][2][PLANE];   // [buf][hi, lo][cell][k]
-  __shared__ int4 qinfo[T2Q];                  // {x0, y0, live, -}
-  __shared__ int boxp[2][4];                   // per-wave partial boxes (waves 0, 1)
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  int tile = blockIdx.x;
-  {
-    const int n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = tile % 8;
-    tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + tile / 8;
-  }
-  const int tx = tile % tiles_x, ty = tile / tiles_x;
-  const AltLevel lv = g.lv[blockIdx.y];
-  const int z = blockIdx.z, bf = z / g.Nc;
-  const float* cz = coords + (long long)z * g.coord_zstride;
-  const float* f1b = f1 + (long long)bf * g.f1_bstride;
-  const float* f2b = lv.f2 + (long long)bf * lv.H2 * lv.W2 * g.C;
-  const int H1 = g.N / W1;
-  const int nks = g.C / 16;
-
-  // query index qi = 32 w + j: wave w holds the 4 x 8 sub-tile (w >> 1, w & 1)
-  auto qpos = [&](int qi, int& qy, int& qx) {
-    const int w = qi >> 5, jj = qi & 31;
-    qy = ty * T2Y + (w >> 1) * 4 + (jj >> 3);
-    qx = tx * T2X + (w & 1) * 8 + (jj & 7);
-  };
-
-  // ---- query coordinates, window origins, the windows' union box
-  if (tid < T2Q) {
-    int qy, qx;
-    qpos(tid, qy, qx);
-    int x0 = 0, y0 = 0, live = 0;
-    if (qy < H1 && qx < W1) {
-      const int q = qy * W1 + qx;
-      const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
-      const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
-      const float xf = floorf(x), yf = floorf(y);
-      if (fabsf(xf) < 1.0e8f && fabsf(yf) < 1.0e8f) {
-        x0 = (int)xf - R;
-        y0 = (int)yf - R;
-        live = (x0 + RD1 > 0 && x0 < lv.W2 && y0 + RD1 > 0 && y0 < lv.H2) ? 1 : 0;
-      }
-    }
-    qinfo[tid] = make_int4(x0, y0, live, 0);
-    int lx0 = live ? max(x0, 0) : 0x7fffffff, ly0 = live ? max(y0, 0) : 0x7fffffff;
-    int lx1 = live ? min(x0 + RD1, lv.W2) : -1, ly1 = live ? min(y0 + RD1, lv.H2) : -1;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      lx0 = min(lx0, __shfl_xor(lx0, o));
-      ly0 = min(ly0, __shfl_xor(ly0, o));
-      lx1 = max(lx1, __shfl_xor(lx1, o));
-      ly1 = max(ly1, __shfl_xor(ly1, o));
-    }
-    if (lane == 0) {
-      boxp[wave][0] = lx0;
-      boxp[wave][1] = ly0;
-      boxp[wave][2] = lx1;
-      boxp[wave][3] = ly1;
-    }
-  }
-  for (int i = tid; i < T2Q * NCELL; i += 256) S[i] = 0.f;
-
-  // this wave's queries as f16 pairs, all k steps, in registers (B operand:
-  // lane -> query j = lane & 31, channels 16 ks + 8 kh .. + 8)
-  const int j = lane & 31, kh = lane >> 5, qi = wave * 32 + j;
-  int mqy, mqx;
-  qpos(qi, mqy, mqx);
-  const float* qsrc = f1b + (long long)(min(mqy, H1 - 1) * W1 + min(mqx, W1 - 1)) * g.C + 8 * kh;
-  uint4 qh[16], ql[16];
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks) {
-    if (ks < nks) {
-      const float4 u = *reinterpret_cast<const float4*>(qsrc + ks * 16);
-      const float4 w = *reinterpret_cast<const float4*>(qsrc + ks * 16 + 4);
-      const float x[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
-      alt_split8h(x, qh[ks], ql[ks]);
-    }
-  }
-  __syncthreads();
-
-  int bx0, by0, bw, bh;
-  {
-    const int lx0 = min(boxp[0][0], boxp[1][0]), ly0 = min(boxp[0][1], boxp[1][1]);
-    const int lx1 = max(boxp[0][2], boxp[1][2]), ly1 = max(boxp[0][3], boxp[1][3]);
-    const bool any = lx1 > lx0;
-    bx0 = any ? lx0 : 0;
-    by0 = any ? ly0 : 0;
-    bw = any ? lx1 - lx0 : 0;
-    bh = any ? ly1 - ly0 : 0;
-  }
-  const int ncells = bw * bh;
-  const int4 qinf = qinfo[qi];
-  const int sc = tid >> 2, sp = tid & 3;       // staging: chunk cell, 4-channel part
-  for (int c0 = 0; c0 < ncells; c0 += CH) {
-    const float* tsrc;
-    {
-      const int c = min(c0 + sc, ncells - 1);
-      const int cy = c / bw, cx = c - cy * bw;
-      tsrc = f2b + ((long long)(by0 + cy) * lv.W2 + bx0 + cx) * g.C + 4 * sp;
-    }
-    auto stage = [&](const float4 v, int buf) {
-      uint2 h, l;
-      alt_split4h(v, h, l);
-      *reinterpret_cast<uint2*>(&cst[buf][0][sc * PN + 4 * sp]) = h;
-      *reinterpret_cast<uint2*>(&cst[buf][1][sc * PN + 4 * sp]) = l;
-    };
-    af16 acc[2], acc2[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[t][r] = acc2[t][r] = 0.f;
-    stage(*reinterpret_cast<const float4*>(tsrc), 0);
-    __syncthreads();
-#pragma unroll
-    for (int ks = 0; ks < 16; ++ks) {
-      if (ks < nks) {
-        float4 nv;
-        if (ks + 1 < nks) nv = *reinterpret_cast<const float4*>(tsrc + (ks + 1) * 16);
-        const int buf = ks & 1;
-        const ah8 qhv = __builtin_bit_cast(ah8, qh[ks]), qlv = __builtin_bit_cast(ah8, ql[ks]);
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const int o = (t * 32 + j) * PN + 8 * kh;
-          const ah8 th = *reinterpret_cast<const ah8*>(&cst[buf][0][o]);
-          const ah8 tl = *reinterpret_cast<const ah8*>(&cst[buf][1][o]);
-          acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qhv, acc2[t], 0, 0, 0);
-          acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qlv, acc2[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qhv, acc[t], 0, 0, 0);
-        }
-        if (ks + 1 < nks) stage(nv, buf ^ 1);
-        __syncthreads();
-      }
-    }
-    bool bad = false;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        acc[t][r] = __builtin_fmaf(acc2[t][r], 0x1p-11f, acc[t][r]);
-        bad |= !(__builtin_fabsf(acc[t][r]) <= 3.40282347e38f);
-      }
-    if (__ballot(bad) != 0) {
-      // 3-way bf16 split from global memory, this wave only (no barriers)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int c = min(c0 + t * 32 + j, ncells - 1);
-        const int cy = c / bw, cx = c - cy * bw;
-        const float* csrc = f2b + ((long long)(by0 + cy) * lv.W2 + bx0 + cx) * g.C + 8 * kh;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-        for (int ks = 0; ks < nks; ++ks) {
-          const float4 u = *reinterpret_cast<const float4*>(qsrc + ks * 16);
-          const float4 w = *reinterpret_cast<const float4*>(qsrc + ks * 16 + 4);
-          const float4 a = *reinterpret_cast<const float4*>(csrc + ks * 16);
-          const float4 bq = *reinterpret_cast<const float4*>(csrc + ks * 16 + 4);
-          const float xq[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
-          const float xc[8] = {a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w};
-          uint4 h, m, l, ch, cm, cl;
-          alt_split8(xq, h, m, l);
-          alt_split8(xc, ch, cm, cl);
-          const abf8 qh3 = __builtin_bit_cast(abf8, h), qm3 = __builtin_bit_cast(abf8, m),
-                     ql3 = __builtin_bit_cast(abf8, l);
-          const abf8 th3 = __builtin_bit_cast(abf8, ch), tm3 = __builtin_bit_cast(abf8, cm),
-                     tl3 = __builtin_bit_cast(abf8, cl);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm3, qm3, acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl3, qh3, acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th3, ql3, acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm3, qh3, acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th3, qm3, acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th3, qh3, acc[t], 0, 0, 0);
-        }
-      }
-    }
-    // keep the entries inside query qi's window: D row = (r & 3) + 8 (r >> 2) + 4 kh
-    if (qinf.z) {
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int c = c0 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-          if (c < ncells) {
-            const int cy = c / bw, cx = c - cy * bw;
-            const int iy = by0 + cy - qinf.y, ix = bx0 + cx - qinf.x;
-            if ((unsigned)iy < (unsigned)RD1 && (unsigned)ix < (unsigned)RD1)
-              S[qi * NCELL + iy * RD1 + ix] = acc[t][r];
-          }
-        }
-    }
-  }
-  __syncthreads();
-
-  // ---- bilinear combination, as alt_corr_mfma_kernel
-  const int oq = tid & (T2Q - 1), cls = tid / T2Q;
-  int oqy, oqx;
-  qpos(oq, oqy, oqx);
-  if (oqy >= H1 || oqx >= W1) return;
-  const int q = oqy * W1 + oqx;
-  const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
-  const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
-  const float dx = x - floorf(x), dy = y - floorf(y);
-  const float* s = S + oq * NCELL;
-  float* o = out + (long long)z * g.cout * g.N + (long long)lv.ch_off * g.N + q;
-  for (int ox = cls; ox < RD; ox += 256 / T2Q) {
-#pragma unroll
-    for (int oy = 0; oy < RD; ++oy) {
-      const float s00 = s[oy * RD1 + ox], s01 = s[oy * RD1 + ox + 1];
-      const float s10 = s[(oy + 1) * RD1 + ox], s11 = s[(oy + 1) * RD1 + ox + 1];
-      float v = __fmul_rn(__fmul_rn(s00, 1.f - dy), 1.f - dx);
-      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s01, 1.f - dy), dx));
-      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s10, dy), 1.f - dx));
-      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s11, dy), dx));
-      o[(long long)(oy + RD * ox) * g.N] = v / g.divisor;
-    }
-  }
-}
-
-#endif  // DXR_EXPERIMENTS
-
-#ifdef DXR_EXPERIMENTS
-// Two alternative forms of alt_corr_mfma_kernel, measured at 1080p (12 coordinate
-// sets, scripts/xp_alt.py) and kept only in the experiments target: both are
-// bit-identical (rq) or f32-class (grouped) but slower than the product kernel
-// (258 us): register queries 368 us, grouped 16x16x32 308 us (NRB 1) / 351 us
-// (NRB 2).  The product kernel is bound by its scattered cell-vector loads, not by
-// MFMA issue (grouped: -30% MFMA work, slower) nor by occupancy (rq: 2x the waves,
-// slower).
-// ---------------------------------------------------------------------------
-// Register-query MFMA form: as alt_corr_mfma_kernel (4 x 8 query tile, union
-// box, v_mfma_f32_32x32x16_bf16, f32-class split), but the query operand is
-// loaded and split per k step in registers (each wave reads its lanes' 32
-// queries x 16 channels from the NHWC fmap1 — L1/L2-resident) instead of
-// staged once as 49 KB of split planes in LDS.  LDS falls to the window dot
-// products (12.8 KB), so 4+ workgroups fit per CU instead of 2.
-// ---------------------------------------------------------------------------
-template <int R, int MINW>
-__global__ __launch_bounds__(256, MINW) void alt_corr_mfma_rq_kernel(const float* __restrict__ f1,
-                                                                     const float* __restrict__ coords,
-                                                                     float* __restrict__ out,
-                                                                     AltGeom g, int W1, int tiles_x) {
-  constexpr int RD = 2 * R + 1, RD1 = RD + 1, NCELL = RD1 * RD1;
-  constexpr int CHUNK = 4 * 32;                             // box cells per chunk
-  __shared__ float S[TQ * NCELL];                           // window dot products
-  __shared__ int4 qinfo[TQ];                                // {x0, y0, live, -}
-  __shared__ int box[4];                                    // bx0, by0, bw, bh
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  int tile = blockIdx.x;
-  {
-    const int n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = tile % 8;
-    tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + tile / 8;
-  }
-  const int tx = tile % tiles_x, ty = tile / tiles_x;
-  const AltLevel lv = g.lv[blockIdx.y];
-  const int z = blockIdx.z, bf = z / g.Nc;
-  const float* cz = coords + (long long)z * g.coord_zstride;
-  const float* f1b = f1 + (long long)bf * g.f1_bstride;
-  const float* f2b = lv.f2 + (long long)bf * lv.H2 * lv.W2 * g.C;
-  const int H1 = g.N / W1;
-  const int nks = g.C / 16;
-
-  if (tid < TQ) {
-    const int qy = ty * TQY + tid / TQX, qx = tx * TQX + tid % TQX;
-    int x0 = 0, y0 = 0, live = 0;
-    if (qy < H1 && qx < W1) {
-      const int q = qy * W1 + qx;
-      const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
-      const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
-      const float xf = floorf(x), yf = floorf(y);
-      if (fabsf(xf) < 1.0e8f && fabsf(yf) < 1.0e8f) {
-        x0 = (int)xf - R;
-        y0 = (int)yf - R;
-        live = (x0 + RD1 > 0 && x0 < lv.W2 && y0 + RD1 > 0 && y0 < lv.H2) ? 1 : 0;
-      }
-    }
-    qinfo[tid] = make_int4(x0, y0, live, 0);
-    int lx0 = live ? max(x0, 0) : 0x7fffffff, ly0 = live ? max(y0, 0) : 0x7fffffff;
-    int lx1 = live ? min(x0 + RD1, lv.W2) : -1, ly1 = live ? min(y0 + RD1, lv.H2) : -1;
-#pragma unroll
-    for (int o = 1; o < TQ; o <<= 1) {
-      lx0 = min(lx0, __shfl_xor(lx0, o));
-      ly0 = min(ly0, __shfl_xor(ly0, o));
-      lx1 = max(lx1, __shfl_xor(lx1, o));
-      ly1 = max(ly1, __shfl_xor(ly1, o));
-    }
-    if (tid == 0) {
-      const bool any = lx1 > lx0;
-      box[0] = any ? lx0 : 0;
-      box[1] = any ? ly0 : 0;
-      box[2] = any ? lx1 - lx0 : 0;
-      box[3] = any ? ly1 - ly0 : 0;
-    }
-  }
-  for (int i = tid; i < TQ * NCELL; i += 256) S[i] = 0.f;
-  __syncthreads();
-
-  const int bx0 = box[0], by0 = box[1], bw = box[2], bh = box[3];
-  const int ncells = bw * bh;
-  const int j = lane & 31, kh = lane >> 5;
-  const int4 qi = qinfo[j];
-  // this lane's query operand row: query j of the tile (clamped), channels 8 kh .. + 8 per k16
-  const int qy = min(ty * TQY + j / TQX, H1 - 1), qx = min(tx * TQX + j % TQX, W1 - 1);
-  const float* qsrc = f1b + (long long)(qy * W1 + qx) * g.C + 8 * kh;
-  for (int c0 = 0; c0 < ncells; c0 += CHUNK) {
-    af16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const int c = min(c0 + wave * 32 + j, ncells - 1);
-    const int cy = c / bw, cx = c - cy * bw;
-    const float* src = f2b + ((long long)(by0 + cy) * lv.W2 + bx0 + cx) * g.C + 8 * kh;
-    float4 ca = *reinterpret_cast<const float4*>(src), cb = *reinterpret_cast<const float4*>(src + 4);
-    float4 qa = *reinterpret_cast<const float4*>(qsrc), qb = *reinterpret_cast<const float4*>(qsrc + 4);
-    for (int ks = 0; ks < nks; ++ks) {
-      float4 na, nb, nqa, nqb;
-      if (ks + 1 < nks) {
-        na = *reinterpret_cast<const float4*>(src + (ks + 1) * 16);
-        nb = *reinterpret_cast<const float4*>(src + (ks + 1) * 16 + 4);
-        nqa = *reinterpret_cast<const float4*>(qsrc + (ks + 1) * 16);
-        nqb = *reinterpret_cast<const float4*>(qsrc + (ks + 1) * 16 + 4);
-      }
-      uint4 qh4, qm4, ql4, h, m, l;
-      {
-        const float x[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
-        alt_split8(x, qh4, qm4, ql4);
-      }
-      {
-        const float x[8] = {ca.x, ca.y, ca.z, ca.w, cb.x, cb.y, cb.z, cb.w};
-        alt_split8(x, h, m, l);
-      }
-      const abf8 qh = __builtin_bit_cast(abf8, qh4), qm = __builtin_bit_cast(abf8, qm4),
-                 ql = __builtin_bit_cast(abf8, ql4);
-      const abf8 th = __builtin_bit_cast(abf8, h), tm = __builtin_bit_cast(abf8, m),
-                 tl = __builtin_bit_cast(abf8, l);
-      // small terms first
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, ql, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qh, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qm, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh, acc, 0, 0, 0);
-      if (ks + 1 < nks) {
-        ca = na; cb = nb; qa = nqa; qb = nqb;
-      }
-    }
-    if (qi.z) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int cc = c0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-        if (cc < ncells) {
-          const int ccy = cc / bw, ccx = cc - ccy * bw;
-          const int iy = by0 + ccy - qi.y, ix = bx0 + ccx - qi.x;
-          if ((unsigned)iy < (unsigned)RD1 && (unsigned)ix < (unsigned)RD1)
-            S[j * NCELL + iy * RD1 + ix] = acc[r];
-        }
-      }
-    }
-  }
-  __syncthreads();
-
-  const int qq = tid & (TQ - 1), cls = tid / TQ;
-  const int oqy = ty * TQY + qq / TQX, oqx = tx * TQX + qq % TQX;
-  if (oqy >= H1 || oqx >= W1) return;
-  const int q = oqy * W1 + oqx;
-  const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
-  const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
-  const float dx = x - floorf(x), dy = y - floorf(y);
-  const float* sq = S + qq * NCELL;
-  float* o = out + (long long)z * g.cout * g.N + (long long)lv.ch_off * g.N + q;
-  for (int ox = cls; ox < RD; ox += 256 / TQ) {
-#pragma unroll
-    for (int oy = 0; oy < RD; ++oy) {
-      const float s00 = sq[oy * RD1 + ox], s01 = sq[oy * RD1 + ox + 1];
-      const float s10 = sq[(oy + 1) * RD1 + ox], s11 = sq[(oy + 1) * RD1 + ox + 1];
-      float v = __fmul_rn(__fmul_rn(s00, 1.f - dy), 1.f - dx);
-      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s01, 1.f - dy), dx));
-      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s10, dy), 1.f - dx));
-      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s11, dy), dx));
-      o[(long long)(oy + RD * ox) * g.N] = v / g.divisor;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Grouped MFMA form (experiment).  As alt_corr_mfma_kernel,
-// but the tile's 32 queries are ranked by window origin x (off-level windows
-// last) and split into two groups of 16, each with the union box of ITS windows,
-// and the box GEMMs run on v_mfma_f32_16x16x32_bf16 (16 cells x 16 queries x
-// 32 channels).  With scattered coordinates (the benchmark's i.i.d. N(0, 4^2)
-// flows) two narrower boxes cover ~0.7x the (cell, query) pairs of the single
-// 4 x 8 box (level 0: 4.4x instead of 7.3x the compulsory window pairs).  Same
-// products, same f32-class split, same bilinear stage and output.
-// ---------------------------------------------------------------------------
-typedef float af4 __attribute__((ext_vector_type(4)));
-
-template <int R, int NRB, int CMAX>
-__global__ __launch_bounds__(256, 2) void alt_corr_mfma16_kernel(const float* __restrict__ f1,
-                                                                 const float* __restrict__ coords,
-                                                                 float* __restrict__ out,
-                                                                 AltGeom g, int W1, int tiles_x) {
-  constexpr int RD = 2 * R + 1, RD1 = RD + 1, NCELL = RD1 * RD1;
-  constexpr int CHUNK = 4 * 16 * NRB;                       // box cells per chunk
-  constexpr int KB = CMAX / 8;                              // 8-channel blocks
-  __shared__ __attribute__((aligned(16))) uint4 qplanes[3 * KB * TQ];   // [plane][kb][q]
-  __shared__ float S[TQ * NCELL];                           // window dot products
-  __shared__ int4 qinfo[TQ];                                // {x0, y0, live, key}
-  __shared__ int gq[2][16];                                 // group -> member query
-  __shared__ int box[2][4];                                 // per group bx0, by0, bw, bh
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  int tile = blockIdx.x;
-  {
-    const int n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = tile % 8;
-    tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + tile / 8;
-  }
-  const int tx = tile % tiles_x, ty = tile / tiles_x;
-  const AltLevel lv = g.lv[blockIdx.y];
-  const int z = blockIdx.z, bf = z / g.Nc;
-  const float* cz = coords + (long long)z * g.coord_zstride;
-  const float* f1b = f1 + (long long)bf * g.f1_bstride;
-  const float* f2b = lv.f2 + (long long)bf * lv.H2 * lv.W2 * g.C;
-  const int H1 = g.N / W1;
-  const int nkb = g.C / 8;
-
-  // ---- query coordinates, window origins, sort key (window x origin; off-level last)
-  if (tid < TQ) {
-    const int qy = ty * TQY + tid / TQX, qx = tx * TQX + tid % TQX;
-    int x0 = 0, y0 = 0, live = 0;
-    if (qy < H1 && qx < W1) {
-      const int q = qy * W1 + qx;
-      const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
-      const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
-      const float xf = floorf(x), yf = floorf(y);
-      if (fabsf(xf) < 1.0e8f && fabsf(yf) < 1.0e8f) {
-        x0 = (int)xf - R;
-        y0 = (int)yf - R;
-        live = (x0 + RD1 > 0 && x0 < lv.W2 && y0 + RD1 > 0 && y0 < lv.H2) ? 1 : 0;
-      }
-    }
-    qinfo[tid] = make_int4(x0, y0, live, live ? x0 : 0x7fffffff);
-  }
-  for (int i = tid; i < TQ * NCELL; i += 256) S[i] = 0.f;
-  // query operand planes: unit (kb, q) -> f1[q][8 kb .. 8 kb + 8), split once
-  for (int u = tid; u < nkb * TQ; u += 256) {
-    const int kb = u / TQ, qq = u - kb * TQ;
-    const int qy = min(ty * TQY + qq / TQX, H1 - 1), qx = min(tx * TQX + qq % TQX, W1 - 1);
-    const float* src = f1b + (long long)(qy * W1 + qx) * g.C + kb * 8;
-    const float4 a = *reinterpret_cast<const float4*>(src);
-    const float4 c = *reinterpret_cast<const float4*>(src + 4);
-    const float x[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
-    uint4 h, m, l;
-    alt_split8(x, h, m, l);
-    qplanes[(0 * KB + kb) * TQ + qq] = h;
-    qplanes[(1 * KB + kb) * TQ + qq] = m;
-    qplanes[(2 * KB + kb) * TQ + qq] = l;
-  }
-  __syncthreads();
-  if (tid < TQ) {
-    const int4 me = qinfo[tid];
-    int rank = 0;
-    for (int i = 0; i < TQ; ++i) {
-      const int k = qinfo[i].w;
-      rank += (k < me.w || (k == me.w && i < tid)) ? 1 : 0;
-    }
-    gq[rank >> 4][rank & 15] = tid;
-  }
-  __syncthreads();
-  if (tid < TQ) {     // lane (group tid >> 4, slot tid & 15): union box of the group's live windows
-    const int4 qi = qinfo[gq[tid >> 4][tid & 15]];
-    int lx0 = qi.z ? max(qi.x, 0) : 0x7fffffff, ly0 = qi.z ? max(qi.y, 0) : 0x7fffffff;
-    int lx1 = qi.z ? min(qi.x + RD1, lv.W2) : -1, ly1 = qi.z ? min(qi.y + RD1, lv.H2) : -1;
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      lx0 = min(lx0, __shfl_xor(lx0, o));
-      ly0 = min(ly0, __shfl_xor(ly0, o));
-      lx1 = max(lx1, __shfl_xor(lx1, o));
-      ly1 = max(ly1, __shfl_xor(ly1, o));
-    }
-    if ((tid & 15) == 0) {
-      const bool any = lx1 > lx0;
-      box[tid >> 4][0] = any ? lx0 : 0;
-      box[tid >> 4][1] = any ? ly0 : 0;
-      box[tid >> 4][2] = any ? lx1 - lx0 : 0;
-      box[tid >> 4][3] = any ? ly1 - ly0 : 0;
-    }
-  }
-  __syncthreads();
-
-  const int j = lane & 15, kq = lane >> 4;
-#pragma unroll 1
-  for (int grp = 0; grp < 2; ++grp) {
-    const int bx0 = box[grp][0], by0 = box[grp][1], bw = box[grp][2], bh = box[grp][3];
-    const int ncells = bw * bh;
-    const int jq = gq[grp][j];                  // this lane's accumulator column (query)
-    const int4 qi = qinfo[jq];
-    for (int c0 = 0; c0 < ncells; c0 += CHUNK) {
-      af4 acc[NRB];
-      const float* src[NRB];
-#pragma unroll
-      for (int rb = 0; rb < NRB; ++rb) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[rb][r] = 0.f;
-        // A operand lane -> cell c0 + 16 (wave NRB + rb) + j, channels 8 kq .. + 8 per k32
-        const int c = min(c0 + (wave * NRB + rb) * 16 + j, ncells - 1);
-        const int cy = c / bw, cx = c - cy * bw;
-        src[rb] = f2b + ((long long)(by0 + cy) * lv.W2 + bx0 + cx) * g.C + 8 * kq;
-      }
-      float4 ca[NRB], cb[NRB];
-#pragma unroll
-      for (int rb = 0; rb < NRB; ++rb) {
-        ca[rb] = *reinterpret_cast<const float4*>(src[rb]);
-        cb[rb] = *reinterpret_cast<const float4*>(src[rb] + 4);
-      }
-      for (int ks = 0; ks < nkb / 4; ++ks) {
-        float4 na[NRB], nb[NRB];
-        if (ks + 1 < nkb / 4) {
-#pragma unroll
-          for (int rb = 0; rb < NRB; ++rb) {
-            na[rb] = *reinterpret_cast<const float4*>(src[rb] + (ks + 1) * 32);
-            nb[rb] = *reinterpret_cast<const float4*>(src[rb] + (ks + 1) * 32 + 4);
-          }
-        }
-        const int kb = 4 * ks + kq;
-        const abf8 qh = __builtin_bit_cast(abf8, qplanes[(0 * KB + kb) * TQ + jq]);
-        const abf8 qm = __builtin_bit_cast(abf8, qplanes[(1 * KB + kb) * TQ + jq]);
-        const abf8 ql = __builtin_bit_cast(abf8, qplanes[(2 * KB + kb) * TQ + jq]);
-#pragma unroll
-        for (int rb = 0; rb < NRB; ++rb) {
-          const float4 a = ca[rb], b = cb[rb];
-          const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-          uint4 h, m, l;
-          alt_split8(x, h, m, l);
-          const abf8 th = __builtin_bit_cast(abf8, h), tm = __builtin_bit_cast(abf8, m),
-                     tl = __builtin_bit_cast(abf8, l);
-          // small terms first
-          acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tm, qm, acc[rb], 0, 0, 0);
-          acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tl, qh, acc[rb], 0, 0, 0);
-          acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(th, ql, acc[rb], 0, 0, 0);
-          acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tm, qh, acc[rb], 0, 0, 0);
-          acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(th, qm, acc[rb], 0, 0, 0);
-          acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(th, qh, acc[rb], 0, 0, 0);
-        }
-        if (ks + 1 < nkb / 4) {
-#pragma unroll
-          for (int rb = 0; rb < NRB; ++rb) {
-            ca[rb] = na[rb];
-            cb[rb] = nb[rb];
-          }
-        }
-      }
-      // keep the entries inside query jq's window: D row = 4 kq + r
-      if (qi.z) {
-#pragma unroll
-        for (int rb = 0; rb < NRB; ++rb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int c = c0 + (wave * NRB + rb) * 16 + 4 * kq + r;
-            if (c < ncells) {
-              const int cy = c / bw, cx = c - cy * bw;
-              const int iy = by0 + cy - qi.y, ix = bx0 + cx - qi.x;
-              if ((unsigned)iy < (unsigned)RD1 && (unsigned)ix < (unsigned)RD1)
-                S[jq * NCELL + iy * RD1 + ix] = acc[rb][r];
-            }
-          }
-      }
-    }
-  }
-  __syncthreads();
-
-  // ---- bilinear combination, as the per-query form (reference order)
-  const int qq = tid & (TQ - 1), cls = tid / TQ;
-  const int qy = ty * TQY + qq / TQX, qx = tx * TQX + qq % TQX;
-  if (qy >= H1 || qx >= W1) return;
-  const int q = qy * W1 + qx;
-  const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
-  const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
-  const float dx = x - floorf(x), dy = y - floorf(y);
-  const float* s = S + qq * NCELL;
-  float* o = out + (long long)z * g.cout * g.N + (long long)lv.ch_off * g.N + q;
-  for (int ox = cls; ox < RD; ox += 256 / TQ) {
-#pragma unroll
-    for (int oy = 0; oy < RD; ++oy) {
-      const float s00 = s[oy * RD1 + ox], s01 = s[oy * RD1 + ox + 1];
-      const float s10 = s[(oy + 1) * RD1 + ox], s11 = s[(oy + 1) * RD1 + ox + 1];
-      float v = __fmul_rn(__fmul_rn(s00, 1.f - dy), 1.f - dx);
-      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s01, 1.f - dy), dx));
-      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s10, dy), 1.f - dx));
-      v = __fadd_rn(v, __fmul_rn(__fmul_rn(s11, dy), dx));
-      o[(long long)(oy + RD * ox) * g.N] = v / g.divisor;
-    }
-  }
-}
-#endif  // DXR_EXPERIMENTS
-
-#ifdef DXR_EXPERIMENTS   // query binning: experiments target only
-// ---------------------------------------------------------------------------
-// Query binning for the on-the-fly block (BIN form of alt_corr_mfma_kernel).
-// One workgroup per (level, coordinate set): a counting sort of the N queries by
-// the bin of their window position — floor of the level coordinate, clamped to
-// the level, in bins of 2^bsx x 2^bsy cells (about 32 queries per bin at the
-// level's query density) walked in snake order, so consecutive bins are
-// neighbours; non-finite coordinates go last.  perm[(z * levels + l) * N + i].
-// The order inside a bin follows the LDS atomics (not fixed); every query's
-// outputs are computed on their own, so they do not depend on it.
-// ---------------------------------------------------------------------------
-constexpr int BIN_MAX = 8192;
-struct BinGeom {
-  int bsx[8], bsy[8], nbx[8], nby[8];
-};
-
-BinGeom make_bins(const AltGeom& g, int levels) {
-  BinGeom b;
-  for (int l = 0; l < levels; ++l) {
-    const int h2 = g.lv[l].H2, w2 = g.lv[l].W2;
-    const double dens = (double)g.N / ((double)h2 * w2);
-    int lg = 0;
-    while ((1 << lg) * dens < 32.0 && lg < 12) ++lg;   // bin area 2^lg ~ 32 queries
-    int by = lg / 2, bx = lg - by;
-    while (((w2 + (1 << bx) - 1) >> bx) * ((h2 + (1 << by) - 1) >> by) > BIN_MAX) {
-      if (bx <= by) ++bx; else ++by;
-    }
-    b.bsx[l] = bx;
-    b.bsy[l] = by;
-    b.nbx[l] = (w2 + (1 << bx) - 1) >> bx;
-    b.nby[l] = (h2 + (1 << by) - 1) >> by;
-  }
-  return b;
-}
-
-__global__ __launch_bounds__(1024) void alt_bin_kernel(const float* __restrict__ coords,
-                                                       int* __restrict__ perm, AltGeom g,
-                                                       BinGeom bg, int NP) {
-  __shared__ int cnt[BIN_MAX + 1];
-  __shared__ int wsum[16];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int l = blockIdx.x, z = blockIdx.y;
-  const AltLevel lv = g.lv[l];
-  const int nbx = bg.nbx[l], nb = nbx * bg.nby[l], bsx = bg.bsx[l], bsy = bg.bsy[l];
-  const float* cz = coords + (long long)z * g.coord_zstride;
-  for (int i = tid; i <= nb; i += 1024) cnt[i] = 0;
-  __syncthreads();
-  auto bin_of = [&](int q) -> int {
-    const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
-    const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
-    const float xf = floorf(x), yf = floorf(y);
-    if (!(fabsf(xf) < 1.0e8f && fabsf(yf) < 1.0e8f)) return nb;
-    const int cx = min(max((int)xf, 0), lv.W2 - 1), cy = min(max((int)yf, 0), lv.H2 - 1);
-    const int byi = cy >> bsy;
-    int bxi = cx >> bsx;
-    if (byi & 1) bxi = nbx - 1 - bxi;
-    return byi * nbx + bxi;
-  };
-  for (int q = tid; q < g.N; q += 1024) atomicAdd(&cnt[bin_of(q)], 1);
-  __syncthreads();
-  // exclusive scan of cnt[0..nb]: thread t owns a run of `per` bins
-  const int per = (nb + 1 + 1023) / 1024;
-  int loc = 0;
-  for (int k = 0; k < per; ++k) {
-    const int b = tid * per + k;
-    if (b <= nb) loc += cnt[b];
-  }
-  int v = loc;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(v, o);
-    if (lane >= o) v += t;
-  }
-  if (lane == 63) wsum[wave] = v;
-  __syncthreads();
-  if (tid == 0) {
-    int acc = 0;
-    for (int w = 0; w < 16; ++w) {
-      const int t = wsum[w];
-      wsum[w] = acc;
-      acc += t;
-    }
-  }
-  __syncthreads();
-  int run = wsum[wave] + v - loc;
-  for (int k = 0; k < per; ++k) {
-    const int b = tid * per + k;
-    if (b <= nb) {
-      const int c = cnt[b];
-      cnt[b] = run;
-      run += c;
-    }
-  }
-  __syncthreads();
-  int* pz = perm + ((long long)z * gridDim.x + l) * NP;
-  for (int q = tid; q < g.N; q += 1024) pz[atomicAdd(&cnt[bin_of(q)], 1)] = q;
-  for (int i = g.N + tid; i < NP; i += 1024) pz[i] = -1;
-}
-
-// Parallel form of the binning (three launches per call) with a per-list choice
-// of the order: K1 (alt_bin_count_kernel) walks the queries in 4 x 8-tile order,
-// counts them per bin and sums the union-box area of every spatial tile (the
-// cells the spatial order would multiply); K2 (alt_bin_scan_kernel) scans the
-// counts and keeps the binned order only where its estimated box area is smaller;
-// K3 (alt_bin_scatter_kernel) writes the list: bin order, or the tile order
-// itself (then the main kernel is the spatial form, bit for bit).
-// Workspace (ints): cnt [Z][L][CNT_STRIDE] (bins and the far bin, then the
-// spatial cost and the decision), binid [Z][L][NP], perm [Z][L][NP];
-// NP = whole 4 x 8 tiles x 32.  cnt must be zero before K1.
-constexpr int CNT_STRIDE = BIN_MAX + 4;
-constexpr int CNT_COST = BIN_MAX + 2, CNT_FLAG = BIN_MAX + 3;
-
-__device__ __forceinline__ int bin_of_xy(float xf, float yf, const AltLevel& lv, int nbx, int nb,
-                                         int bsx, int bsy) {
-  if (!(fabsf(xf) < 1.0e8f && fabsf(yf) < 1.0e8f)) return nb;
-  const int cx = min(max((int)xf, 0), lv.W2 - 1), cy = min(max((int)yf, 0), lv.H2 - 1);
-  const int byi = cy >> bsy;
-  int bxi = cx >> bsx;
-  if (byi & 1) bxi = nbx - 1 - bxi;
-  return byi * nbx + bxi;
-}
-
-template <int R>
-__global__ __launch_bounds__(256) void alt_bin_count_kernel(const float* __restrict__ coords,
-                                                            AltGeom g, BinGeom bg, int W1,
-                                                            int tiles_x, int* __restrict__ cnt,
-                                                            int* __restrict__ binid, int NP) {
-  constexpr int RD1 = 2 * R + 2;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  const int l = blockIdx.y, z = blockIdx.z;
-  const long long zl = (long long)z * gridDim.y + l;
-  const AltLevel lv = g.lv[l];
-  const int H1 = g.N / W1;
-  const int tile = i / TQ, slot = i % TQ;
-  const int qy = (tile / tiles_x) * TQY + slot / TQX, qx = (tile % tiles_x) * TQX + slot % TQX;
-  int* c = cnt + zl * CNT_STRIDE;
-  int lx0 = 0x7fffffff, ly0 = 0x7fffffff, lx1 = -1, ly1 = -1;
-  if (i < NP && qy < H1 && qx < W1) {
-    const int q = qy * W1 + qx;
-    const float* cz = coords + (long long)z * g.coord_zstride;
-    const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
-    const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
-    const float xf = floorf(x), yf = floorf(y);
-    const int nbx = bg.nbx[l], nb = nbx * bg.nby[l];
-    const int bin = bin_of_xy(xf, yf, lv, nbx, nb, bg.bsx[l], bg.bsy[l]);
-    binid[zl * NP + q] = bin;
-    atomicAdd(&c[bin], 1);
-    if (bin < nb) {   // the main kernel's live window, clipped to the level
-      const int x0 = (int)xf - R, y0 = (int)yf - R;
-      if (x0 + RD1 > 0 && x0 < lv.W2 && y0 + RD1 > 0 && y0 < lv.H2) {
-        lx0 = max(x0, 0);
-        ly0 = max(y0, 0);
-        lx1 = min(x0 + RD1, lv.W2);
-        ly1 = min(y0 + RD1, lv.H2);
-      }
-    }
-  }
-#pragma unroll
-  for (int o = 1; o < TQ; o <<= 1) {   // union box of this tile (32 lanes)
-    lx0 = min(lx0, __shfl_xor(lx0, o));
-    ly0 = min(ly0, __shfl_xor(ly0, o));
-    lx1 = max(lx1, __shfl_xor(lx1, o));
-    ly1 = max(ly1, __shfl_xor(ly1, o));
-  }
-  if (slot == 0 && lx1 > lx0) atomicAdd(&c[CNT_COST], (lx1 - lx0) * (ly1 - ly0));
-}
-
-template <int R>
-__global__ __launch_bounds__(1024) void alt_bin_scan_kernel(int* __restrict__ cnt, AltGeom g,
-                                                            BinGeom bg) {
-  __shared__ int wsum[16];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int l = blockIdx.x, z = blockIdx.y;
-  int* c = cnt + ((long long)z * gridDim.x + l) * CNT_STRIDE;
-  const int nb = bg.nbx[l] * bg.nby[l];
-  const int per = (nb + 1 + 1023) / 1024;
-  int loc = 0;
-  for (int k = 0; k < per; ++k) {
-    const int b = tid * per + k;
-    if (b <= nb) loc += c[b];
-  }
-  int v = loc;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(v, o);
-    if (lane >= o) v += t;
-  }
-  if (lane == 63) wsum[wave] = v;
-  __syncthreads();
-  if (tid == 0) {
-    int acc = 0;
-    for (int w = 0; w < 16; ++w) {
-      const int t = wsum[w];
-      wsum[w] = acc;
-      acc += t;
-    }
-    // binned estimate: every chunk of 32 spans about one and a half bins along x
-    const int bw = 1 << bg.bsx[l], bh = 1 << bg.bsy[l];
-    const long long est = (long long)((g.N + TQ - 1) / TQ) *
-                          min(bw + bw / 2 + 2 * R + 1, g.lv[l].W2) * min(bh + 2 * R + 1, g.lv[l].H2);
-    c[CNT_FLAG] = est < (long long)c[CNT_COST] ? 1 : 0;
-  }
-  __syncthreads();
-  int run = wsum[wave] + v - loc;
-  for (int k = 0; k < per; ++k) {
-    const int b = tid * per + k;
-    if (b <= nb) {
-      const int t = c[b];
-      c[b] = run;
-      run += t;
-    }
-  }
-}
-
-__global__ __launch_bounds__(256) void alt_bin_scatter_kernel(AltGeom g, int W1, int tiles_x,
-                                                              int* __restrict__ cnt,
-                                                              const int* __restrict__ binid,
-                                                              int* __restrict__ perm, int NP) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= NP) return;
-  const int l = blockIdx.y, z = blockIdx.z;
-  const long long zl = (long long)z * gridDim.y + l;
-  int* c = cnt + zl * CNT_STRIDE;
-  int* pz = perm + zl * NP;
-  if (c[CNT_FLAG]) {   // bin order: thread i places query i
-    if (i < g.N) pz[atomicAdd(&c[binid[zl * NP + i]], 1)] = i;
-    else pz[i] = -1;
-  } else {             // tile order
-    const int H1 = g.N / W1;
-    const int tile = i / TQ, slot = i % TQ;
-    const int qy = (tile / tiles_x) * TQY + slot / TQX, qx = (tile % tiles_x) * TQX + slot % TQX;
-    pz[i] = (qy < H1 && qx < W1) ? qy * W1 + qx : -1;
-  }
-}
-
-// Binned on-the-fly lookup (K1-K3 + the BIN form).  ws: workspace of
-// alt_ws_ints(...) ints.
-long long alt_ws_ints(long long Z, int levels, int NP) {
-  return Z * levels * ((long long)CNT_STRIDE + 2LL * NP);
-}
-
-template <int R>
-int launch_alt_binned_r(const float* f1, const float* coords, float* out, const AltGeom& g,
-                        int levels, int Z, int W1, int* ws, hipStream_t stream, int upto = 4) {
-  const int H1 = g.N / W1;
-  const int tiles_x = (W1 + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
-  const int NP = tiles_x * tiles_y * TQ;
-  int* cnt = ws;
-  int* binid = cnt + (long long)Z * levels * CNT_STRIDE;
-  int* perm = binid + (long long)Z * levels * NP;
-  const BinGeom bg = make_bins(g, levels);
-  if (hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)Z * levels * CNT_STRIDE, stream) != hipSuccess)
-    return DXR_EHIP;
-  const dim3 gq((unsigned)((NP + 255) / 256), (unsigned)levels, (unsigned)Z);
-  if (upto < 1) return dxr::launch_status();
-  hipLaunchKernelGGL((alt_bin_count_kernel<R>), gq, dim3(256), 0, stream, coords, g, bg, W1, tiles_x,
-                     cnt, binid, NP);
-  if (upto < 2) return dxr::launch_status();
-  hipLaunchKernelGGL((alt_bin_scan_kernel<R>), dim3((unsigned)levels, (unsigned)Z), dim3(1024), 0,
-                     stream, cnt, g, bg);
-  if (upto < 3) return dxr::launch_status();
-  hipLaunchKernelGGL(alt_bin_scatter_kernel, gq, dim3(256), 0, stream, g, W1, tiles_x, cnt, binid,
-                     perm, NP);
-  if (upto < 4) return dxr::launch_status();
-  const dim3 grid((unsigned)(NP / TQ), (unsigned)levels, (unsigned)Z);
-  hipLaunchKernelGGL((alt_corr_mfma_kernel<R, 1, 256, true, 3, 0, true>), grid, dim3(256), 0, stream,
-                     f1, coords, out, g, W1, NP / TQ, perm);
-  return dxr::launch_status();
-}
-
-#endif  // DXR_EXPERIMENTS
 
 template <int R, int NRB>
 int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const AltGeom& g,
@@ -1879,197 +960,3 @@ extern "C" int dxr_alt_corr_lookup(const float* fmap1, const float* const* fmap2
   return launch_alt(fmap1, coords, out, g, num_levels, (int)B, radius, vec, stream, (int)W);
 }
 
-#ifdef DXR_EXPERIMENTS
-// Experiments build target only: the fused on-the-fly lookup with a chosen kernel
-// (0: 4x8-box 32x32x16 form, 1: grouped 16x16x32 form NRB 2, 2: NRB 1).
-namespace {
-template <int NRB>
-int xp_alt16(const float* f1, const float* coords, float* out, const AltGeom& g, int levels, int Z,
-             int W1, hipStream_t stream) {
-  const int H1 = g.N / W1;
-  const int tiles_x = (W1 + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
-  const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)levels, (unsigned)Z);
-  hipLaunchKernelGGL((alt_corr_mfma16_kernel<4, NRB, 256>), grid, dim3(256), 0, stream, f1, coords,
-                     out, g, W1, tiles_x);
-  return dxr::launch_status();
-}
-}  // namespace
-
-constexpr long long XP_PERM_MAX = 1LL << 22;
-int xp_np(const AltGeom& g, int W1) {   // perm entries per list: whole 4 x 8 tiles
-  const int H1 = g.N / W1;
-  return ((W1 + TQX - 1) / TQX) * ((H1 + TQY - 1) / TQY) * TQ;
-}
-__device__ int xp_perm[XP_PERM_MAX];   // experiments: binned-form query lists
-
-extern "C" int dxr_xp_alt(const float* fmap1, const float* const* fmap2_levels, const float* coords,
-                          float* out, int64_t B, int64_t H, int64_t W, int64_t C, int num_levels,
-                          float divisor, int xp, hipStream_t stream) {
-  dxr::Levels L;
-  if (!dxr::make_levels(B, H, W, num_levels, &L) || C != 256) return DXR_EINVAL;
-  AltGeom g;
-  g.N = (int)(H * W);
-  g.C = (int)C;
-  g.Nc = 1;
-  g.cout = num_levels * 81;
-  g.divisor = divisor;
-  g.div_recip = pow2_recip(divisor);
-  g.f1_bstride = H * W * C;
-  g.coord_zstride = 2 * H * W;
-  g.coord_cstride = H * W;
-  g.coord_qstride = 1;
-  for (int l = 0; l < num_levels; ++l)
-    g.lv[l] = AltLevel{fmap2_levels[l], L.h[l], L.w[l], 1.f / (float)(1 << l), l * 81};
-  if (xp == 0) return launch_alt_mfma_r<4, 1>(fmap1, coords, out, g, num_levels, (int)B, (int)W, stream);
-  if (xp == 1) return xp_alt16<2>(fmap1, coords, out, g, num_levels, (int)B, (int)W, stream);
-  if (xp == 2) return xp_alt16<1>(fmap1, coords, out, g, num_levels, (int)B, (int)W, stream);
-  if (xp == 8) {
-    const int H1 = g.N / (int)W;
-    const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
-    const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
-    hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 2, 256, true, 3>), grid, dim3(256), 0, stream,
-                       fmap1, coords, out, g, (int)W, tiles_x, nullptr);
-    return dxr::launch_status();
-  }
-  if (xp >= 40 && xp <= 42) {
-    // binned form: 40 = binning + binned kernel, 41 = binning only, 42 = binned
-    // kernel only (the perm of the previous call)
-    if ((long long)B * num_levels * xp_np(g, (int)W) > XP_PERM_MAX) return DXR_EUNSUPPORTED;
-    int* perm = nullptr;
-    if (hipGetSymbolAddress(reinterpret_cast<void**>(&perm), HIP_SYMBOL(xp_perm)) != hipSuccess)
-      return DXR_EINVAL;
-    if (xp != 42) {
-      hipLaunchKernelGGL(alt_bin_kernel, dim3((unsigned)num_levels, (unsigned)B), dim3(1024), 0,
-                         stream, coords, perm, g, make_bins(g, num_levels), xp_np(g, (int)W));
-      if (xp == 41) return dxr::launch_status();
-    }
-    const int nchunk = xp_np(g, (int)W) / TQ;
-    const dim3 grid((unsigned)nchunk, (unsigned)num_levels, (unsigned)B);
-    hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3, 0, true>), grid, dim3(256), 0,
-                       stream, fmap1, coords, out, g, (int)W, nchunk, perm);
-    return dxr::launch_status();
-  }
-  if (xp >= 50 && xp <= 54) {   // parallel binning with the per-list order choice (51-54: phases)
-    const int NP = xp_np(g, (int)W);
-    if (alt_ws_ints(B, num_levels, NP) > XP_PERM_MAX) return DXR_EUNSUPPORTED;
-    int* ws = nullptr;
-    if (hipGetSymbolAddress(reinterpret_cast<void**>(&ws), HIP_SYMBOL(xp_perm)) != hipSuccess)
-      return DXR_EINVAL;
-    return launch_alt_binned_r<4>(fmap1, coords, out, g, num_levels, (int)B, (int)W, ws, stream,
-                                  xp == 50 ? 4 : xp - 51);
-  }
-  if (xp == 55) {   // the per-level order decisions of the last xp 50 call -> out[0..levels)
-    int* ws = nullptr;
-    if (hipGetSymbolAddress(reinterpret_cast<void**>(&ws), HIP_SYMBOL(xp_perm)) != hipSuccess)
-      return DXR_EINVAL;
-    for (int l = 0; l < num_levels; ++l) {
-      int v[2];
-      hipMemcpy(v, ws + l * CNT_STRIDE + CNT_COST, 8, hipMemcpyDeviceToHost);
-      const float f[2] = {(float)v[0], (float)v[1]};
-      hipMemcpy(out + 2 * l, f, 8, hipMemcpyHostToDevice);
-    }
-    return DXR_OK;
-  }
-  if (xp >= 43 && xp <= 46) {
-    // binned form with PF k steps of cell loads in flight: 43 PF 4, 44 PF 6, 45 PF 8,
-    // 46 PF 4 at two workgroups per CU
-    if ((long long)B * num_levels * xp_np(g, (int)W) > XP_PERM_MAX) return DXR_EUNSUPPORTED;
-    int* perm = nullptr;
-    if (hipGetSymbolAddress(reinterpret_cast<void**>(&perm), HIP_SYMBOL(xp_perm)) != hipSuccess)
-      return DXR_EINVAL;
-    hipLaunchKernelGGL(alt_bin_kernel, dim3((unsigned)num_levels, (unsigned)B), dim3(1024), 0,
-                       stream, coords, perm, g, make_bins(g, num_levels), xp_np(g, (int)W));
-    const int nchunk = xp_np(g, (int)W) / TQ;
-    const dim3 grid((unsigned)nchunk, (unsigned)num_levels, (unsigned)B);
-    if (xp == 43)
-      hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3, 0, true, 4>), grid, dim3(256), 0,
-                         stream, fmap1, coords, out, g, (int)W, nchunk, perm);
-    else if (xp == 44)
-      hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3, 0, true, 6>), grid, dim3(256), 0,
-                         stream, fmap1, coords, out, g, (int)W, nchunk, perm);
-    else if (xp == 45)
-      hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3, 0, true, 8>), grid, dim3(256), 0,
-                         stream, fmap1, coords, out, g, (int)W, nchunk, perm);
-    else
-      hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 2, 0, true, 4>), grid, dim3(256), 0,
-                         stream, fmap1, coords, out, g, (int)W, nchunk, perm);
-    return dxr::launch_status();
-  }
-  if (xp == 47 || xp == 48) {   // spatial tiles with PF 4 / 8
-    const int H1 = g.N / (int)W;
-    const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
-    const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
-    if (xp == 47)
-      hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3, 0, false, 4>), grid, dim3(256),
-                         0, stream, fmap1, coords, out, g, (int)W, tiles_x, nullptr);
-    else
-      hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3, 0, false, 8>), grid, dim3(256),
-                         0, stream, fmap1, coords, out, g, (int)W, tiles_x, nullptr);
-    return dxr::launch_status();
-  }
-  if (xp == 60) {   // r02 index arithmetic (integer / IEEE divisions)
-    const int H1 = g.N / (int)W;
-    const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
-    const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
-    hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3, 0, false, 1, true>), grid, dim3(256),
-                       0, stream, fmap1, coords, out, g, (int)W, tiles_x, nullptr);
-    return dxr::launch_status();
-  }
-  if (xp == 30) {   // sc1 (write-through) output stores
-    const int H1 = g.N / (int)W;
-    const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
-    const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
-    hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3, 1>), grid, dim3(256), 0, stream,
-                       fmap1, coords, out, g, (int)W, tiles_x, nullptr);
-    return dxr::launch_status();
-  }
-  if (xp == 9) {   // the r01 form: 3-way bf16 split, 2 workgroups/CU
-    const int H1 = g.N / (int)W;
-    const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
-    const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
-    hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, false, 2>), grid, dim3(256), 0, stream,
-                       fmap1, coords, out, g, (int)W, tiles_x, nullptr);
-    return dxr::launch_status();
-  }
-  if (xp == 20 || xp == 21) {   // 8 x 16 query tiles, cells shared through LDS
-    const int H1 = g.N / (int)W;
-    const int tiles_x = ((int)W + T2X - 1) / T2X, tiles_y = (H1 + T2Y - 1) / T2Y;
-    const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
-    if (xp == 20)
-      hipLaunchKernelGGL((alt_corr_tile_kernel<4, 2>), grid, dim3(256), 0, stream, fmap1, coords,
-                         out, g, (int)W, tiles_x);
-    else
-      hipLaunchKernelGGL((alt_corr_tile_kernel<4, 1>), grid, dim3(256), 0, stream, fmap1, coords,
-                         out, g, (int)W, tiles_x);
-    return dxr::launch_status();
-  }
-  if (xp == 6 || xp == 7) {
-    const int H1 = g.N / (int)W;
-    const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
-    const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
-    if (xp == 6)
-      hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 3>), grid, dim3(256), 0, stream,
-                         fmap1, coords, out, g, (int)W, tiles_x, nullptr);
-    else
-      hipLaunchKernelGGL((alt_corr_mfma_kernel<4, 1, 256, true, 2>), grid, dim3(256), 0, stream,
-                         fmap1, coords, out, g, (int)W, tiles_x, nullptr);
-    return dxr::launch_status();
-  }
-  if (xp == 3 || xp == 4 || xp == 5) {
-    const int H1 = g.N / (int)W;
-    const int tiles_x = ((int)W + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
-    const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)num_levels, (unsigned)B);
-    if (xp == 3)
-      hipLaunchKernelGGL((alt_corr_mfma_rq_kernel<4, 2>), grid, dim3(256), 0, stream, fmap1, coords,
-                         out, g, (int)W, tiles_x);
-    else if (xp == 4)
-      hipLaunchKernelGGL((alt_corr_mfma_rq_kernel<4, 4>), grid, dim3(256), 0, stream, fmap1, coords,
-                         out, g, (int)W, tiles_x);
-    else
-      hipLaunchKernelGGL((alt_corr_mfma_rq_kernel<4, 6>), grid, dim3(256), 0, stream, fmap1, coords,
-                         out, g, (int)W, tiles_x);
-    return dxr::launch_status();
-  }
-  return DXR_EUNSUPPORTED;
-}
-#endif

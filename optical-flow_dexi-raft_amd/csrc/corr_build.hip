@@ -218,9 +218,9 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 // ((v00+v01)+v10)+v11 (F.avg_pool2d), then rounded to OT once.
 // `wave`: which 32 queries of the page this wave holds (and its private LDS
 // staging region).
-// EX (experiments): bit 0 syncs only the wave around its private staging
-// region instead of the workgroup; bit 1 streams the pyramid with non-temporal
-// stores.
+// EX: bit 0 syncs only the wave around its private staging region instead of
+// the workgroup; bit 1 streams the pyramid with non-temporal stores; bit 2 with
+// write-through (sc1) buffer stores.
 template <int EX>
 __device__ __forceinline__ void epi_sync() {
   if constexpr ((EX & 1) != 0) {
@@ -232,11 +232,10 @@ __device__ __forceinline__ void epi_sync() {
   }
 }
 // EX bit 2: buffer stores from a workgroup-uniform base `ub` (a level's page)
-// with cache-policy bits AUX = EX >> 8 (16 = sc1, write-through; 18 = sc1 nt;
-// 17 = sc0 sc1; 2 = nt), 16 when EX >> 8 is 0.
+// with the sc1 cache-policy bit (write-through).
 template <int EX, typename V, typename T>
 __device__ __forceinline__ void epi_put(T* ub, T* p, const V v) {
-  constexpr int AUX = (EX >> 8) ? (EX >> 8) : 16;
+  constexpr int AUX = 16;
   if constexpr ((EX & 4) != 0) {
     const __amdgpu_buffer_rsrc_t r =
         __builtin_amdgcn_make_buffer_rsrc(ub, (short)0, 0x7fffffff, 0x00020000);
@@ -371,17 +370,6 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
     OT* pg2 = pb2 + (long long)wave * 32 * 8 + j * 8 + 4 * h;
     if constexpr (sizeof(OT) == 4) {
       epi_put<EX>(pb2, pg2, f32x4v{l2[h][0], l2[h][1], l2[h][2], l2[h][3]});
-    } else if constexpr ((EX & 8) != 0) {
-      // wide form: lane j (both rows of query j live in every lane) writes the
-      // query's 8 bf16 as one 16-byte store
-      if (h == 0) {
-        u32x4v w;
-        w.x = (uint32_t)to_out<OT>(l2[0][0]) | ((uint32_t)to_out<OT>(l2[0][1]) << 16);
-        w.y = (uint32_t)to_out<OT>(l2[0][2]) | ((uint32_t)to_out<OT>(l2[0][3]) << 16);
-        w.z = (uint32_t)to_out<OT>(l2[1][0]) | ((uint32_t)to_out<OT>(l2[1][1]) << 16);
-        w.w = (uint32_t)to_out<OT>(l2[1][2]) | ((uint32_t)to_out<OT>(l2[1][3]) << 16);
-        epi_put<EX>(pb2, pg2, w);
-      }
     } else {
       u32x2v w;
       w.x = (uint32_t)to_out<OT>(l2[h][0]) | ((uint32_t)to_out<OT>(l2[h][1]) << 16);
@@ -398,22 +386,7 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
     l3[v] = (((l2[0][2 * v] + l2[0][2 * v + 1]) + l2[1][2 * v]) + l2[1][2 * v + 1]) * 0.25f;
   OT* const pb3 = pyr + g.loff[3] + page * (BM * 2);
   OT* pg3 = pb3 + (long long)wave * 32 * 2;
-  if constexpr ((EX & 8) != 0 && sizeof(OT) == 4) {
-    // wide form: lane L < 16 writes queries 2L, 2L+1 (both cells each) as one
-    // 16-byte store; every lane holds both cells of its query
-    const float a0 = __shfl(l3[0], (2 * lane) & 63), a1 = __shfl(l3[1], (2 * lane) & 63);
-    const float n0 = __shfl(l3[0], (2 * lane + 1) & 63), n1 = __shfl(l3[1], (2 * lane + 1) & 63);
-    if (lane < 16) epi_put<EX>(pb3, pg3 + lane * 4, f32x4v{a0, a1, n0, n1});
-  } else if constexpr ((EX & 8) != 0) {
-    // wide form (bf16): lane L < 8 writes queries 4L .. 4L+3 as one 16-byte store
-    const uint32_t pr = (uint32_t)to_out<OT>(l3[0]) | ((uint32_t)to_out<OT>(l3[1]) << 16);
-    const uint32_t p1 = __shfl(pr, (4 * lane + 1) & 63), p2 = __shfl(pr, (4 * lane + 2) & 63),
-                   p3 = __shfl(pr, (4 * lane + 3) & 63);
-    const uint32_t p0 = __shfl(pr, (4 * lane) & 63);
-    if (lane < 8) epi_put<EX>(pb3, pg3 + lane * 8, u32x4v{p0, p1, p2, p3});
-  } else {
-    epi_put<EX>(pb3, pg3 + j * 2 + h, to_out<OT>(l3[h]));
-  }
+  epi_put<EX>(pb3, pg3 + j * 2 + h, to_out<OT>(l3[h]));
 }
 
 // PAGED: write the paged pyramid (levels 1..4 fused).  !PAGED: write level 0
@@ -581,9 +554,7 @@ __device__ __forceinline__ int tgt_col(int r, int c) {
   return (r >> 1) * 32 + (c & 3) + 4 * (r & 1) + 8 * (c >> 2);
 }
 
-// XP: timing ablations (experiments build target only): bit 0 skips the epilogue
-// stores, 1 the MFMAs, 2 the in-loop global loads.
-template <bool VEC, typename OT, bool DIV, int MINW, bool REMAP = false, int XP = 0>
+template <bool VEC, typename OT, bool DIV, int MINW, bool REMAP = false>
 __global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_t* __restrict__ f1,
                                                              const uint16_t* __restrict__ f2,
                                                              OT* __restrict__ pyr, BuildGeom g) {
@@ -633,9 +604,6 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_
     }
   }
   auto load = [&](int k0) {
-    if constexpr ((XP & 4) != 0) {
-      if (k0 > 0) return;
-    }
     if constexpr (VEC) {
       const int so = k0 * g.N * 2;
 #pragma unroll
@@ -709,13 +677,8 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_
         const uint16_t* pb = Bt + kk * PH + rd_off + t * 32;
         const s8v tv = __builtin_shufflevector(tr_read(pb), tr_read(pb + 4 * PH), 0, 1, 2, 3, 4,
                                                5, 6, 7);
-        if constexpr ((XP & 2) != 0) {
-          const s8v x = tv ^ qv;
-          acc[t][0] += (float)(x[0] + x[3] + x[5] + x[7]);
-        } else {
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8v, tv), qf, acc[t],
-                                                           0, 0, 0);
-        }
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8v, tv), qf, acc[t],
+                                                         0, 0, 0);
       }
     }
     if (ks + 1 < nk) store(buf ^ 1);
@@ -723,17 +686,7 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_
   }
 
   scale_acc<DIV>(acc, g);
-  if constexpr ((XP & 1) != 0) {
-    float sum = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sum += acc[t][r];
-    if (sum == 1234.5f) pyr[tid] = to_out<OT>(sum);  // keeps the K loop live
-    return;
-  }
-  paged_epilogue<OT, (XP >> 5) & 3>(acc, reinterpret_cast<float*>(smem), pyr, g, pc.page, wave,
-                                    lane);
+  paged_epilogue<OT, 0>(acc, reinterpret_cast<float*>(smem), pyr, g, pc.page, wave, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -749,8 +702,16 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_bf16_kernel(const uint16_
 // workgroup (both with their r02 epilogues; K loop alone 295 vs 391 us).
 // ---------------------------------------------------------------------------
 constexpr int STAGE_Q2 = 3 * BKH * PH;  // A0, A1, target images (bf16 elements)
+// NHWC (channels-last bf16 fmaps): the three images are
+// stored row-major, one row per query / target (MFMA row order) holding the
+// stage's 32 k, at an 80-byte pitch: a ds_read_b128 hands lane l row l & 31,
+// k 8 (l >> 5) .. +7 — the operand the two transposed reads of the NCHW form
+// assemble — and its 16-lane groups hit 16 distinct 16-byte bank slots
+// (row stride 5 slots).  Same operands, same products: bit-identical pages.
+constexpr int PQN = BKH + 8;             // NHWC row pitch (bf16 elements)
+static_assert(BM * PQN == BKH * PH, "an NHWC image is the size of an NCHW one");
 
-template <typename OT, bool DIV, int MINW, int XP = 0>
+template <typename OT, bool DIV, int MINW, bool NHWC = false>
 __global__ __launch_bounds__(2 * NT, MINW) void corr_build_bf16_q2_kernel(
     const uint16_t* __restrict__ f1, const uint16_t* __restrict__ f2, OT* __restrict__ pyr,
     BuildGeom g) {
@@ -761,15 +722,6 @@ __global__ __launch_bounds__(2 * NT, MINW) void corr_build_bf16_q2_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int half = wave >> 2, w4 = wave & 3;
-  if constexpr ((XP & 768) != 0) {
-    // XP bits 8-9 (experiments): the workgroups of the first dispatch wave in CU
-    // slot 1 (linear id 256..511, breadth-first dispatch) sleep k * 8K cycles,
-    // k = (XP >> 8) & 3, so the two slots' epilogues fall at different times.
-    const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-    if (L >= 256 && L < 512) {
-      for (int i = 0; i < ((XP >> 8) & 3); ++i) __builtin_amdgcn_s_sleep(127);
-    }
-  }
   const PageCoord pc = page_coord<true, 2>(g);
   const int th0 = pc.tyi * TH, tw0 = pc.txi * TW;
   const int q0 = pc.qblk * BM;                      // first of the two blocks
@@ -783,49 +735,84 @@ __global__ __launch_bounds__(2 * NT, MINW) void corr_build_bf16_q2_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
-  // Staging units of 4 bf16 (8 B): thread unit s covers idx = tid + 512 s;
+  // NCHW staging units of 4 bf16 (8 B): thread unit s covers idx = tid + 512 s;
   // s = 0,1 -> image A0, 2,3 -> A1, 4,5 -> targets; u = idx & 1023 within the
-  // image: k = u >> 5, 4 consecutive queries / target cols (buffer loads,
-  // out-of-range units read zeros).  Host side guarantees D * N * 2 < 2^31.
+  // image: k = u >> 5, 4 consecutive queries / target cols.
+  // NHWC units of 8 bf16 (16 B, 8 consecutive k of one pixel): unit s covers
+  // idx = tid + 512 s, image idx >> 9 (A0, A1, targets), u = idx & 511: row
+  // u >> 2, k 8 (u & 3) .. +7.
+  // Buffer loads, out-of-range units read zeros.  Host side guarantees
+  // D * N * 2 < 2^31 (and D % 32 == 0 for NHWC).
+  constexpr int NU = NHWC ? 3 : 6;
   const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t*>(f1b), (short)0, g.D * g.N * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t*>(f2b), (short)0, g.D * g.N * 2, 0x00020000);
-  uint32_t vo[6];
-  int lo[6];
+  uint32_t vo[NU];
+  int lo[NU];
 #pragma unroll
-  for (int s = 0; s < 6; ++s) {
-    const int u = (tid + 2 * NT * s) & 1023, img = s >> 1;
-    const int k = u >> 5;
-    if (img < 2) {
-      const int q = q0 + img * BM + (u & 31) * 4;
-      vo[s] = q < g.N ? (uint32_t)(k * g.N + q) * 2u : 0x80000000u;
-      lo[s] = img * BKH * PH + k * PH + (u & 31) * 4;
+  for (int s = 0; s < NU; ++s) {
+    if constexpr (NHWC) {
+      const int idx = tid + 2 * NT * s, img = idx >> 9, u = idx & 511;
+      const int row = u >> 2, kq = u & 3;
+      if (img < 2) {
+        const int q = q0 + img * BM + row;
+        vo[s] = q < g.N ? (uint32_t)(q * g.D + 8 * kq) * 2u : 0x80000000u;
+        lo[s] = (img * BM + row) * PQN + 8 * kq;
+      } else {
+        const int r = row >> 4, c = row & 15, hh = th0 + r, ww = tw0 + c;
+        vo[s] = (hh < g.H && ww < g.W) ? (uint32_t)((hh * g.W + ww) * g.D + 8 * kq) * 2u
+                                       : 0x80000000u;
+        lo[s] = (2 * BM + tgt_col(r, c)) * PQN + 8 * kq;
+      }
     } else {
-      const int r = (u >> 2) & 7, c = (u & 3) * 4, hh = th0 + r, ww = tw0 + c;
-      vo[s] = (hh < g.H && ww < g.W) ? (uint32_t)(k * g.N + hh * g.W + ww) * 2u : 0x80000000u;
-      lo[s] = 2 * BKH * PH + k * PH + tgt_col(r, c);
+      const int u = (tid + 2 * NT * s) & 1023, img = s >> 1;
+      const int k = u >> 5;
+      if (img < 2) {
+        const int q = q0 + img * BM + (u & 31) * 4;
+        vo[s] = q < g.N ? (uint32_t)(k * g.N + q) * 2u : 0x80000000u;
+        lo[s] = img * BKH * PH + k * PH + (u & 31) * 4;
+      } else {
+        const int r = (u >> 2) & 7, c = (u & 3) * 4, hh = th0 + r, ww = tw0 + c;
+        vo[s] = (hh < g.H && ww < g.W) ? (uint32_t)(k * g.N + hh * g.W + ww) * 2u : 0x80000000u;
+        lo[s] = 2 * BKH * PH + k * PH + tgt_col(r, c);
+      }
     }
   }
-  uint2 rr[6];
+  using Unit = std::conditional_t<NHWC, uint4, uint2>;
+  Unit rr[NU];
   auto load = [&](int k0) {
-    if constexpr ((XP & 4) != 0) {
-      if (k0 > 0) return;
-    }
-    const int so = k0 * g.N * 2;
+    const int so = NHWC ? k0 * 2 : k0 * g.N * 2;
 #pragma unroll
-    for (int s = 0; s < 6; ++s)
-      rr[s] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(s < 4 ? rsa : rsb,
-                                                                              vo[s], so, 0));
+    for (int s = 0; s < NU; ++s) {
+      const __amdgpu_buffer_rsrc_t r = (s < (NHWC ? 2 : 4)) ? rsa : rsb;
+      if constexpr (NHWC)
+        rr[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, vo[s], so, 0));
+      else
+        rr[s] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, vo[s], so, 0));
+    }
   };
   auto store = [&](int buf) {
     uint16_t* S = lh + buf * STAGE_Q2;
 #pragma unroll
-    for (int s = 0; s < 6; ++s) *reinterpret_cast<uint2*>(S + lo[s]) = rr[s];
+    for (int s = 0; s < NU; ++s) *reinterpret_cast<Unit*>(S + lo[s]) = rr[s];
   };
 
   const int li = lane & 15;
-  const int rd_off = (li >> 2) * PH + 4 * (li & 3) + 16 * ((lane >> 4) & 1) + 8 * (lane >> 5) * PH;
+  const int rd_off = NHWC ? (lane & 31) * PQN + 8 * (lane >> 5)
+                          : (li >> 2) * PH + 4 * (li & 3) + 16 * ((lane >> 4) & 1) +
+                                8 * (lane >> 5) * PH;
+  auto frag = [&](const uint16_t* p) -> bf8v {
+    if constexpr (NHWC) {
+      return *reinterpret_cast<const bf8v*>(p);
+    } else {
+      return __builtin_bit_cast(bf8v, __builtin_shufflevector(tr_read(p), tr_read(p + 4 * PH), 0,
+                                                              1, 2, 3, 4, 5, 6, 7));
+    }
+  };
+  constexpr int KSTEP = NHWC ? 1 : PH;          // LDS elements per k
+  constexpr int RSTEP = NHWC ? 32 * PQN : 32;   // LDS elements per 32 MFMA rows
+  constexpr int IMG = BKH * PH;                 // LDS elements per image (both layouts)
   const int nk = (g.D + BKH - 1) / BKH;
   load(0);
   store(0);
@@ -833,26 +820,15 @@ __global__ __launch_bounds__(2 * NT, MINW) void corr_build_bf16_q2_kernel(
   for (int ks = 0; ks < nk; ++ks) {
     const int buf = ks & 1;
     if (ks + 1 < nk) load((ks + 1) * BKH);
-    const uint16_t* A = lh + buf * STAGE_Q2 + half * BKH * PH;
-    const uint16_t* Bt = lh + buf * STAGE_Q2 + 2 * BKH * PH;
+    const uint16_t* A = lh + buf * STAGE_Q2 + half * IMG;
+    const uint16_t* Bt = lh + buf * STAGE_Q2 + 2 * IMG;
 #pragma unroll
     for (int kk = 0; kk < BKH; kk += 16) {
-      const uint16_t* pa = A + kk * PH + rd_off + w4 * 32;
-      const s8v qv = __builtin_shufflevector(tr_read(pa), tr_read(pa + 4 * PH), 0, 1, 2, 3, 4, 5,
-                                             6, 7);
-      const bf8v qf = __builtin_bit_cast(bf8v, qv);
+      const bf8v qf = frag(A + kk * KSTEP + rd_off + w4 * RSTEP);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const uint16_t* pb = Bt + kk * PH + rd_off + t * 32;
-        const s8v tv = __builtin_shufflevector(tr_read(pb), tr_read(pb + 4 * PH), 0, 1, 2, 3, 4,
-                                               5, 6, 7);
-        if constexpr ((XP & 2) != 0) {
-          const s8v x = tv ^ qv;
-          acc[t][0] += (float)(x[0] + x[3] + x[5] + x[7]);
-        } else {
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8v, tv), qf, acc[t],
-                                                           0, 0, 0);
-        }
+        const bf8v tv = frag(Bt + kk * KSTEP + rd_off + t * RSTEP);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tv, qf, acc[t], 0, 0, 0);
       }
     }
     if (ks + 1 < nk) store(buf ^ 1);
@@ -861,22 +837,11 @@ __global__ __launch_bounds__(2 * NT, MINW) void corr_build_bf16_q2_kernel(
 
   if (pc.qblk + half >= g.qt) return;   // past the last query block: no page
   scale_acc<DIV>(acc, g);
-  if constexpr ((XP & 1) != 0) {
-    float sum = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sum += acc[t][r];
-    if (sum == 1234.5f) pyr[tid] = to_out<OT>(sum);  // keeps the K loop live
-    return;
-  }
   const long long page = pc.page + (long long)half * g.tiles_h * g.tiles_w;
-  // non-temporal pyramid stores (KITTI B=8: 556 vs 606 us; the 1.13 GB pyramid
-  // outgrows the caches anyway); XP bit 6 turns them off
-  // XP bit 11 (experiments): buffer stores with cache policy bits 12-16 (default
-  // sc1) instead of nt; write-through is slower here (KITTI B=8 step 1,258 -> 1,345 us)
-  constexpr int EX = ((XP & 2048) ? (5 | (((XP >> 12) & 31) << 8)) : (XP & 64) ? 1 : 3) |
-                     ((XP & (1 << 17)) ? 8 : 0);   // bit 17: 16-byte level-2/3 stores
+  // wave-local staging syncs and non-temporal pyramid stores (KITTI B=8: 556 vs
+  // 606 us; the 1.13 GB pyramid outgrows the caches anyway; write-through sc1
+  // stores are slower here: step 1,258 -> 1,345 us)
+  constexpr int EX = 3;
   paged_epilogue<OT, EX>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0, pyr, g, page,
                          w4, lane);
 }
@@ -954,17 +919,10 @@ __device__ __forceinline__ uint32_t cvt_pk_f16(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2_t));
 }
 
-__device__ __forceinline__ Split2 split2h(float a, float b) {
-  const uint32_t h = cvt_pk_f16(a, b);
-  const f16x2_t hv = __builtin_bit_cast(f16x2_t, h);
-  const float ra = (a - (float)hv[0]) * 2048.f, rb = (b - (float)hv[1]) * 2048.f;
-  return {h, cvt_pk_f16(ra, rb)};
-}
-
-// The same split with the residual formed and rounded by mixed-precision FMAs:
+// The residual is formed and rounded by mixed-precision FMAs:
 // lo = RNE_f16(fma(hi, -2048, 2048 x)).  2048 x and 2048 hi are exact and so is
-// their difference (= 2048 (x - hi)), so the single rounding is the same RNE as
-// split2h's; hi stays an f16 operand (v_fma_mix*_f16), no conversion back.
+// their difference (= 2048 (x - hi)), so the single rounding is the RNE of
+// (x - hi) * 2^11; hi stays an f16 operand (v_fma_mix*_f16), no conversion back.
 __device__ __forceinline__ Split2 split2h_mix(float a, float b) {
   const uint32_t h = cvt_pk_f16(a, b);
   const f16x2_t hv = __builtin_bit_cast(f16x2_t, h);
@@ -992,14 +950,6 @@ __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t voff
   return make_float4(v.x, v.y, v.z, v.w);
 }
 
-#ifdef DXR_EXPERIMENTS
-// XP bit 10 (experiments): per-workgroup timeline of wave 0 — CU identity and
-// shader-clock stamps at start, after the K loop, after the epilogue's stores
-// are issued and after they complete; read back with dxr_xp_trace_read.
-constexpr int XP_TRACE_WG = 32768;
-__device__ unsigned long long xp_trace[XP_TRACE_WG * 5];
-#endif
-
 // BV: target staging width in floats — 4 (float4 units; W % 4 == 0) or 2
 // (float2 units; W even, e.g. Chairs' 62-wide fmaps).
 // NHWC: channels-last fmaps [B, H, W, D]: every operand
@@ -1007,12 +957,9 @@ __device__ unsigned long long xp_trace[XP_TRACE_WG * 5];
 // loads per lane and the target tile is staged target-major ([target][k] planes,
 // read with ds_read_b128) instead of k-major; same products, same order, same
 // bits as the NCHW build.
-// XP: timing ablations, instantiated only by the experiments build target
-// (DXR_EXPERIMENTS, libdexiraft_corr_exp.so; never by the product library):
-// bit 0 skips the epilogue stores, 1 the MFMAs, 2 the in-loop global loads,
-// 3 the operand split (hi only), 4 the in-loop barrier.
-template <typename OT, bool DIV, int MINW, int BV = 4, int XP = 0, bool NHWC = false,
-          bool H2 = false, bool REMAP = false>
+// H2: the f16 pair split (3 products) with the 3-way bf16 split as the
+// per-page overflow fallback; !H2: the 3-way bf16 split only.
+template <typename OT, bool DIV, int MINW, int BV = 4, bool NHWC = false, bool H2 = false>
 __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float* __restrict__ f1,
                                                                     const float* __restrict__ f2,
                                                                     OT* __restrict__ pyr,
@@ -1025,20 +972,7 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (H2 && tid == 0) redo = 0;
-#ifdef DXR_EXPERIMENTS
-  const unsigned long long xt0 = (XP & 1024) ? __builtin_amdgcn_s_memtime() : 0ull;
-#endif
-  if constexpr ((XP & 768) != 0) {
-    // XP bits 8-9 (experiments): stagger the first wave of workgroups — the one
-    // in CU slot s (linear id / 256, breadth-first dispatch) sleeps s * k * 8K
-    // cycles, k = (XP >> 8) & 3, so the slots' epilogues fall at different times.
-    const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-    if (L < 768) {
-      const int n = (L >> 8) * ((XP >> 8) & 3);
-      for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
-    }
-  }
-  const PageCoord pc = page_coord<REMAP>(g);
+  const PageCoord pc = page_coord<false>(g);
   const int txi = pc.txi, tyi = pc.tyi;
   const int th0 = tyi * TH, tw0 = txi * TW;
   const int q0 = pc.qblk * BM;
@@ -1094,15 +1028,9 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     if (!(th0 + r < g.H && tw0 + c < g.W)) vb[s] = 0x80000000u;
   }
 
-  // Operand split by mixed-precision FMAs (split2h_mix: 44 instead of 68 VALU per
-  // k step, bit-identical; Sintel step 225.4 -> 223.6 us); XP bit 21 restores split2h.
-  constexpr bool MIXS = (XP & (1 << 21)) == 0;
-  float an[8], an2[8];
-  float4 bn[NBS], bn2[NBS];
-  auto load_to = [&](int k0, auto& an, auto& bn) {
-    if constexpr ((XP & 4) != 0) {
-      if (k0 > 0) return;
-    }
+  float an[8];
+  float4 bn[NBS];
+  auto load = [&](int k0) {
     if constexpr (NHWC) {
       const float4 u = bload4(ra, va, k0 * 4), v = bload4(ra, va, k0 * 4 + 16);
       an[0] = u.x; an[1] = u.y; an[2] = u.z; an[3] = u.w;
@@ -1124,29 +1052,22 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
       }
     }
   };
-  auto load = [&](int k0) { load_to(k0, an, bn); };
   s8v ah, am, al;   // split query operand of the current stage (H2: ah, al)
   using S3 = std::integral_constant<bool, false>;
   using S2 = std::integral_constant<bool, true>;
-  auto split3x = [&](float a, float bb) -> Split3 {
-    if constexpr ((XP & 8) != 0) {
-      const uint32_t h = cvt_pk_bf16(a, bb);
-      return {h, h, h};
-    } else {
-      return split3(a, bb);
-    }
-  };
-  auto split_a_from = [&](auto mode, auto& an) {
+  // Operand split by mixed-precision FMAs (split2h_mix: 44 instead of 68 VALU per
+  // k step, bit-identical to split2h; Sintel step 225.4 -> 223.6 us).
+  auto split_a = [&](auto mode) {
     uint32_t h[4], m[4], l[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       if constexpr (decltype(mode)::value) {
-        const Split2 x = MIXS ? split2h_mix(an[2 * e], an[2 * e + 1]) : split2h(an[2 * e], an[2 * e + 1]);
+        const Split2 x = split2h_mix(an[2 * e], an[2 * e + 1]);
         h[e] = x.h;
         m[e] = 0;
         l[e] = x.l;
       } else {
-        const Split3 x = split3x(an[2 * e], an[2 * e + 1]);
+        const Split3 x = split3(an[2 * e], an[2 * e + 1]);
         h[e] = x.h;
         m[e] = x.m;
         l[e] = x.l;
@@ -1156,22 +1077,21 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     am = __builtin_bit_cast(s8v, make_uint4(m[0], m[1], m[2], m[3]));
     al = __builtin_bit_cast(s8v, make_uint4(l[0], l[1], l[2], l[3]));
   };
-  auto split_a = [&](auto mode) { split_a_from(mode, an); };
   // NHWC target planes: [target (MFMA row order)][16 k] bf16 at a 48-byte
   // pitch, which keeps the ds_read_b128 lane groups bank-conflict free.
   constexpr int PN = 24;                      // NHWC plane row pitch (bf16)
   constexpr int PLANE_N = NTGT * PN;          // bf16 elements per NHWC plane
   constexpr int PLANE = NHWC ? PLANE_N : PLANE_S;
   // Target planes of a stage: hi, mid, lo (bf16) or hi, lo (H2: f16).
-  auto store_b_from = [&](int buf, auto mode, auto& bn) {
+  auto store_b = [&](int buf, auto mode) {
     uint16_t* P = lh + buf * 3 * PLANE;
 #pragma unroll
     for (int s = 0; s < NBS; ++s) {
       const int o = NHWC ? bcol[s] * PN + bk[s] : bk[s] * PH + bcol[s];
       if constexpr (decltype(mode)::value) {
-        const Split2 x = MIXS ? split2h_mix(bn[s].x, bn[s].y) : split2h(bn[s].x, bn[s].y);
+        const Split2 x = split2h_mix(bn[s].x, bn[s].y);
         if constexpr (BV == 4) {
-          const Split2 z = MIXS ? split2h_mix(bn[s].z, bn[s].w) : split2h(bn[s].z, bn[s].w);
+          const Split2 z = split2h_mix(bn[s].z, bn[s].w);
           *reinterpret_cast<uint2*>(P + o) = make_uint2(x.h, z.h);
           *reinterpret_cast<uint2*>(P + PLANE + o) = make_uint2(x.l, z.l);
         } else {
@@ -1179,9 +1099,9 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
           *reinterpret_cast<uint32_t*>(P + PLANE + o) = x.l;
         }
       } else {
-        const Split3 x = split3x(bn[s].x, bn[s].y);
+        const Split3 x = split3(bn[s].x, bn[s].y);
         if constexpr (BV == 4) {
-          const Split3 z = split3x(bn[s].z, bn[s].w);
+          const Split3 z = split3(bn[s].z, bn[s].w);
           *reinterpret_cast<uint2*>(P + o) = make_uint2(x.h, z.h);
           *reinterpret_cast<uint2*>(P + PLANE + o) = make_uint2(x.m, z.m);
           *reinterpret_cast<uint2*>(P + 2 * PLANE + o) = make_uint2(x.l, z.l);
@@ -1194,7 +1114,6 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     }
   };
 
-  auto store_b = [&](int buf, auto mode) { store_b_from(buf, mode, bn); };
   const int li = lane & 15;
   const int rd_off = NHWC ? (lane & 31) * PN + 8 * (lane >> 5)
                           : (li >> 2) * PH + 4 * (li & 3) + 16 * ((lane >> 4) & 1) +
@@ -1224,12 +1143,6 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
       const uint16_t* P = lh + buf * 3 * PLANE + rd_off;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        if constexpr ((XP & 2) != 0) {
-          const s8v x = __builtin_bit_cast(s8v, frag(P + t * tstride)) ^
-                        __builtin_bit_cast(s8v, frag(P + PLANE + t * tstride)) ^ ah ^ am ^ al;
-          acc[t][0] += (float)(x[0] + x[3] + x[5] + x[7]);
-          continue;
-        }
         if constexpr (M2) {
           const h8v th = __builtin_bit_cast(h8v, frag(P + t * tstride)),
                     tl = __builtin_bit_cast(h8v, frag(P + PLANE + t * tstride));
@@ -1255,150 +1168,11 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
         store_b(buf ^ 1, mode);
         split_a(mode);
       }
-      if constexpr ((XP & 16) == 0) __syncthreads();
+      __syncthreads();
     }
   };
 
-  // XP bit 18 (experiments): the f16-pair K loop with loads two k steps ahead
-  // (a second register stage, the loop unrolled by two; nk even).
-  auto mfma2 = [&](int buf) {
-    const uint16_t* P = lh + buf * 3 * PLANE + rd_off;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const h8v th = __builtin_bit_cast(h8v, frag(P + t * tstride)),
-                tl = __builtin_bit_cast(h8v, frag(P + PLANE + t * tstride));
-      const h8v qh = __builtin_bit_cast(h8v, ah), ql = __builtin_bit_cast(h8v, al);
-      acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc2[t], 0, 0, 0);
-      acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc2[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qh, acc[t], 0, 0, 0);
-    }
-  };
-  auto kloop_pd2 = [&]() {
-    load_to(0, an, bn);
-    load_to(BKS, an2, bn2);
-    store_b_from(0, S2{}, bn);
-    split_a_from(S2{}, an);
-    __syncthreads();
-    for (int ks = 0; ks < nk; ks += 2) {
-      if (ks + 2 < nk) load_to((ks + 2) * BKS, an, bn);
-      mfma2(0);
-      store_b_from(1, S2{}, bn2);
-      split_a_from(S2{}, an2);
-      __syncthreads();
-      if (ks + 3 < nk) load_to((ks + 3) * BKS, an2, bn2);
-      mfma2(1);
-      if (ks + 2 < nk) {
-        store_b_from(0, S2{}, bn);
-        split_a_from(S2{}, an);
-      }
-      __syncthreads();
-    }
-  };
-  // XP bit 19 (experiments; H2, NCHW, float4 units, nk even): the target tile
-  // travels by LDS-DMA (buffer_load ... lds) into a two-stage raw f32 ring and the
-  // query operand through a two-stage register ring, both two k steps ahead.
-  // Every wave DMAs exactly the 16-byte units its own lanes split afterwards, so
-  // a wave-local vmcnt wait publishes them (no extra barrier), and the DMA stages
-  // hold no VGPRs while in flight.
-  // XP bit 20: the target tile by LDS-DMA two k steps ahead, the query operand
-  // in registers one step ahead (as the product), so no second register stage.
-  constexpr bool DMA1 = (XP & (1 << 20)) != 0;
-  constexpr bool DMA = (XP & (1 << 19)) != 0 || DMA1;
-  __shared__ __attribute__((aligned(16))) float raw[DMA ? 2 * BKS * NTGT : 4];
-  auto kloop_dma = [&]() {
-    if constexpr (DMA && !NHWC && BV == 4) {
-      uint32_t vdma[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int k = 2 * wave + 8 * i + (lane >> 5), u = lane & 31;
-        const int r = u >> 2, c = 4 * (u & 3);
-        vdma[i] = (th0 + r < g.H && tw0 + c < g.W)
-                      ? (uint32_t)(k * g.N + (th0 + r) * g.W + tw0 + c) * 4u : 0x80000000u;
-      }
-      auto dma = [&](int k0, int st) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              rb, (__attribute__((address_space(3))) void*)(raw + st * BKS * NTGT + (2 * wave + 8 * i) * NTGT),
-              16, vdma[i], k0 * g.N * 4, 0, 0);
-      };
-      auto loadq = [&](int k0, float (&A)[8]) {
-        const int rowb = g.N * 4;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) A[e] = bload1(ra, va, (k0 + e) * rowb);
-      };
-      auto split_raw = [&](int st, int buf) {
-        float4 v[NBS];
-#pragma unroll
-        for (int s2 = 0; s2 < NBS; ++s2) {
-          const int idx = tid + NT * s2;
-          v[s2] = *reinterpret_cast<const float4*>(raw + st * BKS * NTGT + (idx >> 5) * NTGT + (idx & 31) * 4);
-        }
-        store_b_from(buf, S2{}, v);
-      };
-      if constexpr (DMA1) {
-        // per step: query loads for ks+1 first, then the DMA for ks+2, so a
-        // vmcnt(2) wait completes the former and leaves the latter in flight
-        dma(0, 0);
-        loadq(0, an);
-        dma(BKS, 1);
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        split_raw(0, 0);
-        split_a_from(S2{}, an);
-        __syncthreads();
-        for (int ks = 0; ks < nk; ++ks) {
-          const int buf = ks & 1;
-          if (ks + 1 < nk) loadq((ks + 1) * BKS, an);
-          if (ks + 2 < nk) dma((ks + 2) * BKS, buf);
-          mfma2(buf);
-          if (ks + 1 < nk) {
-            if (ks + 2 < nk) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            split_raw(buf ^ 1, buf ^ 1);
-            split_a_from(S2{}, an);
-          }
-          __syncthreads();
-        }
-        return;
-      }
-      dma(0, 0);
-      loadq(0, an);
-      dma(BKS, 1);
-      loadq(BKS, an2);
-      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-      split_raw(0, 0);
-      split_a_from(S2{}, an);
-      __syncthreads();
-      for (int ks = 0; ks < nk; ks += 2) {
-        if (ks + 2 < nk) {
-          dma((ks + 2) * BKS, 0);
-          loadq((ks + 2) * BKS, an);
-        }
-        mfma2(0);
-        if (ks + 2 < nk) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        split_raw(1, 1);
-        split_a_from(S2{}, an2);
-        __syncthreads();
-        if (ks + 3 < nk) {
-          dma((ks + 3) * BKS, 1);
-          loadq((ks + 3) * BKS, an2);
-        }
-        mfma2(1);
-        if (ks + 2 < nk) {
-          if (ks + 3 < nk) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          split_raw(0, 0);
-          split_a_from(S2{}, an);
-        }
-        __syncthreads();
-      }
-    }
-  };
-  constexpr bool PD2 = (XP & (1 << 18)) != 0;
   if constexpr (H2) {
-    if constexpr (DMA) kloop_dma(); else
-    if constexpr (PD2) kloop_pd2(); else
     kloop(S2{});
     // Combine (one rounding) and vote: a non-finite sum means an operand of the
     // page overflowed f16 (|x| >= 65520) or was itself inf/NaN; the page is then
@@ -1425,50 +1199,14 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
     kloop(S3{});
   }
 
-#ifdef DXR_EXPERIMENTS
-  const unsigned long long xt1 = (XP & 1024) ? __builtin_amdgcn_s_memtime() : 0ull;
-#endif
   scale_acc<DIV>(acc, g);
-  if constexpr ((XP & 1) != 0) {
-    float sum = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sum += acc[t][r];
-    if (sum == 1234.5f) pyr[tid] = to_out<OT>(sum);  // keeps the K loop live
-    return;
-  }
-  // Wave-local syncs around the per-wave staging (r02: -2 % per Sintel step);
-  // XP bit 5 restores workgroup barriers, bit 6 selects non-temporal stores
-  // (faster build alone than plain stores, no faster step).
+  // Wave-local syncs around the per-wave staging (r02: -2 % per Sintel step).
   // Pyramid stores are write-through (sc1, round 2): no dirty lines pile up in
   // the XCDs' L2s for the K loops' operand reads to evict around, and none are
   // left for the kernel boundary to write back (Sintel B=1 step 232 -> 211 us
-  // with the lookups' sc1 stores, scripts/xp_step.py; build alone 125 -> 115).
-  // XP (experiments): bit 6 non-temporal stores instead, bit 11 plain stores,
-  // bits 12-16 another buffer-store cache policy.
-  constexpr int EX = ((XP & 32) ? 0 : 1) | ((XP & 64) ? 2 : (XP & 2048) ? 0 : 4) |
-                     (((XP >> 12) & 31) << 8) | ((XP & (1 << 17)) ? 8 : 0);
-  // XP bit 7 (experiments): workgroups write a 32-page ring — the epilogue's
-  // instructions, LDS transposes and stores, with the writes L2-resident
-  paged_epilogue<OT, EX>(acc, reinterpret_cast<float*>(smem), pyr, g, (XP & 128) ? (pc.page & 31) : pc.page,
-                         wave, lane);
-#ifdef DXR_EXPERIMENTS
-  if constexpr ((XP & 1024) != 0) {
-    const unsigned long long xt2 = __builtin_amdgcn_s_memtime();
-    __builtin_amdgcn_s_waitcnt(0);
-    const unsigned long long xt3 = __builtin_amdgcn_s_memtime();
-    const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-    if (wave == 0 && lane < 5 && L < XP_TRACE_WG) {
-      const unsigned long long id =
-          (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
-          ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(20 | (15 << 11)) << 32);
-      const unsigned long long v = lane == 0 ? id : lane == 1 ? xt0 : lane == 2 ? xt1
-                                 : lane == 3 ? xt2 : xt3;
-      xp_trace[L * 5 + lane] = v;
-    }
-  }
-#endif
+  // with the lookups' sc1 stores; build alone 125 -> 115).
+  constexpr int EX = 1 | 4;
+  paged_epilogue<OT, EX>(acc, reinterpret_cast<float*>(smem), pyr, g, pc.page, wave, lane);
 }
 
 // Floor-mode 2x2 average pool of one pyramid level into the next, for levels
@@ -1670,6 +1408,21 @@ int launch_f32(bool vec, const float* f1, const float* f2, OT* pyr, const BuildG
 // the 4 workgroups per CU its 40 KB of LDS allows) and the XCD-aware page order
 // (r01 KITTI b8: 721 us vs 837 in grid order).  The scalar-staging path keeps
 // the compiler's choice (it would spill at 3) and the grid order.
+// Channels-last bf16 fmaps: the two-block kernel's NHWC form (D % 32 == 0,
+// 16-byte aligned pixels; checked by the caller).
+template <typename OT>
+int launch_build_bf16_nhwc(const uint16_t* f1, const uint16_t* f2, OT* pyr, const BuildGeom& g,
+                           int B, hipStream_t stream) {
+  const dim3 rg = remap_grid(g, B, 2);
+  if (g.recip == 0.f)
+    hipLaunchKernelGGL((corr_build_bf16_q2_kernel<OT, true, 4, true>), rg, dim3(2 * NT), 0, stream,
+                       f1, f2, pyr, g);
+  else
+    hipLaunchKernelGGL((corr_build_bf16_q2_kernel<OT, false, 4, true>), rg, dim3(2 * NT), 0, stream,
+                       f1, f2, pyr, g);
+  return dxr::launch_status();
+}
+
 template <typename OT>
 int launch_build_bf16(bool vec, const uint16_t* f1, const uint16_t* f2, OT* pyr,
                       const BuildGeom& g, int B, hipStream_t stream) {
@@ -1705,10 +1458,10 @@ int launch_split(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, 
   const dim3 grid = build_grid(g, B);
   if (grid.y > 65535) return DXR_EINVAL;
   if (g.recip == 0.f)
-    hipLaunchKernelGGL((corr_build_split_kernel<OT, true, 3, BV, 0, NHWC, true>), grid, dim3(NT),
+    hipLaunchKernelGGL((corr_build_split_kernel<OT, true, 3, BV, NHWC, true>), grid, dim3(NT),
                        0, stream, f1, f2, pyr, g);
   else
-    hipLaunchKernelGGL((corr_build_split_kernel<OT, false, 3, BV, 0, NHWC, true>), grid, dim3(NT),
+    hipLaunchKernelGGL((corr_build_split_kernel<OT, false, 3, BV, NHWC, true>), grid, dim3(NT),
                        0, stream, f1, f2, pyr, g);
   return dxr::launch_status();
 }
@@ -1787,11 +1540,23 @@ extern "C" int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int 
   if (algo == DXR_BUILD_EXACT_F32 && in_dtype != DXR_F32) return DXR_EUNSUPPORTED;
   const BuildGeom g = make_geom(D, H, W, divisor, L);
   int st;
-  if (fmap_layout == DXR_NHWC) {
-    // channels-last operands: the split build's NHWC form, where the NCHW build
+  if (fmap_layout == DXR_NHWC && in_dtype == DXR_BF16) {
+    // channels-last bf16 operands (the bf16 mode's encoders, core/extractor.py:168-192):
+    // the two-block bf16 build's NHWC form, bit-identical to the NCHW build;
+    // D % 32 == 0 (whole 32-channel stages) and 16-byte aligned pixels
+    if (D % 32 != 0 || D * H * W >= (1LL << 30) || !aligned16(fmap1) || !aligned16(fmap2) ||
+        !aligned16(pyramid))
+      return DXR_EUNSUPPORTED;
+    const uint16_t* f1 = static_cast<const uint16_t*>(fmap1);
+    const uint16_t* f2 = static_cast<const uint16_t*>(fmap2);
+    st = pyr_dtype == DXR_F32
+             ? launch_build_bf16_nhwc(f1, f2, static_cast<float*>(pyramid), g, (int)B, stream)
+             : launch_build_bf16_nhwc(f1, f2, static_cast<uint16_t*>(pyramid), g, (int)B, stream);
+  } else if (fmap_layout == DXR_NHWC) {
+    // channels-last f32 operands: the split build's NHWC form, where the NCHW build
     // would also be the split build (f32 fmaps, D % 16 == 0, even W: same bits),
     // with 16-byte aligned rows; other requests are unsupported (callers transpose)
-    if (in_dtype != DXR_F32 || algo != DXR_BUILD_AUTO || D % 16 != 0 || W % 2 != 0 ||
+    if (algo != DXR_BUILD_AUTO || D % 16 != 0 || W % 2 != 0 ||
         D * H * W >= (1LL << 29) || !aligned16(fmap1) || !aligned16(fmap2) || !aligned16(pyramid))
       return DXR_EUNSUPPORTED;
     const float* f1 = static_cast<const float*>(fmap1);
@@ -1912,179 +1677,3 @@ extern "C" int dxr_pyramid_backward(const void* grad_pyramid, int grad_dtype, in
   return dxr::launch_status();
 }
 
-#ifdef DXR_EXPERIMENTS
-// Experiments build target only (libdexiraft_corr_exp.so): the f32 split build
-// with timing ablation bits `xp` (see corr_build_split_kernel), into a paged
-// f32 pyramid.  NCHW f32 fmaps, W % 4 == 0, D % 16 == 0, power-of-two sqrt(D).
-namespace {
-template <int XP>
-int xp_split(const float* f1, const float* f2, float* pyr, const BuildGeom& g, int B,
-             hipStream_t stream) {
-  hipLaunchKernelGGL((corr_build_split_kernel<float, false, 4, 4, XP>), build_grid(g, B), dim3(NT),
-                     0, stream, f1, f2, pyr, g);
-  return dxr::launch_status();
-}
-template <int XP>
-int xp_h2(const float* f1, const float* f2, float* pyr, const BuildGeom& g, int B,
-          hipStream_t stream) {
-  hipLaunchKernelGGL((corr_build_split_kernel<float, false, 3, 4, XP, false, true>),
-                     build_grid(g, B), dim3(NT), 0, stream, f1, f2, pyr, g);
-  return dxr::launch_status();
-}
-}  // namespace
-
-template <int XP>
-int xp_bf16(const uint16_t* f1, const uint16_t* f2, uint16_t* pyr, const BuildGeom& g, int B,
-            hipStream_t stream) {
-  hipLaunchKernelGGL((corr_build_bf16_kernel<true, uint16_t, false, 3, true, XP>), remap_grid(g, B),
-                     dim3(NT), 0, stream, f1, f2, pyr, g);
-  return dxr::launch_status();
-}
-
-template <int XP, int MINW>
-int xp_bf16q2(const uint16_t* f1, const uint16_t* f2, uint16_t* pyr, const BuildGeom& g, int B,
-              hipStream_t stream) {
-  hipLaunchKernelGGL((corr_build_bf16_q2_kernel<uint16_t, false, MINW, XP>), remap_grid(g, B, 2),
-                     dim3(2 * NT), 0, stream, f1, f2, pyr, g);
-  return dxr::launch_status();
-}
-
-// Copies the XP-bit-10 timeline (5 x u64 per workgroup) to host memory.
-extern "C" int dxr_xp_trace_read(void* host, int64_t bytes) {
-  if (bytes > (int64_t)sizeof(unsigned long long) * XP_TRACE_WG * 5) return DXR_EINVAL;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(xp_trace), (size_t)bytes, 0, hipMemcpyDeviceToHost) ==
-                 hipSuccess
-             ? DXR_OK
-             : DXR_EINVAL;
-}
-
-// bf16 fmaps and pyramid, W % 4 == 0: the bf16 build with ablation bits.
-extern "C" int dxr_xp_build_bf16(const void* f1, const void* f2, int64_t B, int64_t D, int64_t H,
-                                 int64_t W, void* pyr, int xp, hipStream_t stream) {
-  dxr::Levels L;
-  if (!dxr::make_levels(B, H, W, 4, &L) || W % 4 != 0) return DXR_EINVAL;
-  const BuildGeom g = make_geom(D, H, W, std::sqrt((float)D), L);
-  const uint16_t* a = static_cast<const uint16_t*>(f1);
-  const uint16_t* b = static_cast<const uint16_t*>(f2);
-  uint16_t* p = static_cast<uint16_t*>(pyr);
-  switch (xp) {
-    case 0: return xp_bf16<0>(a, b, p, g, (int)B, stream);
-    case 1: return xp_bf16<1>(a, b, p, g, (int)B, stream);
-    case 2: return xp_bf16<2>(a, b, p, g, (int)B, stream);
-    case 3: return xp_bf16<3>(a, b, p, g, (int)B, stream);
-    case 4: return xp_bf16<4>(a, b, p, g, (int)B, stream);
-    case 5: return xp_bf16<5>(a, b, p, g, (int)B, stream);
-    case 100: return xp_bf16q2<0, 4>(a, b, p, g, (int)B, stream);
-    case 101: return xp_bf16q2<1, 4>(a, b, p, g, (int)B, stream);
-    case 104: return xp_bf16q2<4, 4>(a, b, p, g, (int)B, stream);
-    case 105: return xp_bf16q2<5, 4>(a, b, p, g, (int)B, stream);
-    case 130: return xp_bf16q2<0, 3>(a, b, p, g, (int)B, stream);
-    case 132: return xp_bf16<32>(a, b, p, g, (int)B, stream);
-    case 164: return xp_bf16<64>(a, b, p, g, (int)B, stream);
-    case 196: return xp_bf16<96>(a, b, p, g, (int)B, stream);
-    case 264: return xp_bf16q2<64, 4>(a, b, p, g, (int)B, stream);
-    case 2148: return xp_bf16q2<2048, 4>(a, b, p, g, (int)B, stream);   // sc1 stores
-    case 2150: return xp_bf16q2<2048 | (18 << 12), 4>(a, b, p, g, (int)B, stream);   // sc1 nt
-    case 2151: return xp_bf16q2<2048 | (17 << 12), 4>(a, b, p, g, (int)B, stream);   // sc0 sc1
-    case 2200: return xp_bf16q2<1 << 17, 4>(a, b, p, g, (int)B, stream);   // nt, wide levels 2/3 (no gain)
-    case 2300: return xp_bf16q2<256, 4>(a, b, p, g, (int)B, stream);    // slot-1 stagger k = 1
-    case 2301: return xp_bf16q2<512, 4>(a, b, p, g, (int)B, stream);    // k = 2
-    case 2302: return xp_bf16q2<768, 4>(a, b, p, g, (int)B, stream);    // k = 3
-    case 2201: return xp_bf16q2<2048 | (1 << 17), 4>(a, b, p, g, (int)B, stream);   // sc1, wide
-    default: return DXR_EUNSUPPORTED;
-  }
-}
-
-extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t D, int64_t H,
-                            int64_t W, float* pyr, int xp, hipStream_t stream) {
-  dxr::Levels L;
-  if (!dxr::make_levels(B, H, W, 4, &L) || W % 4 != 0 || D % 16 != 0 || D * H * W >= (1LL << 29))
-    return DXR_EINVAL;
-  const BuildGeom g = make_geom(D, H, W, std::sqrt((float)D), L);
-  if (g.recip == 0.f) return DXR_EUNSUPPORTED;
-  switch (xp) {
-    case 0: return xp_split<0>(f1, f2, pyr, g, (int)B, stream);
-    case 1: return xp_split<1>(f1, f2, pyr, g, (int)B, stream);
-    case 2: return xp_split<2>(f1, f2, pyr, g, (int)B, stream);
-    case 3: return xp_split<3>(f1, f2, pyr, g, (int)B, stream);
-    case 4: return xp_split<4>(f1, f2, pyr, g, (int)B, stream);
-    case 5: return xp_split<5>(f1, f2, pyr, g, (int)B, stream);
-    case 8: return xp_split<8>(f1, f2, pyr, g, (int)B, stream);
-    case 9: return xp_split<9>(f1, f2, pyr, g, (int)B, stream);
-    case 13: return xp_split<13>(f1, f2, pyr, g, (int)B, stream);
-    case 16: return xp_split<16>(f1, f2, pyr, g, (int)B, stream);
-    case 17: return xp_split<17>(f1, f2, pyr, g, (int)B, stream);
-    case 21: return xp_split<21>(f1, f2, pyr, g, (int)B, stream);
-    case 3 | 4: return xp_split<7>(f1, f2, pyr, g, (int)B, stream);
-    case 1002:
-      hipLaunchKernelGGL((corr_build_split_kernel<float, false, 2, 4, 0, false, true>),
-                         build_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);
-      return dxr::launch_status();
-    case 1003:
-      hipLaunchKernelGGL((corr_build_split_kernel<float, false, 3, 4, 0, false, true>),
-                         build_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);
-      return dxr::launch_status();
-    case 2001: return xp_h2<1>(f1, f2, pyr, g, (int)B, stream);
-    case 2128: return xp_h2<128>(f1, f2, pyr, g, (int)B, stream);
-    case 3024: return xp_h2<1024>(f1, f2, pyr, g, (int)B, stream);
-    case 3025: return xp_h2<1025>(f1, f2, pyr, g, (int)B, stream);
-    case 2256: return xp_h2<256>(f1, f2, pyr, g, (int)B, stream);
-    case 2512: return xp_h2<512>(f1, f2, pyr, g, (int)B, stream);
-    case 2768: return xp_h2<768>(f1, f2, pyr, g, (int)B, stream);
-    case 2032: return xp_h2<32>(f1, f2, pyr, g, (int)B, stream);
-    case 2064: return xp_h2<64>(f1, f2, pyr, g, (int)B, stream);
-    case 2096: return xp_h2<96>(f1, f2, pyr, g, (int)B, stream);
-    case 2003: return xp_h2<3>(f1, f2, pyr, g, (int)B, stream);
-    case 2005: return xp_h2<5>(f1, f2, pyr, g, (int)B, stream);
-    case 2017: return xp_h2<17>(f1, f2, pyr, g, (int)B, stream);
-    case 2002: return xp_h2<2>(f1, f2, pyr, g, (int)B, stream);
-    case 2004: return xp_h2<4>(f1, f2, pyr, g, (int)B, stream);
-    case 4048: return xp_h2<2048>(f1, f2, pyr, g, (int)B, stream);    // plain pyramid stores
-    case 4050: return xp_h2<18 << 12>(f1, f2, pyr, g, (int)B, stream);   // sc1 nt
-    case 4051: return xp_h2<17 << 12>(f1, f2, pyr, g, (int)B, stream);   // sc0 sc1
-    case 4052: return xp_h2<2 << 12>(f1, f2, pyr, g, (int)B, stream);    // nt (buffer)
-    case 4200: return xp_h2<1 << 17>(f1, f2, pyr, g, (int)B, stream);    // sc1, wide level 3 (no gain)
-    case 4300:   // loads two k steps ahead, 3 waves/SIMD
-      if (D % 32) return DXR_EUNSUPPORTED;
-      return xp_h2<1 << 18>(f1, f2, pyr, g, (int)B, stream);
-    case 4400:   // target tile by LDS-DMA + query registers, both two k steps ahead
-      if (D % 32) return DXR_EUNSUPPORTED;
-      return xp_h2<1 << 19>(f1, f2, pyr, g, (int)B, stream);
-    case 4401:   // the same at 2 waves/SIMD
-      if (D % 32) return DXR_EUNSUPPORTED;
-      hipLaunchKernelGGL((corr_build_split_kernel<float, false, 2, 4, 1 << 19, false, true>),
-                         build_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);
-      return dxr::launch_status();
-    case 4500:   // operand split by split2h (cvt back, sub, mul) instead of the FMA-mix form
-      return xp_h2<1 << 21>(f1, f2, pyr, g, (int)B, stream);
-    case 4402:   // target tile by LDS-DMA two steps ahead, queries one step ahead
-      return xp_h2<1 << 20>(f1, f2, pyr, g, (int)B, stream);
-    case 4301:   // loads two k steps ahead, 2 waves/SIMD
-      if (D % 32) return DXR_EUNSUPPORTED;
-      hipLaunchKernelGGL((corr_build_split_kernel<float, false, 2, 4, 1 << 18, false, true>),
-                         build_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);
-      return dxr::launch_status();
-    case 1012:
-      hipLaunchKernelGGL((corr_build_split_kernel<float, false, 2, 4, 0, false, true, true>),
-                         remap_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);
-      return dxr::launch_status();
-    case 1013:
-      hipLaunchKernelGGL((corr_build_split_kernel<float, false, 3, 4, 0, false, true, true>),
-                         remap_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);
-      return dxr::launch_status();
-    case 210:
-      hipLaunchKernelGGL((corr_build_split_kernel<float, false, 4, 4, 0, false, false, true>),
-                         remap_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);
-      return dxr::launch_status();
-    case 1001:
-      hipLaunchKernelGGL((corr_build_split_kernel<float, false, 2, 4, 1, false, true>),
-                         build_grid(g, (int)B), dim3(NT), 0, stream, f1, f2, pyr, g);
-      return dxr::launch_status();
-    case 200:
-      hipLaunchKernelGGL((corr_build_split_kernel<float, false, 3, 4, 0>), build_grid(g, (int)B),
-                         dim3(NT), 0, stream, f1, f2, pyr, g);
-      return dxr::launch_status();
-    default: return DXR_EUNSUPPORTED;
-  }
-}
-#endif

@@ -124,13 +124,9 @@ struct WideCfg {
 };
 
 // V consecutive cells of one tile row (or of a row-major level), widened to f32.
-template <int V, typename PT, bool NTL = false>
+template <int V, typename PT>
 __device__ __forceinline__ void load_vec(const PT* p, float* v) {
-  if constexpr (sizeof(PT) == 4 && V == 4 && NTL) {
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    const f4v x = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
-    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
-  } else if constexpr (sizeof(PT) == 4 && V == 4) {
+  if constexpr (sizeof(PT) == 4 && V == 4) {
     const float4 x = *reinterpret_cast<const float4*>(p);
     v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
   } else if constexpr (sizeof(PT) == 4 && V == 2) {
@@ -152,7 +148,7 @@ __device__ __forceinline__ void load_vec(const PT* p, float* v) {
 // Phase 1 for one level type: V-cell vectors, 4 per LDS vector slot.  Split in
 // a load half (registers) and a store half (LDS) so a caller can keep several
 // levels' gathers in flight at once (the fused motion kernel).
-template <int R, int NT_, int V, typename PT, bool NTL = false>
+template <int R, int NT_, int V, typename PT>
 __device__ __forceinline__ void gather_load(const PT* __restrict__ base, int qb0, const LevelAddr& A,
                                             const int2* org, int q0, int N, int tid,
                                             float4 (&v)[WideCfg<R, NT_>::VIT]) {
@@ -175,7 +171,7 @@ __device__ __forceinline__ void gather_load(const PT* __restrict__ base, int qb0
           const int x = x0 + h;
           const unsigned e = qoff + (yoff + (unsigned)(x >> A.ltw)) * (unsigned)A.pageS + yin +
                              (unsigned)(x & A.mw);
-          if (V == 4 || x < A.w) load_vec<V, PT, NTL>(base + e, c + h);
+          if (V == 4 || x < A.w) load_vec<V, PT>(base + e, c + h);
         }
 #pragma unroll
         for (int h = 1; h < 4; ++h)
@@ -186,35 +182,27 @@ __device__ __forceinline__ void gather_load(const PT* __restrict__ base, int qb0
   }
 }
 
-// QST: LDS floats per query (default WideCfg::QS, 16-byte aligned rows); a
-// stride of 2 mod 4 (experiments) writes each vector as two 8-byte halves.
-template <int R, int NT_, int QST = -1>
+template <int R, int NT_>
 __device__ __forceinline__ void gather_store(const float4 (&v)[WideCfg<R, NT_>::VIT], float* cells,
                                              int tid) {
   using C = WideCfg<R, NT_>;
-  constexpr int QSv = QST < 0 ? C::QS : QST;
 #pragma unroll
   for (int i = 0; i < C::VIT; ++i) {
     const int s = tid + i * C::NT;
     if (s < C::VSLOTS) {
       const int qq = s / (C::WD * C::NQ), rem = s - qq * (C::WD * C::NQ);
-      if constexpr (QSv % 4 == 0) {
-        *reinterpret_cast<float4*>(cells + qq * QSv + rem * 4) = v[i];
-      } else {
-        *reinterpret_cast<float2*>(cells + qq * QSv + rem * 4) = make_float2(v[i].x, v[i].y);
-        *reinterpret_cast<float2*>(cells + qq * QSv + rem * 4 + 2) = make_float2(v[i].z, v[i].w);
-      }
+      *reinterpret_cast<float4*>(cells + qq * C::QS + rem * 4) = v[i];
     }
   }
 }
 
-template <int R, int NT_, int V, typename PT, bool NTL = false, int QST = -1>
+template <int R, int NT_, int V, typename PT>
 __device__ __forceinline__ void gather_windows(const PT* __restrict__ base, int qb0, const LevelAddr& A,
                                                const int2* org, float* cells, int q0, int N,
                                                int tid) {
   float4 v[WideCfg<R, NT_>::VIT];
-  gather_load<R, NT_, V, PT, NTL>(base, qb0, A, org, q0, N, tid, v);
-  gather_store<R, NT_, QST>(v, cells, tid);
+  gather_load<R, NT_, V, PT>(base, qb0, A, org, q0, N, tid, v);
+  gather_store<R, NT_>(v, cells, tid);
 }
 
 // Phase 0 of the wide lookup (forward and backward): per (query, sample) the
@@ -271,19 +259,13 @@ __device__ __forceinline__ void wide_phase0(const float* __restrict__ coords, co
 
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
-// XP: timing ablations, instantiated only by the experiments build target
-// (DXR_EXPERIMENTS): bit 0 skips the window gathers, 1 the output stores,
-// 2 returns after phase 0; bits 12-14 select another output store form (4: plain).
-template <int R, typename PT, int NT_ = 512, int XP = 0>
+template <int R, typename PT, int NT_ = 512>
 __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
     const PT* __restrict__ pyr, const float* __restrict__ coords, float* __restrict__ out,
     LookupGeom g) {
   using C = WideCfg<R, NT_>;
   constexpr int RD = C::RD, RS = C::RS, K = C::K, QB = C::QB;
-  // XP bit 5 (experiments): query stride 2 mod 4 floats (178 at r = 4), so the 32
-  // queries of a phase-2 read spread over 16 bank pairs instead of 8 bank quads
-  constexpr int QSW = (XP & 32) ? C::WD * C::RS + 2 : C::QS;
-  __shared__ __attribute__((aligned(16))) float cells[QB * QSW];
+  __shared__ __attribute__((aligned(16))) float cells[QB * C::QS];
   __shared__ float4 xs[RD * QB];   // {column in the LDS row (int bits), fx, 1-fx, -}
   __shared__ float4 ys[RD * QB];   // {row offset in LDS (int bits), fy, 1-fy, -}
   __shared__ int2 org[QB];         // window origin (x, y) or FAR_ORIGIN
@@ -297,71 +279,25 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
   wide_phase0<R, NT_>(coords, g, A, b, l, q0, tid, xs, ys, org);
   __syncthreads();
 
-  if constexpr ((XP & 4) != 0) {
-    if (xs[tid % (RD * QB)].y == 1234.5f) out[tid] = 0.f;
-    return;
-  }
-
   // ---- phase 1 (zeros off the level and for far queries)
-  if constexpr ((XP & 1) == 0) {
+  {
     const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
     const int qb0 = q0 & ((1 << A.lqb) - 1);
     if (A.lth == 30)
-      gather_windows<R, NT_, 1, PT, false, QSW>(base, qb0, A, org, cells, q0, g.N, tid);
-    else if (A.tw >= 4)   // XP bit 3 (experiments): non-temporal gather loads
-      gather_windows<R, NT_, 4, PT, (XP & 8) != 0, QSW>(base, qb0, A, org, cells, q0, g.N, tid);
+      gather_windows<R, NT_, 1, PT>(base, qb0, A, org, cells, q0, g.N, tid);
+    else if (A.tw >= 4)
+      gather_windows<R, NT_, 4, PT>(base, qb0, A, org, cells, q0, g.N, tid);
     else if (A.tw == 2)
-      gather_windows<R, NT_, 2, PT, false, QSW>(base, qb0, A, org, cells, q0, g.N, tid);
+      gather_windows<R, NT_, 2, PT>(base, qb0, A, org, cells, q0, g.N, tid);
     else
-      gather_windows<R, NT_, 1, PT, false, QSW>(base, qb0, A, org, cells, q0, g.N, tid);
+      gather_windows<R, NT_, 1, PT>(base, qb0, A, org, cells, q0, g.N, tid);
   }
   __syncthreads();
 
   // ---- phase 2
-  constexpr int STM = (XP >> 12) & 7;
-  if constexpr (STM >= 1 && STM <= 3) {
-    // XP bits 12-14 = 1..3 (experiments): thread = (4 consecutive queries, output
-    // class), one 16-byte store along queries per class — plain (1), nt (2) or
-    // sc1 write-through (3, a buffer store with the sc1 cache-policy bit).
-    // Needs N % 4 == 0 (checked by the host).
-    constexpr int QG = QB / 4, NC4 = C::NT / QG;
-    const int qa = 4 * (tid % QG), cls4 = tid / QG;
-    if (q0 + qa >= g.N) return;
-    float* ob4 = out + ((long long)b * g.cout + (long long)l * K) * g.N + q0;
-    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(ob4, (short)0, 0x7fffffff,
-                                                                        0x00020000);
-    for (int k = cls4; k < K; k += NC4) {
-      const int ox = k / RD, oy = k - ox * RD;
-      float r4[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int qi = qa + i;
-        const float4 xd = xs[ox * QB + qi], yd = ys[oy * QB + qi];
-        const float* p = cells + qi * QSW + __float_as_int(yd.x) + __float_as_int(xd.x);
-        const float v00 = p[0], v01 = p[1], v10 = p[RS], v11 = p[RS + 1];
-        const float nw = __fmul_rn(yd.z, xd.z), ne = __fmul_rn(yd.z, xd.y);
-        const float sw = __fmul_rn(yd.y, xd.z), se = __fmul_rn(yd.y, xd.y);
-        float r = __fmul_rn(nw, v00);
-        r = __builtin_fmaf(ne, v01, r);
-        r = __builtin_fmaf(sw, v10, r);
-        r4[i] = __builtin_fmaf(se, v11, r);
-      }
-      typedef float f4v __attribute__((ext_vector_type(4)));
-      const f4v w = {r4[0], r4[1], r4[2], r4[3]};
-      const unsigned eo = (unsigned)(k * g.N + qa);
-      if constexpr (STM == 1) {
-        *reinterpret_cast<f4v*>(ob4 + eo) = w;
-      } else if constexpr (STM == 2) {
-        __builtin_nontemporal_store(w, reinterpret_cast<f4v*>(ob4 + eo));
-      } else {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, w), ro, eo * 4u, 0, 16);
-      }
-    }
-    return;
-  }
   const int qq = tid % QB, cls = tid / QB;
   if (q0 + qq >= g.N) return;
-  const float* cq = cells + qq * QSW;
+  const float* cq = cells + qq * C::QS;
   float* ob = out + ((long long)b * g.cout + (long long)l * K) * g.N + q0 + qq;
   for (int k = cls; k < K; k += C::NCLS) {
     const int ox = k / RD, oy = k - ox * RD;
@@ -374,251 +310,12 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
     r = __builtin_fmaf(ne, v01, r);
     r = __builtin_fmaf(sw, v10, r);
     r = __builtin_fmaf(se, v11, r);
-    if constexpr ((XP & 2) != 0) {
-      if (r == 1234.5f) ob[(unsigned)(k * g.N)] = r;
-    } else if constexpr (STM == 0) {
-      // write-through (sc1) output stores (round 2): the outputs leave the XCD's
-      // L2 while the kernel runs instead of as dirty lines the next kernel
-      // boundary writes back (Sintel B=1 9.5 -> 8.5 us, B=8 58.0 -> 54.6 us)
-      __hip_atomic_store(ob + (unsigned)(k * g.N), r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if constexpr (STM >= 5) {   // experiments: buffer stores, policy sc1 nt / sc0 sc1 / nt
-      constexpr int AUX = STM == 5 ? 18 : STM == 6 ? 17 : 2;
-      float* ob0 = out + ((long long)b * g.cout + (long long)l * K) * g.N + q0;
-      const __amdgpu_buffer_rsrc_t ro =
-          __builtin_amdgcn_make_buffer_rsrc(ob0, (short)0, 0x7fffffff, 0x00020000);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r), ro, (unsigned)(k * g.N + qq) * 4u, 0,
-                                            AUX);
-    } else {
-      ob[(unsigned)(k * g.N)] = r;
-    }
+    // write-through (sc1) output stores (round 2): the outputs leave the XCD's
+    // L2 while the kernel runs instead of as dirty lines the next kernel
+    // boundary writes back (Sintel B=1 9.5 -> 8.5 us, B=8 58.0 -> 54.6 us)
+    __hip_atomic_store(ob + (unsigned)(k * g.N), r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
-
-#ifdef DXR_EXPERIMENTS
-// ---------------------------------------------------------------------------
-// Pipelined persistent lookup (experiment).  A workgroup walks items (32
-// queries x one level of one pair) item = blockIdx.x + k * gridDim.x; while item
-// k's taps are combined and stored (phase 2), item k+1's windows are already in
-// flight (its phase 0 ran before, its coordinates one item earlier still).
-// Same per-sample arithmetic and fused sum as corr_lookup_wide_kernel.
-// One cells buffer (written only after the top barrier, when the previous
-// item's phase 2 is done), double tap data (phase 0 of item k+1 runs while
-// item k's taps are still to be read).
-// ---------------------------------------------------------------------------
-template <int R, int NT_>
-__device__ __forceinline__ void wide_phase0_xy(float cx, float cy, const LevelAddr& A, int l,
-                                               int tid, float4* xs, float4* ys, int2* org) {
-  using C = WideCfg<R, NT_>;
-  constexpr int RD = C::RD, WD = C::WD, RS = C::RS, QB = C::QB, G = C::G;
-  static_assert(C::SIT == 1, "one phase-0 slot per thread");
-  const int Hl = A.h, Wl = A.w;
-  const int slot = tid;
-  if (slot >= QB * G) return;   // whole waves
-  const int j = slot & (G - 1), qq = slot >> C::LG;
-  const float inv = 1.f / (float)(1 << l);
-  const float wm1 = (float)(Wl - 1), hm1 = (float)(Hl - 1);
-  const float ux = sample_coord(__fadd_rn(cx * inv, (float)(j - R)), wm1, wm1 / 2.f);
-  const float uy = sample_coord(__fadd_rn(cy * inv, (float)(j - R)), hm1, hm1 / 2.f);
-  const float flx = floorf(ux), fly = floorf(uy);
-  const bool act = j < RD;
-  int mx = 0x7fffffff, my = 0x7fffffff;
-  if (act) {
-    const bool bad = !(fabsf(flx) < 1.0e7f) || !(fabsf(fly) < 1.0e7f);
-    mx = bad ? FAR_ORIGIN : (int)flx - j;
-    my = bad ? FAR_ORIGIN : (int)fly - j;
-  }
-#pragma unroll
-  for (int o = 1; o < G; o <<= 1) {
-    mx = min(mx, __shfl_xor(mx, o));
-    my = min(my, __shfl_xor(my, o));
-  }
-  const bool far = mx + WD <= 0 || mx >= Wl || my + WD <= 0 || my >= Hl;
-  if (j == 0) org[qq] = far ? make_int2(FAR_ORIGIN, FAR_ORIGIN) : make_int2(mx, my);
-  if (act) {
-    const float fx = __fsub_rn(ux, flx), fy = __fsub_rn(uy, fly);
-    const int col = far ? 0 : (int)flx - (mx & ~3);
-    const int row = far ? 0 : ((int)fly - my) * RS;
-    xs[j * QB + qq] = make_float4(__int_as_float(col), fx, __fsub_rn(1.f, fx), 0.f);
-    ys[j * QB + qq] = make_float4(__int_as_float(row), fy, __fsub_rn(1.f, fy), 0.f);
-  }
-}
-
-template <int R, typename PT, int NT_ = 512>
-__global__ __launch_bounds__(NT_) void corr_lookup_pipe_kernel(const PT* __restrict__ pyr,
-                                                               const float* __restrict__ coords,
-                                                               float* __restrict__ out,
-                                                               LookupGeom g, int B) {
-  using C = WideCfg<R, NT_>;
-  constexpr int RD = C::RD, RS = C::RS, K = C::K, QB = C::QB;
-  __shared__ __attribute__((aligned(16))) float cells[QB * C::QS];
-  __shared__ float4 xs[2][RD * QB];
-  __shared__ float4 ys[2][RD * QB];
-  __shared__ int2 org[2][QB];
-  const int tid = threadIdx.x;
-  const int nqb = (g.N + QB - 1) / QB;
-  const int nitems = nqb * g.levels * B;
-  const int stride = gridDim.x;
-  int it = blockIdx.x;
-  if (it >= nitems) return;
-  auto decode = [&](int i, int& b, int& l, int& q0) {
-    const int qb = i % nqb, r = i / nqb;
-    l = r % g.levels;
-    b = r / g.levels;
-    q0 = qb * QB;
-  };
-  auto load_xy = [&](int i, float& cx, float& cy) {
-    cx = 0.f;
-    cy = 0.f;
-    if (i >= nitems) return;
-    int b, l, q0;
-    decode(i, b, l, q0);
-    const int q = q0 + (tid >> C::LG);
-    if (q < g.N && (tid >> C::LG) < QB) {
-      cx = coords[((long long)b * 2 + 0) * g.N + q];
-      cy = coords[((long long)b * 2 + 1) * g.N + q];
-    }
-  };
-  auto gather = [&](int i, const int2* o, float4 (&v)[C::VIT]) {
-    int b, l, q0;
-    decode(i, b, l, q0);
-    const LevelAddr& A = g.lv[l];
-    const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
-    const int qb0 = q0 & ((1 << A.lqb) - 1);
-    if (A.lth == 30)
-      gather_load<R, NT_, 1>(base, qb0, A, o, q0, g.N, tid, v);
-    else if (A.tw >= 4)
-      gather_load<R, NT_, 4>(base, qb0, A, o, q0, g.N, tid, v);
-    else if (A.tw == 2)
-      gather_load<R, NT_, 2>(base, qb0, A, o, q0, g.N, tid, v);
-    else
-      gather_load<R, NT_, 1>(base, qb0, A, o, q0, g.N, tid, v);
-  };
-
-  float cx, cy, ncx, ncy;
-  load_xy(it, cx, cy);
-  {
-    int b, l, q0;
-    decode(it, b, l, q0);
-    wide_phase0_xy<R, NT_>(cx, cy, g.lv[l], l, tid, xs[0], ys[0], org[0]);
-  }
-  load_xy(it + stride, ncx, ncy);
-  __syncthreads();
-  float4 v[C::VIT];
-  gather(it, org[0], v);
-  for (int k = 0;; ++k) {
-    const int buf = k & 1;
-    __syncthreads();                       // phase 2 of the previous item is done
-    gather_store<R, NT_>(v, cells, tid);
-    const int nx = it + stride;
-    if (nx < nitems) {
-      int b, l, q0;
-      decode(nx, b, l, q0);
-      wide_phase0_xy<R, NT_>(ncx, ncy, g.lv[l], l, tid, xs[buf ^ 1], ys[buf ^ 1], org[buf ^ 1]);
-      load_xy(nx + stride, ncx, ncy);
-    }
-    __syncthreads();                       // cells of `it`, taps of `nx` ready
-    if (nx < nitems) gather(nx, org[buf ^ 1], v);
-    // phase 2 of `it`
-    {
-      int b, l, q0;
-      decode(it, b, l, q0);
-      const int qq = tid % QB, cls = tid / QB;
-      if (q0 + qq < g.N) {
-        const float* cq = cells + qq * C::QS;
-        float* ob = out + ((long long)b * g.cout + (long long)l * K) * g.N + q0 + qq;
-        for (int kk = cls; kk < K; kk += C::NCLS) {
-          const int ox = kk / RD, oy = kk - ox * RD;
-          const float4 xd = xs[buf][ox * QB + qq], yd = ys[buf][oy * QB + qq];
-          const float* p = cq + __float_as_int(yd.x) + __float_as_int(xd.x);
-          const float v00 = p[0], v01 = p[1], v10 = p[RS], v11 = p[RS + 1];
-          const float nw = __fmul_rn(yd.z, xd.z), ne = __fmul_rn(yd.z, xd.y);
-          const float sw = __fmul_rn(yd.y, xd.z), se = __fmul_rn(yd.y, xd.y);
-          float r = __fmul_rn(nw, v00);
-          r = __builtin_fmaf(ne, v01, r);
-          r = __builtin_fmaf(sw, v10, r);
-          r = __builtin_fmaf(se, v11, r);
-          __hip_atomic_store(ob + (unsigned)(kk * g.N), r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-    }
-    it = nx;
-    if (it >= nitems) break;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Two-level lookup (experiment): a workgroup handles the same 32 queries on
-// levels 2y and 2y+1: phase 0 of both, BOTH levels' window gathers issued into
-// registers before either is staged (twice the loads in flight per thread),
-// then level 2y's windows -> LDS -> outputs, level 2y+1's windows -> the same
-// LDS -> outputs.  Same arithmetic as corr_lookup_wide_kernel; measured slower
-// (xp 100 in scripts/xp_lookup.py), kept in the experiments target only.
-// ---------------------------------------------------------------------------
-template <int R, typename PT, int NT_ = 512>
-__global__ __launch_bounds__(NT_) void corr_lookup_wide2_kernel(
-    const PT* __restrict__ pyr, const float* __restrict__ coords, float* __restrict__ out,
-    LookupGeom g) {
-  using C = WideCfg<R, NT_>;
-  constexpr int RD = C::RD, RS = C::RS, K = C::K, QB = C::QB;
-  __shared__ __attribute__((aligned(16))) float cells[QB * C::QS];
-  __shared__ float4 xs[2][RD * QB];
-  __shared__ float4 ys[2][RD * QB];
-  __shared__ int2 org[2][QB];
-
-  const int tid = threadIdx.x;
-  const int b = blockIdx.z;
-  const int q0 = blockIdx.x * QB;
-  const int l0 = 2 * blockIdx.y;
-  const int nl = min(2, g.levels - l0);
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-    if (u < nl) wide_phase0<R, NT_>(coords, g, g.lv[l0 + u], b, l0 + u, q0, tid, xs[u], ys[u], org[u]);
-  __syncthreads();
-  float4 win[2][C::VIT];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    if (u >= nl) break;
-    const LevelAddr& A = g.lv[l0 + u];
-    const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
-    const int qb0 = q0 & ((1 << A.lqb) - 1);
-    if (A.lth == 30)
-      gather_load<R, NT_, 1>(base, qb0, A, org[u], q0, g.N, tid, win[u]);
-    else if (A.tw >= 4)
-      gather_load<R, NT_, 4>(base, qb0, A, org[u], q0, g.N, tid, win[u]);
-    else if (A.tw == 2)
-      gather_load<R, NT_, 2>(base, qb0, A, org[u], q0, g.N, tid, win[u]);
-    else
-      gather_load<R, NT_, 1>(base, qb0, A, org[u], q0, g.N, tid, win[u]);
-  }
-  const int qq = tid % QB, cls = tid / QB;
-  const bool live = q0 + qq < g.N;
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    if (u >= nl) break;
-    if (u > 0) __syncthreads();          // level u-1's phase 2 is done with the cells
-    gather_store<R, NT_>(win[u], cells, tid);
-    __syncthreads();
-    if (live) {
-      const float* cq = cells + qq * C::QS;
-      float* ob = out + ((long long)b * g.cout + (long long)(l0 + u) * K) * g.N + q0 + qq;
-      for (int k = cls; k < K; k += C::NCLS) {
-        const int ox = k / RD, oy = k - ox * RD;
-        const float4 xd = xs[u][ox * QB + qq], yd = ys[u][oy * QB + qq];
-        const float* p = cq + __float_as_int(yd.x) + __float_as_int(xd.x);
-        const float v00 = p[0], v01 = p[1], v10 = p[RS], v11 = p[RS + 1];
-        const float nw = __fmul_rn(yd.z, xd.z), ne = __fmul_rn(yd.z, xd.y);
-        const float sw = __fmul_rn(yd.y, xd.z), se = __fmul_rn(yd.y, xd.y);
-        float r = __fmul_rn(nw, v00);
-        r = __builtin_fmaf(ne, v01, r);
-        r = __builtin_fmaf(sw, v10, r);
-        r = __builtin_fmaf(se, v11, r);
-        ob[(unsigned)(k * g.N)] = r;
-      }
-    }
-  }
-}
-
-#endif  // DXR_EXPERIMENTS
 
 // ---------------------------------------------------------------------------
 // Lookup backward (training: train.py:175-178 backpropagates through the
@@ -859,204 +556,6 @@ __global__ __launch_bounds__(256) void conv1x1_pack_weight_kernel(const float* _
   pairs[2LL * u + 1] = l;
 }
 
-#ifdef DXR_EXPERIMENTS
-// r01 form (experiments target only since r02; see corr_lookup_conv1x1_h2_kernel).
-// NT threads per workgroup (1024 by default: the four levels' lookup phases
-// are latency-bound at 8 waves per CU).  With 16 waves the GEMM splits K in two
-// halves per output block: waves 8..15 add their partial accumulators through
-// LDS (the lookup's staging area, free by then).
-template <int R, typename PT, int NT = 1024, int PF = 4>
-__global__ __launch_bounds__(NT) void corr_lookup_conv1x1_kernel(
-    const PT* __restrict__ pyr, const float* __restrict__ coords, const float4* __restrict__ wpk,
-    const float* __restrict__ bias, float* __restrict__ out, LookupGeom g, int cout, int relu) {
-  using C = WideCfg<R, NT>;
-  using M = MotionCfg<R>;
-  constexpr int RD = C::RD, RS = C::RS, K = C::K, QB = C::QB, KB = M::KB;
-  constexpr int NW = NT / 64, KSPLIT = NW >= 16 ? 2 : 1;
-  static_assert(NW == 8 || NW == 16, "8 output blocks of 32 per pass");
-  // lookup staging (cells | xs | ys | org), reused as the K-split reduction area
-  constexpr int CELLS_B = QB * C::QS * 4, XS_B = M::LMAX * RD * QB * 16, ORG_B = M::LMAX * QB * 8;
-  constexpr int STAGE_B = CELLS_B + 2 * XS_B + ORG_B, RED_B = KSPLIT > 1 ? 8 * 16 * 64 * 4 : 0;
-  __shared__ __attribute__((aligned(16))) char stage[STAGE_B > RED_B ? STAGE_B : RED_B];
-  __shared__ __attribute__((aligned(16))) uint4 cpl[3 * KB * QB];   // [plane][kb][q] x 8 bf16
-  float* cells = reinterpret_cast<float*>(stage);
-  float4* xs = reinterpret_cast<float4*>(stage + CELLS_B);   // per level, as the lookup's phase 0
-  float4* ys = reinterpret_cast<float4*>(stage + CELLS_B + XS_B);
-  int2* org = reinterpret_cast<int2*>(stage + CELLS_B + 2 * XS_B);
-  float* red = reinterpret_cast<float*>(stage);
-  uint16_t* cph = reinterpret_cast<uint16_t*>(cpl);
-
-  const int tid = threadIdx.x;
-  const int b = blockIdx.y;
-  const int q0 = blockIdx.x * QB;
-  const int cin = g.cout;                  // levels * (2r+1)^2 <= M::KP
-  const int kpad = (cin + 15) & ~15;
-
-  // GEMM roles: wave -> output block (wave % 8) + 8i, K half (wave / 8).  The A
-  // operand (weight fragments, f32, split in registers) streams from L2 with PF
-  // k steps in flight; the first PF are requested before the lookup phases.
-  const int lane = tid & 63, wave = tid >> 6, j = lane & 31, kh = lane >> 5;
-  const int wob = wave & 7, khalf = wave >> 3;
-  const int nks = kpad / 16;
-  const int kbeg = khalf * nks / KSPLIT, kend = (khalf + 1) * nks / KSPLIT;
-  const int nob = cout / 32;
-  float4 wbuf[PF][2];
-  auto wload = [&](float4* dst, int ob, int ks) {
-    const float4* wp = wpk + 2 * ((long long)(2 * ks + kh) * cout + ob * 32 + j);
-    dst[0] = wp[0];
-    dst[1] = wp[1];
-  };
-  auto preload = [&](int ob) {
-#pragma unroll
-    for (int s = 0; s < PF; ++s) wload(wbuf[s], ob, min(kbeg + s, kend - 1));
-  };
-  if (wob < nob) preload(wob);
-
-  // zero the channel padding [cin, kpad) of the three planes
-  {
-    const int np = kpad - cin;
-    for (int i = tid; i < 3 * QB * np; i += NT) {
-      const int p = i / (QB * np), rem = i - p * (QB * np);
-      const int qq = rem / np, c = cin + rem - qq * np;
-      cph[((p * KB + (c >> 3)) * QB + qq) * 8 + (c & 7)] = 0;
-    }
-  }
-
-  // phase 0 of every level, then every level's window gathers in flight at
-  // once (registers), then per level: windows -> LDS, samples -> operand planes
-#pragma unroll
-  for (int l = 0; l < M::LMAX; ++l)
-    if (l < g.levels)
-      wide_phase0<R, NT>(coords, g, g.lv[l], b, l, q0, tid, xs + l * RD * QB, ys + l * RD * QB,
-                         org + l * QB);
-  __syncthreads();
-  float4 win[M::LMAX][C::VIT];
-#pragma unroll
-  for (int l = 0; l < M::LMAX; ++l) {
-    if (l < g.levels) {
-      const LevelAddr& A = g.lv[l];
-      const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
-      const int qb0 = q0 & ((1 << A.lqb) - 1);
-      // paged levels 0..3: level-l tiles are (16 >> l) cells wide
-      if (l < 3)
-        gather_load<R, NT, 4>(base, qb0, A, org + l * QB, q0, g.N, tid, win[l]);
-      else
-        gather_load<R, NT, 2>(base, qb0, A, org + l * QB, q0, g.N, tid, win[l]);
-    }
-  }
-#pragma unroll
-  for (int l = 0; l < M::LMAX; ++l) {
-    if (l >= g.levels) break;
-    gather_store<R, NT>(win[l], cells, tid);
-    __syncthreads();
-    {
-      const float4* xl = xs + l * RD * QB;
-      const float4* yl = ys + l * RD * QB;
-      const int qq = tid % QB, cls = tid / QB;
-      const bool live = q0 + qq < g.N;
-      const float* cq = cells + qq * C::QS;
-      for (int k = cls; k < K; k += C::NCLS) {
-        const int ox = k / RD, oy = k - ox * RD;
-        const float4 xd = xl[ox * QB + qq], yd = yl[oy * QB + qq];
-        const float* p = cq + __float_as_int(yd.x) + __float_as_int(xd.x);
-        const float v00 = p[0], v01 = p[1], v10 = p[RS], v11 = p[RS + 1];
-        const float nw = __fmul_rn(yd.z, xd.z), ne = __fmul_rn(yd.z, xd.y);
-        const float sw = __fmul_rn(yd.y, xd.z), se = __fmul_rn(yd.y, xd.y);
-        float r = __fmul_rn(nw, v00);
-        r = __builtin_fmaf(ne, v01, r);
-        r = __builtin_fmaf(sw, v10, r);
-        r = __builtin_fmaf(se, v11, r);
-        if (!live) r = 0.f;                // queries past N: finite zeros
-        uint16_t h, m, lo;
-        split3(r, h, m, lo);
-        const int c = l * K + k;
-        const int e = ((c >> 3) * QB + qq) * 8 + (c & 7);
-        cph[e] = h;
-        cph[KB * QB * 8 + e] = m;
-        cph[2 * KB * QB * 8 + e] = lo;
-      }
-    }
-    __syncthreads();   // cells are rewritten by the next level (and the staging
-                       // area becomes the reduction area after the last one)
-  }
-
-  // ---- (Cout x 32 queries x Cin) GEMM, f32 class
-  const int q = q0 + j;
-  for (int ob0 = 0; ob0 < nob; ob0 += 8) {   // uniform trip count: barriers inside
-    const int ob = ob0 + wob;
-    const bool act = ob < nob;
-    mf16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    if (act) {
-      if (ob0 > 0) preload(ob);
-      // One k step: split the weight fragment of slot sl in registers, refill the
-      // slot PF steps ahead (unconditionally, clamped: a conditional refill makes
-      // the compiler wait for it at once), six MFMAs.
-      auto kstep = [&](int ks, int sl, bool refill) {
-        // keep each step's split behind its own waits: hoisted into the previous
-        // step's MFMA shadow, it makes that step wait for the refill in flight
-        __builtin_amdgcn_sched_barrier(0);
-        const int kb = 2 * ks + kh;
-        uint4 wh, wm, wl;
-        {
-          const float4 a = wbuf[sl][0], c = wbuf[sl][1];
-          const float x[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
-          dxr::split8(x, wh, wm, wl);
-        }
-        if (refill) wload(wbuf[sl], ob, min(ks + PF, kend - 1));
-        const mbf8 th = __builtin_bit_cast(mbf8, wh);
-        const mbf8 tm = __builtin_bit_cast(mbf8, wm);
-        const mbf8 tl = __builtin_bit_cast(mbf8, wl);
-        const mbf8 qh = __builtin_bit_cast(mbf8, cpl[(0 * KB + kb) * QB + j]);
-        const mbf8 qm = __builtin_bit_cast(mbf8, cpl[(1 * KB + kb) * QB + j]);
-        const mbf8 ql = __builtin_bit_cast(mbf8, cpl[(2 * KB + kb) * QB + j]);
-        // small terms first
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, ql, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qh, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qm, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh, acc, 0, 0, 0);
-      };
-      const int nfull = kbeg + (kend - kbeg) / PF * PF;
-#pragma unroll 1
-      for (int k0 = kbeg; k0 < nfull; k0 += PF) {
-#pragma unroll
-        for (int sl = 0; sl < PF; ++sl) kstep(k0 + sl, sl, true);
-      }
-#pragma unroll
-      for (int sl = 0; sl < PF; ++sl)   // tail: no refills
-        if (nfull + sl < kend) kstep(nfull + sl, sl, false);
-    }
-    if constexpr (KSPLIT > 1) {
-      // the upper K half hands its partial sums to the lower half's wave
-      if (khalf == 1 && act) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) red[(wob * 16 + r) * 64 + lane] = acc[r];
-      }
-      __syncthreads();
-      if (khalf == 0 && act) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] += red[(wob * 16 + r) * 64 + lane];
-      }
-      __syncthreads();
-    }
-    if (khalf == 0 && act && q < g.N) {
-      float* ob_out = out + (long long)b * cout * g.N + q;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int orow = ob * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-        float v = acc[r] + (bias ? bias[orow] : 0.f);
-        if (relu && v < 0.f) v = 0.f;      // NaN stays NaN, as torch.relu
-        ob_out[(long long)orow * g.N] = v;
-      }
-    }
-  }
-}
-
-#endif  // DXR_EXPERIMENTS
-
 // ---------------------------------------------------------------------------
 // Round-2 form: two workgroups per CU.  The r01 kernel staged all four levels'
 // tap data and kept three bf16 sample planes (125 KB of LDS: one workgroup per
@@ -1071,8 +570,7 @@ __global__ __launch_bounds__(NT) void corr_lookup_conv1x1_kernel(
 // ---------------------------------------------------------------------------
 typedef _Float16 mh8 __attribute__((ext_vector_type(8)));
 
-// ST (experiments): 1 = write-through (sc1) output stores.
-template <int R, typename PT, int NT = 512, int PF = 4, int ST = 0>
+template <int R, typename PT, int NT = 512, int PF = 4>
 __global__ __launch_bounds__(NT, 4) void corr_lookup_conv1x1_h2_kernel(
     const PT* __restrict__ pyr, const float* __restrict__ coords, const float4* __restrict__ wpk,
     const float* __restrict__ bias, float* __restrict__ out, LookupGeom g, int cout, int relu) {
@@ -1249,11 +747,7 @@ __global__ __launch_bounds__(NT, 4) void corr_lookup_conv1x1_h2_kernel(
           const int orow = ob * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
           float v = acc[r] + (bias ? bias[orow] : 0.f);
           if (relu && v < 0.f) v = 0.f;      // NaN stays NaN, as torch.relu
-          if constexpr (ST == 1)
-            __hip_atomic_store(ob_out + (long long)orow * g.N, v, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-          else
-            ob_out[(long long)orow * g.N] = v;
+          ob_out[(long long)orow * g.N] = v;
         }
       }
     }
@@ -1395,136 +889,3 @@ extern "C" int dxr_corr_lookup_conv1x1(const void* pyramid, int pyr_dtype, int64
   return DXR_EINVAL;
 }
 
-#ifdef DXR_EXPERIMENTS
-// Experiments build target only: the radius-4 lookup with ablation bits `xp`.
-namespace {
-template <int XP, typename PT>
-int xp_lookup_k(const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
-                hipStream_t stream) {
-  using W = WideCfg<4>;
-  const dim3 grid((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
-  hipLaunchKernelGGL((corr_lookup_wide_kernel<4, PT, 512, XP>), grid, dim3(W::NT), 0, stream, pyr,
-                     coords, out, g);
-  return dxr::launch_status();
-}
-template <int NT2, typename PT>
-int xp_lookup_nt(const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
-                 hipStream_t stream) {
-  using W = WideCfg<4, NT2>;
-  const dim3 grid((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
-  hipLaunchKernelGGL((corr_lookup_wide_kernel<4, PT, NT2, 0>), grid, dim3(W::NT), 0, stream, pyr,
-                     coords, out, g);
-  return dxr::launch_status();
-}
-template <typename PT>
-int xp_lookup_pipe(const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
-                   int per_cu, hipStream_t stream) {
-  using W = WideCfg<4>;
-  const int nitems = ((g.N + W::QB - 1) / W::QB) * g.levels * B;
-  const int grid = nitems < 256 * per_cu ? nitems : 256 * per_cu;
-  hipLaunchKernelGGL((corr_lookup_pipe_kernel<4, PT>), dim3((unsigned)grid), dim3(W::NT), 0, stream,
-                     pyr, coords, out, g, B);
-  return dxr::launch_status();
-}
-template <typename PT>
-int xp_lookup2(const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
-               hipStream_t stream) {
-  using W = WideCfg<4>;
-  const dim3 grid((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)((g.levels + 1) / 2),
-                  (unsigned)B);
-  hipLaunchKernelGGL((corr_lookup_wide2_kernel<4, PT>), grid, dim3(W::NT), 0, stream, pyr, coords,
-                     out, g);
-  return dxr::launch_status();
-}
-}  // namespace
-
-extern "C" int dxr_xp_lookup(const void* pyramid, int pyr_dtype, int64_t B, int64_t H, int64_t W,
-                             const float* coords, float* out, int xp, hipStream_t stream) {
-  dxr::Levels L;
-  if (!dxr::make_levels(B, H, W, 4, &L)) return DXR_EINVAL;
-  LookupGeom g;
-  g.N = (int)(H * W);
-  g.levels = 4;
-  g.cout = 4 * 81;
-  for (int l = 0; l < 4; ++l) g.lv[l] = level_addr(L.lay[l]);
-  if (pyr_dtype == DXR_F32) {
-    const float* p = static_cast<const float*>(pyramid);
-    switch (xp) {
-      case 0: return xp_lookup_k<0>(p, coords, out, g, (int)B, stream);
-      case 1: return xp_lookup_k<1>(p, coords, out, g, (int)B, stream);
-      case 2: return xp_lookup_k<2>(p, coords, out, g, (int)B, stream);
-      case 3: return xp_lookup_k<3>(p, coords, out, g, (int)B, stream);
-      case 4: return xp_lookup_k<4>(p, coords, out, g, (int)B, stream);
-      case 8: return xp_lookup_k<8>(p, coords, out, g, (int)B, stream);
-      case 32: return xp_lookup_k<32>(p, coords, out, g, (int)B, stream);
-      case 100: return xp_lookup2(p, coords, out, g, (int)B, stream);
-      case 256: return xp_lookup_nt<256>(p, coords, out, g, (int)B, stream);
-      case 1024: return xp_lookup_nt<1024>(p, coords, out, g, (int)B, stream);
-      // store forms (bits 12-14): 16-byte plain / nt / sc1, scalar plain (r02 before sc1),
-      // scalar buffer stores sc1 nt / sc0 sc1 / nt
-      case 0x1000: return g.N % 4 ? DXR_EUNSUPPORTED : xp_lookup_k<0x1000>(p, coords, out, g, (int)B, stream);
-      case 0x2000: return g.N % 4 ? DXR_EUNSUPPORTED : xp_lookup_k<0x2000>(p, coords, out, g, (int)B, stream);
-      case 0x3000: return g.N % 4 ? DXR_EUNSUPPORTED : xp_lookup_k<0x3000>(p, coords, out, g, (int)B, stream);
-      case 0x4000: return xp_lookup_k<0x4000>(p, coords, out, g, (int)B, stream);
-      case 201: case 202: case 203: case 204: case 206: case 208:
-        return xp_lookup_pipe(p, coords, out, g, (int)B, xp - 200, stream);
-      case 0x5000: return xp_lookup_k<0x5000>(p, coords, out, g, (int)B, stream);
-      case 0x6000: return xp_lookup_k<0x6000>(p, coords, out, g, (int)B, stream);
-      case 0x7000: return xp_lookup_k<0x7000>(p, coords, out, g, (int)B, stream);
-      default: return DXR_EUNSUPPORTED;
-    }
-  }
-  const uint16_t* p = static_cast<const uint16_t*>(pyramid);
-  switch (xp) {
-    case 100: return xp_lookup2(p, coords, out, g, (int)B, stream);
-    case 256: return xp_lookup_nt<256>(p, coords, out, g, (int)B, stream);
-    case 0: return xp_lookup_k<0>(p, coords, out, g, (int)B, stream);
-    case 1: return xp_lookup_k<1>(p, coords, out, g, (int)B, stream);
-    case 2: return xp_lookup_k<2>(p, coords, out, g, (int)B, stream);
-    case 32: return xp_lookup_k<32>(p, coords, out, g, (int)B, stream);
-    case 0x1000: return g.N % 4 ? DXR_EUNSUPPORTED : xp_lookup_k<0x1000>(p, coords, out, g, (int)B, stream);
-    case 0x3000: return g.N % 4 ? DXR_EUNSUPPORTED : xp_lookup_k<0x3000>(p, coords, out, g, (int)B, stream);
-    case 0x4000: return xp_lookup_k<0x4000>(p, coords, out, g, (int)B, stream);
-    case 201: case 202: case 203: case 204: case 206: case 208:
-      return xp_lookup_pipe(p, coords, out, g, (int)B, xp - 200, stream);
-    default: return DXR_EUNSUPPORTED;
-  }
-}
-#endif
-
-#ifdef DXR_EXPERIMENTS
-// Experiments target only: the fused lookup + 1x1 conv with a chosen kernel —
-// xp 0: the r01 form (three bf16 sample planes, all levels staged, one
-// workgroup per CU; reads the f32 half of the packed weight), 1: the product's
-// (512 threads, two workgroups per CU), 2: the product's form at 1024 threads.
-extern "C" int dxr_xp_lookup_conv1x1(const float* pyramid, int64_t B, int64_t H, int64_t W,
-                                     const float* coords, const void* weight_packed,
-                                     const float* bias, int64_t cout, float* out, int xp,
-                                     hipStream_t stream) {
-  dxr::Levels L;
-  if (!dxr::make_levels(B, H, W, 4, &L) || cout % 32 != 0) return DXR_EINVAL;
-  LookupGeom g;
-  g.N = (int)(H * W);
-  g.levels = 4;
-  g.cout = 4 * 81;
-  for (int l = 0; l < L.n; ++l) g.lv[l] = level_addr(L.lay[l]);
-  const float4* wpl = static_cast<const float4*>(weight_packed);
-  const dim3 grid((unsigned)((g.N + 31) / 32), (unsigned)B);
-  if (xp == 0)
-    hipLaunchKernelGGL((corr_lookup_conv1x1_kernel<4, float, 1024, 4>), grid, dim3(1024), 0, stream,
-                       pyramid, coords, wpl, bias, out, g, (int)cout, 1);
-  else if (xp == 1)
-    hipLaunchKernelGGL((corr_lookup_conv1x1_h2_kernel<4, float, 512, 4>), grid, dim3(512), 0,
-                       stream, pyramid, coords, wpl, bias, out, g, (int)cout, 1);
-  else if (xp == 2)
-    hipLaunchKernelGGL((corr_lookup_conv1x1_h2_kernel<4, float, 1024, 4>), grid, dim3(1024), 0,
-                       stream, pyramid, coords, wpl, bias, out, g, (int)cout, 1);
-  else if (xp == 3)   // sc1 output stores, 512 threads
-    hipLaunchKernelGGL((corr_lookup_conv1x1_h2_kernel<4, float, 512, 4, 1>), grid, dim3(512), 0,
-                       stream, pyramid, coords, wpl, bias, out, g, (int)cout, 1);
-  else   // sc1 output stores, 1024 threads
-    hipLaunchKernelGGL((corr_lookup_conv1x1_h2_kernel<4, float, 1024, 4, 1>), grid, dim3(1024), 0,
-                       stream, pyramid, coords, wpl, bias, out, g, (int)cout, 1);
-  return dxr::launch_status();
-}
-#endif

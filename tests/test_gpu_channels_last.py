@@ -109,7 +109,8 @@ def test_alternate_block_channels_last_matches_oracle(dx):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_corr_block_channels_last_bit_identical(dx, dtype, shape):
     """Channels-last fmaps give the NCHW block's bits: f32 with even W takes the
-    split build's NHWC operand loads (no layout pass), other cases one transpose."""
+    split build's NHWC operand loads, bf16 with D % 32 == 0 the two-block bf16
+    build's (no layout pass); other cases one transpose."""
     B, D, H, W = shape
     f1 = _t(dg.fmap(51, B, D, H, W, "fnet")).to(dtype)
     f2 = _t(dg.fmap(52, B, D, H, W, "fnet")).to(dtype)
@@ -165,3 +166,63 @@ def test_nhwc_build_entry_point(dx):
                                     H, 39, 4, 11.3137, bufs[0].data_ptr(), nat.DXR_F32,
                                     nat.DXR_BUILD_AUTO, nat.stream_of(g1))
     assert st == nat.DXR_EUNSUPPORTED             # odd W: the NCHW build is exact-f32 there
+
+
+@pytest.mark.parametrize("W", [40, 39])
+@pytest.mark.parametrize("pyr_dt", ["f32", "bf16"])
+def test_nhwc_bf16_build_entry_point(dx, W, pyr_dt):
+    """dxr_corr_pyramid_build with bf16 DXR_NHWC operands (the bf16 mode's
+    channels-last encoders, core/extractor.py:168-192) reads them in place and
+    writes the NCHW bf16 build's pyramid bit for bit, page padding included —
+    also for W % 4 != 0, where the NCHW build is the one-block kernel.  D % 32
+    != 0 is DXR_EUNSUPPORTED (the shell transposes)."""
+    from dexiraft_amd import _native as nat
+    lib = nat.load()
+    B, D, H = 2, 128, 21
+    f1 = _t(dg.fmap(81, B, D, H, W, "fnet")).bfloat16()
+    f2 = _t(dg.fmap(82, B, D, H, W, "fnet")).bfloat16()
+    n = lib.dxr_pyramid_numel(B, H, W, 4)
+    tdt, code = (torch.float32, nat.DXR_F32) if pyr_dt == "f32" else (torch.bfloat16, nat.DXR_BF16)
+    bufs = []
+    for layout, a, b in ((nat.DXR_NCHW, f1, f2), (nat.DXR_NHWC, _cl(f1), _cl(f2))):
+        buf = torch.full((n,), float("nan"), device=DEV, dtype=tdt)
+        st = lib.dxr_corr_pyramid_build(a.data_ptr(), b.data_ptr(), nat.DXR_BF16, layout, B, D, H,
+                                        W, 4, float(np.sqrt(np.float32(D))), buf.data_ptr(),
+                                        code, nat.DXR_BUILD_AUTO, nat.stream_of(a))
+        assert st == 0
+        bufs.append(buf)
+    torch.cuda.synchronize()
+    assert not torch.isnan(bufs[1].float()).any()   # every page written
+    assert torch.equal(bufs[0], bufs[1])
+    g1 = _cl(_t(dg.fmap(83, B, 48, H, W)).bfloat16())
+    st = lib.dxr_corr_pyramid_build(g1.data_ptr(), g1.data_ptr(), nat.DXR_BF16, nat.DXR_NHWC, B,
+                                    48, H, W, 4, 6.9282, bufs[0].data_ptr(), code,
+                                    nat.DXR_BUILD_AUTO, nat.stream_of(g1))
+    assert st == nat.DXR_EUNSUPPORTED
+
+
+def test_kitti_b8_bf16_channels_last_bit_identical(dx, monkeypatch):
+    """C3 at full size (KITTI 375x1242 -> fmap 47x156, B = 8, D = 256, bf16):
+    channels-last fmaps are read in place by the bf16 build (no dxr_transpose)
+    and give the NCHW block's pyramid and lookups bit for bit."""
+    B, D, H, W = 8, 256, 47, 156
+    g = torch.Generator(device=DEV)
+    g.manual_seed(2024)
+    f1 = torch.randn((B, D, H, W), generator=g, device=DEV).bfloat16()
+    f2 = torch.randn((B, D, H, W), generator=g, device=DEV).bfloat16()
+    c = _t(dg.coords(93, B, H, W, "normal", 4.0))
+    with torch.no_grad():
+        a = dx.CorrBlock(f1, f2)
+        ga = a(c)
+        buf_a = a._buf
+        del a
+        import sys
+        corr_mod = sys.modules[dx.CorrBlock.__module__]
+
+        def no_transpose(t):
+            raise AssertionError("channels-last bf16 fmaps must not be transposed")
+        monkeypatch.setattr(corr_mod, "_nchw", no_transpose)
+        b = dx.CorrBlock(_cl(f1), _cl(f2))
+        assert torch.equal(buf_a, b._buf)             # every page, padding included
+        del buf_a
+        assert torch.equal(ga, b(c))
