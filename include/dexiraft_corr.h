@@ -73,7 +73,7 @@ extern "C" {
 /* HIP's own definition; repeating an identical typedef is legal in C11/C++. */
 typedef struct ihipStream_t* hipStream_t;
 
-#define DXR_ABI_VERSION 5
+#define DXR_ABI_VERSION 6
 
 enum dxr_status {
   DXR_OK = 0,
@@ -137,6 +137,37 @@ int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int in_dtype,
                            int64_t W, int num_levels, float divisor,
                            void* pyramid, int pyr_dtype, int algo,
                            hipStream_t stream);
+
+/*
+ * Bytes of device workspace dxr_corr_pyramid_build_ws uses for B pairs of
+ * D x H x W fmaps of in_dtype (0: that request needs none; -1: bad geometry).
+ * ABI 6.
+ */
+int64_t dxr_build_workspace_bytes(int in_dtype, int64_t B, int64_t D, int64_t H,
+                                  int64_t W);
+
+/*
+ * dxr_corr_pyramid_build with a caller-owned workspace (16-byte aligned, at
+ * least dxr_build_workspace_bytes; contents need no initialisation and are
+ * dead after the build).  Same arguments, same result contract; with DXR_F32
+ * fmaps, algo DXR_BUILD_AUTO and D % 16 == 0 it runs the pre-split build:
+ * one pass scales every pixel's channel vector by a power of two 2^s
+ * (|x 2^s| < 2^14) and splits it into an f16 pair x 2^s = hi + 2^-11 lo in the
+ * workspace, then the build's K loop moves those pairs by LDS-DMA and runs the
+ * same three f16 MFMA products per f32 product, undoing both scales exactly in
+ * its epilogue — f32-class error (<= 2^-22 |x| per operand element near its
+ * pixel's max) at any fmap scale, bit-identical for NCHW and NHWC fmaps and
+ * exactly linear in power-of-two scalings of either fmap.  Pages whose sums
+ * are not finite (an inf/NaN operand) are recomputed on the exact three-way
+ * bf16 split.  A NULL or short workspace runs dxr_corr_pyramid_build.
+ * Replaces the same reference lines: core/corr.py:52-60 + :21-27.  ABI 6.
+ */
+int dxr_corr_pyramid_build_ws(const void* fmap1, const void* fmap2, int in_dtype,
+                              int fmap_layout, int64_t B, int64_t D, int64_t H,
+                              int64_t W, int num_levels, float divisor,
+                              void* pyramid, int pyr_dtype, int algo,
+                              void* workspace, int64_t workspace_bytes,
+                              hipStream_t stream);
 
 /*
  * CorrBlock.corr: the level-0 volume alone, row-major [B, H, W, 1, H, W]

@@ -15,7 +15,7 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_PATH = Path(__file__).resolve().with_name("libdexiraft_corr.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 DXR_OK, DXR_EINVAL, DXR_EUNSUPPORTED, DXR_EHIP = 0, 1, 2, -1
 DXR_F32, DXR_BF16 = 0, 1
@@ -35,6 +35,9 @@ SIGNATURES: dict[str, tuple[object, list[object]]] = {
     "dxr_pyramid_level_offset": (_i64, [_i64, _i64, _i64, _int]),
     "dxr_corr_pyramid_build": (_int, [_vp, _vp, _int, _int, _i64, _i64, _i64, _i64, _int, _f32,
                                       _vp, _int, _int, _vp]),
+    "dxr_build_workspace_bytes": (_i64, [_int, _i64, _i64, _i64, _i64]),
+    "dxr_corr_pyramid_build_ws": (_int, [_vp, _vp, _int, _int, _i64, _i64, _i64, _i64, _int,
+                                         _f32, _vp, _int, _int, _vp, _i64, _vp]),
     "dxr_corr_volume": (_int, [_vp, _vp, _int, _i64, _i64, _i64, _i64, _f32, _vp, _vp]),
     "dxr_pyramid_unpack": (_int, [_vp, _int, _i64, _i64, _i64, _int, _int, _vp, _vp]),
     "dxr_pyramid_pack": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _int, _vp]),

@@ -46,7 +46,9 @@ def hipcc() -> str:
 
 
 def _sources(experiments: bool = False) -> list[Path]:
-    return sorted((EXP_DIR if experiments else CSRC).glob("*.hip"))
+    if experiments:   # each experiment includes its product source; capi.hip once
+        return sorted(EXP_DIR.glob("*.hip")) + [CSRC / "capi.hip"]
+    return sorted(CSRC.glob("*.hip"))
 
 
 def _deps(experiments: bool = False) -> list[Path]:
@@ -70,8 +72,8 @@ FILE_FLAGS = {"corr_build.hip": ["-fno-slp-vectorize"], "corr_lookup.hip": ["-fn
 
 def _compile(src: Path, extra: list[str], out_dir: Path = BUILD_DIR) -> Path:
     obj = out_dir / (src.stem + ".o")
-    cmd = [hipcc(), *CXXFLAGS, *FILE_FLAGS.get(src.name, []), *extra, "-c", str(src), "-o",
-           str(obj)]
+    flags = FILE_FLAGS.get(src.name.replace("xp_", "corr_"), [])
+    cmd = [hipcc(), *CXXFLAGS, *flags, *extra, "-c", str(src), "-o", str(obj)]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{' '.join(cmd)}\n{res.stderr}")

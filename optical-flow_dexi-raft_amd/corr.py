@@ -357,30 +357,38 @@ class CorrBlock:
 
     def _launch_build(self, fmap1, fmap2, grad=False):
         """One build launch into this block's pyramid buffer.  Returns the operand
-        tensors the kernel read and the status."""
+        tensors the kernel read and the status.
+
+        f32 fmaps get a workspace from torch's caching allocator (freed when the
+        build's stream work is done) for the pre-split build
+        (``dxr_corr_pyramid_build_ws``: operands scaled and split into f16 pairs
+        once, then moved by LDS-DMA)."""
         B, D, H, W = self._geom
         lib = nat.load()
+        nbytes = lib.dxr_build_workspace_bytes(self._in_dt, B, D, H, W)
+        ws = torch.empty(max(nbytes, 0), dtype=torch.uint8, device=self._device) \
+            if nbytes > 0 else None
+
+        def launch(f1, f2, layout):
+            with _Launch(self._device):
+                return lib.dxr_corr_pyramid_build_ws(
+                    f1.data_ptr(), f2.data_ptr(), self._in_dt, layout, B, D, H, W,
+                    self.num_levels, _sqrt_dim(D), self._buf.data_ptr(), self._pyr_dt,
+                    nat.DXR_BUILD_AUTO, nat.ptr(ws), max(nbytes, 0), nat.stream_of(f1))
+
         st = nat.DXR_EUNSUPPORTED
         if not grad and _channels_last(fmap1) and _channels_last(fmap2):
             # channels-last fmaps (SURVEY §8(f) row 4): read in place by the
-            # build's NHWC operand loads (f32: the split build, bf16: the two-block
-            # bf16 build), no layout pass
+            # build's NHWC operand loads (f32: the pre-split pass, bf16: the
+            # two-block bf16 build), no layout pass
             f1, f2 = fmap1, fmap2
-            with _Launch(self._device):
-                st = lib.dxr_corr_pyramid_build(
-                    f1.data_ptr(), f2.data_ptr(), self._in_dt, nat.DXR_NHWC, B, D, H, W,
-                    self.num_levels, _sqrt_dim(D), self._buf.data_ptr(), self._pyr_dt,
-                    nat.DXR_BUILD_AUTO, nat.stream_of(f1))
+            st = launch(f1, f2, nat.DXR_NHWC)
         if st == nat.DXR_EUNSUPPORTED:
             if grad:
                 f1, f2 = fmap1.contiguous(), fmap2.contiguous()   # tracked by autograd
             else:
                 f1, f2 = _nchw(fmap1), _nchw(fmap2)
-            with _Launch(self._device):
-                st = lib.dxr_corr_pyramid_build(
-                    f1.data_ptr(), f2.data_ptr(), self._in_dt, nat.DXR_NCHW, B, D, H, W,
-                    self.num_levels, _sqrt_dim(D), self._buf.data_ptr(), self._pyr_dt,
-                    nat.DXR_BUILD_AUTO, nat.stream_of(f1))
+            st = launch(f1, f2, nat.DXR_NCHW)
         return f1, f2, st
 
     @property

@@ -1209,6 +1209,416 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
   paged_epilogue<OT, EX>(acc, reinterpret_cast<float*>(smem), pyr, g, pc.page, wave, lane);
 }
 
+// ---------------------------------------------------------------------------
+// Round 3: the f32 build as a pure f16 GEMM on pre-split operands.
+//
+// (1) split_pairs_kernel, once per build: every pixel's f32 channel vector is
+//     scaled by a power of two 2^s (s = 14 - e for max_k |x| = f 2^e, f in
+//     [0.5, 1), so |x 2^s| < 2^14) and split into an f16 pair
+//     x 2^s = hi + 2^-11 lo (hi = RNE_f16(x 2^s), lo = RNE_f16((x 2^s - hi) 2^11),
+//     split2h_mix's single rounding).  The scaling is exact, so the pair keeps
+//     <= 2^-22 |x| of every element whose magnitude is within 2^-10 of its pixel's
+//     max (and <= 2^-36 max below that) whatever the fmaps' scale — the r02 build
+//     split unscaled values and lost precision below |x| ~ 2^-14.
+//     Output per pair: SP [D/16][N][hi 16 k | lo 16 k] f16 (64 B per pixel and
+//     16-channel block) and E [N] int32 exponents s.  A pixel with a non-finite
+//     channel keeps s = 0: its inf/NaN reaches the accumulators and the build
+//     recomputes those pages from the f32 operands (three-way bf16 split).
+// (2) corr_build_dma_kernel: the K loop moves operands only by LDS-DMA
+//     (buffer_load ... lds, 16 B per lane) into a 3-stage ring — 16 KB per
+//     16-k step: each wave's 32 queries (2 KB, contiguous in SP) and the 8x16
+//     target tile (8 tile rows of 1 KB) — so no VGPRs are held by loads in
+//     flight and no VALU splits in the loop: per step a wave waits for its own
+//     DMAs of the step (vmcnt), one barrier publishes the tile, then 10
+//     conflict-free ds_read_b128 and 12 f16 MFMAs (hi*hi into acc, hi*lo and
+//     lo*hi into acc2, as the r02 split build).  The epilogue combines
+//     acc + 2^-11 acc2, undoes both pixels' scales (ldexp by -(s_q + s_t)) and
+//     writes the paged pyramid as before.
+// LDS image rows are 64 B (hi k0-7, hi k8-15, lo k0-7, lo k8-15 in 16-B slots);
+// the slots of a row are XOR-permuted by a row key so that every 16-lane group
+// of a ds_read_b128 hits 16 distinct bank slots; the DMA writes lane-linearly,
+// so each lane fetches the logical slot its physical slot holds (the source
+// side of the permutation).  Query rows: key (row >> 2) & 3 (lanes read rows
+// j = lane & 31); target rows (LDS row = tile row * 16 + tile col): key
+// ((row >> 2) & 1) | ((row >> 3) & 2) (MFMA row j reads tile row 2t + ((j>>2)&1),
+// col (j & 3) + 4 (j >> 3)).
+// ---------------------------------------------------------------------------
+constexpr int SPLIT_S_TOP = 14;          // |x 2^s| < 2^SPLIT_S_TOP
+constexpr int DMA_RING = 3;              // ring stages (k16 steps in LDS)
+constexpr int DMA_STAGE = 16384;         // bytes per stage: 4 x 2 KB queries + 8 KB tile
+constexpr int DMA_TILE = 8192;           // byte offset of the tile within a stage
+
+__device__ __forceinline__ int pixel_scale(float m, bool finite) {
+  if (!finite || !(m > 0.f)) return 0;
+  int e;
+  (void)__builtin_frexpf(m, &e);
+  const int s = SPLIT_S_TOP - e;
+  return s < -125 ? -125 : (s > 125 ? 125 : s);
+}
+
+// Split 16 consecutive channels of one pixel (already scaled) into the 64-B
+// SP record: hi 16 f16 then lo 16 f16.
+__device__ __forceinline__ void store_pair_block(uint4* dst, const float (&x)[16]) {
+  uint32_t h[8], l[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const Split2 p = split2h_mix(x[2 * e], x[2 * e + 1]);
+    h[e] = p.h;
+    l[e] = p.l;
+  }
+  dst[0] = make_uint4(h[0], h[1], h[2], h[3]);
+  dst[1] = make_uint4(h[4], h[5], h[6], h[7]);
+  dst[2] = make_uint4(l[0], l[1], l[2], l[3]);
+  dst[3] = make_uint4(l[4], l[5], l[6], l[7]);
+}
+
+// One thread per (pixel, pair, fmap): grid (ceil(N / 256), B, 2).  NCHW reads
+// are coalesced along pixels; NHWC threads read their pixel's channels as float4.
+template <bool NHWC>
+__global__ __launch_bounds__(256) void split_pairs_kernel(const float* __restrict__ f1,
+                                                          const float* __restrict__ f2,
+                                                          uint4* __restrict__ sp1,
+                                                          uint4* __restrict__ sp2,
+                                                          int* __restrict__ e1, int* __restrict__ e2,
+                                                          int D, int N) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= N) return;
+  const int b = blockIdx.y;
+  const float* src = (blockIdx.z == 0 ? f1 : f2) + (long long)b * D * N;
+  uint4* sp = (blockIdx.z == 0 ? sp1 : sp2) + (long long)b * (D / 16) * N * 4;
+  int* ex = (blockIdx.z == 0 ? e1 : e2) + (long long)b * N;
+  const int nkb = D / 16;
+  auto load16 = [&](int kb, float (&x)[16]) {
+    if constexpr (NHWC) {
+      const float4* s4 = reinterpret_cast<const float4*>(src + (long long)p * D + kb * 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float4 v = s4[i];
+        x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) x[i] = src[(long long)(kb * 16 + i) * N + p];
+    }
+  };
+  float m = 0.f;
+  bool finite = true;
+  for (int kb = 0; kb < nkb; ++kb) {
+    float x[16];
+    load16(kb, x);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float a = __builtin_fabsf(x[i]);
+      finite &= a <= 3.40282347e38f;
+      m = a > m ? a : m;
+    }
+  }
+  const int s = pixel_scale(m, finite);
+  ex[p] = s;
+  for (int kb = 0; kb < nkb; ++kb) {
+    float x[16];
+    load16(kb, x);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = __builtin_ldexpf(x[i], s);
+    store_pair_block(sp + ((long long)kb * N + p) * 4, x);
+  }
+}
+
+// The page's K loop on the exact three-way bf16 split from the f32 operands
+// (register staging, as the r02 split build's fallback): pages whose pre-split
+// sums are not finite.  Leaves the f32 sums in acc.
+template <int BV, bool NHWC>
+__device__ __forceinline__ void page_kloop_split3(const float* __restrict__ f1b,
+                                               const float* __restrict__ f2b, const BuildGeom& g,
+                                               int q0, int th0, int tw0, uint16_t* lh,
+                                               f32x16 (&acc)[4]) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(f1b, g.D * g.N);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(f2b, g.D * g.N);
+  const int qa = min(q0 + wave * 32 + (lane & 31), g.N - 1);
+  const uint32_t va = NHWC ? (uint32_t)(qa * g.D + 8 * (lane >> 5)) * 4u
+                           : (uint32_t)(qa + 8 * (lane >> 5) * g.N) * 4u;
+  constexpr int UPR = TW / BV;
+  constexpr int NBS = BKS * NTGT / BV / NT;
+  constexpr int PN = 24;
+  constexpr int PLANE = NHWC ? NTGT * PN : PLANE_S;
+  int bk[NBS], bcol[NBS];
+  uint32_t vb[NBS];
+#pragma unroll
+  for (int s = 0; s < NBS; ++s) {
+    const int idx = tid + NT * s;
+    int r, c;
+    if constexpr (NHWC) {
+      const int p = idx >> 2;
+      r = p >> 4;
+      c = p & 15;
+      bk[s] = 4 * (idx & 3);
+      vb[s] = (uint32_t)(((th0 + r) * g.W + tw0 + c) * g.D + bk[s]) * 4u;
+    } else {
+      r = (idx / UPR) & 7;
+      c = (idx % UPR) * BV;
+      bk[s] = idx / (8 * UPR);
+      vb[s] = (uint32_t)(bk[s] * g.N + (th0 + r) * g.W + tw0 + c) * 4u;
+    }
+    bcol[s] = tgt_col(r, c);
+    if (!(th0 + r < g.H && tw0 + c < g.W)) vb[s] = 0x80000000u;
+  }
+  const int li = lane & 15;
+  const int rd_off = NHWC ? (lane & 31) * PN + 8 * (lane >> 5)
+                          : (li >> 2) * PH + 4 * (li & 3) + 16 * ((lane >> 4) & 1) +
+                                8 * (lane >> 5) * PH;
+  const int tstride = NHWC ? 32 * PN : 32;
+  auto frag = [&](const uint16_t* p) {
+    if constexpr (NHWC) {
+      return *reinterpret_cast<const bf8v*>(p);
+    } else {
+      return __builtin_bit_cast(bf8v, __builtin_shufflevector(tr_read(p), tr_read(p + 4 * PH), 0,
+                                                              1, 2, 3, 4, 5, 6, 7));
+    }
+  };
+  float an[8];
+  float4 bn[NBS];
+  auto load = [&](int k0) {
+    if constexpr (NHWC) {
+      const float4 u = bload4(ra, va, k0 * 4), v = bload4(ra, va, k0 * 4 + 16);
+      an[0] = u.x; an[1] = u.y; an[2] = u.z; an[3] = u.w;
+      an[4] = v.x; an[5] = v.y; an[6] = v.z; an[7] = v.w;
+#pragma unroll
+      for (int s = 0; s < NBS; ++s) bn[s] = bload4(rb, vb[s], k0 * 4);
+    } else {
+      const int rowb = g.N * 4;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) an[e] = bload1(ra, va, (k0 + e) * rowb);
+#pragma unroll
+      for (int s = 0; s < NBS; ++s) {
+        if constexpr (BV == 4) {
+          bn[s] = bload4(rb, vb[s], k0 * rowb);
+        } else {
+          const float2 v = bload2(rb, vb[s], k0 * rowb);
+          bn[s] = make_float4(v.x, v.y, 0.f, 0.f);
+        }
+      }
+    }
+  };
+  s8v ah, am, al;
+  auto split_a = [&]() {
+    uint32_t h[4], m[4], l[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const Split3 x = split3(an[2 * e], an[2 * e + 1]);
+      h[e] = x.h; m[e] = x.m; l[e] = x.l;
+    }
+    ah = __builtin_bit_cast(s8v, make_uint4(h[0], h[1], h[2], h[3]));
+    am = __builtin_bit_cast(s8v, make_uint4(m[0], m[1], m[2], m[3]));
+    al = __builtin_bit_cast(s8v, make_uint4(l[0], l[1], l[2], l[3]));
+  };
+  auto store_b = [&](int buf) {
+    uint16_t* P = lh + buf * 3 * PLANE;
+#pragma unroll
+    for (int s = 0; s < NBS; ++s) {
+      const int o = NHWC ? bcol[s] * PN + bk[s] : bk[s] * PH + bcol[s];
+      const Split3 x = split3(bn[s].x, bn[s].y);
+      if constexpr (BV == 4) {
+        const Split3 z = split3(bn[s].z, bn[s].w);
+        *reinterpret_cast<uint2*>(P + o) = make_uint2(x.h, z.h);
+        *reinterpret_cast<uint2*>(P + PLANE + o) = make_uint2(x.m, z.m);
+        *reinterpret_cast<uint2*>(P + 2 * PLANE + o) = make_uint2(x.l, z.l);
+      } else {
+        *reinterpret_cast<uint32_t*>(P + o) = x.h;
+        *reinterpret_cast<uint32_t*>(P + PLANE + o) = x.m;
+        *reinterpret_cast<uint32_t*>(P + 2 * PLANE + o) = x.l;
+      }
+    }
+  };
+  const int nk = g.D / BKS;
+  load(0);
+  store_b(0);
+  split_a();
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) load((ks + 1) * BKS);
+    const uint16_t* P = lh + buf * 3 * PLANE + rd_off;
+    const bf8v qh = __builtin_bit_cast(bf8v, ah), qm = __builtin_bit_cast(bf8v, am),
+               ql = __builtin_bit_cast(bf8v, al);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const bf8v th = frag(P + t * tstride), tm = frag(P + PLANE + t * tstride),
+                 tl = frag(P + 2 * PLANE + t * tstride);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, ql, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qh, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qm, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh, acc[t], 0, 0, 0);
+    }
+    if (ks + 1 < nk) {
+      store_b(buf ^ 1);
+      split_a();
+    }
+    __syncthreads();
+  }
+}
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// BV / NHWC describe the f32 operands for the fallback path only; the main
+// loop reads the pre-split SP records, which are layout-independent.
+template <typename OT, bool DIV, int BV, bool NHWC>
+__global__ __launch_bounds__(NT, 3) void corr_build_dma_kernel(
+    const float* __restrict__ f1, const float* __restrict__ f2, const uint8_t* __restrict__ sp1,
+    const uint8_t* __restrict__ sp2, const int* __restrict__ ex1, const int* __restrict__ ex2,
+    OT* __restrict__ pyr, BuildGeom g) {
+  constexpr int LDS_RING = DMA_RING * DMA_STAGE;
+  constexpr int LDS_E = WAVES * 16 * P0 * 4;          // epilogue staging bytes
+  constexpr int LDS_F = 2 * 3 * PLANE_S * 2;          // fallback planes (NCHW) bytes
+  static_assert(LDS_E <= LDS_RING && LDS_F <= LDS_RING && 2 * 3 * NTGT * 24 * 2 <= LDS_RING,
+                "epilogue and fallback alias the ring");
+  // one LDS array (cdna_hip_programming.md §5 item 4(a)): ring | target
+  // exponents (128 int) | redo flag
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_RING + NTGT * 4 + 16];
+  int* const sexp = reinterpret_cast<int*>(smem + LDS_RING);
+  int* const redo = reinterpret_cast<int*>(smem + LDS_RING + NTGT * 4);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  // wave-uniform (SGPR): the DMA's LDS base must be, or the compiler emits a
+  // waterfall loop around every buffer_load ... lds
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const PageCoord pc = page_coord<false>(g);
+  const int th0 = pc.tyi * TH, tw0 = pc.txi * TW;
+  const int q0 = pc.qblk * BM;
+  const int b = pc.b;
+  const int j = lane & 31, kh = lane >> 5;
+  const long long spstride = (long long)g.D * g.N * 4;   // SP bytes per pair
+
+  // exponents: the lane's query, the tile's 128 targets (LDS, by tile pixel)
+  const int qj = q0 + wave * 32 + j;
+  const int sq = qj < g.N ? ex1[(long long)b * g.N + qj] : 0;
+  if (tid < NTGT) {
+    const int r = tid >> 4, c = tid & 15;
+    const bool in = th0 + r < g.H && tw0 + c < g.W;
+    sexp[tid] = in ? ex2[(long long)b * g.N + (th0 + r) * g.W + tw0 + c] : 0;
+  }
+  if (tid == 0) *redo = 0;
+
+  const __amdgpu_buffer_rsrc_t rq =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sp1 + b * spstride), (short)0,
+                                        (int)spstride, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rt =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sp2 + b * spstride), (short)0,
+                                        (int)spstride, 0x00020000);
+  // DMA source offsets (fixed over K; the step's offset ks * N * 64 in soffset).
+  // Query instruction i of this wave: LDS rows 16 i + (lane >> 2) of the wave's
+  // 2 KB region; target instruction i: tile row r = 2 wave + i.
+  uint32_t vq[2], vt[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 16 * i + (lane >> 2), ps = lane & 3;
+    const int q = q0 + wave * 32 + row;
+    const int cq = ps ^ ((row >> 2) & 3);
+    vq[i] = q < g.N ? (uint32_t)(q * 64 + 16 * cq) : 0x80000000u;
+    const int r = 2 * wave + i, col = lane >> 2, trow = r * 16 + col;
+    const int ct = ps ^ (((trow >> 2) & 1) | ((trow >> 3) & 2));
+    const int hh = th0 + r, ww = tw0 + col;
+    vt[i] = (hh < g.H && ww < g.W) ? (uint32_t)((hh * g.W + ww) * 64 + 16 * ct) : 0x80000000u;
+  }
+  auto dma = [&](int ks) {
+    unsigned char* st = smem + (ks % DMA_RING) * DMA_STAGE;
+    const int so = ks * g.N * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rq, (lds_void_t*)(st + wave * 2048 + i * 1024), 16, vq[i], so, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rt, (lds_void_t*)(st + DMA_TILE + (2 * wave + i) * 1024), 16, vt[i], so, 0, 0);
+  };
+  // fragment byte offsets within a stage (hi; lo = the other two slots)
+  const int kq = (j >> 2) & 3;
+  const int qh_off = wave * 2048 + j * 64 + 16 * (kh ^ kq);
+  const int ql_off = wave * 2048 + j * 64 + 16 * ((2 + kh) ^ kq);
+  const int trow0 = ((j >> 2) & 1) * 16 + (j & 3) + 4 * (j >> 3);     // tile t adds 32 rows
+  const int kt = ((trow0 >> 2) & 1) | ((trow0 >> 3) & 2);
+  const int th_off = DMA_TILE + trow0 * 64 + 16 * (kh ^ kt);
+  const int tl_off = DMA_TILE + trow0 * 64 + 16 * ((2 + kh) ^ kt);
+
+  f32x16 acc[4], acc2[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = acc2[t][r] = 0.f;
+
+  // exponent loads and LDS writes above must not count against the ring's vmcnt
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int nk = g.D / BKS;
+  dma(0);
+  if (nk > 1) dma(1);
+  for (int ks = 0; ks < nk; ++ks) {
+    // this wave's 4 DMAs of step ks have landed (those of ks + 1 stay in flight);
+    // the barrier publishes every wave's, and orders the ring slot's previous
+    // readers (step ks - 1) before the refill below
+    if (ks + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (ks + 2 < nk) dma(ks + 2);
+    const unsigned char* st = smem + (ks % DMA_RING) * DMA_STAGE;
+    const h8v qh = *reinterpret_cast<const h8v*>(st + qh_off);
+    const h8v ql = *reinterpret_cast<const h8v*>(st + ql_off);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const h8v th = *reinterpret_cast<const h8v*>(st + th_off + t * 2048);
+      const h8v tl = *reinterpret_cast<const h8v*>(st + tl_off + t * 2048);
+      acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc2[t], 0, 0, 0);
+      acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc2[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qh, acc[t], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();   // ring reads done: the LDS is free for reuse
+
+  // combine (one rounding) and vote: a non-finite sum means an operand pixel
+  // was not finite; the page is then recomputed from the f32 operands
+  bool bad = false;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      acc[t][r] = __builtin_fmaf(acc2[t][r], 0x1p-11f, acc[t][r]);
+      bad |= !(__builtin_fabsf(acc[t][r]) <= 3.40282347e38f);
+    }
+  if (bad) *redo = 1;
+  __syncthreads();
+  if (*redo) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    const long long fstride = (long long)g.D * g.N;
+    page_kloop_split3<BV, NHWC>(f1 + b * fstride, f2 + b * fstride, g, q0, th0, tw0,
+                                reinterpret_cast<uint16_t*>(smem), acc);
+  } else {
+    // undo the pixel scales: acc[t][r] is query qj x tile pixel (row 2t + kh, col r)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int4* se = reinterpret_cast<const int4*>(sexp + (2 * t + kh) * 16);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int4 s4 = se[u];
+        acc[t][4 * u + 0] = __builtin_ldexpf(acc[t][4 * u + 0], -(sq + s4.x));
+        acc[t][4 * u + 1] = __builtin_ldexpf(acc[t][4 * u + 1], -(sq + s4.y));
+        acc[t][4 * u + 2] = __builtin_ldexpf(acc[t][4 * u + 2], -(sq + s4.z));
+        acc[t][4 * u + 3] = __builtin_ldexpf(acc[t][4 * u + 3], -(sq + s4.w));
+      }
+    }
+  }
+  __syncthreads();   // exponent reads / fallback planes done before the staging reuse
+  scale_acc<DIV>(acc, g);
+  paged_epilogue<OT, 1 | 4>(acc, reinterpret_cast<float*>(smem), pyr, g, pc.page, wave, lane);
+}
+
 // Floor-mode 2x2 average pool of one pyramid level into the next, for levels
 // beyond the fused four (any layout, addressed through dxr::cell_index).
 __global__ __launch_bounds__(256) void pool_level_kernel(float* __restrict__ pyr,
@@ -1466,6 +1876,37 @@ int launch_split(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, 
   return dxr::launch_status();
 }
 
+// Pre-split + LDS-DMA f32 build (round 3): workspace = SP1 | SP2 | E1 | E2.
+long long align256(long long x) { return (x + 255) & ~255LL; }
+long long dma_workspace_bytes(long long B, long long D, long long N) {
+  return 2 * align256(B * D * N * 4) + 2 * align256(B * N * 4);
+}
+
+template <typename OT, int BV, bool NHWC>
+int launch_dma(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, int B, void* ws,
+               hipStream_t stream) {
+  const dim3 grid = build_grid(g, B);
+  if (grid.y > 65535) return DXR_EINVAL;
+  const long long N = g.N, spb = align256((long long)B * g.D * N * 4), eb = align256((long long)B * N * 4);
+  uint8_t* w = static_cast<uint8_t*>(ws);
+  uint8_t* sp1 = w;
+  uint8_t* sp2 = w + spb;
+  int* e1 = reinterpret_cast<int*>(w + 2 * spb);
+  int* e2 = reinterpret_cast<int*>(w + 2 * spb + eb);
+  hipLaunchKernelGGL((split_pairs_kernel<NHWC>), dim3((unsigned)((N + 255) / 256), (unsigned)B, 2),
+                     dim3(256), 0, stream, f1, f2, reinterpret_cast<uint4*>(sp1),
+                     reinterpret_cast<uint4*>(sp2), e1, e2, g.D, g.N);
+  int st = dxr::launch_status();
+  if (st != DXR_OK) return st;
+  if (g.recip == 0.f)
+    hipLaunchKernelGGL((corr_build_dma_kernel<OT, true, BV, NHWC>), grid, dim3(NT), 0, stream, f1,
+                       f2, sp1, sp2, e1, e2, pyr, g);
+  else
+    hipLaunchKernelGGL((corr_build_dma_kernel<OT, false, BV, NHWC>), grid, dim3(NT), 0, stream, f1,
+                       f2, sp1, sp2, e1, e2, pyr, g);
+  return dxr::launch_status();
+}
+
 // f32 fmaps: the split build when its layout conditions hold (D % 16 == 0;
 // float4 target units for W % 4 == 0, float2 units for even W), else — or on
 // request (DXR_BUILD_EXACT_F32) — the exact-f32 MFMA build.
@@ -1525,10 +1966,11 @@ extern "C" int dxr_avg_pool2x2(const float* in, float* out, int64_t planes, int6
   return launch_avg_pool(in, out, planes, (int)H, (int)W, stream);
 }
 
-extern "C" int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int in_dtype,
-                                      int fmap_layout, int64_t B, int64_t D, int64_t H,
-                                      int64_t W, int num_levels, float divisor, void* pyramid,
-                                      int pyr_dtype, int algo, hipStream_t stream) {
+namespace {
+int pyramid_build(const void* fmap1, const void* fmap2, int in_dtype, int fmap_layout, int64_t B,
+                  int64_t D, int64_t H, int64_t W, int num_levels, float divisor, void* pyramid,
+                  int pyr_dtype, int algo, void* workspace, int64_t workspace_bytes,
+                  hipStream_t stream) {
   dxr::Levels L;
   if (!dxr::make_levels(B, H, W, num_levels, &L)) return DXR_EINVAL;
   if (fmap_layout != DXR_NCHW && fmap_layout != DXR_NHWC) return DXR_EINVAL;
@@ -1539,8 +1981,34 @@ extern "C" int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int 
   if (L.n > dxr::TILED_LEVELS && pyr_dtype != DXR_F32) return DXR_EUNSUPPORTED;
   if (algo == DXR_BUILD_EXACT_F32 && in_dtype != DXR_F32) return DXR_EUNSUPPORTED;
   const BuildGeom g = make_geom(D, H, W, divisor, L);
-  int st;
-  if (fmap_layout == DXR_NHWC && in_dtype == DXR_BF16) {
+  int st = PROCEED;
+  // f32 operands with a workspace: pre-split f16 pairs + the LDS-DMA build,
+  // where the split build applies (its layout conditions select the f32
+  // fallback's operand form).
+  const bool dma_ok = in_dtype == DXR_F32 && algo == DXR_BUILD_AUTO && D % 16 == 0 &&
+                      D * H * W < (1LL << 29) && workspace != nullptr && aligned16(workspace) &&
+                      workspace_bytes >= dma_workspace_bytes(B, D, H * W) && aligned16(pyramid);
+  if (dma_ok) {
+    const float* f1 = static_cast<const float*>(fmap1);
+    const float* f2 = static_cast<const float*>(fmap2);
+    float* pf = static_cast<float*>(pyramid);
+    uint16_t* ph = static_cast<uint16_t*>(pyramid);
+    const bool f32p = pyr_dtype == DXR_F32;
+    if (fmap_layout == DXR_NHWC) {
+      if (W % 2 == 0 && aligned16(f1) && aligned16(f2))
+        st = f32p ? launch_dma<float, 4, true>(f1, f2, pf, g, (int)B, workspace, stream)
+                  : launch_dma<uint16_t, 4, true>(f1, f2, ph, g, (int)B, workspace, stream);
+    } else if (W % 4 == 0 && aligned16(f1) && aligned16(f2)) {
+      st = f32p ? launch_dma<float, 4, false>(f1, f2, pf, g, (int)B, workspace, stream)
+                : launch_dma<uint16_t, 4, false>(f1, f2, ph, g, (int)B, workspace, stream);
+    } else if (W % 2 == 0 && ((uintptr_t)f1 % 8) == 0 && ((uintptr_t)f2 % 8) == 0) {
+      st = f32p ? launch_dma<float, 2, false>(f1, f2, pf, g, (int)B, workspace, stream)
+                : launch_dma<uint16_t, 2, false>(f1, f2, ph, g, (int)B, workspace, stream);
+    }
+  }
+  if (st != PROCEED) {
+    // done by the DMA build
+  } else if (fmap_layout == DXR_NHWC && in_dtype == DXR_BF16) {
     // channels-last bf16 operands (the bf16 mode's encoders, core/extractor.py:168-192):
     // the two-block bf16 build's NHWC form, bit-identical to the NCHW build;
     // D % 32 == 0 (whole 32-channel stages) and 16-byte aligned pixels
@@ -1593,6 +2061,31 @@ extern "C" int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int 
     if (st != DXR_OK) return st;
   }
   return DXR_OK;
+}
+}  // namespace
+
+extern "C" int64_t dxr_build_workspace_bytes(int in_dtype, int64_t B, int64_t D, int64_t H,
+                                             int64_t W) {
+  if (B < 0 || D < 1 || H < 1 || W < 1 || H * W > (1LL << 30)) return -1;
+  if (in_dtype != DXR_F32 || D % 16 != 0) return 0;
+  return dma_workspace_bytes(B, D, H * W);
+}
+
+extern "C" int dxr_corr_pyramid_build_ws(const void* fmap1, const void* fmap2, int in_dtype,
+                                         int fmap_layout, int64_t B, int64_t D, int64_t H,
+                                         int64_t W, int num_levels, float divisor, void* pyramid,
+                                         int pyr_dtype, int algo, void* workspace,
+                                         int64_t workspace_bytes, hipStream_t stream) {
+  return pyramid_build(fmap1, fmap2, in_dtype, fmap_layout, B, D, H, W, num_levels, divisor,
+                       pyramid, pyr_dtype, algo, workspace, workspace_bytes, stream);
+}
+
+extern "C" int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int in_dtype,
+                                      int fmap_layout, int64_t B, int64_t D, int64_t H,
+                                      int64_t W, int num_levels, float divisor, void* pyramid,
+                                      int pyr_dtype, int algo, hipStream_t stream) {
+  return pyramid_build(fmap1, fmap2, in_dtype, fmap_layout, B, D, H, W, num_levels, divisor,
+                       pyramid, pyr_dtype, algo, nullptr, 0, stream);
 }
 
 extern "C" int dxr_corr_volume(const void* fmap1, const void* fmap2, int in_dtype, int64_t B,

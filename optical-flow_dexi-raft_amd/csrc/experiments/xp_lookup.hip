@@ -1,0 +1,173 @@
+// Experiments target only (libdexiraft_corr_exp.so, build.py --experiments):
+// timing ablations and layout variants of the lookup (csrc/corr_lookup.hip).
+// Never loaded by the package.
+#include "../corr_lookup.hip"
+
+namespace {
+
+// XP bits: 0 skip the window gathers, 1 skip phase 2 (return after the gather),
+// 2 return after phase 0, 3 synthetic coordinates (the grid: no coords loads),
+// 8 record a per-workgroup timeline (s_memrealtime at start, after phase 0,
+// after the gather, at the end; plus the hardware id) into `trace`.
+template <int R, typename PT, int XP>
+__global__ __launch_bounds__(512) void xp_lookup_kernel(const PT* __restrict__ pyr,
+                                                        const float* __restrict__ coords,
+                                                        float* __restrict__ out, LookupGeom g,
+                                                        unsigned long long* __restrict__ trace) {
+  using C = WideCfg<R, 512>;
+  constexpr int RD = C::RD, RS = C::RS, K = C::K, QB = C::QB;
+  __shared__ __attribute__((aligned(16))) float cells[QB * C::QS];
+  __shared__ float4 xs[RD * QB];
+  __shared__ float4 ys[RD * QB];
+  __shared__ int2 org[QB];
+  const unsigned long long t0 = (XP & 256) ? __builtin_amdgcn_s_memrealtime() : 0ull;
+
+  const int tid = threadIdx.x;
+  const int l = blockIdx.y, b = blockIdx.z;
+  const int q0 = blockIdx.x * QB;
+  const LevelAddr A = g.lv[l];
+
+  if constexpr ((XP & 8) != 0) {
+    // synthetic coordinates: the identity grid scaled, no global loads
+    using CC = WideCfg<R, 512>;
+    const int slot = tid;
+    if (slot < QB * CC::G) {
+      const int j = slot & (CC::G - 1), qq = slot >> CC::LG, q = q0 + qq;
+      const int W1 = 128;
+      const float cx = (float)(q % W1) + 0.37f, cy = (float)(q / W1) + 0.61f;
+      const float inv = 1.f / (float)(1 << l);
+      const float wm1 = (float)(A.w - 1), hm1 = (float)(A.h - 1);
+      const float ux = sample_coord(__fadd_rn(cx * inv, (float)(j - R)), wm1, wm1 / 2.f);
+      const float uy = sample_coord(__fadd_rn(cy * inv, (float)(j - R)), hm1, hm1 / 2.f);
+      const float flx = floorf(ux), fly = floorf(uy);
+      const bool act = j < RD;
+      int mx = act ? (int)flx - j : 0x7fffffff, my = act ? (int)fly - j : 0x7fffffff;
+#pragma unroll
+      for (int o = 1; o < CC::G; o <<= 1) {
+        mx = min(mx, __shfl_xor(mx, o));
+        my = min(my, __shfl_xor(my, o));
+      }
+      const bool far = mx + CC::WD <= 0 || mx >= A.w || my + CC::WD <= 0 || my >= A.h;
+      if (j == 0) org[qq] = far ? make_int2(FAR_ORIGIN, FAR_ORIGIN) : make_int2(mx, my);
+      if (act) {
+        const float fx = __fsub_rn(ux, flx), fy = __fsub_rn(uy, fly);
+        const int col = far ? 0 : (int)flx - (mx & ~3);
+        const int row = far ? 0 : ((int)fly - my) * RS;
+        xs[j * QB + qq] = make_float4(__int_as_float(col), fx, __fsub_rn(1.f, fx), 0.f);
+        ys[j * QB + qq] = make_float4(__int_as_float(row), fy, __fsub_rn(1.f, fy), 0.f);
+      }
+    }
+  } else {
+    wide_phase0<R, 512>(coords, g, A, b, l, q0, tid, xs, ys, org);
+  }
+  __syncthreads();
+  const unsigned long long t1 = (XP & 256) ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  auto record = [&](unsigned long long t2, unsigned long long t3) {
+    if constexpr ((XP & 256) != 0) {
+      if (tid < 5) {
+        const long long wg = ((long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+        const unsigned long long hw = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+                                      ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(20 | (15 << 11)) << 32);
+        const unsigned long long v = tid == 0 ? t0 : tid == 1 ? t1 : tid == 2 ? t2 : tid == 3 ? t3 : hw;
+        trace[wg * 5 + tid] = v;
+      }
+    }
+  };
+  if constexpr ((XP & 4) != 0) {
+    if (xs[tid % (RD * QB)].y == 1234.5f) out[tid] = 0.f;
+    record(t1, t1);
+    return;
+  }
+
+  if constexpr ((XP & 1) == 0) {
+    const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
+    const int qb0 = q0 & ((1 << A.lqb) - 1);
+    if (A.lth == 30)
+      gather_windows<R, 512, 1, PT>(base, qb0, A, org, cells, q0, g.N, tid);
+    else if (A.tw >= 4)
+      gather_windows<R, 512, 4, PT>(base, qb0, A, org, cells, q0, g.N, tid);
+    else if (A.tw == 2)
+      gather_windows<R, 512, 2, PT>(base, qb0, A, org, cells, q0, g.N, tid);
+    else
+      gather_windows<R, 512, 1, PT>(base, qb0, A, org, cells, q0, g.N, tid);
+  }
+  __syncthreads();
+  const unsigned long long t2 = (XP & 256) ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  if constexpr ((XP & 2) != 0) {
+    if (cells[tid] == 1234.5f) out[tid] = 0.f;
+    record(t2, t2);
+    return;
+  }
+
+  const int qq = tid % QB, cls = tid / QB;
+  if (q0 + qq < g.N) {
+    const float* cq = cells + qq * C::QS;
+    float* ob = out + ((long long)b * g.cout + (long long)l * K) * g.N + q0 + qq;
+    for (int k = cls; k < K; k += C::NCLS) {
+      const int ox = k / RD, oy = k - ox * RD;
+      const float4 xd = xs[ox * QB + qq], yd = ys[oy * QB + qq];
+      const float* p = cq + __float_as_int(yd.x) + __float_as_int(xd.x);
+      const float v00 = p[0], v01 = p[1], v10 = p[RS], v11 = p[RS + 1];
+      const float nw = __fmul_rn(yd.z, xd.z), ne = __fmul_rn(yd.z, xd.y);
+      const float sw = __fmul_rn(yd.y, xd.z), se = __fmul_rn(yd.y, xd.y);
+      float r = __fmul_rn(nw, v00);
+      r = __builtin_fmaf(ne, v01, r);
+      r = __builtin_fmaf(sw, v10, r);
+      r = __builtin_fmaf(se, v11, r);
+      __hip_atomic_store(ob + (unsigned)(k * g.N), r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if constexpr ((XP & 256) != 0) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    record(t2, __builtin_amdgcn_s_memrealtime());
+  }
+}
+
+template <int XP, typename PT>
+int xp_launch(const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
+              unsigned long long* trace, hipStream_t stream) {
+  using W = WideCfg<4>;
+  const dim3 grid((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
+  hipLaunchKernelGGL((xp_lookup_kernel<4, PT, XP>), grid, dim3(512), 0, stream, pyr, coords, out,
+                     g, trace);
+  return dxr::launch_status();
+}
+
+template <typename PT>
+int xp_dispatch(int xp, const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
+                unsigned long long* trace, hipStream_t stream) {
+  switch (xp) {
+    case 0: return xp_launch<0>(pyr, coords, out, g, B, trace, stream);
+    case 1: return xp_launch<1>(pyr, coords, out, g, B, trace, stream);
+    case 2: return xp_launch<2>(pyr, coords, out, g, B, trace, stream);
+    case 4: return xp_launch<4>(pyr, coords, out, g, B, trace, stream);
+    case 8: return xp_launch<8>(pyr, coords, out, g, B, trace, stream);
+    case 12: return xp_launch<12>(pyr, coords, out, g, B, trace, stream);
+    case 256: return xp_launch<256>(pyr, coords, out, g, B, trace, stream);
+    case 258: return xp_launch<258>(pyr, coords, out, g, B, trace, stream);
+    case 260: return xp_launch<260>(pyr, coords, out, g, B, trace, stream);
+    default: return DXR_EINVAL;
+  }
+}
+
+}  // namespace
+
+// Variant `xp` of the radius-4 lookup (see xp_lookup_kernel); trace: 5 x u64
+// per workgroup when xp has bit 8.
+extern "C" int dxr_xp_lookup(const void* pyramid, int pyr_dtype, int64_t B, int64_t H, int64_t W,
+                             int num_levels, const float* coords, float* out, int xp,
+                             unsigned long long* trace, hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, num_levels, &L) || num_levels > 4) return DXR_EINVAL;
+  LookupGeom g;
+  g.N = (int)(H * W);
+  g.levels = num_levels;
+  g.cout = num_levels * 81;
+  for (int l = 0; l < L.n; ++l) g.lv[l] = level_addr(L.lay[l]);
+  if (pyr_dtype == DXR_F32)
+    return xp_dispatch(xp, static_cast<const float*>(pyramid), coords, out, g, (int)B, trace,
+                       stream);
+  return xp_dispatch(xp, static_cast<const uint16_t*>(pyramid), coords, out, g, (int)B, trace,
+                     stream);
+}

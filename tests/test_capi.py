@@ -37,6 +37,7 @@ def test_header_declares_the_documented_entry_points():
     assert declared() == {
         "dxr_abi_version", "dxr_status_string", "dxr_last_hip_error", "dxr_pyramid_numel",
         "dxr_pyramid_level_offset", "dxr_corr_pyramid_build", "dxr_corr_lookup",
+        "dxr_build_workspace_bytes", "dxr_corr_pyramid_build_ws",
         "dxr_avg_pool2x2", "dxr_alt_corr_forward", "dxr_alt_corr_lookup", "dxr_corr_volume",
         "dxr_pyramid_unpack", "dxr_pyramid_pack",
         "dxr_corr_lookup_backward", "dxr_pyramid_backward", "dxr_alt_corr_backward",
@@ -65,7 +66,7 @@ def test_library_is_gfx950_code(nat):
 
 def test_abi_version_and_status_strings(nat):
     lib = nat.load()
-    assert lib.dxr_abi_version() == nat.ABI_VERSION == 5
+    assert lib.dxr_abi_version() == nat.ABI_VERSION == 6
     assert lib.dxr_status_string(0) == b"ok"
     assert lib.dxr_status_string(1) == b"invalid argument"
     assert lib.dxr_status_string(2) == b"unsupported by this build"
@@ -192,3 +193,23 @@ def test_check_maps_status_to_reference_exceptions(nat):
         nat.check(1, "x")
     with pytest.raises(NotImplementedError):
         nat.check(2, "x")
+
+
+def test_build_workspace_bytes(nat):
+    """The pre-split f32 build's workspace (ABI 6): two f16-pair operand copies
+    (4 B per f32 element) and two int32 exponents per pixel, each 256-B aligned;
+    bf16 fmaps and D % 16 != 0 need none; bad geometry is -1."""
+    lib = nat.load()
+    al = lambda x: (x + 255) // 256 * 256   # noqa: E731
+    for B, D, H, W in ((1, 256, 55, 128), (8, 256, 47, 156), (2, 64, 13, 19)):
+        N = H * W
+        assert lib.dxr_build_workspace_bytes(nat.DXR_F32, B, D, H, W) == \
+            2 * al(B * D * N * 4) + 2 * al(B * N * 4)
+    assert lib.dxr_build_workspace_bytes(nat.DXR_BF16, 1, 256, 55, 128) == 0
+    assert lib.dxr_build_workspace_bytes(nat.DXR_F32, 1, 24, 55, 128) == 0
+    assert lib.dxr_build_workspace_bytes(nat.DXR_F32, -1, 256, 55, 128) == -1
+    P = 1 << 12
+    bw = lib.dxr_corr_pyramid_build_ws
+    # validation is the plain build's: same statuses before any launch
+    assert bw(P, P, 0, 0, 1, 0, 8, 8, 4, 16.0, P, 0, 0, P, 1 << 20, None) == nat.DXR_EINVAL
+    assert bw(P, P, 0, 0, 0, 256, 8, 8, 4, 16.0, None, 0, 0, None, 0, None) == nat.DXR_OK

@@ -177,18 +177,25 @@ def test_batch_independence_and_determinism(dx):
 
 def test_linearity(dx):
     """Scaling fmap1 by 2 scales the pyramid by 2 (the reference's f32 matmul does
-    so bit for bit).  Bit for bit on the exact-f32 build; on the default split
-    build to within 2^-20 of max|.|: its f16 pair split rounds residuals below
-    2^-14 on f16's fixed subnormal grid, which doubling does not commute with."""
+    so bit for bit).  Bit for bit on the default (pre-split) build, whose
+    per-pixel power-of-two scaling absorbs the factor, and on the exact-f32
+    build; the r02 workspace-less split build (unscaled f16 pairs) only to within
+    2^-20 of max|.|: its residuals below 2^-14 round on f16's fixed subnormal
+    grid, which doubling does not commute with."""
     f1, f2 = _pair(H=21, W=36, seed=11)
     a = dx.CorrBlock(f1, f2)
     b = dx.CorrBlock(2.0 * f1, f2)
+    c = dx.CorrBlock(f1, 0.25 * f2)
     for lvl in range(4):
-        d = (b.corr_pyramid[lvl] - 2.0 * a.corr_pyramid[lvl]).abs().max().item()
-        assert d <= 2.0 ** -20 * a.corr_pyramid[lvl].abs().max().item(), (lvl, d)
+        assert torch.equal(b.corr_pyramid[lvl], 2.0 * a.corr_pyramid[lvl]), lvl
+        assert torch.equal(c.corr_pyramid[lvl], 0.25 * a.corr_pyramid[lvl]), lvl
     ea, eb = _build_exact_f32(f1, f2), _build_exact_f32(2.0 * f1, f2)
     for lvl in range(4):
         assert torch.equal(eb[lvl], 2.0 * ea[lvl])
+    sa, sb = _build_no_workspace(f1, f2), _build_no_workspace(2.0 * f1, f2)
+    for lvl in range(4):
+        d = (sb[lvl] - 2.0 * sa[lvl]).abs().max().item()
+        assert d <= 2.0 ** -20 * sa[lvl].abs().max().item(), (lvl, d)
 
 
 def test_fused_pooling_matches_torch_avg_pool(dx):
@@ -431,16 +438,47 @@ def test_split_build_overflow_fallback(dx):
     assert (lv0[rest] - base[0][rest]).abs().max().item() <= 1e-5 * base[0].abs().max().item()
 
 
-def _build_exact_f32(f1: torch.Tensor, f2: torch.Tensor, num_levels: int = 4):
+@pytest.mark.parametrize("W,layout", [(62, "nchw"), (32, "nhwc"), (44, "nchw")])
+def test_prescaled_build_nonfinite_fallback_forms(dx, W, layout):
+    """Pages that see an inf/NaN operand are recomputed from the f32 operands on
+    the three-way bf16 split, in every operand form of that fallback (float2 /
+    float4 NCHW target units, NHWC): NaN where the reference's f32 matmul has
+    NaN, inf x finite = inf, and f32 class everywhere else."""
+    H = 20
+    f1, f2 = _pair(H=H, W=W, seed=181)
+    f1, f2 = f1.clone(), f2.clone()
+    f2[0, 3, 4, 5] = float("nan")                # target (4, 5): NaN for every query
+    f1[0, 9, 2, 7] = float("inf")                # query (2, 7): +-inf / NaN row
+    base = _build_exact_f32(f1, f2)
+    if layout == "nhwc":
+        f1 = f1.contiguous(memory_format=torch.channels_last)
+        f2 = f2.contiguous(memory_format=torch.channels_last)
+    cb = dx.CorrBlock(f1, f2)
+    got, ref = cb.corr_pyramid[0][:, 0], base[0]
+    assert torch.equal(torch.isnan(got), torch.isnan(ref))
+    assert torch.equal(torch.isinf(got), torch.isinf(ref))
+    fin = torch.isfinite(ref)
+    assert (got[fin] - ref[fin]).abs().max().item() <= 1e-5 * ref[fin].abs().max().item()
+    for lvl in range(1, 4):
+        g, r = cb.corr_pyramid[lvl][:, 0], base[lvl]
+        assert torch.equal(torch.isnan(g), torch.isnan(r)), lvl
+        fin = torch.isfinite(r)
+        assert (g[fin] - r[fin]).abs().max().item() <= 1e-5 * r[fin].abs().max().item(), lvl
+
+
+def _build_exact_f32(f1: torch.Tensor, f2: torch.Tensor, num_levels: int = 4,
+                     algo: int | None = None):
     """The exact-f32 MFMA build (DXR_BUILD_EXACT_F32) through the C-ABI, as
-    reference-layout levels [B*H*W, H_l, W_l]."""
+    reference-layout levels [B*H*W, H_l, W_l] (``algo`` DXR_BUILD_AUTO: the
+    workspace-less entry point's f16-pair split build of round 2)."""
     from dexiraft_amd import _native as nat
     lib = nat.load()
     B, D, H, W = (int(v) for v in f1.shape)
     buf = torch.empty(lib.dxr_pyramid_numel(B, H, W, num_levels), device=DEV)
     st = lib.dxr_corr_pyramid_build(f1.data_ptr(), f2.data_ptr(), nat.DXR_F32, nat.DXR_NCHW, B, D,
                                     H, W, num_levels, float(np.sqrt(np.float32(D))),
-                                    buf.data_ptr(), nat.DXR_F32, nat.DXR_BUILD_EXACT_F32,
+                                    buf.data_ptr(), nat.DXR_F32,
+                                    nat.DXR_BUILD_EXACT_F32 if algo is None else algo,
                                     nat.stream_of(f1))
     assert st == 0
     out, h, w = [], H, W
@@ -452,6 +490,51 @@ def _build_exact_f32(f1: torch.Tensor, f2: torch.Tensor, num_levels: int = 4):
                                       t.data_ptr(), nat.stream_of(t)) == 0
         out.append(t)
     return out
+
+
+def _build_no_workspace(f1, f2, num_levels=4):
+    from dexiraft_amd import _native as nat
+    return _build_exact_f32(f1, f2, num_levels, algo=nat.DXR_BUILD_AUTO)
+
+
+@pytest.mark.parametrize("scale", [1.0, 1e-4, 1e-6, 3e3])
+def test_prescaled_split_build_accuracy_is_scale_free(dx, scale):
+    """the f16 pair split loses precision where a residual falls on
+    f16's subnormal grid.  The default build scales each pixel by a power of two
+    first, so its error relative to max|ref| does not grow as the fmaps shrink:
+    within 2x the exact-f32 MFMA build's error against float64 at every scale
+    (fnet-like fmaps x scale, Sintel shape)."""
+    H, W = 55, 128
+    f1 = (dg.fmap(151, 1, 256, H, W, "fnet") * np.float32(scale)).astype(np.float32)
+    f2 = (dg.fmap(152, 1, 256, H, W, "fnet") * np.float32(scale)).astype(np.float32)
+    pyr = oracle.corr_pyramid(f1, f2, 4, np.float64)
+    base = _build_exact_f32(_t(f1), _t(f2))
+    cb = dx.CorrBlock(_t(f1), _t(f2))
+    for lvl in range(4):
+        got = cb.corr_pyramid[lvl][:, 0].cpu().numpy()
+        e_ws = np.abs(got - pyr[lvl]).max()
+        e_mfma = np.abs(base[lvl].cpu().numpy() - pyr[lvl]).max()
+        m = np.abs(pyr[lvl]).max()
+        print(f"scale {scale:g} level {lvl}: max|err| pre-split {e_ws:.3e}, f32 mfma "
+              f"{e_mfma:.3e}, max|ref| {m:.3e}")
+        assert e_ws <= 2 * e_mfma + 1e-7 * m
+
+
+def test_prescaled_build_agrees_with_workspaceless_build(dx):
+    """The pre-split build (workspace) and the r02 split build (no workspace,
+    dxr_corr_pyramid_build) agree to f32 rounding; NCHW and NHWC operands give
+    the pre-split build's pyramid bit for bit."""
+    from dexiraft_amd import _native as nat
+    f1, f2 = _pair(B=2, H=30, W=44, seed=171, dist="fnet")
+    ref = _build_no_workspace(f1, f2)
+    cb = dx.CorrBlock(f1, f2)
+    for lvl in range(4):
+        a, b = cb.corr_pyramid[lvl][:, 0], ref[lvl]
+        assert (a - b).abs().max().item() <= 2e-6 * b.abs().max().item(), lvl
+    cl = dx.CorrBlock(f1.contiguous(memory_format=torch.channels_last),
+                      f2.contiguous(memory_format=torch.channels_last))
+    assert torch.equal(cb._buf, cl._buf)
+    assert nat.load().dxr_build_workspace_bytes(nat.DXR_F32, 2, 256, 30, 44) > 0
 
 
 @pytest.mark.parametrize("shape", [(2, 47, 156), (1, 55, 100)])
