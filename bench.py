@@ -101,7 +101,8 @@ def build_kernel(dtype, H, W):
             return "corr_build_bf16_q2_kernel", 1, PEAK_BF16_TFLOPS, "bf16"
         return "corr_build_bf16_kernel", 1, PEAK_BF16_TFLOPS, "bf16"
     if D % 16 == 0 and W % 2 == 0:
-        return ("corr_build_split_kernel (f32 operands as f16 pairs hi + 2^-11 lo, "
+        return ("corr_build_dma_kernel (after split_pairs_kernel: f32 operands pre-split into "
+                "per-pixel power-of-two scaled f16 pairs hi + 2^-11 lo; LDS-DMA ring, "
                 "3 f16 MFMA products, f32 accumulate)", SPLIT_PRODUCTS, PEAK_BF16_TFLOPS,
                 "f16 MFMA, f32 accumulate")
     return "corr_build_f32_kernel", 1, PEAK_F32_TFLOPS, "f32"

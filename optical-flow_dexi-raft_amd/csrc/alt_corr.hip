@@ -215,7 +215,8 @@ __device__ __forceinline__ void alt_split8(const float (&x)[8], uint4& h, uint4&
   for (int e = 0; e < 4; ++e) {
     const float a = x[2 * e], b = x[2 * e + 1];
     const uint32_t hp = alt_cvt_pk(a, b);
-    const float ra = a - __uint_as_float(hp << 16), rb = b - __uint_as_float(hp & 0xffff0000u);
+    const float ha = __uint_as_float(hp << 16), hb = __uint_as_float(hp & 0xffff0000u);
+    const float ra = __builtin_isinf(ha) ? 0.f : a - ha, rb = __builtin_isinf(hb) ? 0.f : b - hb;
     const uint32_t mp = alt_cvt_pk(ra, rb);
     const float la = ra - __uint_as_float(mp << 16), lb = rb - __uint_as_float(mp & 0xffff0000u);
     hh[e] = hp;

@@ -893,7 +893,9 @@ __device__ __forceinline__ uint32_t pack_hi(uint32_t a, uint32_t b) {
 // Exact 3-way split of two floats (see above), packed for the MFMA operands.
 __device__ __forceinline__ Split3 split3(float a, float b) {
   const uint32_t h = cvt_pk_bf16(a, b);
-  const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
+  // an infinite hi keeps mid = lo = 0 (inf - inf would make them NaN: x*y must stay +-inf)
+  const float ha = __uint_as_float(h << 16), hb = __uint_as_float(h & 0xffff0000u);
+  const float ra = __builtin_isinf(ha) ? 0.f : a - ha, rb = __builtin_isinf(hb) ? 0.f : b - hb;
   const uint32_t m = cvt_pk_bf16(ra, rb);
   const float la = ra - __uint_as_float(m << 16), lb = rb - __uint_as_float(m & 0xffff0000u);
   return {h, m, pack_hi(__float_as_uint(la), __float_as_uint(lb))};

@@ -124,7 +124,9 @@ __device__ __forceinline__ void split8(const float (&x)[8], uint4& h, uint4& m, 
   for (int e = 0; e < 4; ++e) {
     const float a = x[2 * e], b = x[2 * e + 1];
     const uint32_t hp = cvt_pk_bf16(a, b);
-    const float ra = a - __uint_as_float(hp << 16), rb = b - __uint_as_float(hp & 0xffff0000u);
+    // an infinite hi keeps mid = lo = 0 (inf - inf would turn +-inf products into NaN)
+    const float ha = __uint_as_float(hp << 16), hb = __uint_as_float(hp & 0xffff0000u);
+    const float ra = __builtin_isinf(ha) ? 0.f : a - ha, rb = __builtin_isinf(hb) ? 0.f : b - hb;
     const uint32_t mp = cvt_pk_bf16(ra, rb);
     const float la = ra - __uint_as_float(mp << 16), lb = rb - __uint_as_float(mp & 0xffff0000u);
     hh[e] = hp;
