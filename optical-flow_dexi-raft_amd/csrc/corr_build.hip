@@ -111,8 +111,10 @@ __device__ __forceinline__ PageCoord page_coord(const BuildGeom& g) {
 // Global -> register staging of one BK slice of the query panel (A: [BK][BM])
 // and the target tile (B: [BK][TH][TW]).  VEC: W % 4 == 0, so every float4 is
 // fully inside or fully outside the map; outside elements stage as zero.
-template <bool VEC, int BK>
+// NHWC (scalar form only): channels-last fmaps [H*W][D].
+template <bool VEC, int BK, bool NHWC = false>
 struct Stage {
+  static_assert(!(VEC && NHWC), "channels-last staging is scalar");
   static constexpr int NA = VEC ? BK * BM / 4 / NT : BK * BM / NT;    // per-thread units
   static constexpr int NB = VEC ? BK * NTGT / 4 / NT : BK * NTGT / NT;
   static_assert(NA >= 1 && NB >= 1, "tile too small for the thread count");
@@ -136,7 +138,8 @@ struct Stage {
       } else {
         const int k = idx / BM, c = idx % BM;
         const int kk = k0 + k, q = q0 + c;
-        a[s] = (kk < g.D && q < g.N) ? f1b[(long long)kk * g.N + q] : 0.f;
+        a[s] = (kk < g.D && q < g.N)
+                   ? f1b[NHWC ? (long long)q * g.D + kk : (long long)kk * g.N + q] : 0.f;
       }
     }
 #pragma unroll
@@ -152,7 +155,8 @@ struct Stage {
       } else {
         const int k = idx >> 7, r = (idx >> 4) & 7, c = idx & 15;
         const int kk = k0 + k, hh = th0 + r, ww = tw0 + c;
-        b[s] = (kk < g.D && hh < g.H && ww < g.W) ? f2b[(long long)kk * g.N + hh * g.W + ww]
+        const long long p = (long long)hh * g.W + ww;
+        b[s] = (kk < g.D && hh < g.H && ww < g.W) ? f2b[NHWC ? p * g.D + kk : kk * g.N + p]
                                                   : 0.f;
       }
     }
@@ -414,7 +418,7 @@ __device__ __forceinline__ void scale_acc(f32x16 (&acc)[4], const BuildGeom& g) 
     }
 }
 
-template <bool VEC, int BK, bool PAGED, typename OT, bool DIV>
+template <bool VEC, int BK, bool PAGED, typename OT, bool DIV, bool NHWC = false>
 __device__ __forceinline__ void build_page_f32(const float* __restrict__ f1,
                                                const float* __restrict__ f2,
                                                OT* __restrict__ pyr, const BuildGeom& g,
@@ -467,7 +471,7 @@ __device__ __forceinline__ void build_page_f32(const float* __restrict__ f1,
     }
   };
   {
-    Stage<VEC, BK> st;
+    Stage<VEC, BK, NHWC> st;
     st.load(f1b, f2b, 0, q0, th0, tw0, g, tid);
     st.store(As(0), Bs(0), tid);
     __syncthreads();
@@ -1225,7 +1229,7 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
 //     Output per pair: SP [D/16][N][hi 16 k | lo 16 k] f16 (64 B per pixel and
 //     16-channel block) and E [N] int32 exponents s.  A pixel with a non-finite
 //     channel keeps s = 0: its inf/NaN reaches the accumulators and the build
-//     recomputes those pages from the f32 operands (three-way bf16 split).
+//     recomputes those pages from the f32 operands on the exact-f32 MFMA.
 // (2) corr_build_dma_kernel: the K loop moves operands only by LDS-DMA
 //     (buffer_load ... lds, 16 B per lane) into a 3-stage ring — 16 KB per
 //     16-k step: each wave's 32 queries (2 KB, contiguous in SP) and the 8x16
@@ -1326,146 +1330,11 @@ __global__ __launch_bounds__(256) void split_pairs_kernel(const float* __restric
   }
 }
 
-// The page's K loop on the exact three-way bf16 split from the f32 operands
-// (register staging, as the r02 split build's fallback): pages whose pre-split
-// sums are not finite.  Leaves the f32 sums in acc.
-template <int BV, bool NHWC>
-__device__ __forceinline__ void page_kloop_split3(const float* __restrict__ f1b,
-                                               const float* __restrict__ f2b, const BuildGeom& g,
-                                               int q0, int th0, int tw0, uint16_t* lh,
-                                               f32x16 (&acc)[4]) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(f1b, g.D * g.N);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(f2b, g.D * g.N);
-  const int qa = min(q0 + wave * 32 + (lane & 31), g.N - 1);
-  const uint32_t va = NHWC ? (uint32_t)(qa * g.D + 8 * (lane >> 5)) * 4u
-                           : (uint32_t)(qa + 8 * (lane >> 5) * g.N) * 4u;
-  constexpr int UPR = TW / BV;
-  constexpr int NBS = BKS * NTGT / BV / NT;
-  constexpr int PN = 24;
-  constexpr int PLANE = NHWC ? NTGT * PN : PLANE_S;
-  int bk[NBS], bcol[NBS];
-  uint32_t vb[NBS];
-#pragma unroll
-  for (int s = 0; s < NBS; ++s) {
-    const int idx = tid + NT * s;
-    int r, c;
-    if constexpr (NHWC) {
-      const int p = idx >> 2;
-      r = p >> 4;
-      c = p & 15;
-      bk[s] = 4 * (idx & 3);
-      vb[s] = (uint32_t)(((th0 + r) * g.W + tw0 + c) * g.D + bk[s]) * 4u;
-    } else {
-      r = (idx / UPR) & 7;
-      c = (idx % UPR) * BV;
-      bk[s] = idx / (8 * UPR);
-      vb[s] = (uint32_t)(bk[s] * g.N + (th0 + r) * g.W + tw0 + c) * 4u;
-    }
-    bcol[s] = tgt_col(r, c);
-    if (!(th0 + r < g.H && tw0 + c < g.W)) vb[s] = 0x80000000u;
-  }
-  const int li = lane & 15;
-  const int rd_off = NHWC ? (lane & 31) * PN + 8 * (lane >> 5)
-                          : (li >> 2) * PH + 4 * (li & 3) + 16 * ((lane >> 4) & 1) +
-                                8 * (lane >> 5) * PH;
-  const int tstride = NHWC ? 32 * PN : 32;
-  auto frag = [&](const uint16_t* p) {
-    if constexpr (NHWC) {
-      return *reinterpret_cast<const bf8v*>(p);
-    } else {
-      return __builtin_bit_cast(bf8v, __builtin_shufflevector(tr_read(p), tr_read(p + 4 * PH), 0,
-                                                              1, 2, 3, 4, 5, 6, 7));
-    }
-  };
-  float an[8];
-  float4 bn[NBS];
-  auto load = [&](int k0) {
-    if constexpr (NHWC) {
-      const float4 u = bload4(ra, va, k0 * 4), v = bload4(ra, va, k0 * 4 + 16);
-      an[0] = u.x; an[1] = u.y; an[2] = u.z; an[3] = u.w;
-      an[4] = v.x; an[5] = v.y; an[6] = v.z; an[7] = v.w;
-#pragma unroll
-      for (int s = 0; s < NBS; ++s) bn[s] = bload4(rb, vb[s], k0 * 4);
-    } else {
-      const int rowb = g.N * 4;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) an[e] = bload1(ra, va, (k0 + e) * rowb);
-#pragma unroll
-      for (int s = 0; s < NBS; ++s) {
-        if constexpr (BV == 4) {
-          bn[s] = bload4(rb, vb[s], k0 * rowb);
-        } else {
-          const float2 v = bload2(rb, vb[s], k0 * rowb);
-          bn[s] = make_float4(v.x, v.y, 0.f, 0.f);
-        }
-      }
-    }
-  };
-  s8v ah, am, al;
-  auto split_a = [&]() {
-    uint32_t h[4], m[4], l[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const Split3 x = split3(an[2 * e], an[2 * e + 1]);
-      h[e] = x.h; m[e] = x.m; l[e] = x.l;
-    }
-    ah = __builtin_bit_cast(s8v, make_uint4(h[0], h[1], h[2], h[3]));
-    am = __builtin_bit_cast(s8v, make_uint4(m[0], m[1], m[2], m[3]));
-    al = __builtin_bit_cast(s8v, make_uint4(l[0], l[1], l[2], l[3]));
-  };
-  auto store_b = [&](int buf) {
-    uint16_t* P = lh + buf * 3 * PLANE;
-#pragma unroll
-    for (int s = 0; s < NBS; ++s) {
-      const int o = NHWC ? bcol[s] * PN + bk[s] : bk[s] * PH + bcol[s];
-      const Split3 x = split3(bn[s].x, bn[s].y);
-      if constexpr (BV == 4) {
-        const Split3 z = split3(bn[s].z, bn[s].w);
-        *reinterpret_cast<uint2*>(P + o) = make_uint2(x.h, z.h);
-        *reinterpret_cast<uint2*>(P + PLANE + o) = make_uint2(x.m, z.m);
-        *reinterpret_cast<uint2*>(P + 2 * PLANE + o) = make_uint2(x.l, z.l);
-      } else {
-        *reinterpret_cast<uint32_t*>(P + o) = x.h;
-        *reinterpret_cast<uint32_t*>(P + PLANE + o) = x.m;
-        *reinterpret_cast<uint32_t*>(P + 2 * PLANE + o) = x.l;
-      }
-    }
-  };
-  const int nk = g.D / BKS;
-  load(0);
-  store_b(0);
-  split_a();
-  __syncthreads();
-  for (int ks = 0; ks < nk; ++ks) {
-    const int buf = ks & 1;
-    if (ks + 1 < nk) load((ks + 1) * BKS);
-    const uint16_t* P = lh + buf * 3 * PLANE + rd_off;
-    const bf8v qh = __builtin_bit_cast(bf8v, ah), qm = __builtin_bit_cast(bf8v, am),
-               ql = __builtin_bit_cast(bf8v, al);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const bf8v th = frag(P + t * tstride), tm = frag(P + PLANE + t * tstride),
-                 tl = frag(P + 2 * PLANE + t * tstride);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, ql, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qh, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qm, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh, acc[t], 0, 0, 0);
-    }
-    if (ks + 1 < nk) {
-      store_b(buf ^ 1);
-      split_a();
-    }
-    __syncthreads();
-  }
-}
-
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-// BV / NHWC describe the f32 operands for the fallback path only; the main
-// loop reads the pre-split SP records, which are layout-independent.
+// BV / NHWC describe the f32 operands for the fallback path only (BV 4: float4
+// staging); the main loop reads the pre-split SP records, which are
+// layout-independent.
 template <typename OT, bool DIV, int BV, bool NHWC>
 __global__ __launch_bounds__(NT, 3) void corr_build_dma_kernel(
     const float* __restrict__ f1, const float* __restrict__ f2, const uint8_t* __restrict__ sp1,
@@ -1473,9 +1342,8 @@ __global__ __launch_bounds__(NT, 3) void corr_build_dma_kernel(
     OT* __restrict__ pyr, BuildGeom g) {
   constexpr int LDS_RING = DMA_RING * DMA_STAGE;
   constexpr int LDS_E = WAVES * 16 * P0 * 4;          // epilogue staging bytes
-  constexpr int LDS_F = 2 * 3 * PLANE_S * 2;          // fallback planes (NCHW) bytes
-  static_assert(LDS_E <= LDS_RING && LDS_F <= LDS_RING && 2 * 3 * NTGT * 24 * 2 <= LDS_RING,
-                "epilogue and fallback alias the ring");
+  constexpr int LDS_F = build_lds_floats<16>() * 4;   // exact-f32 fallback page bytes
+  static_assert(LDS_E <= LDS_RING && LDS_F <= LDS_RING, "epilogue and fallback alias the ring");
   // one LDS array (cdna_hip_programming.md §5 item 4(a)): ring | target
   // exponents (128 int) | redo flag
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_RING + NTGT * 4 + 16];
@@ -1594,13 +1462,12 @@ __global__ __launch_bounds__(NT, 3) void corr_build_dma_kernel(
   if (bad) *redo = 1;
   __syncthreads();
   if (*redo) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-    const long long fstride = (long long)g.D * g.N;
-    page_kloop_split3<BV, NHWC>(f1 + b * fstride, f2 + b * fstride, g, q0, th0, tw0,
-                                reinterpret_cast<uint16_t*>(smem), acc);
+    // IEEE semantics for the page (inf x finite = inf, inf x 0 = NaN, NaN
+    // propagates) as the reference's f32 matmul: the exact-f32 MFMA page build,
+    // K loop and epilogue (a split operand cannot carry inf: inf - inf = NaN)
+    build_page_f32<BV == 4 && !NHWC, 16, true, OT, DIV, NHWC>(
+        f1, f2, pyr, g, reinterpret_cast<float*>(smem), pc.page);
+    return;
   } else {
     // undo the pixel scales: acc[t][r] is query qj x tile pixel (row 2t + kh, col r)
 #pragma unroll

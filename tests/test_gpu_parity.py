@@ -412,10 +412,11 @@ def test_bf16_build_batched_odd_stages(dx, D):
 
 
 def test_split_build_overflow_fallback(dx):
-    """Operands beyond the f16 pair split's range (|x| >= 65520) or not finite make
-    their pages non-finite; those pages are re-run on the 3-way bf16 split, so the
-    result stays f32-class over the whole f32 range and NaN rows stay NaN, as in
-    the reference's f32 matmul."""
+    """Operands beyond the f16 range (|x| >= 65520) are scaled into it by the
+    pre-split pass (per-pixel powers of two), so the result stays f32-class over
+    the whole f32 range; non-finite operands make their pages non-finite and
+    those pages are re-run on the exact-f32 MFMA, so NaN rows stay NaN, as in the
+    reference's f32 matmul."""
     f1, f2 = _pair(H=24, W=32, seed=61)
     f1, f2 = f1.clone(), f2.clone()
     f1[0, :, 3, 5] *= 1.0e5                      # query (3, 5) far out of f16 range
@@ -441,9 +442,9 @@ def test_split_build_overflow_fallback(dx):
 @pytest.mark.parametrize("W,layout", [(62, "nchw"), (32, "nhwc"), (44, "nchw")])
 def test_prescaled_build_nonfinite_fallback_forms(dx, W, layout):
     """Pages that see an inf/NaN operand are recomputed from the f32 operands on
-    the three-way bf16 split, in every operand form of that fallback (float2 /
-    float4 NCHW target units, NHWC): NaN where the reference's f32 matmul has
-    NaN, inf x finite = inf, and f32 class everywhere else."""
+    the exact-f32 MFMA, in every operand form of that fallback (float4 / scalar
+    NCHW staging, NHWC): NaN where the reference's f32 matmul has NaN,
+    inf x finite = inf, and f32 class everywhere else."""
     H = 20
     f1, f2 = _pair(H=H, W=W, seed=181)
     f1, f2 = f1.clone(), f2.clone()
