@@ -99,6 +99,60 @@ __global__ __launch_bounds__(512) void xp_lookup_kernel(const PT* __restrict__ p
     return;
   }
 
+  if constexpr ((XP & 16) != 0) {
+    // outputs of the thread's (query, class) slots in registers, then through
+    // LDS as [k][QB] rows, stored as 16-byte write-through (sc1) vectors of 4
+    // consecutive queries (N % 4 == 0, checked by the host)
+    constexpr int NKT = (K + C::NCLS - 1) / C::NCLS;
+    const int qq = tid % QB, cls = tid / QB;
+    float rv[NKT];
+    {
+      const float* cq = cells + qq * C::QS;
+#pragma unroll
+      for (int i = 0; i < NKT; ++i) {
+        const int k = cls + i * C::NCLS;
+        rv[i] = 0.f;
+        if (k < K) {
+          const int ox = k / RD, oy = k - ox * RD;
+          const float4 xd = xs[ox * QB + qq], yd = ys[oy * QB + qq];
+          const float* p = cq + __float_as_int(yd.x) + __float_as_int(xd.x);
+          const float v00 = p[0], v01 = p[1], v10 = p[RS], v11 = p[RS + 1];
+          const float nw = __fmul_rn(yd.z, xd.z), ne = __fmul_rn(yd.z, xd.y);
+          const float sw = __fmul_rn(yd.y, xd.z), se = __fmul_rn(yd.y, xd.y);
+          float r = __fmul_rn(nw, v00);
+          r = __builtin_fmaf(ne, v01, r);
+          r = __builtin_fmaf(sw, v10, r);
+          rv[i] = __builtin_fmaf(se, v11, r);
+        }
+      }
+    }
+    __syncthreads();   // cells are free
+#pragma unroll
+    for (int i = 0; i < NKT; ++i) {
+      const int k = cls + i * C::NCLS;
+      if (k < K) cells[k * QB + qq] = rv[i];
+    }
+    __syncthreads();
+    float* ob0 = out + ((long long)b * g.cout + (long long)l * K) * g.N + q0;
+    const __amdgpu_buffer_rsrc_t ro =
+        __builtin_amdgcn_make_buffer_rsrc(ob0, (short)0, 0x7fffffff, 0x00020000);
+    for (int s = tid; s < K * (QB / 4); s += C::NT) {
+      const int k = s / (QB / 4), qa = 4 * (s % (QB / 4));
+      const float4 v = *reinterpret_cast<const float4*>(cells + k * QB + qa);
+      if (q0 + qa + 3 < g.N) {
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        const u4 w = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
+                      __float_as_uint(v.w)};
+        __builtin_amdgcn_raw_buffer_store_b128(w, ro, (unsigned)(k * g.N + qa) * 4u, 0, 16);
+      }
+    }
+    if constexpr ((XP & 256) != 0) {
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      record(t2, __builtin_amdgcn_s_memrealtime());
+    }
+    return;
+  }
   const int qq = tid % QB, cls = tid / QB;
   if (q0 + qq < g.N) {
     const float* cq = cells + qq * C::QS;
@@ -144,7 +198,10 @@ int xp_dispatch(int xp, const PT* pyr, const float* coords, float* out, const Lo
     case 4: return xp_launch<4>(pyr, coords, out, g, B, trace, stream);
     case 8: return xp_launch<8>(pyr, coords, out, g, B, trace, stream);
     case 12: return xp_launch<12>(pyr, coords, out, g, B, trace, stream);
+    case 16: return xp_launch<16>(pyr, coords, out, g, B, trace, stream);
     case 256: return xp_launch<256>(pyr, coords, out, g, B, trace, stream);
+    case 272: return xp_launch<272>(pyr, coords, out, g, B, trace, stream);
+    case 264: return xp_launch<264>(pyr, coords, out, g, B, trace, stream);
     case 258: return xp_launch<258>(pyr, coords, out, g, B, trace, stream);
     case 260: return xp_launch<260>(pyr, coords, out, g, B, trace, stream);
     default: return DXR_EINVAL;

@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Same-process A/B of the f32 builds through the C-ABI (build only, no lookups).
+
+  ws   : dxr_corr_pyramid_build_ws (pre-split pass + LDS-DMA build, round 3)
+  nows : dxr_corr_pyramid_build    (register-split build, round 2)
+  exact: DXR_BUILD_EXACT_F32       (exact-f32 MFMA build)
+
+Each variant is captured as a HIP graph of --reps back-to-back builds and the
+graphs are replayed in interleaved rounds after a clock warm-up (HIP events;
+a build plus its same-stream boundary).  Run it under
+``rocprofv3 --kernel-trace --stats`` for per-kernel durations.
+Usage: python scripts/ab_build.py [--shapes 1x55x128 8x55x128 1x46x62]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", nargs="+", default=["1x55x128", "8x55x128", "1x46x62"])
+    ap.add_argument("--variants", nargs="+", default=["ws", "nows"])
+    ap.add_argument("--layout", default="nchw", choices=["nchw", "nhwc"])
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=7)
+    a = ap.parse_args()
+    import dexiraft_amd
+    from dexiraft_amd import _native as nat
+    lib = dexiraft_amd.load_native()
+    dev = torch.device("cuda", 0)
+    D = 256
+    stream = torch.cuda.Stream(device=dev)
+    for shp in a.shapes:
+        B, H, W = (int(v) for v in shp.split("x"))
+        g = torch.Generator(device=dev)
+        g.manual_seed(7)
+        f1 = torch.randn((B, D, H, W), generator=g, device=dev)
+        f2 = torch.randn((B, D, H, W), generator=g, device=dev)
+        layout = nat.DXR_NCHW
+        if a.layout == "nhwc":
+            f1 = f1.contiguous(memory_format=torch.channels_last)
+            f2 = f2.contiguous(memory_format=torch.channels_last)
+            layout = nat.DXR_NHWC
+        n = lib.dxr_pyramid_numel(B, H, W, 4)
+        pyr = torch.empty(n, device=dev)
+        wsb = lib.dxr_build_workspace_bytes(nat.DXR_F32, B, D, H, W)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        div = float(np.sqrt(np.float32(D)))
+
+        def build(v):
+            s = stream.cuda_stream
+            if v == "ws":
+                st = lib.dxr_corr_pyramid_build_ws(f1.data_ptr(), f2.data_ptr(), nat.DXR_F32,
+                                                   layout, B, D, H, W, 4, div, pyr.data_ptr(),
+                                                   nat.DXR_F32, nat.DXR_BUILD_AUTO, ws.data_ptr(),
+                                                   wsb, s)
+            else:
+                algo = nat.DXR_BUILD_EXACT_F32 if v == "exact" else nat.DXR_BUILD_AUTO
+                st = lib.dxr_corr_pyramid_build(f1.data_ptr(), f2.data_ptr(), nat.DXR_F32, layout,
+                                                B, D, H, W, 4, div, pyr.data_ptr(), nat.DXR_F32,
+                                                algo, s)
+            assert st == 0, (v, st)
+
+        graphs = {}
+        with torch.cuda.stream(stream):
+            for v in a.variants:
+                build(v)
+                torch.cuda.synchronize()
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr, stream=stream):
+                    for _ in range(a.reps):
+                        build(v)
+                graphs[v] = gr
+            for _ in range(10):
+                for v in a.variants:
+                    graphs[v].replay()
+            torch.cuda.synchronize()
+            res = {v: [] for v in a.variants}
+            for _ in range(a.rounds):
+                for v in a.variants:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    graphs[v].replay()
+                    e1.record(stream)
+                    torch.cuda.synchronize()
+                    res[v].append(e0.elapsed_time(e1) * 1e3 / a.reps)
+        print(json.dumps({"shape": [B, D, H, W], "layout": a.layout,
+                          "us_per_build_min_med": {v: [round(min(x), 1), round(float(np.median(x)), 1)]
+                                                   for v, x in res.items()}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
