@@ -1278,17 +1278,24 @@ __device__ __forceinline__ void store_pair_block(uint4* dst, const float (&x)[16
   dst[3] = make_uint4(l[4], l[5], l[6], l[7]);
 }
 
-// One thread per (pixel, pair, fmap): grid (ceil(N / 256), B, 2).  NCHW reads
-// are coalesced along pixels; NHWC threads read their pixel's channels as float4.
+// One thread per (pixel, 16-channel block): 1024-thread blocks of 64 pixels x
+// 16 channel blocks (more blocks loop), grid (ceil(N / 64), B, 2 fmaps).  NCHW:
+// wave = channel block, lane = pixel, so every load is 256 contiguous bytes;
+// NHWC: 16 lanes per pixel read its channels as 64-byte runs.  The pixel max
+// (and a non-finite flag, -1) is reduced through LDS; the values stay in
+// registers between the two passes when D <= 256.
 template <bool NHWC>
-__global__ __launch_bounds__(256) void split_pairs_kernel(const float* __restrict__ f1,
-                                                          const float* __restrict__ f2,
-                                                          uint4* __restrict__ sp1,
-                                                          uint4* __restrict__ sp2,
-                                                          int* __restrict__ e1, int* __restrict__ e2,
-                                                          int D, int N) {
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= N) return;
+__global__ __launch_bounds__(1024) void split_pairs_kernel(const float* __restrict__ f1,
+                                                           const float* __restrict__ f2,
+                                                           uint4* __restrict__ sp1,
+                                                           uint4* __restrict__ sp2,
+                                                           int* __restrict__ e1, int* __restrict__ e2,
+                                                           int D, int N) {
+  __shared__ float red[16][65];
+  const int tid = threadIdx.x;
+  const int kb0 = NHWC ? (tid & 15) : (tid >> 6), pl = NHWC ? (tid >> 4) : (tid & 63);
+  const int p = blockIdx.x * 64 + pl;
+  const bool live = p < N;
   const int b = blockIdx.y;
   const float* src = (blockIdx.z == 0 ? f1 : f2) + (long long)b * D * N;
   uint4* sp = (blockIdx.z == 0 ? sp1 : sp2) + (long long)b * (D / 16) * N * 4;
@@ -1307,23 +1314,29 @@ __global__ __launch_bounds__(256) void split_pairs_kernel(const float* __restric
       for (int i = 0; i < 16; ++i) x[i] = src[(long long)(kb * 16 + i) * N + p];
     }
   };
+  float x[16];
   float m = 0.f;
-  bool finite = true;
-  for (int kb = 0; kb < nkb; ++kb) {
-    float x[16];
+  for (int kb = kb0; kb < nkb && live; kb += 16) {
     load16(kb, x);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const float a = __builtin_fabsf(x[i]);
-      finite &= a <= 3.40282347e38f;
-      m = a > m ? a : m;
+      m = (m < 0.f || !(a <= 3.40282347e38f)) ? -1.f : (a > m ? a : m);
     }
   }
-  const int s = pixel_scale(m, finite);
-  ex[p] = s;
-  for (int kb = 0; kb < nkb; ++kb) {
-    float x[16];
-    load16(kb, x);
+  red[kb0][pl] = m;
+  __syncthreads();
+  float mm = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const float v = red[k][pl];
+    mm = (mm < 0.f || v < 0.f) ? -1.f : (v > mm ? v : mm);
+  }
+  if (!live) return;
+  const int s = pixel_scale(mm < 0.f ? 0.f : mm, mm >= 0.f);
+  if (kb0 == 0) ex[p] = s;
+  for (int kb = kb0; kb < nkb; kb += 16) {
+    if (nkb > 16) load16(kb, x);      // D <= 256: the first pass's values
 #pragma unroll
     for (int i = 0; i < 16; ++i) x[i] = __builtin_ldexpf(x[i], s);
     store_pair_block(sp + ((long long)kb * N + p) * 4, x);
@@ -1762,8 +1775,8 @@ int launch_dma(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, in
   uint8_t* sp2 = w + spb;
   int* e1 = reinterpret_cast<int*>(w + 2 * spb);
   int* e2 = reinterpret_cast<int*>(w + 2 * spb + eb);
-  hipLaunchKernelGGL((split_pairs_kernel<NHWC>), dim3((unsigned)((N + 255) / 256), (unsigned)B, 2),
-                     dim3(256), 0, stream, f1, f2, reinterpret_cast<uint4*>(sp1),
+  hipLaunchKernelGGL((split_pairs_kernel<NHWC>), dim3((unsigned)((N + 63) / 64), (unsigned)B, 2),
+                     dim3(1024), 0, stream, f1, f2, reinterpret_cast<uint4*>(sp1),
                      reinterpret_cast<uint4*>(sp2), e1, e2, g.D, g.N);
   int st = dxr::launch_status();
   if (st != DXR_OK) return st;
