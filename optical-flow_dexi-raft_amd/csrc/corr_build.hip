@@ -418,14 +418,15 @@ __device__ __forceinline__ void scale_acc(f32x16 (&acc)[4], const BuildGeom& g) 
     }
 }
 
+// `tid`: the thread's index among the page's NT threads (its workgroup may hold
+// several such groups, each with its own `lds` region, running in step).
 template <bool VEC, int BK, bool PAGED, typename OT, bool DIV, bool NHWC = false>
 __device__ __forceinline__ void build_page_f32(const float* __restrict__ f1,
                                                const float* __restrict__ f2,
                                                OT* __restrict__ pyr, const BuildGeom& g,
-                                               float* lds, long long page) {
+                                               float* lds, long long page, int tid) {
   constexpr int KP = BK / 2;                        // MFMA k-pairs per stage
 
-  const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   // Page coordinates in 32-bit arithmetic (pages < 2^31; 64-bit division expands
@@ -524,7 +525,7 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_f32_kernel(const float* _
   __shared__ float lds[build_lds_floats<BK>()];
   const long long page =
       ((long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-  build_page_f32<VEC, BK, PAGED, OT, DIV>(f1, f2, pyr, g, lds, page);
+  build_page_f32<VEC, BK, PAGED, OT, DIV>(f1, f2, pyr, g, lds, page, (int)threadIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -1221,25 +1222,28 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
 // (1) split_pairs_kernel, once per build: every pixel's f32 channel vector is
 //     scaled by a power of two 2^s (s = 14 - e for max_k |x| = f 2^e, f in
 //     [0.5, 1), so |x 2^s| < 2^14) and split into an f16 pair
-//     x 2^s = hi + 2^-11 lo (hi = RNE_f16(x 2^s), lo = RNE_f16((x 2^s - hi) 2^11),
-//     split2h_mix's single rounding).  The scaling is exact, so the pair keeps
-//     <= 2^-22 |x| of every element whose magnitude is within 2^-10 of its pixel's
-//     max (and <= 2^-36 max below that) whatever the fmaps' scale — the r02 build
+//     x 2^s = hi + lo (hi = RNE_f16(x 2^s), lo = RNE_f16(x 2^s - hi), one rounding
+//     of an exact residual).  The scaling is exact, so the pair represents every
+//     element to <= 2^-23 |x| unless it is more than 2^16 below its pixel's max
+//     (then to <= 2^-39 of that max) whatever the fmaps' scale — the r02 build
 //     split unscaled values and lost precision below |x| ~ 2^-14.
 //     Output per pair: SP [D/16][N][hi 16 k | lo 16 k] f16 (64 B per pixel and
 //     16-channel block) and E [N] int32 exponents s.  A pixel with a non-finite
 //     channel keeps s = 0: its inf/NaN reaches the accumulators and the build
 //     recomputes those pages from the f32 operands on the exact-f32 MFMA.
-// (2) corr_build_dma_kernel: the K loop moves operands only by LDS-DMA
-//     (buffer_load ... lds, 16 B per lane) into a 3-stage ring — 16 KB per
-//     16-k step: each wave's 32 queries (2 KB, contiguous in SP) and the 8x16
-//     target tile (8 tile rows of 1 KB) — so no VGPRs are held by loads in
-//     flight and no VALU splits in the loop: per step a wave waits for its own
-//     DMAs of the step (vmcnt), one barrier publishes the tile, then 10
-//     conflict-free ds_read_b128 and 12 f16 MFMAs (hi*hi into acc, hi*lo and
-//     lo*hi into acc2, as the r02 split build).  The epilogue combines
-//     acc + 2^-11 acc2, undoes both pixels' scales (ldexp by -(s_q + s_t)) and
-//     writes the paged pyramid as before.
+// (2) corr_build_dma_kernel: 8 waves = two query blocks (waves 0-3, 4-7) x one
+//     8x16 target tile, the tile shared by both (24 KB per 16-k step instead of
+//     2 x 16 KB for two single-block pages).  The K loop moves operands only by
+//     LDS-DMA (buffer_load ... lds, 16 B per lane) into a 3-stage ring, so no
+//     VGPRs are held by loads in flight and no VALU splits in the loop: per step
+//     a wave waits for its own 3 DMAs of the step (vmcnt), one barrier publishes
+//     the tile, then 10 conflict-free ds_read_b128 and 12 f16 MFMAs — lo*hi,
+//     hi*lo, hi*hi into ONE f32 accumulator (f16 x f16 products are exact in
+//     f32; 3 roundings per 16 k against the exact-f32 MFMA's 8).  With a single
+//     accumulator per output (64 VGPRs instead of the r02 split build's 128) the
+//     kernel fits 4 waves per SIMD: two workgroups per CU.  The epilogue undoes
+//     both pixels' scales (ldexp by -(s_q + s_t), exact) and writes the paged
+//     pyramid as before.
 // LDS image rows are 64 B (hi k0-7, hi k8-15, lo k0-7, lo k8-15 in 16-B slots);
 // the slots of a row are XOR-permuted by a row key so that every 16-lane group
 // of a ds_read_b128 hits 16 distinct bank slots; the DMA writes lane-linearly,
@@ -1251,8 +1255,8 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
 // ---------------------------------------------------------------------------
 constexpr int SPLIT_S_TOP = 14;          // |x 2^s| < 2^SPLIT_S_TOP
 constexpr int DMA_RING = 3;              // ring stages (k16 steps in LDS)
-constexpr int DMA_STAGE = 16384;         // bytes per stage: 4 x 2 KB queries + 8 KB tile
-constexpr int DMA_TILE = 8192;           // byte offset of the tile within a stage
+constexpr int DMA_TILE = 16384;          // tile offset in a stage: 8 waves x 2 KB queries
+constexpr int DMA_STAGE = DMA_TILE + 8192;   // bytes per stage
 
 __device__ __forceinline__ int pixel_scale(float m, bool finite) {
   if (!finite || !(m > 0.f)) return 0;
@@ -1263,14 +1267,25 @@ __device__ __forceinline__ int pixel_scale(float m, bool finite) {
 }
 
 // Split 16 consecutive channels of one pixel (already scaled) into the 64-B
-// SP record: hi 16 f16 then lo 16 f16.
+// SP record: hi 16 f16 then lo 16 f16.  LO11: lo = RNE_f16((x - hi) 2^11) (the
+// r02 pair, for experiments), else lo = RNE_f16(x - hi).
+template <bool LO11 = false>
 __device__ __forceinline__ void store_pair_block(uint4* dst, const float (&x)[16]) {
   uint32_t h[8], l[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const Split2 p = split2h_mix(x[2 * e], x[2 * e + 1]);
-    h[e] = p.h;
-    l[e] = p.l;
+    if constexpr (LO11) {
+      const Split2 p = split2h_mix(x[2 * e], x[2 * e + 1]);
+      h[e] = p.h;
+      l[e] = p.l;
+    } else {
+      h[e] = cvt_pk_f16(x[2 * e], x[2 * e + 1]);
+      const f16x2_t hv = __builtin_bit_cast(f16x2_t, h[e]);
+      f16x2_t lv;
+      lv[0] = (_Float16)__builtin_fmaf((float)hv[0], -1.f, x[2 * e]);
+      lv[1] = (_Float16)__builtin_fmaf((float)hv[1], -1.f, x[2 * e + 1]);
+      l[e] = __builtin_bit_cast(uint32_t, lv);
+    }
   }
   dst[0] = make_uint4(h[0], h[1], h[2], h[3]);
   dst[1] = make_uint4(h[4], h[5], h[6], h[7]);
@@ -1284,15 +1299,16 @@ __device__ __forceinline__ void store_pair_block(uint4* dst, const float (&x)[16
 // NHWC: 16 lanes per pixel read its channels as 64-byte runs.  The pixel max
 // (and a non-finite flag, -1) is reduced through LDS; the values stay in
 // registers between the two passes when D <= 256.
-template <bool NHWC>
+template <bool NHWC, bool LO11 = false>
 __global__ __launch_bounds__(1024) void split_pairs_kernel(const float* __restrict__ f1,
                                                            const float* __restrict__ f2,
                                                            uint4* __restrict__ sp1,
                                                            uint4* __restrict__ sp2,
                                                            int* __restrict__ e1, int* __restrict__ e2,
-                                                           int D, int N) {
+                                                           int D, int N, int* __restrict__ redo) {
   __shared__ float red[16][65];
   const int tid = threadIdx.x;
+  if (redo && (blockIdx.x | blockIdx.y | blockIdx.z | tid) == 0) *redo = 0;   // the build's list
   const int kb0 = NHWC ? (tid & 15) : (tid >> 6), pl = NHWC ? (tid >> 4) : (tid & 63);
   const int p = blockIdx.x * 64 + pl;
   const bool live = p < N;
@@ -1339,24 +1355,23 @@ __global__ __launch_bounds__(1024) void split_pairs_kernel(const float* __restri
     if (nkb > 16) load16(kb, x);      // D <= 256: the first pass's values
 #pragma unroll
     for (int i = 0; i < 16; ++i) x[i] = __builtin_ldexpf(x[i], s);
-    store_pair_block(sp + ((long long)kb * N + p) * 4, x);
+    store_pair_block<LO11>(sp + ((long long)kb * N + p) * 4, x);
   }
 }
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-// BV / NHWC describe the f32 operands for the fallback path only (BV 4: float4
-// staging); the main loop reads the pre-split SP records, which are
-// layout-independent.
-template <typename OT, bool DIV, int BV, bool NHWC>
-__global__ __launch_bounds__(NT, 3) void corr_build_dma_kernel(
-    const float* __restrict__ f1, const float* __restrict__ f2, const uint8_t* __restrict__ sp1,
-    const uint8_t* __restrict__ sp2, const int* __restrict__ ex1, const int* __restrict__ ex2,
-    OT* __restrict__ pyr, BuildGeom g) {
+// Pages whose sums are not finite (an inf/NaN operand pixel) are not written
+// here: their indices go to `redo` (count in redo[0], pages from redo[1]) for
+// corr_build_redo_kernel, launched after this kernel.  Grid:
+// remap_grid(g, B, 2) (page_coord<true, 2>).
+template <typename OT, bool DIV>
+__global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
+    const uint8_t* __restrict__ sp1, const uint8_t* __restrict__ sp2, const int* __restrict__ ex1,
+    const int* __restrict__ ex2, OT* __restrict__ pyr, int* __restrict__ redo_list, BuildGeom g) {
   constexpr int LDS_RING = DMA_RING * DMA_STAGE;
-  constexpr int LDS_E = WAVES * 16 * P0 * 4;          // epilogue staging bytes
-  constexpr int LDS_F = build_lds_floats<16>() * 4;   // exact-f32 fallback page bytes
-  static_assert(LDS_E <= LDS_RING && LDS_F <= LDS_RING, "epilogue and fallback alias the ring");
+  constexpr int LDS_E = 2 * WAVES * 16 * P0 * 4;          // epilogue staging (8 waves)
+  static_assert(LDS_E <= LDS_RING, "the epilogue staging aliases the ring");
   // one LDS array (cdna_hip_programming.md §5 item 4(a)): ring | target
   // exponents (128 int) | redo flag
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_RING + NTGT * 4 + 16];
@@ -1367,9 +1382,10 @@ __global__ __launch_bounds__(NT, 3) void corr_build_dma_kernel(
   // wave-uniform (SGPR): the DMA's LDS base must be, or the compiler emits a
   // waterfall loop around every buffer_load ... lds
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const PageCoord pc = page_coord<false>(g);
+  const int half = wave >> 2, w4 = wave & 3;
+  const PageCoord pc = page_coord<true, 2>(g);
   const int th0 = pc.tyi * TH, tw0 = pc.txi * TW;
-  const int q0 = pc.qblk * BM;
+  const int q0 = pc.qblk * BM;                        // first of the two blocks
   const int b = pc.b;
   const int j = lane & 31, kh = lane >> 5;
   const long long spstride = (long long)g.D * g.N * 4;   // SP bytes per pair
@@ -1392,18 +1408,20 @@ __global__ __launch_bounds__(NT, 3) void corr_build_dma_kernel(
                                         (int)spstride, 0x00020000);
   // DMA source offsets (fixed over K; the step's offset ks * N * 64 in soffset).
   // Query instruction i of this wave: LDS rows 16 i + (lane >> 2) of the wave's
-  // 2 KB region; target instruction i: tile row r = 2 wave + i.
-  uint32_t vq[2], vt[2];
+  // 2 KB region; target instruction: tile row r = wave.
+  uint32_t vq[2], vt;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = 16 * i + (lane >> 2), ps = lane & 3;
     const int q = q0 + wave * 32 + row;
     const int cq = ps ^ ((row >> 2) & 3);
     vq[i] = q < g.N ? (uint32_t)(q * 64 + 16 * cq) : 0x80000000u;
-    const int r = 2 * wave + i, col = lane >> 2, trow = r * 16 + col;
+  }
+  {
+    const int ps = lane & 3, r = wave, col = lane >> 2, trow = r * 16 + col;
     const int ct = ps ^ (((trow >> 2) & 1) | ((trow >> 3) & 2));
     const int hh = th0 + r, ww = tw0 + col;
-    vt[i] = (hh < g.H && ww < g.W) ? (uint32_t)((hh * g.W + ww) * 64 + 16 * ct) : 0x80000000u;
+    vt = (hh < g.H && ww < g.W) ? (uint32_t)((hh * g.W + ww) * 64 + 16 * ct) : 0x80000000u;
   }
   auto dma = [&](int ks) {
     unsigned char* st = smem + (ks % DMA_RING) * DMA_STAGE;
@@ -1412,10 +1430,8 @@ __global__ __launch_bounds__(NT, 3) void corr_build_dma_kernel(
     for (int i = 0; i < 2; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rq, (lds_void_t*)(st + wave * 2048 + i * 1024), 16, vq[i], so, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rt, (lds_void_t*)(st + DMA_TILE + (2 * wave + i) * 1024), 16, vt[i], so, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (lds_void_t*)(st + DMA_TILE + wave * 1024), 16,
+                                             vt, so, 0, 0);
   };
   // fragment byte offsets within a stage (hi; lo = the other two slots)
   const int kq = (j >> 2) & 3;
@@ -1426,11 +1442,11 @@ __global__ __launch_bounds__(NT, 3) void corr_build_dma_kernel(
   const int th_off = DMA_TILE + trow0 * 64 + 16 * (kh ^ kt);
   const int tl_off = DMA_TILE + trow0 * 64 + 16 * ((2 + kh) ^ kt);
 
-  f32x16 acc[4], acc2[4];
+  f32x16 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = acc2[t][r] = 0.f;
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
   // exponent loads and LDS writes above must not count against the ring's vmcnt
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1438,10 +1454,10 @@ __global__ __launch_bounds__(NT, 3) void corr_build_dma_kernel(
   dma(0);
   if (nk > 1) dma(1);
   for (int ks = 0; ks < nk; ++ks) {
-    // this wave's 4 DMAs of step ks have landed (those of ks + 1 stay in flight);
+    // this wave's 3 DMAs of step ks have landed (those of ks + 1 stay in flight);
     // the barrier publishes every wave's, and orders the ring slot's previous
     // readers (step ks - 1) before the refill below
-    if (ks + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if (ks + 1 < nk) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -1454,33 +1470,36 @@ __global__ __launch_bounds__(NT, 3) void corr_build_dma_kernel(
     for (int t = 0; t < 4; ++t) {
       const h8v th = *reinterpret_cast<const h8v*>(st + th_off + t * 2048);
       const h8v tl = *reinterpret_cast<const h8v*>(st + tl_off + t * 2048);
-      acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc2[t], 0, 0, 0);
-      acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc2[t], 0, 0, 0);
+      // small terms first
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc[t], 0, 0, 0);
       acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qh, acc[t], 0, 0, 0);
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();   // ring reads done: the LDS is free for reuse
 
-  // combine (one rounding) and vote: a non-finite sum means an operand pixel
-  // was not finite; the page is then recomputed from the f32 operands
+  // vote: a non-finite sum means an operand pixel was not finite; the
+  // workgroup's pages are then recomputed from the f32 operands
   bool bad = false;
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      acc[t][r] = __builtin_fmaf(acc2[t][r], 0x1p-11f, acc[t][r]);
-      bad |= !(__builtin_fabsf(acc[t][r]) <= 3.40282347e38f);
-    }
+    for (int r = 0; r < 16; ++r) bad |= !(__builtin_fabsf(acc[t][r]) <= 3.40282347e38f);
   if (bad) *redo = 1;
   __syncthreads();
+  const bool live = pc.qblk + half < g.qt;            // this half's query block exists
+  const long long page = pc.page + (live ? (long long)half * g.tiles_h * g.tiles_w : 0);
   if (*redo) {
-    // IEEE semantics for the page (inf x finite = inf, inf x 0 = NaN, NaN
-    // propagates) as the reference's f32 matmul: the exact-f32 MFMA page build,
-    // K loop and epilogue (a split operand cannot carry inf: inf - inf = NaN)
-    build_page_f32<BV == 4 && !NHWC, 16, true, OT, DIV, NHWC>(
-        f1, f2, pyr, g, reinterpret_cast<float*>(smem), pc.page);
-    return;
+    // IEEE semantics (inf x finite = inf, inf x 0 = NaN, NaN propagates) as the
+    // reference's f32 matmul: corr_build_redo_kernel recomputes the pages on the
+    // exact-f32 MFMA
+    if (tid == 0) {
+      const int n = pc.qblk + 1 < g.qt ? 2 : 1;
+      const int at = atomicAdd(redo_list, n);
+      for (int h = 0; h < n; ++h)
+        redo_list[1 + at + h] = (int)(pc.page + (long long)h * g.tiles_h * g.tiles_w);
+    }
   } else {
     // undo the pixel scales: acc[t][r] is query qj x tile pixel (row 2t + kh, col r)
 #pragma unroll
@@ -1495,10 +1514,12 @@ __global__ __launch_bounds__(NT, 3) void corr_build_dma_kernel(
         acc[t][4 * u + 3] = __builtin_ldexpf(acc[t][4 * u + 3], -(sq + s4.w));
       }
     }
+    if (live) {   // a half past the last query block has no page (epilogue syncs per wave)
+      scale_acc<DIV>(acc, g);
+      paged_epilogue<OT, 1 | 4>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0, pyr,
+                                g, page, w4, lane);
+    }
   }
-  __syncthreads();   // exponent reads / fallback planes done before the staging reuse
-  scale_acc<DIV>(acc, g);
-  paged_epilogue<OT, 1 | 4>(acc, reinterpret_cast<float*>(smem), pyr, g, pc.page, wave, lane);
 }
 
 // Floor-mode 2x2 average pool of one pyramid level into the next, for levels
@@ -1758,10 +1779,32 @@ int launch_split(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, 
   return dxr::launch_status();
 }
 
-// Pre-split + LDS-DMA f32 build (round 3): workspace = SP1 | SP2 | E1 | E2.
+// The pages corr_build_dma_kernel listed as not finite, on the exact-f32 MFMA
+// (normally none: every workgroup reads the count and leaves).
+template <typename OT, bool DIV, bool VEC, bool NHWC>
+__global__ __launch_bounds__(NT) void corr_build_redo_kernel(const float* __restrict__ f1,
+                                                             const float* __restrict__ f2,
+                                                             OT* __restrict__ pyr,
+                                                             const int* __restrict__ redo_list,
+                                                             BuildGeom g) {
+  __shared__ float lds[build_lds_floats<16>()];
+  const int n = redo_list[0];
+  for (int i = blockIdx.x; i < n; i += gridDim.x)
+    build_page_f32<VEC, 16, true, OT, DIV, NHWC>(f1, f2, pyr, g, lds, redo_list[1 + i],
+                                                 (int)threadIdx.x);
+}
+
+// Pre-split + LDS-DMA f32 build (round 3): workspace = SP1 | SP2 | E1 | E2 |
+// redo list (count + one int per page).
 long long align256(long long x) { return (x + 255) & ~255LL; }
-long long dma_workspace_bytes(long long B, long long D, long long N) {
-  return 2 * align256(B * D * N * 4) + 2 * align256(B * N * 4);
+long long dma_pages(long long B, long long D, long long H, long long W) {
+  (void)D;
+  return B * ((H * W + BM - 1) / BM) * ((H + TH - 1) / TH) * ((W + TW - 1) / TW);
+}
+long long dma_workspace_bytes(long long B, long long D, long long H, long long W) {
+  const long long N = H * W;
+  return 2 * align256(B * D * N * 4) + 2 * align256(B * N * 4) +
+         align256(4 * (1 + dma_pages(B, D, H, W)));
 }
 
 template <typename OT, int BV, bool NHWC>
@@ -1775,17 +1818,28 @@ int launch_dma(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, in
   uint8_t* sp2 = w + spb;
   int* e1 = reinterpret_cast<int*>(w + 2 * spb);
   int* e2 = reinterpret_cast<int*>(w + 2 * spb + eb);
+  int* redo = reinterpret_cast<int*>(w + 2 * spb + 2 * eb);
   hipLaunchKernelGGL((split_pairs_kernel<NHWC>), dim3((unsigned)((N + 63) / 64), (unsigned)B, 2),
                      dim3(1024), 0, stream, f1, f2, reinterpret_cast<uint4*>(sp1),
-                     reinterpret_cast<uint4*>(sp2), e1, e2, g.D, g.N);
+                     reinterpret_cast<uint4*>(sp2), e1, e2, g.D, g.N, redo);
   int st = dxr::launch_status();
   if (st != DXR_OK) return st;
+  const dim3 rg = remap_grid(g, B, 2);
   if (g.recip == 0.f)
-    hipLaunchKernelGGL((corr_build_dma_kernel<OT, true, BV, NHWC>), grid, dim3(NT), 0, stream, f1,
-                       f2, sp1, sp2, e1, e2, pyr, g);
+    hipLaunchKernelGGL((corr_build_dma_kernel<OT, true>), rg, dim3(2 * NT), 0, stream, sp1, sp2,
+                       e1, e2, pyr, redo, g);
   else
-    hipLaunchKernelGGL((corr_build_dma_kernel<OT, false, BV, NHWC>), grid, dim3(NT), 0, stream, f1,
-                       f2, sp1, sp2, e1, e2, pyr, g);
+    hipLaunchKernelGGL((corr_build_dma_kernel<OT, false>), rg, dim3(2 * NT), 0, stream, sp1, sp2,
+                       e1, e2, pyr, redo, g);
+  st = dxr::launch_status();
+  if (st != DXR_OK) return st;
+  constexpr bool VEC = BV == 4 && !NHWC;
+  if (g.recip == 0.f)
+    hipLaunchKernelGGL((corr_build_redo_kernel<OT, true, VEC, NHWC>), dim3(64), dim3(NT), 0, stream,
+                       f1, f2, pyr, redo, g);
+  else
+    hipLaunchKernelGGL((corr_build_redo_kernel<OT, false, VEC, NHWC>), dim3(64), dim3(NT), 0,
+                       stream, f1, f2, pyr, redo, g);
   return dxr::launch_status();
 }
 
@@ -1869,7 +1923,7 @@ int pyramid_build(const void* fmap1, const void* fmap2, int in_dtype, int fmap_l
   // fallback's operand form).
   const bool dma_ok = in_dtype == DXR_F32 && algo == DXR_BUILD_AUTO && D % 16 == 0 &&
                       D * H * W < (1LL << 29) && workspace != nullptr && aligned16(workspace) &&
-                      workspace_bytes >= dma_workspace_bytes(B, D, H * W) && aligned16(pyramid);
+                      workspace_bytes >= dma_workspace_bytes(B, D, H, W) && aligned16(pyramid);
   if (dma_ok) {
     const float* f1 = static_cast<const float*>(fmap1);
     const float* f2 = static_cast<const float*>(fmap2);
@@ -1950,7 +2004,7 @@ extern "C" int64_t dxr_build_workspace_bytes(int in_dtype, int64_t B, int64_t D,
                                              int64_t W) {
   if (B < 0 || D < 1 || H < 1 || W < 1 || H * W > (1LL << 30)) return -1;
   if (in_dtype != DXR_F32 || D % 16 != 0) return 0;
-  return dma_workspace_bytes(B, D, H * W);
+  return dma_workspace_bytes(B, D, H, W);
 }
 
 extern "C" int dxr_corr_pyramid_build_ws(const void* fmap1, const void* fmap2, int in_dtype,

@@ -6,18 +6,17 @@
 namespace {
 
 // XP bits: 0 skip the epilogue stores (K loop kept live), 1 skip the MFMAs,
-// 2 no in-loop DMA (the ring's first two stages only), 8 record per-workgroup
-// s_memrealtime stamps {start, K loop done, epilogue stores done, hw id}.
-template <typename OT, bool DIV, int BV, bool NHWC, int XP>
-__global__ __launch_bounds__(NT, 3) void xp_build_dma_kernel(
-    const float* __restrict__ f1, const float* __restrict__ f2, const uint8_t* __restrict__ sp1,
-    const uint8_t* __restrict__ sp2, const int* __restrict__ ex1, const int* __restrict__ ex2,
-    OT* __restrict__ pyr, BuildGeom g, unsigned long long* __restrict__ trace) {
+// 8 record per-workgroup s_memrealtime stamps {start, K loop done, epilogue
+// stores done, hw id}.
+template <typename OT, bool DIV, int XP>
+__global__ __launch_bounds__(2 * NT, 4) void xp_build_dma_kernel(
+    const uint8_t* __restrict__ sp1, const uint8_t* __restrict__ sp2, const int* __restrict__ ex1,
+    const int* __restrict__ ex2, OT* __restrict__ pyr, int* __restrict__ redo_list, BuildGeom g,
+    unsigned long long* __restrict__ trace) {
   const unsigned long long xt0 = (XP & 256) ? __builtin_amdgcn_s_memrealtime() : 0ull;
   constexpr int LDS_RING = DMA_RING * DMA_STAGE;
-  constexpr int LDS_E = WAVES * 16 * P0 * 4;          // epilogue staging bytes
-  constexpr int LDS_F = build_lds_floats<16>() * 4;   // exact-f32 fallback page bytes
-  static_assert(LDS_E <= LDS_RING && LDS_F <= LDS_RING, "epilogue and fallback alias the ring");
+  constexpr int LDS_E = 2 * WAVES * 16 * P0 * 4;          // epilogue staging (8 waves)
+  static_assert(LDS_E <= LDS_RING, "the epilogue staging aliases the ring");
   // one LDS array (cdna_hip_programming.md §5 item 4(a)): ring | target
   // exponents (128 int) | redo flag
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_RING + NTGT * 4 + 16];
@@ -28,9 +27,10 @@ __global__ __launch_bounds__(NT, 3) void xp_build_dma_kernel(
   // wave-uniform (SGPR): the DMA's LDS base must be, or the compiler emits a
   // waterfall loop around every buffer_load ... lds
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const PageCoord pc = page_coord<false>(g);
+  const int half = wave >> 2, w4 = wave & 3;
+  const PageCoord pc = page_coord<true, 2>(g);
   const int th0 = pc.tyi * TH, tw0 = pc.txi * TW;
-  const int q0 = pc.qblk * BM;
+  const int q0 = pc.qblk * BM;                        // first of the two blocks
   const int b = pc.b;
   const int j = lane & 31, kh = lane >> 5;
   const long long spstride = (long long)g.D * g.N * 4;   // SP bytes per pair
@@ -53,18 +53,20 @@ __global__ __launch_bounds__(NT, 3) void xp_build_dma_kernel(
                                         (int)spstride, 0x00020000);
   // DMA source offsets (fixed over K; the step's offset ks * N * 64 in soffset).
   // Query instruction i of this wave: LDS rows 16 i + (lane >> 2) of the wave's
-  // 2 KB region; target instruction i: tile row r = 2 wave + i.
-  uint32_t vq[2], vt[2];
+  // 2 KB region; target instruction: tile row r = wave.
+  uint32_t vq[2], vt;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = 16 * i + (lane >> 2), ps = lane & 3;
     const int q = q0 + wave * 32 + row;
     const int cq = ps ^ ((row >> 2) & 3);
     vq[i] = q < g.N ? (uint32_t)(q * 64 + 16 * cq) : 0x80000000u;
-    const int r = 2 * wave + i, col = lane >> 2, trow = r * 16 + col;
+  }
+  {
+    const int ps = lane & 3, r = wave, col = lane >> 2, trow = r * 16 + col;
     const int ct = ps ^ (((trow >> 2) & 1) | ((trow >> 3) & 2));
     const int hh = th0 + r, ww = tw0 + col;
-    vt[i] = (hh < g.H && ww < g.W) ? (uint32_t)((hh * g.W + ww) * 64 + 16 * ct) : 0x80000000u;
+    vt = (hh < g.H && ww < g.W) ? (uint32_t)((hh * g.W + ww) * 64 + 16 * ct) : 0x80000000u;
   }
   auto dma = [&](int ks) {
     unsigned char* st = smem + (ks % DMA_RING) * DMA_STAGE;
@@ -73,10 +75,8 @@ __global__ __launch_bounds__(NT, 3) void xp_build_dma_kernel(
     for (int i = 0; i < 2; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rq, (lds_void_t*)(st + wave * 2048 + i * 1024), 16, vq[i], so, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rt, (lds_void_t*)(st + DMA_TILE + (2 * wave + i) * 1024), 16, vt[i], so, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (lds_void_t*)(st + DMA_TILE + wave * 1024), 16,
+                                             vt, so, 0, 0);
   };
   // fragment byte offsets within a stage (hi; lo = the other two slots)
   const int kq = (j >> 2) & 3;
@@ -87,11 +87,11 @@ __global__ __launch_bounds__(NT, 3) void xp_build_dma_kernel(
   const int th_off = DMA_TILE + trow0 * 64 + 16 * (kh ^ kt);
   const int tl_off = DMA_TILE + trow0 * 64 + 16 * ((2 + kh) ^ kt);
 
-  f32x16 acc[4], acc2[4];
+  f32x16 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = acc2[t][r] = 0.f;
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
   // exponent loads and LDS writes above must not count against the ring's vmcnt
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -99,15 +99,15 @@ __global__ __launch_bounds__(NT, 3) void xp_build_dma_kernel(
   dma(0);
   if (nk > 1) dma(1);
   for (int ks = 0; ks < nk; ++ks) {
-    // this wave's 4 DMAs of step ks have landed (those of ks + 1 stay in flight);
+    // this wave's 3 DMAs of step ks have landed (those of ks + 1 stay in flight);
     // the barrier publishes every wave's, and orders the ring slot's previous
     // readers (step ks - 1) before the refill below
-    if (ks + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if (ks + 1 < nk) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (ks + 2 < nk && (XP & 4) == 0) dma(ks + 2);
+    if (ks + 2 < nk) dma(ks + 2);
     const unsigned char* st = smem + (ks % DMA_RING) * DMA_STAGE;
     const h8v qh = *reinterpret_cast<const h8v*>(st + qh_off);
     const h8v ql = *reinterpret_cast<const h8v*>(st + ql_off);
@@ -115,11 +115,12 @@ __global__ __launch_bounds__(NT, 3) void xp_build_dma_kernel(
     for (int t = 0; t < 4; ++t) {
       const h8v th = *reinterpret_cast<const h8v*>(st + th_off + t * 2048);
       const h8v tl = *reinterpret_cast<const h8v*>(st + tl_off + t * 2048);
+      // small terms first
       if constexpr ((XP & 2) != 0) {
         acc[t][0] += (float)(th[0] + tl[1] + qh[2] + ql[3]);
       } else {
-        acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc2[t], 0, 0, 0);
-        acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc2[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc[t], 0, 0, 0);
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qh, acc[t], 0, 0, 0);
       }
     }
@@ -128,25 +129,27 @@ __global__ __launch_bounds__(NT, 3) void xp_build_dma_kernel(
   __builtin_amdgcn_s_barrier();   // ring reads done: the LDS is free for reuse
   const unsigned long long xt1 = (XP & 256) ? __builtin_amdgcn_s_memrealtime() : 0ull;
 
-  // combine (one rounding) and vote: a non-finite sum means an operand pixel
-  // was not finite; the page is then recomputed from the f32 operands
+  // vote: a non-finite sum means an operand pixel was not finite; the
+  // workgroup's pages are then recomputed from the f32 operands
   bool bad = false;
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      acc[t][r] = __builtin_fmaf(acc2[t][r], 0x1p-11f, acc[t][r]);
-      bad |= !(__builtin_fabsf(acc[t][r]) <= 3.40282347e38f);
-    }
+    for (int r = 0; r < 16; ++r) bad |= !(__builtin_fabsf(acc[t][r]) <= 3.40282347e38f);
   if (bad) *redo = 1;
   __syncthreads();
+  const bool live = pc.qblk + half < g.qt;            // this half's query block exists
+  const long long page = pc.page + (live ? (long long)half * g.tiles_h * g.tiles_w : 0);
   if (*redo) {
-    // IEEE semantics for the page (inf x finite = inf, inf x 0 = NaN, NaN
-    // propagates) as the reference's f32 matmul: the exact-f32 MFMA page build,
-    // K loop and epilogue (a split operand cannot carry inf: inf - inf = NaN)
-    build_page_f32<BV == 4 && !NHWC, 16, true, OT, DIV, NHWC>(
-        f1, f2, pyr, g, reinterpret_cast<float*>(smem), pc.page);
-    return;
+    // IEEE semantics (inf x finite = inf, inf x 0 = NaN, NaN propagates) as the
+    // reference's f32 matmul: corr_build_redo_kernel recomputes the pages on the
+    // exact-f32 MFMA
+    if (tid == 0) {
+      const int n = pc.qblk + 1 < g.qt ? 2 : 1;
+      const int at = atomicAdd(redo_list, n);
+      for (int h = 0; h < n; ++h)
+        redo_list[1 + at + h] = (int)(pc.page + (long long)h * g.tiles_h * g.tiles_w);
+    }
   } else {
     // undo the pixel scales: acc[t][r] is query qj x tile pixel (row 2t + kh, col r)
 #pragma unroll
@@ -161,25 +164,27 @@ __global__ __launch_bounds__(NT, 3) void xp_build_dma_kernel(
         acc[t][4 * u + 3] = __builtin_ldexpf(acc[t][4 * u + 3], -(sq + s4.w));
       }
     }
-  }
-  __syncthreads();   // exponent reads / fallback planes done before the staging reuse
-  scale_acc<DIV>(acc, g);
-  if constexpr ((XP & 1) != 0) {
-    float sum = 0.f;
+    if (live) {   // a half past the last query block has no page (epilogue syncs per wave)
+      scale_acc<DIV>(acc, g);
+      if constexpr ((XP & 1) != 0) {
+        float sum = 0.f;
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sum += acc[t][r];
-    if (sum == 1234.5f) pyr[tid] = to_out<OT>(sum);  // keeps the K loop live
-  } else {
-    paged_epilogue<OT, 1 | 4>(acc, reinterpret_cast<float*>(smem), pyr, g, pc.page, wave, lane);
+          for (int r = 0; r < 16; ++r) sum += acc[t][r];
+        if (sum == 1234.5f) pyr[tid] = to_out<OT>(sum);  // keeps the K loop live
+      } else {
+        paged_epilogue<OT, 1 | 4>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0,
+                                  pyr, g, page, w4, lane);
+      }
+    }
   }
   if constexpr ((XP & 256) != 0) {
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     const unsigned long long xt2 = __builtin_amdgcn_s_memrealtime();
     if (tid < 4) {
-      const long long wg = ((long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+      const long long wg = blockIdx.x;
       const unsigned long long hw = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
                                     ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(20 | (15 << 11)) << 32);
       trace[wg * 4 + tid] = tid == 0 ? xt0 : tid == 1 ? xt1 : tid == 2 ? xt2 : hw;
@@ -190,16 +195,18 @@ __global__ __launch_bounds__(NT, 3) void xp_build_dma_kernel(
 template <int XP>
 int xp_dma(const float* f1, const float* f2, float* pyr, const BuildGeom& g, int B, void* ws,
            unsigned long long* trace, hipStream_t stream) {
-  const dim3 grid = build_grid(g, B);
   const long long N = g.N, spb = align256((long long)B * g.D * N * 4), eb = align256((long long)B * N * 4);
   uint8_t* w = static_cast<uint8_t*>(ws);
   int* e1 = reinterpret_cast<int*>(w + 2 * spb);
   int* e2 = reinterpret_cast<int*>(w + 2 * spb + eb);
+  int* redo = reinterpret_cast<int*>(w + 2 * spb + 2 * eb);
   hipLaunchKernelGGL((split_pairs_kernel<false>), dim3((unsigned)((N + 63) / 64), (unsigned)B, 2),
                      dim3(1024), 0, stream, f1, f2, reinterpret_cast<uint4*>(w),
-                     reinterpret_cast<uint4*>(w + spb), e1, e2, g.D, g.N);
-  hipLaunchKernelGGL((xp_build_dma_kernel<float, false, 4, false, XP>), grid, dim3(NT), 0, stream,
-                     f1, f2, w, w + spb, e1, e2, pyr, g, trace);
+                     reinterpret_cast<uint4*>(w + spb), e1, e2, g.D, g.N, redo);
+  hipLaunchKernelGGL((xp_build_dma_kernel<float, false, XP>), remap_grid(g, B, 2), dim3(2 * NT), 0,
+                     stream, w, w + spb, e1, e2, pyr, redo, g, trace);
+  hipLaunchKernelGGL((corr_build_redo_kernel<float, false, true, false>), dim3(64), dim3(NT), 0,
+                     stream, f1, f2, pyr, redo, g);
   return dxr::launch_status();
 }
 
@@ -207,7 +214,7 @@ int xp_dma(const float* f1, const float* f2, float* pyr, const BuildGeom& g, int
 
 // Variant xp of the pre-split build (f32 NCHW fmaps, W % 4 == 0, D % 16 == 0,
 // sqrt(D) a power of two, 4 levels); ws as dxr_corr_pyramid_build_ws; trace:
-// 4 x u64 per page when xp has bit 8.
+// 4 x u64 per workgroup when xp has bit 8.
 extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t D, int64_t H,
                             int64_t W, float* pyr, void* ws, int xp, unsigned long long* trace,
                             hipStream_t stream) {
@@ -220,8 +227,6 @@ extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t
     case 1: return xp_dma<1>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     case 2: return xp_dma<2>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     case 3: return xp_dma<3>(f1, f2, pyr, g, (int)B, ws, trace, stream);
-    case 4: return xp_dma<4>(f1, f2, pyr, g, (int)B, ws, trace, stream);
-    case 5: return xp_dma<5>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     case 256: return xp_dma<256>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     case 257: return xp_dma<257>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     default: return DXR_EINVAL;
