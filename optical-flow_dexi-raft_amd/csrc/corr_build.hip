@@ -1231,21 +1231,19 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
 //     16-channel block) and E [N] int32 exponents s.  A pixel with a non-finite
 //     channel keeps s = 0: its inf/NaN reaches the accumulators and the build
 //     recomputes those pages from the f32 operands on the exact-f32 MFMA.
-// (2) corr_build_dma_kernel: 16 waves = two query blocks x two 8x16 target
-//     tiles (four pages), each query block shared by the waves of both tiles and
-//     each tile by the waves of both blocks: 32 KB of operands per 16-k step for
-//     four pages (the r02 build: 16 KB per page; operand traffic into the CU —
-//     the texture path, busy 84 % in a two-page form — is what bounds the loop).
-//     The K loop moves operands only by LDS-DMA (buffer_load ... lds, 16 B per
-//     lane) into a 4-stage ring (3 steps in flight), so no VGPRs are held by
-//     loads in flight and no VALU splits in the loop: per step a wave waits for
-//     its own 2 DMAs of the step (vmcnt), one barrier publishes the stage, then
-//     10 conflict-free ds_read_b128 and 12 f16 MFMAs — lo*hi, hi*lo, hi*hi into
-//     ONE f32 accumulator (f16 x f16 products are exact in f32; 3 roundings per
-//     16 k against the exact-f32 MFMA's 8).  With a single accumulator per
-//     output (64 VGPRs instead of the r02 split build's 128) 16 waves fit at 4
-//     per SIMD.  The epilogue undoes both pixels' scales (ldexp by -(s_q + s_t),
-//     exact) and writes the paged pyramid as before.
+// (2) corr_build_dma_kernel: 8 waves = two query blocks (waves 0-3, 4-7) x one
+//     8x16 target tile, the tile shared by both (24 KB per 16-k step instead of
+//     2 x 16 KB for two single-block pages).  The K loop moves operands only by
+//     LDS-DMA (buffer_load ... lds, 16 B per lane) into a 3-stage ring, so no
+//     VGPRs are held by loads in flight and no VALU splits in the loop: per step
+//     a wave waits for its own 3 DMAs of the step (vmcnt), one barrier publishes
+//     the tile, then 10 conflict-free ds_read_b128 and 12 f16 MFMAs — lo*hi,
+//     hi*lo, hi*hi into ONE f32 accumulator (f16 x f16 products are exact in
+//     f32; 3 roundings per 16 k against the exact-f32 MFMA's 8).  With a single
+//     accumulator per output (64 VGPRs instead of the r02 split build's 128) the
+//     kernel fits 4 waves per SIMD: two workgroups per CU.  The epilogue undoes
+//     both pixels' scales (ldexp by -(s_q + s_t), exact) and writes the paged
+//     pyramid as before.
 // LDS image rows are 64 B (hi k0-7, hi k8-15, lo k0-7, lo k8-15 in 16-B slots);
 // the slots of a row are XOR-permuted by a row key so that every 16-lane group
 // of a ds_read_b128 hits 16 distinct bank slots; the DMA writes lane-linearly,
@@ -1256,12 +1254,9 @@ __global__ __launch_bounds__(NT, MINW) void corr_build_split_kernel(const float*
 // col (j & 3) + 4 (j >> 3)).
 // ---------------------------------------------------------------------------
 constexpr int SPLIT_S_TOP = 14;          // |x 2^s| < 2^SPLIT_S_TOP
-constexpr int DMA_RING = 4;              // ring stages (k16 steps in LDS; 3 in flight)
-constexpr int DMA_QB = 2;                // query blocks per workgroup
-constexpr int DMA_TB = 2;                // target tiles per workgroup
-constexpr int DMA_WAVES = 4 * DMA_QB * DMA_TB;       // 16: one wave = 32 queries x one tile
-constexpr int DMA_TILE = DMA_QB * 8192;  // tile images' offset in a stage
-constexpr int DMA_STAGE = DMA_TILE + DMA_TB * 8192;  // bytes per stage (32 KB)
+constexpr int DMA_RING = 3;              // ring stages (k16 steps in LDS)
+constexpr int DMA_TILE = 16384;          // tile offset in a stage: 8 waves x 2 KB queries
+constexpr int DMA_STAGE = DMA_TILE + 8192;   // bytes per stage
 
 __device__ __forceinline__ int pixel_scale(float m, bool finite) {
   if (!finite || !(m > 0.f)) return 0;
@@ -1366,82 +1361,42 @@ __global__ __launch_bounds__(1024) void split_pairs_kernel(const float* __restri
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-// Workgroup -> (pair, query-block pair, tile pair), laid out for the per-XCD
-// L2s as page_coord<true, QB> does for pages: XCD k takes the k-th contiguous
-// band of a linear order that walks strips of STRIP tile pairs query-pair-major.
-struct DmaCoord {
-  int b, qp, tp;   // pair, first query block / 2, first tile / 2
-};
-__device__ __forceinline__ DmaCoord dma_coord(const BuildGeom& g) {
-  const int T2 = (g.tiles_w * g.tiles_h + DMA_TB - 1) / DMA_TB;
-  const int Q2 = (g.qt + DMA_QB - 1) / DMA_QB;
-  const long long per_pair = (long long)Q2 * T2;
-  const long long nwg = gridDim.x, w = blockIdx.x;
-  const long long q8 = nwg / 8, r8 = nwg % 8, xcd = w % 8;
-  const long long wl = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + w / 8;
-  DmaCoord c;
-  c.b = (int)(wl / per_pair);
-  const int rem = (int)(wl - c.b * per_pair);
-  const int nfull = T2 / STRIP;
-  if (rem < nfull * Q2 * STRIP) {
-    const int st = rem / (Q2 * STRIP), in = rem - st * Q2 * STRIP;
-    c.qp = in / STRIP;
-    c.tp = st * STRIP + in % STRIP;
-  } else {
-    const int nl = T2 - nfull * STRIP, in = rem - nfull * Q2 * STRIP;
-    c.qp = in / nl;
-    c.tp = nfull * STRIP + in % nl;
-  }
-  return c;
-}
-
-// One workgroup = 16 waves = DMA_QB (2) query blocks x DMA_TB (2) target tiles
-// (four pages); wave w holds 32 queries of block (w >> 2) & 1 against tile
-// w >> 3.  Per 16-k step the ring stage holds both query blocks (8 KB each)
-// and both tiles (8 KB each): 32 KB for four pages, every image read by the
-// eight waves that need it.
 // Pages whose sums are not finite (an inf/NaN operand pixel) are not written
-// here: their indices go to `redo_list` (count in [0], pages from [1]) for
-// corr_build_redo_kernel, launched after this kernel.  Grid: dma_grid().
+// here: their indices go to `redo` (count in redo[0], pages from redo[1]) for
+// corr_build_redo_kernel, launched after this kernel.  Grid:
+// remap_grid(g, B, 2) (page_coord<true, 2>).
 template <typename OT, bool DIV>
-__global__ __launch_bounds__(DMA_WAVES * 64, 4) void corr_build_dma_kernel(
+__global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
     const uint8_t* __restrict__ sp1, const uint8_t* __restrict__ sp2, const int* __restrict__ ex1,
     const int* __restrict__ ex2, OT* __restrict__ pyr, int* __restrict__ redo_list, BuildGeom g) {
   constexpr int LDS_RING = DMA_RING * DMA_STAGE;
-  constexpr int LDS_E = DMA_WAVES * 16 * P0 * 4;          // epilogue staging (16 waves)
-  constexpr int LDS_MAIN = LDS_RING > LDS_E ? LDS_RING : LDS_E;
-  // one LDS array (cdna_hip_programming.md §5 item 4(a)): ring / staging |
-  // target exponents (DMA_TB x 128 int) | redo flag
-  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_MAIN + DMA_TB * NTGT * 4 + 16];
-  int* const sexp = reinterpret_cast<int*>(smem + LDS_MAIN);
-  int* const redo = reinterpret_cast<int*>(smem + LDS_MAIN + DMA_TB * NTGT * 4);
+  constexpr int LDS_E = 2 * WAVES * 16 * P0 * 4;          // epilogue staging (8 waves)
+  static_assert(LDS_E <= LDS_RING, "the epilogue staging aliases the ring");
+  // one LDS array (cdna_hip_programming.md §5 item 4(a)): ring | target
+  // exponents (128 int) | redo flag
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_RING + NTGT * 4 + 16];
+  int* const sexp = reinterpret_cast<int*>(smem + LDS_RING);
+  int* const redo = reinterpret_cast<int*>(smem + LDS_RING + NTGT * 4);
 
   const int tid = threadIdx.x, lane = tid & 63;
   // wave-uniform (SGPR): the DMA's LDS base must be, or the compiler emits a
   // waterfall loop around every buffer_load ... lds
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int qb = (wave >> 2) & (DMA_QB - 1), tb = wave >> 3, w4 = wave & 3;
-  const DmaCoord dc = dma_coord(g);
-  const int b = dc.b;
-  const int T = g.tiles_w * g.tiles_h;
-  const int q0 = dc.qp * DMA_QB * BM;                 // first query of the workgroup
+  const int half = wave >> 2, w4 = wave & 3;
+  const PageCoord pc = page_coord<true, 2>(g);
+  const int th0 = pc.tyi * TH, tw0 = pc.txi * TW;
+  const int q0 = pc.qblk * BM;                        // first of the two blocks
+  const int b = pc.b;
   const int j = lane & 31, kh = lane >> 5;
   const long long spstride = (long long)g.D * g.N * 4;   // SP bytes per pair
-  auto tile_origin = [&](int t, int& th, int& tw) {       // t: tile index in the image
-    const int ty = t / g.tiles_w;
-    th = ty * TH;
-    tw = (t - ty * g.tiles_w) * TW;
-  };
 
-  // exponents: the lane's query, the tiles' targets (LDS, by tile pixel)
-  const int qj = q0 + qb * BM + w4 * 32 + j;
+  // exponents: the lane's query, the tile's 128 targets (LDS, by tile pixel)
+  const int qj = q0 + wave * 32 + j;
   const int sq = qj < g.N ? ex1[(long long)b * g.N + qj] : 0;
-  if (tid < DMA_TB * NTGT) {
-    const int t = dc.tp * DMA_TB + (tid >> 7), r = (tid >> 4) & 7, c = tid & 15;
-    int th, tw;
-    tile_origin(t, th, tw);
-    const bool in = t < T && th + r < g.H && tw + c < g.W;
-    sexp[tid] = in ? ex2[(long long)b * g.N + (th + r) * g.W + tw + c] : 0;
+  if (tid < NTGT) {
+    const int r = tid >> 4, c = tid & 15;
+    const bool in = th0 + r < g.H && tw0 + c < g.W;
+    sexp[tid] = in ? ex2[(long long)b * g.N + (th0 + r) * g.W + tw0 + c] : 0;
   }
   if (tid == 0) *redo = 0;
 
@@ -1451,55 +1406,41 @@ __global__ __launch_bounds__(DMA_WAVES * 64, 4) void corr_build_dma_kernel(
   const __amdgpu_buffer_rsrc_t rt =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sp2 + b * spstride), (short)0,
                                         (int)spstride, 0x00020000);
-  // DMA instructions of a step: 8 per query block (16 rows x 64 B each), then
-  // 8 per tile (one tile row each); wave w issues numbers 2w and 2w + 1.
-  uint32_t vsrc[2];
-  bool isq[2];
-  int ldsoff[2];
+  // DMA source offsets (fixed over K; the step's offset ks * N * 64 in soffset).
+  // Query instruction i of this wave: LDS rows 16 i + (lane >> 2) of the wave's
+  // 2 KB region; target instruction: tile row r = wave.
+  uint32_t vq[2], vt;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int n = 2 * wave + i, ps = lane & 3;
-    if (n < DMA_QB * 8) {
-      const int blk = n >> 3, row = 16 * (n & 7) + (lane >> 2);
-      const int q = q0 + blk * BM + row;
-      const int cq = ps ^ ((row >> 2) & 3);
-      vsrc[i] = q < g.N ? (uint32_t)(q * 64 + 16 * cq) : 0x80000000u;
-      isq[i] = true;
-      ldsoff[i] = blk * 8192 + (n & 7) * 1024;
-    } else {
-      const int m = n - DMA_QB * 8, tt = m >> 3, r = m & 7, col = lane >> 2;
-      const int trow = r * 16 + col;
-      const int ct = ps ^ (((trow >> 2) & 1) | ((trow >> 3) & 2));
-      const int t = dc.tp * DMA_TB + tt;
-      int th, tw;
-      tile_origin(t, th, tw);
-      const int hh = th + r, ww = tw + col;
-      vsrc[i] = (t < T && hh < g.H && ww < g.W) ? (uint32_t)((hh * g.W + ww) * 64 + 16 * ct)
-                                                 : 0x80000000u;
-      isq[i] = false;
-      ldsoff[i] = DMA_TILE + tt * 8192 + r * 1024;
-    }
+    const int row = 16 * i + (lane >> 2), ps = lane & 3;
+    const int q = q0 + wave * 32 + row;
+    const int cq = ps ^ ((row >> 2) & 3);
+    vq[i] = q < g.N ? (uint32_t)(q * 64 + 16 * cq) : 0x80000000u;
   }
-  const bool q0s = isq[0], q1s = isq[1];   // wave-uniform
-  const int l0 = __builtin_amdgcn_readfirstlane(ldsoff[0]);
-  const int l1 = __builtin_amdgcn_readfirstlane(ldsoff[1]);
+  {
+    const int ps = lane & 3, r = wave, col = lane >> 2, trow = r * 16 + col;
+    const int ct = ps ^ (((trow >> 2) & 1) | ((trow >> 3) & 2));
+    const int hh = th0 + r, ww = tw0 + col;
+    vt = (hh < g.H && ww < g.W) ? (uint32_t)((hh * g.W + ww) * 64 + 16 * ct) : 0x80000000u;
+  }
   auto dma = [&](int ks) {
     unsigned char* st = smem + (ks % DMA_RING) * DMA_STAGE;
     const int so = ks * g.N * 64;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(q0s ? rq : rt, (lds_void_t*)(st + l0), 16, vsrc[0],
-                                             so, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(q1s ? rq : rt, (lds_void_t*)(st + l1), 16, vsrc[1],
-                                             so, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rq, (lds_void_t*)(st + wave * 2048 + i * 1024), 16, vq[i], so, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (lds_void_t*)(st + DMA_TILE + wave * 1024), 16,
+                                             vt, so, 0, 0);
   };
   // fragment byte offsets within a stage (hi; lo = the other two slots)
   const int kq = (j >> 2) & 3;
-  const int qrow = (qb * BM + w4 * 32 + j) * 64;
-  const int qh_off = qrow + 16 * (kh ^ kq);
-  const int ql_off = qrow + 16 * ((2 + kh) ^ kq);
-  const int trow0 = ((j >> 2) & 1) * 16 + (j & 3) + 4 * (j >> 3);     // MFMA tile t adds 32 rows
+  const int qh_off = wave * 2048 + j * 64 + 16 * (kh ^ kq);
+  const int ql_off = wave * 2048 + j * 64 + 16 * ((2 + kh) ^ kq);
+  const int trow0 = ((j >> 2) & 1) * 16 + (j & 3) + 4 * (j >> 3);     // tile t adds 32 rows
   const int kt = ((trow0 >> 2) & 1) | ((trow0 >> 3) & 2);
-  const int th_off = DMA_TILE + tb * 8192 + trow0 * 64 + 16 * (kh ^ kt);
-  const int tl_off = DMA_TILE + tb * 8192 + trow0 * 64 + 16 * ((2 + kh) ^ kt);
+  const int th_off = DMA_TILE + trow0 * 64 + 16 * (kh ^ kt);
+  const int tl_off = DMA_TILE + trow0 * 64 + 16 * ((2 + kh) ^ kt);
 
   f32x16 acc[4];
 #pragma unroll
@@ -1510,21 +1451,18 @@ __global__ __launch_bounds__(DMA_WAVES * 64, 4) void corr_build_dma_kernel(
   // exponent loads and LDS writes above must not count against the ring's vmcnt
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int nk = g.D / BKS;
-  static_assert(DMA_RING == 4, "the vmcnt waits below assume 3 steps in flight");
   dma(0);
   if (nk > 1) dma(1);
-  if (nk > 2) dma(2);
   for (int ks = 0; ks < nk; ++ks) {
-    // this wave's 2 DMAs of step ks have landed (those of ks + 1, ks + 2 stay in
-    // flight); the barrier publishes every wave's, and orders the ring slot's
-    // previous readers (step ks - 1) before the refill below
-    if (ks + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if (ks + 1 < nk) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    // this wave's 3 DMAs of step ks have landed (those of ks + 1 stay in flight);
+    // the barrier publishes every wave's, and orders the ring slot's previous
+    // readers (step ks - 1) before the refill below
+    if (ks + 1 < nk) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (ks + 3 < nk) dma(ks + 3);
+    if (ks + 2 < nk) dma(ks + 2);
     const unsigned char* st = smem + (ks % DMA_RING) * DMA_STAGE;
     const h8v qh = *reinterpret_cast<const h8v*>(st + qh_off);
     const h8v ql = *reinterpret_cast<const h8v*>(st + ql_off);
@@ -1541,7 +1479,8 @@ __global__ __launch_bounds__(DMA_WAVES * 64, 4) void corr_build_dma_kernel(
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();   // ring reads done: the LDS is free for reuse
 
-  // vote: a non-finite sum means an operand pixel was not finite
+  // vote: a non-finite sum means an operand pixel was not finite; the
+  // workgroup's pages are then recomputed from the f32 operands
   bool bad = false;
 #pragma unroll
   for (int t = 0; t < 4; ++t)
@@ -1549,23 +1488,23 @@ __global__ __launch_bounds__(DMA_WAVES * 64, 4) void corr_build_dma_kernel(
     for (int r = 0; r < 16; ++r) bad |= !(__builtin_fabsf(acc[t][r]) <= 3.40282347e38f);
   if (bad) *redo = 1;
   __syncthreads();
-  // this wave's page: query block 2 qp + qb, tile 2 tp + tb (if both exist)
-  const int qblk = dc.qp * DMA_QB + qb, tile = dc.tp * DMA_TB + tb;
-  const bool live = qblk < g.qt && tile < T;
-  const long long page = ((long long)b * g.qt + qblk) * T + tile;
+  const bool live = pc.qblk + half < g.qt;            // this half's query block exists
+  const long long page = pc.page + (live ? (long long)half * g.tiles_h * g.tiles_w : 0);
   if (*redo) {
     // IEEE semantics (inf x finite = inf, inf x 0 = NaN, NaN propagates) as the
-    // reference's f32 matmul: corr_build_redo_kernel recomputes the workgroup's
-    // pages on the exact-f32 MFMA
-    if (live && (lane | w4) == 0) {
-      const int at = atomicAdd(redo_list, 1);
-      redo_list[1 + at] = (int)page;
+    // reference's f32 matmul: corr_build_redo_kernel recomputes the pages on the
+    // exact-f32 MFMA
+    if (tid == 0) {
+      const int n = pc.qblk + 1 < g.qt ? 2 : 1;
+      const int at = atomicAdd(redo_list, n);
+      for (int h = 0; h < n; ++h)
+        redo_list[1 + at + h] = (int)(pc.page + (long long)h * g.tiles_h * g.tiles_w);
     }
   } else {
     // undo the pixel scales: acc[t][r] is query qj x tile pixel (row 2t + kh, col r)
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int4* se = reinterpret_cast<const int4*>(sexp + tb * NTGT + (2 * t + kh) * 16);
+      const int4* se = reinterpret_cast<const int4*>(sexp + (2 * t + kh) * 16);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int4 s4 = se[u];
@@ -1575,10 +1514,10 @@ __global__ __launch_bounds__(DMA_WAVES * 64, 4) void corr_build_dma_kernel(
         acc[t][4 * u + 3] = __builtin_ldexpf(acc[t][4 * u + 3], -(sq + s4.w));
       }
     }
-    if (live) {   // a wave without a page skips the epilogue (its syncs are per wave)
+    if (live) {   // a half past the last query block has no page (epilogue syncs per wave)
       scale_acc<DIV>(acc, g);
-      paged_epilogue<OT, 1 | 4>(acc, reinterpret_cast<float*>(smem) + (wave >> 2) * WAVES * 16 * P0,
-                                pyr, g, page, w4, lane);
+      paged_epilogue<OT, 1 | 4>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0, pyr,
+                                g, page, w4, lane);
     }
   }
 }
@@ -1840,14 +1779,6 @@ int launch_split(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, 
   return dxr::launch_status();
 }
 
-// Grid of corr_build_dma_kernel: one workgroup per (pair, query-block pair,
-// tile pair).
-dim3 dma_grid(const BuildGeom& g, int B) {
-  const long long T2 = (g.tiles_w * g.tiles_h + DMA_TB - 1) / DMA_TB;
-  const long long Q2 = (g.qt + DMA_QB - 1) / DMA_QB;
-  return dim3((unsigned)(B * Q2 * T2));
-}
-
 // The pages corr_build_dma_kernel listed as not finite, on the exact-f32 MFMA
 // (normally none: every workgroup reads the count and leaves).
 template <typename OT, bool DIV, bool VEC, bool NHWC>
@@ -1893,13 +1824,13 @@ int launch_dma(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, in
                      reinterpret_cast<uint4*>(sp2), e1, e2, g.D, g.N, redo);
   int st = dxr::launch_status();
   if (st != DXR_OK) return st;
-  const dim3 rg = dma_grid(g, B);
+  const dim3 rg = remap_grid(g, B, 2);
   if (g.recip == 0.f)
-    hipLaunchKernelGGL((corr_build_dma_kernel<OT, true>), rg, dim3(DMA_WAVES * 64), 0, stream, sp1,
-                       sp2, e1, e2, pyr, redo, g);
+    hipLaunchKernelGGL((corr_build_dma_kernel<OT, true>), rg, dim3(2 * NT), 0, stream, sp1, sp2,
+                       e1, e2, pyr, redo, g);
   else
-    hipLaunchKernelGGL((corr_build_dma_kernel<OT, false>), rg, dim3(DMA_WAVES * 64), 0, stream, sp1,
-                       sp2, e1, e2, pyr, redo, g);
+    hipLaunchKernelGGL((corr_build_dma_kernel<OT, false>), rg, dim3(2 * NT), 0, stream, sp1, sp2,
+                       e1, e2, pyr, redo, g);
   st = dxr::launch_status();
   if (st != DXR_OK) return st;
   constexpr bool VEC = BV == 4 && !NHWC;

@@ -6,49 +6,44 @@
 namespace {
 
 // XP bits: 0 skip the epilogue stores (K loop kept live), 1 skip the MFMAs,
-// 8 record per-workgroup s_memrealtime stamps {start, K loop done, epilogue
-// stores done, hw id}.
+// 2 no DMA after the first two ring stages (the loop reads those two stages
+// again: same finite data, timing only), 3 no barrier in the K loop (timing
+// only), 8 record per-workgroup s_memrealtime stamps {start, K loop done,
+// epilogue stores done, hw id}.
 template <typename OT, bool DIV, int XP>
-__global__ __launch_bounds__(DMA_WAVES * 64, 4) void xp_build_dma_kernel(
+__global__ __launch_bounds__(2 * NT, 4) void xp_build_dma_kernel(
     const uint8_t* __restrict__ sp1, const uint8_t* __restrict__ sp2, const int* __restrict__ ex1,
     const int* __restrict__ ex2, OT* __restrict__ pyr, int* __restrict__ redo_list, BuildGeom g,
     unsigned long long* __restrict__ trace) {
   const unsigned long long xt0 = (XP & 256) ? __builtin_amdgcn_s_memrealtime() : 0ull;
   constexpr int LDS_RING = DMA_RING * DMA_STAGE;
-  constexpr int LDS_E = DMA_WAVES * 16 * P0 * 4;          // epilogue staging (16 waves)
-  constexpr int LDS_MAIN = LDS_RING > LDS_E ? LDS_RING : LDS_E;
-  // one LDS array (cdna_hip_programming.md §5 item 4(a)): ring / staging |
-  // target exponents (DMA_TB x 128 int) | redo flag
-  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_MAIN + DMA_TB * NTGT * 4 + 16];
-  int* const sexp = reinterpret_cast<int*>(smem + LDS_MAIN);
-  int* const redo = reinterpret_cast<int*>(smem + LDS_MAIN + DMA_TB * NTGT * 4);
+  constexpr int LDS_E = 2 * WAVES * 16 * P0 * 4;          // epilogue staging (8 waves)
+  static_assert(LDS_E <= LDS_RING, "the epilogue staging aliases the ring");
+  // one LDS array (cdna_hip_programming.md §5 item 4(a)): ring | target
+  // exponents (128 int) | redo flag
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_RING + NTGT * 4 + 16];
+  int* const sexp = reinterpret_cast<int*>(smem + LDS_RING);
+  int* const redo = reinterpret_cast<int*>(smem + LDS_RING + NTGT * 4);
 
   const int tid = threadIdx.x, lane = tid & 63;
   // wave-uniform (SGPR): the DMA's LDS base must be, or the compiler emits a
   // waterfall loop around every buffer_load ... lds
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int qb = (wave >> 2) & (DMA_QB - 1), tb = wave >> 3, w4 = wave & 3;
-  const DmaCoord dc = dma_coord(g);
-  const int b = dc.b;
-  const int T = g.tiles_w * g.tiles_h;
-  const int q0 = dc.qp * DMA_QB * BM;                 // first query of the workgroup
+  const int half = wave >> 2, w4 = wave & 3;
+  const PageCoord pc = page_coord<true, 2>(g);
+  const int th0 = pc.tyi * TH, tw0 = pc.txi * TW;
+  const int q0 = pc.qblk * BM;                        // first of the two blocks
+  const int b = pc.b;
   const int j = lane & 31, kh = lane >> 5;
   const long long spstride = (long long)g.D * g.N * 4;   // SP bytes per pair
-  auto tile_origin = [&](int t, int& th, int& tw) {       // t: tile index in the image
-    const int ty = t / g.tiles_w;
-    th = ty * TH;
-    tw = (t - ty * g.tiles_w) * TW;
-  };
 
-  // exponents: the lane's query, the tiles' targets (LDS, by tile pixel)
-  const int qj = q0 + qb * BM + w4 * 32 + j;
+  // exponents: the lane's query, the tile's 128 targets (LDS, by tile pixel)
+  const int qj = q0 + wave * 32 + j;
   const int sq = qj < g.N ? ex1[(long long)b * g.N + qj] : 0;
-  if (tid < DMA_TB * NTGT) {
-    const int t = dc.tp * DMA_TB + (tid >> 7), r = (tid >> 4) & 7, c = tid & 15;
-    int th, tw;
-    tile_origin(t, th, tw);
-    const bool in = t < T && th + r < g.H && tw + c < g.W;
-    sexp[tid] = in ? ex2[(long long)b * g.N + (th + r) * g.W + tw + c] : 0;
+  if (tid < NTGT) {
+    const int r = tid >> 4, c = tid & 15;
+    const bool in = th0 + r < g.H && tw0 + c < g.W;
+    sexp[tid] = in ? ex2[(long long)b * g.N + (th0 + r) * g.W + tw0 + c] : 0;
   }
   if (tid == 0) *redo = 0;
 
@@ -58,55 +53,41 @@ __global__ __launch_bounds__(DMA_WAVES * 64, 4) void xp_build_dma_kernel(
   const __amdgpu_buffer_rsrc_t rt =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sp2 + b * spstride), (short)0,
                                         (int)spstride, 0x00020000);
-  // DMA instructions of a step: 8 per query block (16 rows x 64 B each), then
-  // 8 per tile (one tile row each); wave w issues numbers 2w and 2w + 1.
-  uint32_t vsrc[2];
-  bool isq[2];
-  int ldsoff[2];
+  // DMA source offsets (fixed over K; the step's offset ks * N * 64 in soffset).
+  // Query instruction i of this wave: LDS rows 16 i + (lane >> 2) of the wave's
+  // 2 KB region; target instruction: tile row r = wave.
+  uint32_t vq[2], vt;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int n = 2 * wave + i, ps = lane & 3;
-    if (n < DMA_QB * 8) {
-      const int blk = n >> 3, row = 16 * (n & 7) + (lane >> 2);
-      const int q = q0 + blk * BM + row;
-      const int cq = ps ^ ((row >> 2) & 3);
-      vsrc[i] = q < g.N ? (uint32_t)(q * 64 + 16 * cq) : 0x80000000u;
-      isq[i] = true;
-      ldsoff[i] = blk * 8192 + (n & 7) * 1024;
-    } else {
-      const int m = n - DMA_QB * 8, tt = m >> 3, r = m & 7, col = lane >> 2;
-      const int trow = r * 16 + col;
-      const int ct = ps ^ (((trow >> 2) & 1) | ((trow >> 3) & 2));
-      const int t = dc.tp * DMA_TB + tt;
-      int th, tw;
-      tile_origin(t, th, tw);
-      const int hh = th + r, ww = tw + col;
-      vsrc[i] = (t < T && hh < g.H && ww < g.W) ? (uint32_t)((hh * g.W + ww) * 64 + 16 * ct)
-                                                 : 0x80000000u;
-      isq[i] = false;
-      ldsoff[i] = DMA_TILE + tt * 8192 + r * 1024;
-    }
+    const int row = 16 * i + (lane >> 2), ps = lane & 3;
+    const int q = q0 + wave * 32 + row;
+    const int cq = ps ^ ((row >> 2) & 3);
+    vq[i] = q < g.N ? (uint32_t)(q * 64 + 16 * cq) : 0x80000000u;
   }
-  const bool q0s = isq[0], q1s = isq[1];   // wave-uniform
-  const int l0 = __builtin_amdgcn_readfirstlane(ldsoff[0]);
-  const int l1 = __builtin_amdgcn_readfirstlane(ldsoff[1]);
+  {
+    const int ps = lane & 3, r = wave, col = lane >> 2, trow = r * 16 + col;
+    const int ct = ps ^ (((trow >> 2) & 1) | ((trow >> 3) & 2));
+    const int hh = th0 + r, ww = tw0 + col;
+    vt = (hh < g.H && ww < g.W) ? (uint32_t)((hh * g.W + ww) * 64 + 16 * ct) : 0x80000000u;
+  }
   auto dma = [&](int ks) {
     unsigned char* st = smem + (ks % DMA_RING) * DMA_STAGE;
     const int so = ks * g.N * 64;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(q0s ? rq : rt, (lds_void_t*)(st + l0), 16, vsrc[0],
-                                             so, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(q1s ? rq : rt, (lds_void_t*)(st + l1), 16, vsrc[1],
-                                             so, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rq, (lds_void_t*)(st + wave * 2048 + i * 1024), 16, vq[i], so, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (lds_void_t*)(st + DMA_TILE + wave * 1024), 16,
+                                             vt, so, 0, 0);
   };
   // fragment byte offsets within a stage (hi; lo = the other two slots)
   const int kq = (j >> 2) & 3;
-  const int qrow = (qb * BM + w4 * 32 + j) * 64;
-  const int qh_off = qrow + 16 * (kh ^ kq);
-  const int ql_off = qrow + 16 * ((2 + kh) ^ kq);
-  const int trow0 = ((j >> 2) & 1) * 16 + (j & 3) + 4 * (j >> 3);     // MFMA tile t adds 32 rows
+  const int qh_off = wave * 2048 + j * 64 + 16 * (kh ^ kq);
+  const int ql_off = wave * 2048 + j * 64 + 16 * ((2 + kh) ^ kq);
+  const int trow0 = ((j >> 2) & 1) * 16 + (j & 3) + 4 * (j >> 3);     // tile t adds 32 rows
   const int kt = ((trow0 >> 2) & 1) | ((trow0 >> 3) & 2);
-  const int th_off = DMA_TILE + tb * 8192 + trow0 * 64 + 16 * (kh ^ kt);
-  const int tl_off = DMA_TILE + tb * 8192 + trow0 * 64 + 16 * ((2 + kh) ^ kt);
+  const int th_off = DMA_TILE + trow0 * 64 + 16 * (kh ^ kt);
+  const int tl_off = DMA_TILE + trow0 * 64 + 16 * ((2 + kh) ^ kt);
 
   f32x16 acc[4];
 #pragma unroll
@@ -117,22 +98,23 @@ __global__ __launch_bounds__(DMA_WAVES * 64, 4) void xp_build_dma_kernel(
   // exponent loads and LDS writes above must not count against the ring's vmcnt
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int nk = g.D / BKS;
-  static_assert(DMA_RING == 4, "the vmcnt waits below assume 3 steps in flight");
   dma(0);
   if (nk > 1) dma(1);
-  if (nk > 2) dma(2);
   for (int ks = 0; ks < nk; ++ks) {
-    // this wave's 2 DMAs of step ks have landed (those of ks + 1, ks + 2 stay in
-    // flight); the barrier publishes every wave's, and orders the ring slot's
-    // previous readers (step ks - 1) before the refill below
-    if (ks + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if (ks + 1 < nk) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // this wave's 3 DMAs of step ks have landed (those of ks + 1 stay in flight);
+    // the barrier publishes every wave's, and orders the ring slot's previous
+    // readers (step ks - 1) before the refill below
+    if constexpr ((XP & 4) == 0) {
+      if (ks + 1 < nk) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (ks < 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if constexpr ((XP & 8) == 0) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (ks + 3 < nk) dma(ks + 3);
-    const unsigned char* st = smem + (ks % DMA_RING) * DMA_STAGE;
+    if (ks + 2 < nk && (XP & 4) == 0) dma(ks + 2);
+    const unsigned char* st = smem + ((XP & 4) ? (ks & 1) : (ks % DMA_RING)) * DMA_STAGE;
     const h8v qh = *reinterpret_cast<const h8v*>(st + qh_off);
     const h8v ql = *reinterpret_cast<const h8v*>(st + ql_off);
 #pragma unroll
@@ -153,7 +135,8 @@ __global__ __launch_bounds__(DMA_WAVES * 64, 4) void xp_build_dma_kernel(
   __builtin_amdgcn_s_barrier();   // ring reads done: the LDS is free for reuse
   const unsigned long long xt1 = (XP & 256) ? __builtin_amdgcn_s_memrealtime() : 0ull;
 
-  // vote: a non-finite sum means an operand pixel was not finite
+  // vote: a non-finite sum means an operand pixel was not finite; the
+  // workgroup's pages are then recomputed from the f32 operands
   bool bad = false;
 #pragma unroll
   for (int t = 0; t < 4; ++t)
@@ -161,23 +144,23 @@ __global__ __launch_bounds__(DMA_WAVES * 64, 4) void xp_build_dma_kernel(
     for (int r = 0; r < 16; ++r) bad |= !(__builtin_fabsf(acc[t][r]) <= 3.40282347e38f);
   if (bad) *redo = 1;
   __syncthreads();
-  // this wave's page: query block 2 qp + qb, tile 2 tp + tb (if both exist)
-  const int qblk = dc.qp * DMA_QB + qb, tile = dc.tp * DMA_TB + tb;
-  const bool live = qblk < g.qt && tile < T;
-  const long long page = ((long long)b * g.qt + qblk) * T + tile;
+  const bool live = pc.qblk + half < g.qt;            // this half's query block exists
+  const long long page = pc.page + (live ? (long long)half * g.tiles_h * g.tiles_w : 0);
   if (*redo) {
     // IEEE semantics (inf x finite = inf, inf x 0 = NaN, NaN propagates) as the
-    // reference's f32 matmul: corr_build_redo_kernel recomputes the workgroup's
-    // pages on the exact-f32 MFMA
-    if (live && (lane | w4) == 0) {
-      const int at = atomicAdd(redo_list, 1);
-      redo_list[1 + at] = (int)page;
+    // reference's f32 matmul: corr_build_redo_kernel recomputes the pages on the
+    // exact-f32 MFMA
+    if (tid == 0) {
+      const int n = pc.qblk + 1 < g.qt ? 2 : 1;
+      const int at = atomicAdd(redo_list, n);
+      for (int h = 0; h < n; ++h)
+        redo_list[1 + at + h] = (int)(pc.page + (long long)h * g.tiles_h * g.tiles_w);
     }
   } else {
     // undo the pixel scales: acc[t][r] is query qj x tile pixel (row 2t + kh, col r)
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int4* se = reinterpret_cast<const int4*>(sexp + tb * NTGT + (2 * t + kh) * 16);
+      const int4* se = reinterpret_cast<const int4*>(sexp + (2 * t + kh) * 16);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int4 s4 = se[u];
@@ -187,7 +170,7 @@ __global__ __launch_bounds__(DMA_WAVES * 64, 4) void xp_build_dma_kernel(
         acc[t][4 * u + 3] = __builtin_ldexpf(acc[t][4 * u + 3], -(sq + s4.w));
       }
     }
-    if (live) {   // a wave without a page skips the epilogue (its syncs are per wave)
+    if (live) {   // a half past the last query block has no page (epilogue syncs per wave)
       scale_acc<DIV>(acc, g);
       if constexpr ((XP & 1) != 0) {
         float sum = 0.f;
@@ -197,7 +180,7 @@ __global__ __launch_bounds__(DMA_WAVES * 64, 4) void xp_build_dma_kernel(
           for (int r = 0; r < 16; ++r) sum += acc[t][r];
         if (sum == 1234.5f) pyr[tid] = to_out<OT>(sum);  // keeps the K loop live
       } else {
-        paged_epilogue<OT, 1 | 4>(acc, reinterpret_cast<float*>(smem) + (wave >> 2) * WAVES * 16 * P0,
+        paged_epilogue<OT, 1 | 4>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0,
                                   pyr, g, page, w4, lane);
       }
     }
@@ -226,8 +209,8 @@ int xp_dma(const float* f1, const float* f2, float* pyr, const BuildGeom& g, int
   hipLaunchKernelGGL((split_pairs_kernel<false>), dim3((unsigned)((N + 63) / 64), (unsigned)B, 2),
                      dim3(1024), 0, stream, f1, f2, reinterpret_cast<uint4*>(w),
                      reinterpret_cast<uint4*>(w + spb), e1, e2, g.D, g.N, redo);
-  hipLaunchKernelGGL((xp_build_dma_kernel<float, false, XP>), dma_grid(g, B), dim3(DMA_WAVES * 64),
-                     0, stream, w, w + spb, e1, e2, pyr, redo, g, trace);
+  hipLaunchKernelGGL((xp_build_dma_kernel<float, false, XP>), remap_grid(g, B, 2), dim3(2 * NT), 0,
+                     stream, w, w + spb, e1, e2, pyr, redo, g, trace);
   hipLaunchKernelGGL((corr_build_redo_kernel<float, false, true, false>), dim3(64), dim3(NT), 0,
                      stream, f1, f2, pyr, redo, g);
   return dxr::launch_status();
@@ -250,6 +233,11 @@ extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t
     case 1: return xp_dma<1>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     case 2: return xp_dma<2>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     case 3: return xp_dma<3>(f1, f2, pyr, g, (int)B, ws, trace, stream);
+    case 4: return xp_dma<4>(f1, f2, pyr, g, (int)B, ws, trace, stream);
+    case 5: return xp_dma<5>(f1, f2, pyr, g, (int)B, ws, trace, stream);
+    case 12: return xp_dma<12>(f1, f2, pyr, g, (int)B, ws, trace, stream);
+    case 13: return xp_dma<13>(f1, f2, pyr, g, (int)B, ws, trace, stream);
+    case 8: return xp_dma<8>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     case 256: return xp_dma<256>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     case 257: return xp_dma<257>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     default: return DXR_EINVAL;
