@@ -152,14 +152,17 @@ int64_t dxr_build_workspace_bytes(int in_dtype, int64_t B, int64_t D, int64_t H,
  * dead after the build).  Same arguments, same result contract; with DXR_F32
  * fmaps, algo DXR_BUILD_AUTO and D % 16 == 0 it runs the pre-split build:
  * one pass scales every pixel's channel vector by a power of two 2^s
- * (|x 2^s| < 2^14) and splits it into an f16 pair x 2^s = hi + 2^-11 lo in the
- * workspace, then the build's K loop moves those pairs by LDS-DMA and runs the
- * same three f16 MFMA products per f32 product, undoing both scales exactly in
- * its epilogue — f32-class error (<= 2^-22 |x| per operand element near its
- * pixel's max) at any fmap scale, bit-identical for NCHW and NHWC fmaps and
- * exactly linear in power-of-two scalings of either fmap.  Pages whose sums
- * are not finite (an inf/NaN operand) are recomputed on the exact three-way
- * bf16 split.  A NULL or short workspace runs dxr_corr_pyramid_build.
+ * (|x 2^s| < 2^14) and splits it into an f16 pair x 2^s = hi + lo
+ * (lo = RNE_f16(x 2^s - hi)) in the workspace, then the build's K loop moves
+ * those pairs by LDS-DMA and runs three f16 MFMA products per f32 product
+ * (lo.hi + hi.lo + hi.hi into one f32 accumulator), undoing both scales
+ * exactly in its epilogue — f32-class error (the pair holds each element to
+ * <= 2^-23 |x| unless it is more than 2^16 below its pixel's max) at any fmap
+ * scale, bit-identical for NCHW and NHWC fmaps and exactly linear in
+ * power-of-two scalings of either fmap.  A workgroup whose sums are not
+ * finite (an inf/NaN operand) rewrites its pages from the f32 operands on the
+ * exact-f32 MFMA (IEEE inf/NaN semantics).  NHWC fmaps need 16-byte aligned
+ * pixel rows.  A NULL or short workspace runs dxr_corr_pyramid_build.
  * Replaces the same reference lines: core/corr.py:52-60 + :21-27.  ABI 6.
  */
 int dxr_corr_pyramid_build_ws(const void* fmap1, const void* fmap2, int in_dtype,

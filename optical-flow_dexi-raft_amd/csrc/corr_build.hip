@@ -372,12 +372,15 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
   {
     OT* const pb2 = pyr + g.loff[2] + page * (BM * NTGT / 16);
     OT* pg2 = pb2 + (long long)wave * 32 * 8 + j * 8 + 4 * h;
+    // row h of the lane half (selects, not a runtime index into a private array)
+    const float r0 = h ? l2[1][0] : l2[0][0], r1 = h ? l2[1][1] : l2[0][1];
+    const float r2 = h ? l2[1][2] : l2[0][2], r3 = h ? l2[1][3] : l2[0][3];
     if constexpr (sizeof(OT) == 4) {
-      epi_put<EX>(pb2, pg2, f32x4v{l2[h][0], l2[h][1], l2[h][2], l2[h][3]});
+      epi_put<EX>(pb2, pg2, f32x4v{r0, r1, r2, r3});
     } else {
       u32x2v w;
-      w.x = (uint32_t)to_out<OT>(l2[h][0]) | ((uint32_t)to_out<OT>(l2[h][1]) << 16);
-      w.y = (uint32_t)to_out<OT>(l2[h][2]) | ((uint32_t)to_out<OT>(l2[h][3]) << 16);
+      w.x = (uint32_t)to_out<OT>(r0) | ((uint32_t)to_out<OT>(r1) << 16);
+      w.y = (uint32_t)to_out<OT>(r2) | ((uint32_t)to_out<OT>(r3) << 16);
       epi_put<EX>(pb2, pg2, w);
     }
   }
@@ -390,7 +393,7 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
     l3[v] = (((l2[0][2 * v] + l2[0][2 * v + 1]) + l2[1][2 * v]) + l2[1][2 * v + 1]) * 0.25f;
   OT* const pb3 = pyr + g.loff[3] + page * (BM * 2);
   OT* pg3 = pb3 + (long long)wave * 32 * 2;
-  epi_put<EX>(pb3, pg3 + j * 2 + h, to_out<OT>(l3[h]));
+  epi_put<EX>(pb3, pg3 + j * 2 + h, to_out<OT>(h ? l3[1] : l3[0]));
 }
 
 // PAGED: write the paged pyramid (levels 1..4 fused).  !PAGED: write level 0
@@ -1268,9 +1271,13 @@ __device__ __forceinline__ int pixel_scale(float m, bool finite) {
 
 // Split 16 consecutive channels of one pixel (already scaled) into the 64-B
 // SP record: hi 16 f16 then lo 16 f16.  LO11: lo = RNE_f16((x - hi) 2^11) (the
-// r02 pair, for experiments), else lo = RNE_f16(x - hi).
+// r02 pair, for experiments), else lo = RNE_f16(x - hi).  The record is stored
+// at byte `off` of resource `r` as four 16-byte write-through (sc1) stores: the
+// next kernel reads it from every XCD, so it leaves this XCD's L2 at once
+// instead of as dirty lines the kernel boundary writes back.
 template <bool LO11 = false>
-__device__ __forceinline__ void store_pair_block(uint4* dst, const float (&x)[16]) {
+__device__ __forceinline__ void store_pair_block(__amdgpu_buffer_rsrc_t r, unsigned off,
+                                                 const float (&x)[16]) {
   uint32_t h[8], l[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -1287,10 +1294,11 @@ __device__ __forceinline__ void store_pair_block(uint4* dst, const float (&x)[16
       l[e] = __builtin_bit_cast(uint32_t, lv);
     }
   }
-  dst[0] = make_uint4(h[0], h[1], h[2], h[3]);
-  dst[1] = make_uint4(h[4], h[5], h[6], h[7]);
-  dst[2] = make_uint4(l[0], l[1], l[2], l[3]);
-  dst[3] = make_uint4(l[4], l[5], l[6], l[7]);
+  constexpr int SC1 = 16;
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4v{h[0], h[1], h[2], h[3]}, r, off, 0, SC1);
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4v{h[4], h[5], h[6], h[7]}, r, off + 16, 0, SC1);
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4v{l[0], l[1], l[2], l[3]}, r, off + 32, 0, SC1);
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4v{l[4], l[5], l[6], l[7]}, r, off + 48, 0, SC1);
 }
 
 // One thread per (pixel, 16-channel block): 1024-thread blocks of 64 pixels x
@@ -1305,10 +1313,9 @@ __global__ __launch_bounds__(1024) void split_pairs_kernel(const float* __restri
                                                            uint4* __restrict__ sp1,
                                                            uint4* __restrict__ sp2,
                                                            int* __restrict__ e1, int* __restrict__ e2,
-                                                           int D, int N, int* __restrict__ redo) {
+                                                           int D, int N) {
   __shared__ float red[16][65];
   const int tid = threadIdx.x;
-  if (redo && (blockIdx.x | blockIdx.y | blockIdx.z | tid) == 0) *redo = 0;   // the build's list
   const int kb0 = NHWC ? (tid & 15) : (tid >> 6), pl = NHWC ? (tid >> 4) : (tid & 63);
   const int p = blockIdx.x * 64 + pl;
   const bool live = p < N;
@@ -1350,25 +1357,34 @@ __global__ __launch_bounds__(1024) void split_pairs_kernel(const float* __restri
   }
   if (!live) return;
   const int s = pixel_scale(mm < 0.f ? 0.f : mm, mm >= 0.f);
-  if (kb0 == 0) ex[p] = s;
+  // per-pair resources (a pair's SP copy is D * N * 4 < 2^31 bytes)
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(sp, (short)0, 0x7fffffff, 0x00020000);
+  if (kb0 == 0) {
+    const __amdgpu_buffer_rsrc_t re =
+        __builtin_amdgcn_make_buffer_rsrc(ex, (short)0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)s, re, (unsigned)p * 4u, 0, 16);
+  }
   for (int kb = kb0; kb < nkb; kb += 16) {
     if (nkb > 16) load16(kb, x);      // D <= 256: the first pass's values
 #pragma unroll
     for (int i = 0; i < 16; ++i) x[i] = __builtin_ldexpf(x[i], s);
-    store_pair_block<LO11>(sp + ((long long)kb * N + p) * 4, x);
+    store_pair_block<LO11>(rs, (unsigned)((kb * N + p) * 64), x);
   }
 }
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-// Pages whose sums are not finite (an inf/NaN operand pixel) are not written
-// here: their indices go to `redo` (count in redo[0], pages from redo[1]) for
-// corr_build_redo_kernel, launched after this kernel.  Grid:
-// remap_grid(g, B, 2) (page_coord<true, 2>).
+// A workgroup whose sums are not finite (an inf/NaN operand pixel) recomputes
+// its pages from the f32 operands (`f1`, `f2`: element (pixel p, channel k) at
+// p * ps + k * ks of a pair's fmap) on the exact-f32 MFMA, in place: IEEE
+// semantics as the reference's f32 matmul (inf x finite = inf, inf x 0 = NaN,
+// NaN propagates).  Grid: remap_grid(g, B, 2) (page_coord<true, 2>).
 template <typename OT, bool DIV>
 __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
     const uint8_t* __restrict__ sp1, const uint8_t* __restrict__ sp2, const int* __restrict__ ex1,
-    const int* __restrict__ ex2, OT* __restrict__ pyr, int* __restrict__ redo_list, BuildGeom g) {
+    const int* __restrict__ ex2, OT* __restrict__ pyr, const float* __restrict__ f1,
+    const float* __restrict__ f2, int ps, int ks, BuildGeom g) {
   constexpr int LDS_RING = DMA_RING * DMA_STAGE;
   constexpr int LDS_E = 2 * WAVES * 16 * P0 * 4;          // epilogue staging (8 waves)
   static_assert(LDS_E <= LDS_RING, "the epilogue staging aliases the ring");
@@ -1490,35 +1506,64 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
   __syncthreads();
   const bool live = pc.qblk + half < g.qt;            // this half's query block exists
   const long long page = pc.page + (live ? (long long)half * g.tiles_h * g.tiles_w : 0);
-  if (*redo) {
-    // IEEE semantics (inf x finite = inf, inf x 0 = NaN, NaN propagates) as the
-    // reference's f32 matmul: corr_build_redo_kernel recomputes the pages on the
-    // exact-f32 MFMA
-    if (tid == 0) {
-      const int n = pc.qblk + 1 < g.qt ? 2 : 1;
-      const int at = atomicAdd(redo_list, n);
-      for (int h = 0; h < n; ++h)
-        redo_list[1 + at + h] = (int)(pc.page + (long long)h * g.tiles_h * g.tiles_w);
+  // undo the pixel scales: acc[t][r] is query qj x tile pixel (row 2t + kh, col r)
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int4* se = reinterpret_cast<const int4*>(sexp + (2 * t + kh) * 16);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int4 s4 = se[u];
+      acc[t][4 * u + 0] = __builtin_ldexpf(acc[t][4 * u + 0], -(sq + s4.x));
+      acc[t][4 * u + 1] = __builtin_ldexpf(acc[t][4 * u + 1], -(sq + s4.y));
+      acc[t][4 * u + 2] = __builtin_ldexpf(acc[t][4 * u + 2], -(sq + s4.z));
+      acc[t][4 * u + 3] = __builtin_ldexpf(acc[t][4 * u + 3], -(sq + s4.w));
     }
-  } else {
-    // undo the pixel scales: acc[t][r] is query qj x tile pixel (row 2t + kh, col r)
+  }
+  if (live) {   // a half past the last query block has no page (epilogue syncs per wave)
+    scale_acc<DIV>(acc, g);
+    paged_epilogue<OT, 1 | 4>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0, pyr,
+                              g, page, w4, lane);
+  }
+  if (*redo && live) {
+    // The workgroup saw a non-finite sum: its pages are recomputed on the
+    // exact-f32 MFMA (v_mfma_f32_32x32x2_f32: each lane supplies channel k0 + kh
+    // of its A row = target trow0 + 32 t and of its B column = query qj; same
+    // output layout as the f16 products, nothing to undo) and written again over
+    // the first pass's (each wave rewrites only its own rows, in program order).
+    // Rare (non-finite inputs): operands straight from global memory by
+    // range-checked buffer loads, off-map pixels reading as zero.
+    int trw = trow0;
+    asm volatile("" : "+v"(trw));   // keep this path's addressing out of the K loop
+    const long long pb = (long long)b * g.D * g.N;
+    const int nbytes = g.D * g.N * 4;
+    const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(f1 + pb), (short)0, nbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(f2 + pb), (short)0, nbytes, 0x00020000);
+    const unsigned qo = qj < g.N ? (unsigned)qj * (unsigned)ps * 4u : 0x80000000u;
+    unsigned to[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int4* se = reinterpret_cast<const int4*>(sexp + (2 * t + kh) * 16);
+      const int lrow = trw + 32 * t, hh = th0 + (lrow >> 4), ww = tw0 + (lrow & 15);
+      to[t] = (hh < g.H && ww < g.W) ? (unsigned)(hh * g.W + ww) * (unsigned)ps * 4u : 0x80000000u;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int4 s4 = se[u];
-        acc[t][4 * u + 0] = __builtin_ldexpf(acc[t][4 * u + 0], -(sq + s4.x));
-        acc[t][4 * u + 1] = __builtin_ldexpf(acc[t][4 * u + 1], -(sq + s4.y));
-        acc[t][4 * u + 2] = __builtin_ldexpf(acc[t][4 * u + 2], -(sq + s4.z));
-        acc[t][4 * u + 3] = __builtin_ldexpf(acc[t][4 * u + 3], -(sq + s4.w));
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    }
+    const int kstep = ks * 4;
+#pragma unroll 1
+    for (int k = kh; k < g.D; k += 2) {
+      const int ko = k * kstep;
+      const float bq = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r1, qo, ko, 0));
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float at =
+            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r2, to[t], ko, 0));
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(at, bq, acc[t], 0, 0, 0);
       }
     }
-    if (live) {   // a half past the last query block has no page (epilogue syncs per wave)
-      scale_acc<DIV>(acc, g);
-      paged_epilogue<OT, 1 | 4>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0, pyr,
-                                g, page, w4, lane);
-    }
+    scale_acc<DIV>(acc, g);
+    paged_epilogue<OT, 1 | 4>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0, pyr,
+                              g, page, w4, lane);
   }
 }
 
@@ -1779,35 +1824,14 @@ int launch_split(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, 
   return dxr::launch_status();
 }
 
-// The pages corr_build_dma_kernel listed as not finite, on the exact-f32 MFMA
-// (normally none: every workgroup reads the count and leaves).
-template <typename OT, bool DIV, bool VEC, bool NHWC>
-__global__ __launch_bounds__(NT) void corr_build_redo_kernel(const float* __restrict__ f1,
-                                                             const float* __restrict__ f2,
-                                                             OT* __restrict__ pyr,
-                                                             const int* __restrict__ redo_list,
-                                                             BuildGeom g) {
-  __shared__ float lds[build_lds_floats<16>()];
-  const int n = redo_list[0];
-  for (int i = blockIdx.x; i < n; i += gridDim.x)
-    build_page_f32<VEC, 16, true, OT, DIV, NHWC>(f1, f2, pyr, g, lds, redo_list[1 + i],
-                                                 (int)threadIdx.x);
-}
-
-// Pre-split + LDS-DMA f32 build (round 3): workspace = SP1 | SP2 | E1 | E2 |
-// redo list (count + one int per page).
+// Pre-split + LDS-DMA f32 build (round 3): workspace = SP1 | SP2 | E1 | E2.
 long long align256(long long x) { return (x + 255) & ~255LL; }
-long long dma_pages(long long B, long long D, long long H, long long W) {
-  (void)D;
-  return B * ((H * W + BM - 1) / BM) * ((H + TH - 1) / TH) * ((W + TW - 1) / TW);
-}
 long long dma_workspace_bytes(long long B, long long D, long long H, long long W) {
   const long long N = H * W;
-  return 2 * align256(B * D * N * 4) + 2 * align256(B * N * 4) +
-         align256(4 * (1 + dma_pages(B, D, H, W)));
+  return 2 * align256(B * D * N * 4) + 2 * align256(B * N * 4);
 }
 
-template <typename OT, int BV, bool NHWC>
+template <typename OT, bool NHWC>
 int launch_dma(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, int B, void* ws,
                hipStream_t stream) {
   const dim3 grid = build_grid(g, B);
@@ -1818,28 +1842,19 @@ int launch_dma(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, in
   uint8_t* sp2 = w + spb;
   int* e1 = reinterpret_cast<int*>(w + 2 * spb);
   int* e2 = reinterpret_cast<int*>(w + 2 * spb + eb);
-  int* redo = reinterpret_cast<int*>(w + 2 * spb + 2 * eb);
   hipLaunchKernelGGL((split_pairs_kernel<NHWC>), dim3((unsigned)((N + 63) / 64), (unsigned)B, 2),
                      dim3(1024), 0, stream, f1, f2, reinterpret_cast<uint4*>(sp1),
-                     reinterpret_cast<uint4*>(sp2), e1, e2, g.D, g.N, redo);
+                     reinterpret_cast<uint4*>(sp2), e1, e2, g.D, g.N);
   int st = dxr::launch_status();
   if (st != DXR_OK) return st;
   const dim3 rg = remap_grid(g, B, 2);
+  const int ps = NHWC ? g.D : 1, ks = NHWC ? 1 : g.N;   // fallback operand strides
   if (g.recip == 0.f)
     hipLaunchKernelGGL((corr_build_dma_kernel<OT, true>), rg, dim3(2 * NT), 0, stream, sp1, sp2,
-                       e1, e2, pyr, redo, g);
+                       e1, e2, pyr, f1, f2, ps, ks, g);
   else
     hipLaunchKernelGGL((corr_build_dma_kernel<OT, false>), rg, dim3(2 * NT), 0, stream, sp1, sp2,
-                       e1, e2, pyr, redo, g);
-  st = dxr::launch_status();
-  if (st != DXR_OK) return st;
-  constexpr bool VEC = BV == 4 && !NHWC;
-  if (g.recip == 0.f)
-    hipLaunchKernelGGL((corr_build_redo_kernel<OT, true, VEC, NHWC>), dim3(64), dim3(NT), 0, stream,
-                       f1, f2, pyr, redo, g);
-  else
-    hipLaunchKernelGGL((corr_build_redo_kernel<OT, false, VEC, NHWC>), dim3(64), dim3(NT), 0,
-                       stream, f1, f2, pyr, redo, g);
+                       e1, e2, pyr, f1, f2, ps, ks, g);
   return dxr::launch_status();
 }
 
@@ -1918,9 +1933,8 @@ int pyramid_build(const void* fmap1, const void* fmap2, int in_dtype, int fmap_l
   if (algo == DXR_BUILD_EXACT_F32 && in_dtype != DXR_F32) return DXR_EUNSUPPORTED;
   const BuildGeom g = make_geom(D, H, W, divisor, L);
   int st = PROCEED;
-  // f32 operands with a workspace: pre-split f16 pairs + the LDS-DMA build,
-  // where the split build applies (its layout conditions select the f32
-  // fallback's operand form).
+  // f32 operands with a workspace: pre-split f16 pairs + the LDS-DMA build
+  // (any W; D % 16 == 0; NHWC rows 16-byte aligned).
   const bool dma_ok = in_dtype == DXR_F32 && algo == DXR_BUILD_AUTO && D % 16 == 0 &&
                       D * H * W < (1LL << 29) && workspace != nullptr && aligned16(workspace) &&
                       workspace_bytes >= dma_workspace_bytes(B, D, H, W) && aligned16(pyramid);
@@ -1930,17 +1944,13 @@ int pyramid_build(const void* fmap1, const void* fmap2, int in_dtype, int fmap_l
     float* pf = static_cast<float*>(pyramid);
     uint16_t* ph = static_cast<uint16_t*>(pyramid);
     const bool f32p = pyr_dtype == DXR_F32;
-    if (fmap_layout == DXR_NHWC) {
-      if (W % 2 == 0 && aligned16(f1) && aligned16(f2))
-        st = f32p ? launch_dma<float, 4, true>(f1, f2, pf, g, (int)B, workspace, stream)
-                  : launch_dma<uint16_t, 4, true>(f1, f2, ph, g, (int)B, workspace, stream);
-    } else if (W % 4 == 0 && aligned16(f1) && aligned16(f2)) {
-      st = f32p ? launch_dma<float, 4, false>(f1, f2, pf, g, (int)B, workspace, stream)
-                : launch_dma<uint16_t, 4, false>(f1, f2, ph, g, (int)B, workspace, stream);
-    } else if (W % 2 == 0 && ((uintptr_t)f1 % 8) == 0 && ((uintptr_t)f2 % 8) == 0) {
-      st = f32p ? launch_dma<float, 2, false>(f1, f2, pf, g, (int)B, workspace, stream)
-                : launch_dma<uint16_t, 2, false>(f1, f2, ph, g, (int)B, workspace, stream);
-    }
+    // NCHW operands are read as scalars by the split pass; NHWC as float4
+    if (fmap_layout == DXR_NCHW)
+      st = f32p ? launch_dma<float, false>(f1, f2, pf, g, (int)B, workspace, stream)
+                : launch_dma<uint16_t, false>(f1, f2, ph, g, (int)B, workspace, stream);
+    else if (aligned16(f1) && aligned16(f2))
+      st = f32p ? launch_dma<float, true>(f1, f2, pf, g, (int)B, workspace, stream)
+                : launch_dma<uint16_t, true>(f1, f2, ph, g, (int)B, workspace, stream);
   }
   if (st != PROCEED) {
     // done by the DMA build

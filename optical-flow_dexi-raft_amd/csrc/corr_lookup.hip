@@ -148,7 +148,25 @@ __device__ __forceinline__ void load_vec(const PT* p, float* v) {
 // Phase 1 for one level type: V-cell vectors, 4 per LDS vector slot.  Split in
 // a load half (registers) and a store half (LDS) so a caller can keep several
 // levels' gathers in flight at once (the fused motion kernel).
-template <int R, int NT_, int V, typename PT>
+// Slot order: QMAJ = false walks one query's window row by row (consecutive
+// lanes read consecutive 16-B pieces of one window row: levels 0/1, whose tile
+// rows are 32-64 B of one query); QMAJ = true walks the queries fastest, so a
+// wave instruction reads the same window piece of 32 consecutive queries —
+// on levels 2/3, whose pages interleave queries at 32 / 8 B per tile, those
+// are neighbours in one or a few lines instead of 64 separate lines.
+template <int R, int NT_, bool QMAJ>
+__device__ __forceinline__ void gather_slot(int s, int& qq, int& rem) {
+  using C = WideCfg<R, NT_>;
+  if constexpr (QMAJ) {
+    qq = s % C::QB;
+    rem = s / C::QB;
+  } else {
+    qq = s / (C::WD * C::NQ);
+    rem = s - qq * (C::WD * C::NQ);
+  }
+}
+
+template <int R, int NT_, int V, typename PT, bool QMAJ = false>
 __device__ __forceinline__ void gather_load(const PT* __restrict__ base, int qb0, const LevelAddr& A,
                                             const int2* org, int q0, int N, int tid,
                                             float4 (&v)[WideCfg<R, NT_>::VIT]) {
@@ -156,7 +174,8 @@ __device__ __forceinline__ void gather_load(const PT* __restrict__ base, int qb0
 #pragma unroll
   for (int i = 0; i < C::VIT; ++i) {
     const int s = tid + i * C::NT;
-    const int qq = s / (C::WD * C::NQ), rem = s - qq * (C::WD * C::NQ);
+    int qq, rem;
+    gather_slot<R, NT_, QMAJ>(s, qq, rem);
     const int r = rem / C::NQ, k = rem - r * C::NQ;
     float c[4] = {0.f, 0.f, 0.f, 0.f};
     if (s < C::VSLOTS && q0 + qq < N) {
@@ -182,7 +201,7 @@ __device__ __forceinline__ void gather_load(const PT* __restrict__ base, int qb0
   }
 }
 
-template <int R, int NT_>
+template <int R, int NT_, bool QMAJ = false>
 __device__ __forceinline__ void gather_store(const float4 (&v)[WideCfg<R, NT_>::VIT], float* cells,
                                              int tid) {
   using C = WideCfg<R, NT_>;
@@ -190,19 +209,20 @@ __device__ __forceinline__ void gather_store(const float4 (&v)[WideCfg<R, NT_>::
   for (int i = 0; i < C::VIT; ++i) {
     const int s = tid + i * C::NT;
     if (s < C::VSLOTS) {
-      const int qq = s / (C::WD * C::NQ), rem = s - qq * (C::WD * C::NQ);
+      int qq, rem;
+      gather_slot<R, NT_, QMAJ>(s, qq, rem);
       *reinterpret_cast<float4*>(cells + qq * C::QS + rem * 4) = v[i];
     }
   }
 }
 
-template <int R, int NT_, int V, typename PT>
+template <int R, int NT_, int V, typename PT, bool QMAJ = false>
 __device__ __forceinline__ void gather_windows(const PT* __restrict__ base, int qb0, const LevelAddr& A,
                                                const int2* org, float* cells, int q0, int N,
                                                int tid) {
   float4 v[WideCfg<R, NT_>::VIT];
-  gather_load<R, NT_, V, PT>(base, qb0, A, org, q0, N, tid, v);
-  gather_store<R, NT_>(v, cells, tid);
+  gather_load<R, NT_, V, PT, QMAJ>(base, qb0, A, org, q0, N, tid, v);
+  gather_store<R, NT_, QMAJ>(v, cells, tid);
 }
 
 // Phase 0 of the wide lookup (forward and backward): per (query, sample) the

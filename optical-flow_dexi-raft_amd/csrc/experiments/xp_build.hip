@@ -5,7 +5,65 @@
 
 namespace {
 
+// The split pass as first written in round 3 (plain stores), for A/B (XP bit 5).
+__global__ __launch_bounds__(1024) void xp_split_plain_kernel(const float* __restrict__ f1,
+                                                              const float* __restrict__ f2,
+                                                              uint4* __restrict__ sp1,
+                                                              uint4* __restrict__ sp2,
+                                                              int* __restrict__ e1,
+                                                              int* __restrict__ e2, int D, int N) {
+  __shared__ float red[16][65];
+  const int tid = threadIdx.x;
+  const int kb0 = tid >> 6, pl = tid & 63;
+  const int p = blockIdx.x * 64 + pl;
+  const bool live = p < N;
+  const int b = blockIdx.y;
+  const float* src = (blockIdx.z == 0 ? f1 : f2) + (long long)b * D * N;
+  uint4* sp = (blockIdx.z == 0 ? sp1 : sp2) + (long long)b * (D / 16) * N * 4;
+  int* ex = (blockIdx.z == 0 ? e1 : e2) + (long long)b * N;
+  float x[16];
+  float m = 0.f;
+  if (live && kb0 < D / 16) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = src[(long long)(kb0 * 16 + i) * N + p];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float a = __builtin_fabsf(x[i]);
+      m = (m < 0.f || !(a <= 3.40282347e38f)) ? -1.f : (a > m ? a : m);
+    }
+  }
+  red[kb0][pl] = m;
+  __syncthreads();
+  float mm = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const float v = red[k][pl];
+    mm = (mm < 0.f || v < 0.f) ? -1.f : (v > mm ? v : mm);
+  }
+  if (!live || kb0 >= D / 16) return;
+  const int s = pixel_scale(mm < 0.f ? 0.f : mm, mm >= 0.f);
+  if (kb0 == 0) ex[p] = s;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] = __builtin_ldexpf(x[i], s);
+  uint32_t h[8], l[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    h[e] = cvt_pk_f16(x[2 * e], x[2 * e + 1]);
+    const f16x2_t hv = __builtin_bit_cast(f16x2_t, h[e]);
+    f16x2_t lv;
+    lv[0] = (_Float16)__builtin_fmaf((float)hv[0], -1.f, x[2 * e]);
+    lv[1] = (_Float16)__builtin_fmaf((float)hv[1], -1.f, x[2 * e + 1]);
+    l[e] = __builtin_bit_cast(uint32_t, lv);
+  }
+  uint4* dst = sp + ((long long)kb0 * N + p) * 4;
+  dst[0] = make_uint4(h[0], h[1], h[2], h[3]);
+  dst[1] = make_uint4(h[4], h[5], h[6], h[7]);
+  dst[2] = make_uint4(l[0], l[1], l[2], l[3]);
+  dst[3] = make_uint4(l[4], l[5], l[6], l[7]);
+}
+
 // XP bits: 0 skip the epilogue stores (K loop kept live), 1 skip the MFMAs,
+// 5 the split pass with plain stores (A/B of the product's write-through stores),
 // 2 no DMA after the first two ring stages (the loop reads those two stages
 // again: same finite data, timing only), 3 no barrier in the K loop (timing
 // only), 8 record per-workgroup s_memrealtime stamps {start, K loop done,
@@ -13,7 +71,7 @@ namespace {
 template <typename OT, bool DIV, int XP>
 __global__ __launch_bounds__(2 * NT, 4) void xp_build_dma_kernel(
     const uint8_t* __restrict__ sp1, const uint8_t* __restrict__ sp2, const int* __restrict__ ex1,
-    const int* __restrict__ ex2, OT* __restrict__ pyr, int* __restrict__ redo_list, BuildGeom g,
+    const int* __restrict__ ex2, OT* __restrict__ pyr, BuildGeom g,
     unsigned long long* __restrict__ trace) {
   const unsigned long long xt0 = (XP & 256) ? __builtin_amdgcn_s_memrealtime() : 0ull;
   constexpr int LDS_RING = DMA_RING * DMA_STAGE;
@@ -147,15 +205,7 @@ __global__ __launch_bounds__(2 * NT, 4) void xp_build_dma_kernel(
   const bool live = pc.qblk + half < g.qt;            // this half's query block exists
   const long long page = pc.page + (live ? (long long)half * g.tiles_h * g.tiles_w : 0);
   if (*redo) {
-    // IEEE semantics (inf x finite = inf, inf x 0 = NaN, NaN propagates) as the
-    // reference's f32 matmul: corr_build_redo_kernel recomputes the pages on the
-    // exact-f32 MFMA
-    if (tid == 0) {
-      const int n = pc.qblk + 1 < g.qt ? 2 : 1;
-      const int at = atomicAdd(redo_list, n);
-      for (int h = 0; h < n; ++h)
-        redo_list[1 + at + h] = (int)(pc.page + (long long)h * g.tiles_h * g.tiles_w);
-    }
+    // (timing experiments run finite data only)
   } else {
     // undo the pixel scales: acc[t][r] is query qj x tile pixel (row 2t + kh, col r)
 #pragma unroll
@@ -205,14 +255,16 @@ int xp_dma(const float* f1, const float* f2, float* pyr, const BuildGeom& g, int
   uint8_t* w = static_cast<uint8_t*>(ws);
   int* e1 = reinterpret_cast<int*>(w + 2 * spb);
   int* e2 = reinterpret_cast<int*>(w + 2 * spb + eb);
-  int* redo = reinterpret_cast<int*>(w + 2 * spb + 2 * eb);
-  hipLaunchKernelGGL((split_pairs_kernel<false>), dim3((unsigned)((N + 63) / 64), (unsigned)B, 2),
-                     dim3(1024), 0, stream, f1, f2, reinterpret_cast<uint4*>(w),
-                     reinterpret_cast<uint4*>(w + spb), e1, e2, g.D, g.N, redo);
-  hipLaunchKernelGGL((xp_build_dma_kernel<float, false, XP>), remap_grid(g, B, 2), dim3(2 * NT), 0,
-                     stream, w, w + spb, e1, e2, pyr, redo, g, trace);
-  hipLaunchKernelGGL((corr_build_redo_kernel<float, false, true, false>), dim3(64), dim3(NT), 0,
-                     stream, f1, f2, pyr, redo, g);
+  if (XP & 32)   // the r03 split pass with plain (write-back) stores
+    hipLaunchKernelGGL((xp_split_plain_kernel), dim3((unsigned)((N + 63) / 64), (unsigned)B, 2),
+                       dim3(1024), 0, stream, f1, f2, reinterpret_cast<uint4*>(w),
+                       reinterpret_cast<uint4*>(w + spb), e1, e2, g.D, g.N);
+  else
+    hipLaunchKernelGGL((split_pairs_kernel<false>), dim3((unsigned)((N + 63) / 64), (unsigned)B, 2),
+                       dim3(1024), 0, stream, f1, f2, reinterpret_cast<uint4*>(w),
+                       reinterpret_cast<uint4*>(w + spb), e1, e2, g.D, g.N);
+  hipLaunchKernelGGL((xp_build_dma_kernel<float, false, (XP & ~32)>), remap_grid(g, B, 2), dim3(2 * NT), 0,
+                     stream, w, w + spb, e1, e2, pyr, g, trace);
   return dxr::launch_status();
 }
 
@@ -240,6 +292,8 @@ extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t
     case 8: return xp_dma<8>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     case 256: return xp_dma<256>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     case 257: return xp_dma<257>(f1, f2, pyr, g, (int)B, ws, trace, stream);
+    case 32: return xp_dma<32>(f1, f2, pyr, g, (int)B, ws, trace, stream);
+    case 33: return xp_dma<33>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     default: return DXR_EINVAL;
   }
 }

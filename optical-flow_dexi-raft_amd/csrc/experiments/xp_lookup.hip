@@ -7,6 +7,7 @@ namespace {
 
 // XP bits: 0 skip the window gathers, 1 skip phase 2 (return after the gather),
 // 2 return after phase 0, 3 synthetic coordinates (the grid: no coords loads),
+// 5 query-major gather slots on levels 2/3 (gather_slot QMAJ),
 // 8 record a per-workgroup timeline (s_memrealtime at start, after phase 0,
 // after the gather, at the end; plus the hardware id) into `trace`.
 template <int R, typename PT, int XP>
@@ -82,12 +83,15 @@ __global__ __launch_bounds__(512) void xp_lookup_kernel(const PT* __restrict__ p
   if constexpr ((XP & 1) == 0) {
     const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
     const int qb0 = q0 & ((1 << A.lqb) - 1);
+    constexpr bool QM = (XP & 32) != 0;   // query-major slots on levels 2/3
     if (A.lth == 30)
       gather_windows<R, 512, 1, PT>(base, qb0, A, org, cells, q0, g.N, tid);
-    else if (A.tw >= 4)
+    else if (A.tw >= 8)
       gather_windows<R, 512, 4, PT>(base, qb0, A, org, cells, q0, g.N, tid);
+    else if (A.tw == 4)
+      gather_windows<R, 512, 4, PT, QM>(base, qb0, A, org, cells, q0, g.N, tid);
     else if (A.tw == 2)
-      gather_windows<R, 512, 2, PT>(base, qb0, A, org, cells, q0, g.N, tid);
+      gather_windows<R, 512, 2, PT, QM>(base, qb0, A, org, cells, q0, g.N, tid);
     else
       gather_windows<R, 512, 1, PT>(base, qb0, A, org, cells, q0, g.N, tid);
   }
@@ -204,6 +208,8 @@ int xp_dispatch(int xp, const PT* pyr, const float* coords, float* out, const Lo
     case 264: return xp_launch<264>(pyr, coords, out, g, B, trace, stream);
     case 258: return xp_launch<258>(pyr, coords, out, g, B, trace, stream);
     case 260: return xp_launch<260>(pyr, coords, out, g, B, trace, stream);
+    case 32: return xp_launch<32>(pyr, coords, out, g, B, trace, stream);
+    case 288: return xp_launch<288>(pyr, coords, out, g, B, trace, stream);
     default: return DXR_EINVAL;
   }
 }

@@ -27,7 +27,7 @@ def main(path: str) -> None:
             name = r.get("Kernel_Name", "")
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
     rows.sort()
-    prod = ("corr_build", "pool", "transpose")
+    prod = ("corr_build", "split_pairs", "pool", "transpose")
     is_look = [("corr_lookup_wide_kernel" in n or "alt_corr_mfma_kernel" in n) for _, _, n in rows]
     is_prep = [any(p in n for p in prod) and not is_look[i] for i, (_, _, n) in enumerate(rows)]
     # step starts: a build-side kernel right after a lookup (or first in the trace)

@@ -2,8 +2,8 @@
 """Pre-split f32 build: timing ablations and per-page timeline (experiments target).
 
 Variants of csrc/experiments/xp_build.hip (``dxr_xp_build``; each launch = the
-split pass + the build + the redo pass): 0 product, 1 no epilogue stores, 2 no
-MFMAs, 3 both; 256 / 257 record {start, K loop done, stores done} per
+split pass + the build): 0 product, 1 no epilogue stores, 2 no MFMAs, 3 both,
+32 the split pass with plain stores; 256 / 257 record {start, K loop done, stores done} per
 workgroup (two pages; s_memrealtime, 100 MHz).  Interleaved rounds of graphs of --reps
 launches, HIP events.
 Usage: python scripts/xp_build.py [--shape 1x55x128] [--xp 0 1 2 4 5]
@@ -26,7 +26,7 @@ sys.path.insert(0, str(REPO))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="1x55x128")
-    ap.add_argument("--xp", type=int, nargs="+", default=[0, 1, 2, 3, 4, 5, 8, 12, 13])
+    ap.add_argument("--xp", type=int, nargs="+", default=[0, 32, 1, 2, 3, 4, 5])
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
     a = ap.parse_args()
