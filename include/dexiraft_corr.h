@@ -140,7 +140,9 @@ int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int in_dtype,
 
 /*
  * Bytes of device workspace dxr_corr_pyramid_build_ws uses for B pairs of
- * D x H x W fmaps of in_dtype (0: that request needs none; -1: bad geometry).
+ * D x H x W fmaps of in_dtype (0: that request needs none; -1: bad geometry):
+ * f32 with D % 16 == 0 the pre-split operands, bf16 with D % 32 == 0 the pack
+ * pass's blocked copies of NCHW fmaps (channels-last bf16 fmaps need none).
  * ABI 6.
  */
 int64_t dxr_build_workspace_bytes(int in_dtype, int64_t B, int64_t D, int64_t H,
@@ -162,7 +164,10 @@ int64_t dxr_build_workspace_bytes(int in_dtype, int64_t B, int64_t D, int64_t H,
  * power-of-two scalings of either fmap.  A workgroup whose sums are not
  * finite (an inf/NaN operand) rewrites its pages from the f32 operands on the
  * exact-f32 MFMA (IEEE inf/NaN semantics).  NHWC fmaps need 16-byte aligned
- * pixel rows.  A NULL or short workspace runs dxr_corr_pyramid_build.
+ * pixel rows.  With DXR_BF16 NCHW fmaps (D % 32 == 0) a pack pass copies the
+ * operands into 64-byte records of 32 channels per pixel and the bf16 build
+ * runs the same LDS-DMA K loop on them — the workspace-less bf16 build's
+ * pyramid bit for bit.  A NULL or short workspace runs dxr_corr_pyramid_build.
  * Replaces the same reference lines: core/corr.py:52-60 + :21-27.  ABI 6.
  */
 int dxr_corr_pyramid_build_ws(const void* fmap1, const void* fmap2, int in_dtype,

@@ -1271,13 +1271,9 @@ __device__ __forceinline__ int pixel_scale(float m, bool finite) {
 
 // Split 16 consecutive channels of one pixel (already scaled) into the 64-B
 // SP record: hi 16 f16 then lo 16 f16.  LO11: lo = RNE_f16((x - hi) 2^11) (the
-// r02 pair, for experiments), else lo = RNE_f16(x - hi).  The record is stored
-// at byte `off` of resource `r` as four 16-byte write-through (sc1) stores: the
-// next kernel reads it from every XCD, so it leaves this XCD's L2 at once
-// instead of as dirty lines the kernel boundary writes back.
+// r02 pair, for experiments), else lo = RNE_f16(x - hi).
 template <bool LO11 = false>
-__device__ __forceinline__ void store_pair_block(__amdgpu_buffer_rsrc_t r, unsigned off,
-                                                 const float (&x)[16]) {
+__device__ __forceinline__ void split_record(const float (&x)[16], uint4 (&rec)[4]) {
   uint32_t h[8], l[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -1294,11 +1290,10 @@ __device__ __forceinline__ void store_pair_block(__amdgpu_buffer_rsrc_t r, unsig
       l[e] = __builtin_bit_cast(uint32_t, lv);
     }
   }
-  constexpr int SC1 = 16;
-  __builtin_amdgcn_raw_buffer_store_b128(u32x4v{h[0], h[1], h[2], h[3]}, r, off, 0, SC1);
-  __builtin_amdgcn_raw_buffer_store_b128(u32x4v{h[4], h[5], h[6], h[7]}, r, off + 16, 0, SC1);
-  __builtin_amdgcn_raw_buffer_store_b128(u32x4v{l[0], l[1], l[2], l[3]}, r, off + 32, 0, SC1);
-  __builtin_amdgcn_raw_buffer_store_b128(u32x4v{l[4], l[5], l[6], l[7]}, r, off + 48, 0, SC1);
+  rec[0] = make_uint4(h[0], h[1], h[2], h[3]);
+  rec[1] = make_uint4(h[4], h[5], h[6], h[7]);
+  rec[2] = make_uint4(l[0], l[1], l[2], l[3]);
+  rec[3] = make_uint4(l[4], l[5], l[6], l[7]);
 }
 
 // One thread per (pixel, 16-channel block): 1024-thread blocks of 64 pixels x
@@ -1307,6 +1302,14 @@ __device__ __forceinline__ void store_pair_block(__amdgpu_buffer_rsrc_t r, unsig
 // NHWC: 16 lanes per pixel read its channels as 64-byte runs.  The pixel max
 // (and a non-finite flag, -1) is reduced through LDS; the values stay in
 // registers between the two passes when D <= 256.
+// Stores: the next kernel reads the records from every XCD, so they are
+// written through (sc1) — in whole lines: a wave's 64 records (4 KB: 64
+// consecutive pixels of one channel block, NCHW; 4 pixels x 16 blocks, NHWC)
+// go through a per-wave LDS transpose (80-B pitch, conflict-free) so that each
+// 16-B store instruction covers 1 KB of contiguous records.  (Per-lane 64-B
+// records stored directly write every line in four partial pieces: 13.7 vs
+// 9.5 us at Sintel B=1 against plain stores, which in turn leave the build's
+// K loop evicting dirty lines.)
 template <bool NHWC, bool LO11 = false>
 __global__ __launch_bounds__(1024) void split_pairs_kernel(const float* __restrict__ f1,
                                                            const float* __restrict__ f2,
@@ -1315,7 +1318,8 @@ __global__ __launch_bounds__(1024) void split_pairs_kernel(const float* __restri
                                                            int* __restrict__ e1, int* __restrict__ e2,
                                                            int D, int N) {
   __shared__ float red[16][65];
-  const int tid = threadIdx.x;
+  __shared__ __attribute__((aligned(16))) uint4 tr[16][64 * 5];   // per wave: 64 records, 80-B pitch
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kb0 = NHWC ? (tid & 15) : (tid >> 6), pl = NHWC ? (tid >> 4) : (tid & 63);
   const int p = blockIdx.x * 64 + pl;
   const bool live = p < N;
@@ -1355,21 +1359,46 @@ __global__ __launch_bounds__(1024) void split_pairs_kernel(const float* __restri
     const float v = red[k][pl];
     mm = (mm < 0.f || v < 0.f) ? -1.f : (v > mm ? v : mm);
   }
-  if (!live) return;
   const int s = pixel_scale(mm < 0.f ? 0.f : mm, mm >= 0.f);
   // per-pair resources (a pair's SP copy is D * N * 4 < 2^31 bytes)
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(sp, (short)0, 0x7fffffff, 0x00020000);
-  if (kb0 == 0) {
+  if (live && kb0 == 0) {
     const __amdgpu_buffer_rsrc_t re =
         __builtin_amdgcn_make_buffer_rsrc(ex, (short)0, 0x7fffffff, 0x00020000);
     __builtin_amdgcn_raw_buffer_store_b32((uint32_t)s, re, (unsigned)p * 4u, 0, 16);
   }
-  for (int kb = kb0; kb < nkb; kb += 16) {
-    if (nkb > 16) load16(kb, x);      // D <= 256: the first pass's values
+  uint4* tw = tr[wave];
+  const int nit = (nkb + 15) / 16;               // wave-uniform trip count
+  for (int it = 0; it < nit; ++it) {
+    const int kb = kb0 + 16 * it;
+    if (nkb > 16 && live && kb < nkb) load16(kb, x);   // D <= 256: the first pass's values
 #pragma unroll
     for (int i = 0; i < 16; ++i) x[i] = __builtin_ldexpf(x[i], s);
-    store_pair_block<LO11>(rs, (unsigned)((kb * N + p) * 64), x);
+    uint4 rec[4];
+    split_record<LO11>(x, rec);
+    // the lane's record -> LDS record u (NCHW: u = pixel; NHWC: u = 4 block + pixel)
+    const int u = NHWC ? (lane & 15) * 4 + (lane >> 4) : lane;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) tw[u * 5 + c] = rec[c];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      // 1 KB of contiguous records per instruction: LDS record u2, slot c
+      const int u2 = 16 * i + (lane >> 2), c = lane & 3;
+      const int kbs = NHWC ? 16 * it + (u2 >> 2) : kb;
+      const int px = NHWC ? blockIdx.x * 64 + wave * 4 + (u2 & 3) : blockIdx.x * 64 + u2;
+      if (px < N && kbs < nkb) {
+        const uint4 v = tw[u2 * 5 + c];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), rs,
+                                               (unsigned)((kbs * N + px) * 64 + c * 16), 0, 16);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
@@ -1380,11 +1409,21 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 // p * ps + k * ks of a pair's fmap) on the exact-f32 MFMA, in place: IEEE
 // semantics as the reference's f32 matmul (inf x finite = inf, inf x 0 = NaN,
 // NaN propagates).  Grid: remap_grid(g, B, 2) (page_coord<true, 2>).
-template <typename OT, bool DIV>
+//
+// BF (bf16 mode, C3): the same K loop on bf16 operand records — a 64-B record
+// is 32 consecutive channels of one pixel (k 0-7 | 8-15 | 16-23 | 24-31 in the
+// four 16-B slots), so a stage is two 16-deep bf16 MFMA steps (slots kh, then
+// 2 + kh), accumulated in the order of corr_build_bf16_q2_kernel: the same
+// pages bit for bit.  Records come straight from channels-last bf16 fmaps
+// (pixel stride D * 2 B, stage stride 64 B) or from the pack pass's blocked copy
+// of NCHW fmaps (pixel stride 64 B, stage stride N * 64 B): `pstr` / `kstr`.
+// No scales, no non-finite fallback (bf16 MFMA propagates inf/NaN itself), and
+// the bf16 build's non-temporal pyramid stores.
+template <typename OT, bool DIV, bool BF = false>
 __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
     const uint8_t* __restrict__ sp1, const uint8_t* __restrict__ sp2, const int* __restrict__ ex1,
     const int* __restrict__ ex2, OT* __restrict__ pyr, const float* __restrict__ f1,
-    const float* __restrict__ f2, int ps, int ks, BuildGeom g) {
+    const float* __restrict__ f2, int ps, int ks, int pstr, int kstr, BuildGeom g) {
   constexpr int LDS_RING = DMA_RING * DMA_STAGE;
   constexpr int LDS_E = 2 * WAVES * 16 * P0 * 4;          // epilogue staging (8 waves)
   static_assert(LDS_E <= LDS_RING, "the epilogue staging aliases the ring");
@@ -1404,17 +1443,20 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
   const int q0 = pc.qblk * BM;                        // first of the two blocks
   const int b = pc.b;
   const int j = lane & 31, kh = lane >> 5;
-  const long long spstride = (long long)g.D * g.N * 4;   // SP bytes per pair
+  const long long spstride = (long long)g.D * g.N * (BF ? 2 : 4);   // operand bytes per pair
 
   // exponents: the lane's query, the tile's 128 targets (LDS, by tile pixel)
   const int qj = q0 + wave * 32 + j;
-  const int sq = qj < g.N ? ex1[(long long)b * g.N + qj] : 0;
-  if (tid < NTGT) {
-    const int r = tid >> 4, c = tid & 15;
-    const bool in = th0 + r < g.H && tw0 + c < g.W;
-    sexp[tid] = in ? ex2[(long long)b * g.N + (th0 + r) * g.W + tw0 + c] : 0;
+  int sq = 0;
+  if constexpr (!BF) {
+    sq = qj < g.N ? ex1[(long long)b * g.N + qj] : 0;
+    if (tid < NTGT) {
+      const int r = tid >> 4, c = tid & 15;
+      const bool in = th0 + r < g.H && tw0 + c < g.W;
+      sexp[tid] = in ? ex2[(long long)b * g.N + (th0 + r) * g.W + tw0 + c] : 0;
+    }
+    if (tid == 0) *redo = 0;
   }
-  if (tid == 0) *redo = 0;
 
   const __amdgpu_buffer_rsrc_t rq =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sp1 + b * spstride), (short)0,
@@ -1422,7 +1464,7 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
   const __amdgpu_buffer_rsrc_t rt =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sp2 + b * spstride), (short)0,
                                         (int)spstride, 0x00020000);
-  // DMA source offsets (fixed over K; the step's offset ks * N * 64 in soffset).
+  // DMA source offsets (fixed over K; the step's offset ks * kstr in soffset).
   // Query instruction i of this wave: LDS rows 16 i + (lane >> 2) of the wave's
   // 2 KB region; target instruction: tile row r = wave.
   uint32_t vq[2], vt;
@@ -1431,17 +1473,18 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
     const int row = 16 * i + (lane >> 2), ps = lane & 3;
     const int q = q0 + wave * 32 + row;
     const int cq = ps ^ ((row >> 2) & 3);
-    vq[i] = q < g.N ? (uint32_t)(q * 64 + 16 * cq) : 0x80000000u;
+    vq[i] = q < g.N ? (uint32_t)q * (uint32_t)pstr + 16u * cq : 0x80000000u;
   }
   {
     const int ps = lane & 3, r = wave, col = lane >> 2, trow = r * 16 + col;
     const int ct = ps ^ (((trow >> 2) & 1) | ((trow >> 3) & 2));
     const int hh = th0 + r, ww = tw0 + col;
-    vt = (hh < g.H && ww < g.W) ? (uint32_t)((hh * g.W + ww) * 64 + 16 * ct) : 0x80000000u;
+    vt = (hh < g.H && ww < g.W) ? (uint32_t)(hh * g.W + ww) * (uint32_t)pstr + 16u * ct
+                                : 0x80000000u;
   }
   auto dma = [&](int ks) {
     unsigned char* st = smem + (ks % DMA_RING) * DMA_STAGE;
-    const int so = ks * g.N * 64;
+    const int so = ks * kstr;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -1466,7 +1509,7 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
 
   // exponent loads and LDS writes above must not count against the ring's vmcnt
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int nk = g.D / BKS;
+  const int nk = g.D / (BF ? 2 * BKS : BKS);
   dma(0);
   if (nk > 1) dma(1);
   for (int ks = 0; ks < nk; ++ks) {
@@ -1480,20 +1523,46 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
     __builtin_amdgcn_sched_barrier(0);
     if (ks + 2 < nk) dma(ks + 2);
     const unsigned char* st = smem + (ks % DMA_RING) * DMA_STAGE;
-    const h8v qh = *reinterpret_cast<const h8v*>(st + qh_off);
-    const h8v ql = *reinterpret_cast<const h8v*>(st + ql_off);
+    if constexpr (BF) {
+      // k 0-15 of the stage for every tile, then k 16-31 (the q2 kernel's order)
+      const bf8v q0v = *reinterpret_cast<const bf8v*>(st + qh_off);
+      const bf8v q1v = *reinterpret_cast<const bf8v*>(st + ql_off);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const h8v th = *reinterpret_cast<const h8v*>(st + th_off + t * 2048);
-      const h8v tl = *reinterpret_cast<const h8v*>(st + tl_off + t * 2048);
-      // small terms first
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qh, acc[t], 0, 0, 0);
+      for (int t = 0; t < 4; ++t) {
+        const bf8v t0v = *reinterpret_cast<const bf8v*>(st + th_off + t * 2048);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(t0v, q0v, acc[t], 0, 0, 0);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf8v t1v = *reinterpret_cast<const bf8v*>(st + tl_off + t * 2048);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(t1v, q1v, acc[t], 0, 0, 0);
+      }
+    } else {
+      const h8v qh = *reinterpret_cast<const h8v*>(st + qh_off);
+      const h8v ql = *reinterpret_cast<const h8v*>(st + ql_off);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const h8v th = *reinterpret_cast<const h8v*>(st + th_off + t * 2048);
+        const h8v tl = *reinterpret_cast<const h8v*>(st + tl_off + t * 2048);
+        // small terms first
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qh, acc[t], 0, 0, 0);
+      }
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();   // ring reads done: the LDS is free for reuse
+  const bool live = pc.qblk + half < g.qt;            // this half's query block exists
+  const long long page = pc.page + (live ? (long long)half * g.tiles_h * g.tiles_w : 0);
+  if constexpr (BF) {
+    if (live) {
+      scale_acc<DIV>(acc, g);
+      paged_epilogue<OT, 3>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0, pyr, g,
+                            page, w4, lane);
+    }
+    return;
+  }
 
   // vote: a non-finite sum means an operand pixel was not finite; the
   // workgroup's pages are then recomputed from the f32 operands
@@ -1504,8 +1573,6 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
     for (int r = 0; r < 16; ++r) bad |= !(__builtin_fabsf(acc[t][r]) <= 3.40282347e38f);
   if (bad) *redo = 1;
   __syncthreads();
-  const bool live = pc.qblk + half < g.qt;            // this half's query block exists
-  const long long page = pc.page + (live ? (long long)half * g.tiles_h * g.tiles_w : 0);
   // undo the pixel scales: acc[t][r] is query qj x tile pixel (row 2t + kh, col r)
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -1851,10 +1918,102 @@ int launch_dma(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, in
   const int ps = NHWC ? g.D : 1, ks = NHWC ? 1 : g.N;   // fallback operand strides
   if (g.recip == 0.f)
     hipLaunchKernelGGL((corr_build_dma_kernel<OT, true>), rg, dim3(2 * NT), 0, stream, sp1, sp2,
-                       e1, e2, pyr, f1, f2, ps, ks, g);
+                       e1, e2, pyr, f1, f2, ps, ks, 64, g.N * 64, g);
   else
     hipLaunchKernelGGL((corr_build_dma_kernel<OT, false>), rg, dim3(2 * NT), 0, stream, sp1, sp2,
-                       e1, e2, pyr, f1, f2, ps, ks, g);
+                       e1, e2, pyr, f1, f2, ps, ks, 64, g.N * 64, g);
+  return dxr::launch_status();
+}
+
+// bf16 operand records by LDS-DMA (corr_build_dma_kernel<.., BF>): channels-last
+// bf16 fmaps are read in place (pixel stride D * 2 B, stage stride 64 B).
+template <typename OT>
+int launch_dma_bf16_nhwc(const uint16_t* f1, const uint16_t* f2, OT* pyr, const BuildGeom& g,
+                         int B, hipStream_t stream) {
+  const dim3 rg = remap_grid(g, B, 2);
+  const uint8_t* a = reinterpret_cast<const uint8_t*>(f1);
+  const uint8_t* c = reinterpret_cast<const uint8_t*>(f2);
+  if (g.recip == 0.f)
+    hipLaunchKernelGGL((corr_build_dma_kernel<OT, true, true>), rg, dim3(2 * NT), 0, stream, a, c,
+                       nullptr, nullptr, pyr, nullptr, nullptr, 0, 0, g.D * 2, 64, g);
+  else
+    hipLaunchKernelGGL((corr_build_dma_kernel<OT, false, true>), rg, dim3(2 * NT), 0, stream, a, c,
+                       nullptr, nullptr, pyr, nullptr, nullptr, 0, 0, g.D * 2, 64, g);
+  return dxr::launch_status();
+}
+
+// Pack pass of the bf16 DMA build for NCHW fmaps: [D][N] bf16 -> blocked
+// records [D/32][N][32 k] (64 B per pixel and 32-channel block, the layout a
+// channels-last fmap already has per pixel).  Thread = 4 pixels x 8 channels:
+// eight 8-byte loads along pixels (a wave reads 512 contiguous bytes per
+// channel row; VEC: N % 4 == 0 and 8-byte aligned rows), a register transpose,
+// four 16-byte write-through stores (the build reads them from every XCD).
+// Grid (ceil(N / 256), D / 32, 2 B).
+template <bool VEC>
+__global__ __launch_bounds__(256) void pack_bf16_kernel(const uint16_t* __restrict__ f1,
+                                                        const uint16_t* __restrict__ f2,
+                                                        uint8_t* __restrict__ o1,
+                                                        uint8_t* __restrict__ o2, int D, int N) {
+  const int tid = threadIdx.x, quad = tid & 63, cg = tid >> 6;
+  const int kb = blockIdx.y, b = blockIdx.z >> 1, which = blockIdx.z & 1;
+  const long long pbase = (long long)b * D * N;
+  const uint16_t* src = (which ? f2 : f1) + pbase + (long long)(kb * 32 + cg * 8) * N;
+  uint8_t* dst = (which ? o2 : o1) + pbase * 2;
+  const int p0 = blockIdx.x * 256 + quad * 4;
+  uint16_t v[8][4];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    if constexpr (VEC) {
+      uint2 u = make_uint2(0u, 0u);
+      if (p0 < N) u = *reinterpret_cast<const uint2*>(src + (long long)c * N + p0);
+      v[c][0] = (uint16_t)u.x; v[c][1] = (uint16_t)(u.x >> 16);
+      v[c][2] = (uint16_t)u.y; v[c][3] = (uint16_t)(u.y >> 16);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[c][i] = p0 + i < N ? src[(long long)c * N + p0 + i] : (uint16_t)0;
+    }
+  }
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (p0 + i >= N) break;
+    const u32x4v w = {(uint32_t)v[0][i] | ((uint32_t)v[1][i] << 16),
+                      (uint32_t)v[2][i] | ((uint32_t)v[3][i] << 16),
+                      (uint32_t)v[4][i] | ((uint32_t)v[5][i] << 16),
+                      (uint32_t)v[6][i] | ((uint32_t)v[7][i] << 16)};
+    const unsigned off = (unsigned)(((long long)kb * N + p0 + i) * 64 + cg * 16);
+    __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 16);
+  }
+}
+
+long long bf16_pack_bytes(long long B, long long D, long long H, long long W) {
+  return 2 * align256(B * D * H * W * 2);
+}
+
+// NCHW bf16 fmaps with a workspace: pack pass + the bf16 DMA build
+// (blocked records: pixel stride 64 B, stage stride N * 64 B).
+template <typename OT>
+int launch_dma_bf16_nchw(const uint16_t* f1, const uint16_t* f2, OT* pyr, const BuildGeom& g,
+                         int B, void* ws, hipStream_t stream) {
+  const long long half = align256((long long)B * g.D * g.N * 2);
+  uint8_t* o1 = static_cast<uint8_t*>(ws);
+  uint8_t* o2 = o1 + half;
+  const dim3 pg((unsigned)((g.N + 255) / 256), (unsigned)(g.D / 32), (unsigned)(2 * B));
+  const bool vec = g.N % 4 == 0 && ((uintptr_t)f1 % 8) == 0 && ((uintptr_t)f2 % 8) == 0;
+  if (vec)
+    hipLaunchKernelGGL(pack_bf16_kernel<true>, pg, dim3(256), 0, stream, f1, f2, o1, o2, g.D, g.N);
+  else
+    hipLaunchKernelGGL(pack_bf16_kernel<false>, pg, dim3(256), 0, stream, f1, f2, o1, o2, g.D, g.N);
+  int st = dxr::launch_status();
+  if (st != DXR_OK) return st;
+  const dim3 rg = remap_grid(g, B, 2);
+  if (g.recip == 0.f)
+    hipLaunchKernelGGL((corr_build_dma_kernel<OT, true, true>), rg, dim3(2 * NT), 0, stream, o1, o2,
+                       nullptr, nullptr, pyr, nullptr, nullptr, 0, 0, 64, g.N * 64, g);
+  else
+    hipLaunchKernelGGL((corr_build_dma_kernel<OT, false, true>), rg, dim3(2 * NT), 0, stream, o1,
+                       o2, nullptr, nullptr, pyr, nullptr, nullptr, 0, 0, 64, g.N * 64, g);
   return dxr::launch_status();
 }
 
@@ -1952,8 +2111,22 @@ int pyramid_build(const void* fmap1, const void* fmap2, int in_dtype, int fmap_l
       st = f32p ? launch_dma<float, true>(f1, f2, pf, g, (int)B, workspace, stream)
                 : launch_dma<uint16_t, true>(f1, f2, ph, g, (int)B, workspace, stream);
   }
+  // bf16 NCHW operands with a workspace: pack pass + the bf16 DMA build (D % 32,
+  // D * N * 2 < 2^31 per pair)
+  if (st == PROCEED && in_dtype == DXR_BF16 && fmap_layout == DXR_NCHW && D % 32 == 0 &&
+      D * H * W < (1LL << 30) && L.n <= dxr::TILED_LEVELS && workspace != nullptr &&
+      aligned16(workspace) && workspace_bytes >= bf16_pack_bytes(B, D, H, W) &&
+      aligned16(pyramid)) {
+    const uint16_t* f1 = static_cast<const uint16_t*>(fmap1);
+    const uint16_t* f2 = static_cast<const uint16_t*>(fmap2);
+    st = pyr_dtype == DXR_F32
+             ? launch_dma_bf16_nchw(f1, f2, static_cast<float*>(pyramid), g, (int)B, workspace,
+                                    stream)
+             : launch_dma_bf16_nchw(f1, f2, static_cast<uint16_t*>(pyramid), g, (int)B, workspace,
+                                    stream);
+  }
   if (st != PROCEED) {
-    // done by the DMA build
+    // done by a DMA build
   } else if (fmap_layout == DXR_NHWC && in_dtype == DXR_BF16) {
     // channels-last bf16 operands (the bf16 mode's encoders, core/extractor.py:168-192):
     // the two-block bf16 build's NHWC form, bit-identical to the NCHW build;
@@ -1964,8 +2137,8 @@ int pyramid_build(const void* fmap1, const void* fmap2, int in_dtype, int fmap_l
     const uint16_t* f1 = static_cast<const uint16_t*>(fmap1);
     const uint16_t* f2 = static_cast<const uint16_t*>(fmap2);
     st = pyr_dtype == DXR_F32
-             ? launch_build_bf16_nhwc(f1, f2, static_cast<float*>(pyramid), g, (int)B, stream)
-             : launch_build_bf16_nhwc(f1, f2, static_cast<uint16_t*>(pyramid), g, (int)B, stream);
+             ? launch_dma_bf16_nhwc(f1, f2, static_cast<float*>(pyramid), g, (int)B, stream)
+             : launch_dma_bf16_nhwc(f1, f2, static_cast<uint16_t*>(pyramid), g, (int)B, stream);
   } else if (fmap_layout == DXR_NHWC) {
     // channels-last f32 operands: the split build's NHWC form, where the NCHW build
     // would also be the split build (f32 fmaps, D % 16 == 0, even W: same bits),
@@ -2013,6 +2186,7 @@ int pyramid_build(const void* fmap1, const void* fmap2, int in_dtype, int fmap_l
 extern "C" int64_t dxr_build_workspace_bytes(int in_dtype, int64_t B, int64_t D, int64_t H,
                                              int64_t W) {
   if (B < 0 || D < 1 || H < 1 || W < 1 || H * W > (1LL << 30)) return -1;
+  if (in_dtype == DXR_BF16) return D % 32 == 0 ? bf16_pack_bytes(B, D, H, W) : 0;
   if (in_dtype != DXR_F32 || D % 16 != 0) return 0;
   return dma_workspace_bytes(B, D, H, W);
 }

@@ -303,12 +303,16 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
   {
     const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
     const int qb0 = q0 & ((1 << A.lqb) - 1);
+    // levels 2/3 (tile rows of 4 / 2 cells): query-major slots (round 3: Sintel
+    // B=8 51.5 -> 50.1 us, KITTI B=8 bf16 54.1 -> 51.6 us, bit-identical)
     if (A.lth == 30)
       gather_windows<R, NT_, 1, PT>(base, qb0, A, org, cells, q0, g.N, tid);
-    else if (A.tw >= 4)
+    else if (A.tw >= 8)
       gather_windows<R, NT_, 4, PT>(base, qb0, A, org, cells, q0, g.N, tid);
+    else if (A.tw == 4)
+      gather_windows<R, NT_, 4, PT, true>(base, qb0, A, org, cells, q0, g.N, tid);
     else if (A.tw == 2)
-      gather_windows<R, NT_, 2, PT>(base, qb0, A, org, cells, q0, g.N, tid);
+      gather_windows<R, NT_, 2, PT, true>(base, qb0, A, org, cells, q0, g.N, tid);
     else
       gather_windows<R, NT_, 1, PT>(base, qb0, A, org, cells, q0, g.N, tid);
   }
@@ -637,11 +641,16 @@ __global__ __launch_bounds__(NT, 4) void corr_lookup_conv1x1_h2_kernel(
       float4 win[C::VIT];
       const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
       const int qb0 = q0 & ((1 << A.lqb) - 1);
-      if (l < 3)
+      if (l < 2) {
         gather_load<R, NT, 4>(base, qb0, A, org, q0, g.N, tid, win);
-      else
-        gather_load<R, NT, 2>(base, qb0, A, org, q0, g.N, tid, win);
-      gather_store<R, NT>(win, cells, tid);
+        gather_store<R, NT>(win, cells, tid);
+      } else {   // levels 2/3: query-major slots, as the lookup
+        if (l == 2)
+          gather_load<R, NT, 4, PT, true>(base, qb0, A, org, q0, g.N, tid, win);
+        else
+          gather_load<R, NT, 2, PT, true>(base, qb0, A, org, q0, g.N, tid, win);
+        gather_store<R, NT, true>(win, cells, tid);
+      }
     }
     __syncthreads();
     {

@@ -268,6 +268,64 @@ int xp_dma(const float* f1, const float* f2, float* pyr, const BuildGeom& g, int
   return dxr::launch_status();
 }
 
+
+// Split-pass variants for A/B (NCHW, D == 256): PX pixels x 16 channel blocks
+// per workgroup (PX * 16 threads), lane -> pixel fastest; per-lane write-through
+// record stores (the product transposes through LDS for whole-line stores).
+template <int PX>
+__global__ __launch_bounds__(PX * 16) void xp_split_px_kernel(const float* __restrict__ f1,
+                                                              const float* __restrict__ f2,
+                                                              uint4* __restrict__ sp1,
+                                                              uint4* __restrict__ sp2,
+                                                              int* __restrict__ e1,
+                                                              int* __restrict__ e2, int D, int N) {
+  __shared__ float red[16][PX + 1];
+  const int tid = threadIdx.x;
+  const int kb0 = tid / PX, pl = tid % PX;
+  const int p = blockIdx.x * PX + pl;
+  const bool live = p < N;
+  const int b = blockIdx.y;
+  const float* src = (blockIdx.z == 0 ? f1 : f2) + (long long)b * D * N;
+  uint4* sp = (blockIdx.z == 0 ? sp1 : sp2) + (long long)b * (D / 16) * N * 4;
+  int* ex = (blockIdx.z == 0 ? e1 : e2) + (long long)b * N;
+  float x[16];
+  float m = 0.f;
+  if (live) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = src[(long long)(kb0 * 16 + i) * N + p];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float a = __builtin_fabsf(x[i]);
+      m = (m < 0.f || !(a <= 3.40282347e38f)) ? -1.f : (a > m ? a : m);
+    }
+  }
+  red[kb0][pl] = m;
+  __syncthreads();
+  float mm = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const float v = red[k][pl];
+    mm = (mm < 0.f || v < 0.f) ? -1.f : (v > mm ? v : mm);
+  }
+  if (!live) return;
+  const int s = pixel_scale(mm < 0.f ? 0.f : mm, mm >= 0.f);
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(sp, (short)0, 0x7fffffff, 0x00020000);
+  if (kb0 == 0) {
+    const __amdgpu_buffer_rsrc_t re =
+        __builtin_amdgcn_make_buffer_rsrc(ex, (short)0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)s, re, (unsigned)p * 4u, 0, 16);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] = __builtin_ldexpf(x[i], s);
+  uint4 rec[4];
+  split_record<false>(x, rec);
+  const unsigned off = (unsigned)((kb0 * N + p) * 64);
+#pragma unroll
+  for (int c = 0; c < 4; ++c)   // per-lane 64-B records: partial-line write-through stores
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, rec[c]), rs, off + 16 * c, 0, 16);
+}
+
 }  // namespace
 
 // Variant xp of the pre-split build (f32 NCHW fmaps, W % 4 == 0, D % 16 == 0,
@@ -296,4 +354,27 @@ extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t
     case 33: return xp_dma<33>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     default: return DXR_EINVAL;
   }
+}
+
+// Split pass alone (NCHW f32, D == 256), variant v: 0 product (64 px, 1024
+// threads), 1 plain stores, 2 / 3 / 4: 16 / 32 / 128 pixels per workgroup.
+extern "C" int dxr_xp_split(const float* f1, const float* f2, int64_t B, int64_t D, int64_t H,
+                            int64_t W, void* ws, int v, hipStream_t stream) {
+  if (D != 256) return DXR_EINVAL;
+  const long long N = H * W, spb = align256(B * D * N * 4), eb = align256(B * N * 4);
+  uint8_t* w = static_cast<uint8_t*>(ws);
+  uint4* s1 = reinterpret_cast<uint4*>(w);
+  uint4* s2 = reinterpret_cast<uint4*>(w + spb);
+  int* e1 = reinterpret_cast<int*>(w + 2 * spb);
+  int* e2 = reinterpret_cast<int*>(w + 2 * spb + eb);
+  auto grid = [&](int px) { return dim3((unsigned)((N + px - 1) / px), (unsigned)B, 2); };
+  switch (v) {
+    case 0: hipLaunchKernelGGL((split_pairs_kernel<false>), grid(64), dim3(1024), 0, stream, f1, f2, s1, s2, e1, e2, (int)D, (int)N); break;
+    case 1: hipLaunchKernelGGL(xp_split_plain_kernel, grid(64), dim3(1024), 0, stream, f1, f2, s1, s2, e1, e2, (int)D, (int)N); break;
+    case 2: hipLaunchKernelGGL((xp_split_px_kernel<16>), grid(16), dim3(256), 0, stream, f1, f2, s1, s2, e1, e2, (int)D, (int)N); break;
+    case 3: hipLaunchKernelGGL((xp_split_px_kernel<32>), grid(32), dim3(512), 0, stream, f1, f2, s1, s2, e1, e2, (int)D, (int)N); break;
+    case 4: hipLaunchKernelGGL((xp_split_px_kernel<64>), grid(64), dim3(1024), 0, stream, f1, f2, s1, s2, e1, e2, (int)D, (int)N); break;
+    default: return DXR_EINVAL;
+  }
+  return dxr::launch_status();
 }

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--xp", type=int, nargs="+", default=[0, 32, 1, 2, 3, 4, 5])
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--split", type=int, nargs="*", default=[0, 1, 2, 3, 4],
+                    help="split-pass variants timed alone (dxr_xp_split)")
     a = ap.parse_args()
     import dexiraft_amd
     from dexiraft_amd import _native as nat
@@ -37,6 +39,8 @@ def main():
     vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
     lib.dxr_xp_build.restype = i32
     lib.dxr_xp_build.argtypes = [vp, vp, i64, i64, i64, i64, vp, vp, i32, vp, vp]
+    lib.dxr_xp_split.restype = i32
+    lib.dxr_xp_split.argtypes = [vp, vp, i64, i64, i64, i64, vp, i32, vp]
     dev = torch.device("cuda", 0)
     B, H, W = (int(v) for v in a.shape.split("x"))
     D = 256
@@ -91,6 +95,33 @@ def main():
         print(json.dumps({"shape": [B, D, H, W], "us_per_launch_min_med":
                           {x: [round(min(v), 1), round(float(np.median(v)), 1)] for x, v in res.items()}}),
               flush=True)
+        if a.split:
+            ref_ws = None
+            sg = {}
+            for v in a.split:
+                assert lib.dxr_xp_split(f1.data_ptr(), f2.data_ptr(), B, D, H, W, ws.data_ptr(), v,
+                                        stream.cuda_stream) == 0
+                torch.cuda.synchronize()
+                if ref_ws is None:
+                    ref_ws = ws.clone()
+                assert torch.equal(ws, ref_ws), f"split variant {v} differs"
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr, stream=stream):
+                    for _ in range(a.reps):
+                        lib.dxr_xp_split(f1.data_ptr(), f2.data_ptr(), B, D, H, W, ws.data_ptr(), v,
+                                         stream.cuda_stream)
+                sg[v] = gr
+            sres = {v: [] for v in a.split}
+            for _ in range(a.rounds):
+                for v in a.split:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    sg[v].replay()
+                    e1.record(stream)
+                    torch.cuda.synchronize()
+                    sres[v].append(e0.elapsed_time(e1) * 1e3 / a.reps)
+            print(json.dumps({"split_us_min_med": {v: [round(min(t), 2), round(float(np.median(t)), 2)]
+                                                   for v, t in sres.items()}}), flush=True)
         for x in (256, 257):
             for _ in range(3):
                 graphs[a.xp[0]].replay()

@@ -198,14 +198,17 @@ def test_check_maps_status_to_reference_exceptions(nat):
 def test_build_workspace_bytes(nat):
     """The pre-split f32 build's workspace (ABI 6): two f16-pair operand copies
     (4 B per f32 element) and two int32 exponents per pixel, each 256-B aligned;
-    bf16 fmaps and D % 16 != 0 need none; bad geometry is -1."""
+    bf16 fmaps with D % 32 == 0 the pack pass's two blocked copies; other D
+    need none; bad geometry is -1."""
     lib = nat.load()
     al = lambda x: (x + 255) // 256 * 256   # noqa: E731
     for B, D, H, W in ((1, 256, 55, 128), (8, 256, 47, 156), (2, 64, 13, 19)):
         N = H * W
         assert lib.dxr_build_workspace_bytes(nat.DXR_F32, B, D, H, W) == \
             2 * al(B * D * N * 4) + 2 * al(B * N * 4)
-    assert lib.dxr_build_workspace_bytes(nat.DXR_BF16, 1, 256, 55, 128) == 0
+    # bf16: the pack pass's blocked copies of both fmaps (2 B per element)
+    assert lib.dxr_build_workspace_bytes(nat.DXR_BF16, 1, 256, 55, 128) == 2 * al(256 * 7040 * 2)
+    assert lib.dxr_build_workspace_bytes(nat.DXR_BF16, 1, 48, 55, 128) == 0
     assert lib.dxr_build_workspace_bytes(nat.DXR_F32, 1, 24, 55, 128) == 0
     assert lib.dxr_build_workspace_bytes(nat.DXR_F32, -1, 256, 55, 128) == -1
     P = 1 << 12

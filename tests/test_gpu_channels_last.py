@@ -172,10 +172,12 @@ def test_nhwc_build_entry_point(dx):
 @pytest.mark.parametrize("pyr_dt", ["f32", "bf16"])
 def test_nhwc_bf16_build_entry_point(dx, W, pyr_dt):
     """dxr_corr_pyramid_build with bf16 DXR_NHWC operands (the bf16 mode's
-    channels-last encoders, core/extractor.py:168-192) reads them in place and
-    writes the NCHW bf16 build's pyramid bit for bit, page padding included —
-    also for W % 4 != 0, where the NCHW build is the one-block kernel.  D % 32
-    != 0 is DXR_EUNSUPPORTED (the shell transposes)."""
+    channels-last encoders, core/extractor.py:168-192) reads them in place (the
+    bf16 LDS-DMA build) and writes the workspace-less NCHW bf16 build's pyramid
+    bit for bit, page padding included — also for W % 4 != 0, where the NCHW
+    build is the one-block kernel; so does the NCHW build with a workspace
+    (pack pass + the LDS-DMA build).  D % 32 != 0 is DXR_EUNSUPPORTED (the
+    shell transposes)."""
     from dexiraft_amd import _native as nat
     lib = nat.load()
     B, D, H = 2, 128, 21
@@ -191,9 +193,21 @@ def test_nhwc_bf16_build_entry_point(dx, W, pyr_dt):
                                         code, nat.DXR_BUILD_AUTO, nat.stream_of(a))
         assert st == 0
         bufs.append(buf)
+    # NCHW with a workspace: the pack pass + the bf16 LDS-DMA build (scalar pack
+    # loads for W = 39: N = 819 is not a multiple of 4)
+    ws = torch.empty(lib.dxr_build_workspace_bytes(nat.DXR_BF16, B, D, H, W), dtype=torch.uint8,
+                     device=DEV)
+    buf = torch.full((n,), float("nan"), device=DEV, dtype=tdt)
+    st = lib.dxr_corr_pyramid_build_ws(f1.data_ptr(), f2.data_ptr(), nat.DXR_BF16, nat.DXR_NCHW,
+                                       B, D, H, W, 4, float(np.sqrt(np.float32(D))), buf.data_ptr(),
+                                       code, nat.DXR_BUILD_AUTO, ws.data_ptr(), ws.numel(),
+                                       nat.stream_of(f1))
+    assert st == 0
+    bufs.append(buf)
     torch.cuda.synchronize()
     assert not torch.isnan(bufs[1].float()).any()   # every page written
     assert torch.equal(bufs[0], bufs[1])
+    assert torch.equal(bufs[0], bufs[2])
     g1 = _cl(_t(dg.fmap(83, B, 48, H, W)).bfloat16())
     st = lib.dxr_corr_pyramid_build(g1.data_ptr(), g1.data_ptr(), nat.DXR_BF16, nat.DXR_NHWC, B,
                                     48, H, W, 4, 6.9282, bufs[0].data_ptr(), code,
