@@ -33,6 +33,7 @@
  *   dxr_alt_corr_backward    alt_cuda_corr/correlation.cpp:36-48 `backward`
  *                            (alt_cuda_corr/correlation_kernel.cu:288-320)
  *   dxr_alt_corr_lookup      core/corr.py:74-91  AlternateCorrBlock.__call__
+ *   dxr_alt_corr_lookup_ws   the same, queries ordered by window position first
  *                            (all levels in one launch, / sqrt(D) fused)
  *   dxr_corr_lookup_conv1x1  core/corr.py:29-50 CorrBlock.__call__ followed by
  *                            core/update.py:90 F.relu(self.convc1(corr))
@@ -327,6 +328,30 @@ int dxr_alt_corr_lookup(const float* fmap1, const float* const* fmap2_levels,
                         int64_t B, int64_t H, int64_t W, int64_t C,
                         int num_levels, int radius, float divisor,
                         hipStream_t stream);
+
+/*
+ * Bytes of device workspace dxr_alt_corr_lookup_ws uses for B coordinate sets
+ * of H x W queries over num_levels levels (one 16-byte entry per query slot of
+ * every 4 x 8 query tile and level; -1: bad geometry).  ABI 6.
+ */
+int64_t dxr_alt_workspace_bytes(int64_t B, int64_t H, int64_t W, int num_levels);
+
+/*
+ * dxr_alt_corr_lookup with a caller-owned workspace (16-byte aligned, at least
+ * dxr_alt_workspace_bytes; no initialisation needed).  One extra launch orders
+ * each level's queries before the lookup: grouped by window position (bins of
+ * ~32 queries) when the 4 x 8 query tiles' union boxes would be larger than
+ * 1.5x a bin group's (flows that vary pixel to pixel), else in tile order.  The
+ * outputs are the workspace-less call's, bit for bit.  Falls back to
+ * dxr_alt_corr_lookup when the workspace is NULL or short, or an image has
+ * more than 1024 query tiles.  Replaces core/corr.py:74-91 as above.  ABI 6.
+ */
+int dxr_alt_corr_lookup_ws(const float* fmap1, const float* const* fmap2_levels,
+                           const float* coords, float* out,
+                           int64_t B, int64_t H, int64_t W, int64_t C,
+                           int num_levels, int radius, float divisor,
+                           void* workspace, int64_t workspace_bytes,
+                           hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -57,6 +57,9 @@ SIGNATURES: dict[str, tuple[object, list[object]]] = {
     "dxr_avg_pool2x2_nhwc": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _vp]),
     "dxr_alt_corr_lookup": (_int, [_vp, ctypes.POINTER(_vp), _vp, _vp, _i64, _i64, _i64, _i64,
                                    _int, _int, _f32, _vp]),
+    "dxr_alt_workspace_bytes": (_i64, [_i64, _i64, _i64, _int]),
+    "dxr_alt_corr_lookup_ws": (_int, [_vp, ctypes.POINTER(_vp), _vp, _vp, _i64, _i64, _i64, _i64,
+                                      _int, _int, _f32, _vp, _i64, _vp]),
 }
 
 _lock = threading.Lock()

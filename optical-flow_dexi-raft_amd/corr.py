@@ -582,9 +582,14 @@ class AlternateCorrBlock:
         out = torch.empty((B, self.num_levels * rd * rd, H, W), dtype=torch.float32,
                           device=self._device)
         lib = nat.load()
+        # query-order workspace (dxr_alt_corr_lookup_ws), from torch's caching
+        # allocator: freed once the launches that use it have run
+        nbytes = lib.dxr_alt_workspace_bytes(B, H, W, self.num_levels)
+        ws = torch.empty(max(nbytes, 0), dtype=torch.uint8, device=self._device)
         with _Launch(self._device):
-            st = lib.dxr_alt_corr_lookup(self._f1_nhwc.data_ptr(), self._f2_ptrs, c.data_ptr(),
-                                         out.data_ptr(), B, H, W, D, self.num_levels,
-                                         self.radius, _sqrt_dim(D), nat.stream_of(c))
-        nat.check(st, "AlternateCorrBlock lookup (dxr_alt_corr_lookup)")
+            st = lib.dxr_alt_corr_lookup_ws(self._f1_nhwc.data_ptr(), self._f2_ptrs, c.data_ptr(),
+                                            out.data_ptr(), B, H, W, D, self.num_levels,
+                                            self.radius, _sqrt_dim(D), nat.ptr(ws),
+                                            max(nbytes, 0), nat.stream_of(c))
+        nat.check(st, "AlternateCorrBlock lookup (dxr_alt_corr_lookup_ws)")
         return out

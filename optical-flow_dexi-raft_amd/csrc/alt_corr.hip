@@ -254,16 +254,17 @@ __device__ __forceinline__ void alt_split8h(const float (&x)[8], uint4& h, uint4
 // range, or inf/NaN) is recomputed by its wave on the 3-way bf16 split, with
 // the query operand split from fmap1 in registers.
 // BIN: the workgroup's 32 queries are not a 4 x 8 pixel tile but 32 consecutive
-// entries of perm (this coordinate set's and level's query list sorted by window
-// position, alt_bin_kernel), so their windows — and the union box — are compact
-// whatever the flow field; `tile` is then the index of that chunk of 32.
+// entries of `ord` — this coordinate set's and level's query list in the order
+// alt_order_kernel chose (grouped by window position, or the tile order), each
+// entry {query, x, y, -} carrying the query's coordinates, so a workgroup's
+// first global read gives it both.
 // PF: k steps of cell-vector loads kept in flight (a ring of PF register stages).
 template <int R, int NRB, int CMAX, bool H2 = false, int MINW = 2, bool BIN = false, int PF = 1>
 __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* __restrict__ f1,
                                                                const float* __restrict__ coords,
                                                                float* __restrict__ out,
                                                                AltGeom g, int W1, int tiles_x,
-                                                               const int* __restrict__ perm) {
+                                                               const int4* __restrict__ ord) {
   constexpr int RD = 2 * R + 1, RD1 = RD + 1, NCELL = RD1 * RD1;
   constexpr int CHUNK = 4 * 32 * NRB;                       // box cells per chunk
   constexpr int KB = CMAX / 8;                              // 8-channel blocks
@@ -273,6 +274,7 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
   __shared__ int4 qinfo[TQ];                                // {x0, y0, live, -}
   __shared__ int box[4];                                    // bx0, by0, bw, bh
   __shared__ int qlist[TQ];                                 // BIN: query index or -1
+  __shared__ float2 qxy[TQ];                                // BIN: its coordinates
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // Workgroups are dealt round-robin to the 8 XCDs; XCD k takes the k-th
@@ -304,9 +306,11 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
   };
   if constexpr (BIN) {
     if (tid < TQ) {
-      // perm: per (coordinate set, level) gridDim.x * 32 entries, -1 = padding
-      qlist[tid] = perm[((long long)z * gridDim.y + blockIdx.y) * ((long long)gridDim.x * TQ) +
-                        tile * TQ + tid];
+      // per (coordinate set, level) gridDim.x * 32 entries, query -1 = padding
+      const int4 e = ord[((long long)z * gridDim.y + blockIdx.y) * ((long long)gridDim.x * TQ) +
+                         tile * TQ + tid];
+      qlist[tid] = e.x;
+      qxy[tid] = make_float2(__int_as_float(e.y), __int_as_float(e.z));
     }
     __syncthreads();
   }
@@ -317,8 +321,14 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
     int x0 = 0, y0 = 0, live = 0;
     if (qsel >= 0) {
       const int q = qsel;
-      const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
-      const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
+      float x, y;
+      if constexpr (BIN) {
+        x = qxy[tid].x * lv.inv;
+        y = qxy[tid].y * lv.inv;
+      } else {
+        x = cz[(long long)q * g.coord_qstride] * lv.inv;
+        y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
+      }
       const float xf = floorf(x), yf = floorf(y);
       if (fabsf(xf) < 1.0e8f && fabsf(yf) < 1.0e8f) {
         x0 = (int)xf - R;
@@ -531,8 +541,14 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
   const int qq = tid & (TQ - 1), cls = tid / TQ;
   const int q = query_of(qq);
   if (q < 0) return;
-  const float x = cz[(long long)q * g.coord_qstride] * lv.inv;
-  const float y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
+  float x, y;
+  if constexpr (BIN) {
+    x = qxy[qq].x * lv.inv;
+    y = qxy[qq].y * lv.inv;
+  } else {
+    x = cz[(long long)q * g.coord_qstride] * lv.inv;
+    y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
+  }
   const float dx = x - floorf(x), dy = y - floorf(y);
   const float* s = S + qq * NCELL;
   float* o = out + (long long)z * g.cout * g.N + (long long)lv.ch_off * g.N + q;
@@ -551,14 +567,207 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
   }
 }
 
+// ---------------------------------------------------------------------------
+// Query order of the on-the-fly lookup (round 3).  The union box of a 4 x 8
+// query tile is compact for smooth flow fields but ~10x its windows' cells at
+// level 0 for flows that vary pixel to pixel (the bench's i.i.d. N(0, 4^2)
+// model): neighbouring queries' windows are unrelated.  Grouping the queries by
+// window position instead keeps every box near one window whatever the flow.
+// One workgroup per (coordinate set, level), 1024 threads, one launch:
+//   pass 1  thread = 4 x 8 query tile(s): load the tile's coordinates, bin every
+//           query by its window origin (bins of ~32 queries: 2^by x 2^bx origin
+//           cells, snake order over bin rows; non-finite coordinates last), LDS
+//           histogram, and the tile's union box area (the cells the tile order
+//           would multiply);
+//   scan    exclusive prefix of the histogram (wave scans + one LDS pass);
+//   choose  the bin order when the tiles' boxes average more than 1.5x a bin
+//           chunk's estimated box ((2^by + 2r + 1) x (2^bx + 2r + 1)), else the
+//           tile order (then the lookup multiplies exactly the spatial form's
+//           boxes: smooth flows lose nothing but this launch);
+//   pass 2  write the list: entry {query, x, y, 0}, queries of a bin in any
+//           order (the box GEMM's per-(cell, query) sums do not depend on which
+//           queries share a workgroup: outputs are bit-identical either way).
+// ---------------------------------------------------------------------------
+constexpr int BIN_MAX = 4096;
+
+struct BinGeom {
+  int bsx[8], bsy[8], nbx[8], nby[8];
+};
+
+BinGeom make_bins(int N, const AltGeom& g, int levels) {
+  BinGeom b{};
+  for (int l = 0; l < levels; ++l) {
+    const int h2 = g.lv[l].H2, w2 = g.lv[l].W2;
+    const double dens = (double)N / ((double)h2 * w2);
+    int lg = 0;
+    while ((1 << lg) * dens < 32.0 && lg < 12) ++lg;   // bin area 2^lg ~ 32 queries
+    int by = lg / 2, bx = lg - by;
+    while (((w2 + (1 << bx) - 1) >> bx) * ((h2 + (1 << by) - 1) >> by) > BIN_MAX) {
+      if (bx <= by) ++bx; else ++by;
+    }
+    b.bsx[l] = bx;
+    b.bsy[l] = by;
+    b.nbx[l] = (w2 + (1 << bx) - 1) >> bx;
+    b.nby[l] = (h2 + (1 << by) - 1) >> by;
+  }
+  return b;
+}
+
+template <int R>
+__global__ __launch_bounds__(1024) void alt_order_kernel(const float* __restrict__ coords,
+                                                         int4* __restrict__ ord, AltGeom g,
+                                                         BinGeom bg, int W1, int tiles_x,
+                                                         int ntiles) {
+  constexpr int RD1 = 2 * R + 2;
+  __shared__ int cnt[BIN_MAX + 1];
+  __shared__ int wsum[16];
+  __shared__ float wcost[16];
+  __shared__ int use_bins;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l = blockIdx.x, z = blockIdx.y;
+  const AltLevel lv = g.lv[l];
+  const int nbx = bg.nbx[l], nb = nbx * bg.nby[l], bsx = bg.bsx[l], bsy = bg.bsy[l];
+  const float* cz = coords + (long long)z * g.coord_zstride;
+  const int H1 = g.N / W1;
+  const long long NP = (long long)ntiles * TQ;
+  int4* oz = ord + ((long long)z * gridDim.x + l) * NP;
+  for (int i = tid; i <= nb; i += 1024) cnt[i] = 0;
+  __syncthreads();
+
+  // pass 1: thread = tile tid; the bins of its 32 queries stay in registers
+  // (two 16-bit bins per register)
+  uint32_t bins[TQ / 2];
+  float cost = 0.f;
+  const int t = tid;
+  {
+    int lx0 = 0x7fffffff, ly0 = 0x7fffffff, lx1 = -1, ly1 = -1;
+    float cx_[TQ], cy_[TQ];
+#pragma unroll
+    for (int s = 0; s < TQ; ++s) {   // all 64 loads in flight
+      const int qy = (t / tiles_x) * TQY + s / TQX, qx = (t % tiles_x) * TQX + s % TQX;
+      const bool in = t < ntiles && qy < H1 && qx < W1;
+      const int q = in ? qy * W1 + qx : 0;
+      cx_[s] = in ? cz[(long long)q * g.coord_qstride] : __builtin_nanf("");
+      cy_[s] = in ? cz[(long long)q * g.coord_qstride + g.coord_cstride] : __builtin_nanf("");
+    }
+#pragma unroll
+    for (int s = 0; s < TQ; ++s) {
+      const int qy = (t / tiles_x) * TQY + s / TQX, qx = (t % tiles_x) * TQX + s % TQX;
+      const bool in = t < ntiles && qy < H1 && qx < W1;
+      const float x = cx_[s] * lv.inv, y = cy_[s] * lv.inv;
+      const float xf = floorf(x), yf = floorf(y);
+      int bin = nb;
+      if (fabsf(xf) < 1.0e8f && fabsf(yf) < 1.0e8f) {
+        const int cx = min(max((int)xf, 0), lv.W2 - 1), cy = min(max((int)yf, 0), lv.H2 - 1);
+        const int byi = cy >> bsy;
+        int bxi = cx >> bsx;
+        if (byi & 1) bxi = nbx - 1 - bxi;
+        bin = byi * nbx + bxi;
+        const int x0 = (int)xf - R, y0 = (int)yf - R;
+        if (x0 + RD1 > 0 && x0 < lv.W2 && y0 + RD1 > 0 && y0 < lv.H2) {   // live window
+          lx0 = min(lx0, max(x0, 0));
+          ly0 = min(ly0, max(y0, 0));
+          lx1 = max(lx1, min(x0 + RD1, lv.W2));
+          ly1 = max(ly1, min(y0 + RD1, lv.H2));
+        }
+      }
+      if (in) atomicAdd(&cnt[bin], 1);
+      const uint32_t bv = in ? (uint32_t)bin : 0xffffu;
+      if (s & 1) bins[s >> 1] |= bv << 16;
+      else bins[s >> 1] = bv;
+    }
+    if (lx1 > lx0) cost += (float)(lx1 - lx0) * (float)(ly1 - ly0);
+  }
+  // the tiles' box area, summed over the workgroup
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cost += __shfl_xor(cost, o);
+  if (lane == 0) wcost[wave] = cost;
+  __syncthreads();
+
+  // exclusive scan of cnt[0..nb]: thread t owns a run of `per` bins
+  const int per = (nb + 1 + 1023) / 1024;
+  int loc = 0;
+  for (int k = 0; k < per; ++k) {
+    const int b = tid * per + k;
+    if (b <= nb) loc += cnt[b];
+  }
+  int v = loc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(v, o);
+    if (lane >= o) v += t;
+  }
+  if (lane == 63) wsum[wave] = v;
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    float tot = 0.f;
+    for (int w = 0; w < 16; ++w) {
+      const int t = wsum[w];
+      wsum[w] = acc;
+      acc += t;
+      tot += wcost[w];
+    }
+    const float chunk = (float)((1 << bsy) + RD1 - 1) * (float)((1 << bsx) + RD1 - 1);
+    use_bins = tot > 1.5f * chunk * (float)ntiles ? 1 : 0;
+  }
+  __syncthreads();
+  int run = wsum[wave] + v - loc;
+  for (int k = 0; k < per; ++k) {
+    const int b = tid * per + k;
+    if (b <= nb) {
+      const int c = cnt[b];
+      cnt[b] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+
+  // pass 2: the list
+  const bool binned = use_bins != 0;
+  if (t < ntiles) {
+#pragma unroll
+    for (int s = 0; s < TQ; ++s) {
+      const int qy = (t / tiles_x) * TQY + s / TQX, qx = (t % tiles_x) * TQX + s % TQX;
+      const bool in = qy < H1 && qx < W1;
+      const int q = in ? qy * W1 + qx : -1;
+      int4 e = make_int4(-1, 0, 0, 0);
+      if (in) e = make_int4(q, __float_as_int(cz[(long long)q * g.coord_qstride]),
+                            __float_as_int(cz[(long long)q * g.coord_qstride + g.coord_cstride]), 0);
+      if (binned) {
+        const int bin = (int)((bins[s >> 1] >> (16 * (s & 1))) & 0xffffu);
+        if (in) oz[atomicAdd(&cnt[bin], 1)] = e;
+      } else {
+        oz[(long long)t * TQ + s] = e;
+      }
+    }
+  }
+  if (binned)   // entries past the queries: padding
+    for (long long i = g.N + tid; i < NP; i += 1024) oz[i] = make_int4(-1, 0, 0, 0);
+}
+
+long long alt_order_entries(long long H, long long W) {
+  return ((W + TQX - 1) / TQX) * ((H + TQY - 1) / TQY) * (long long)TQ;
+}
+
 template <int R, int NRB>
 int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const AltGeom& g,
-                      int levels, int Z, int W1, hipStream_t stream) {
+                      int levels, int Z, int W1, hipStream_t stream, int4* ord = nullptr) {
   const int H1 = g.N / W1;
   const int tiles_x = (W1 + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
-  const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)levels, (unsigned)Z);
+  const int ntiles = tiles_x * tiles_y;
+  const dim3 grid((unsigned)ntiles, (unsigned)levels, (unsigned)Z);
   if (g.C > 256) return DXR_EUNSUPPORTED;
   // f16 pair split (r02, 1080p: 227 vs 275 us for the 3-way bf16 split), 3 workgroups/CU
+  if (ord != nullptr && ntiles <= 1024 && Z <= 65535) {   // one tile per order thread
+    hipLaunchKernelGGL((alt_order_kernel<R>), dim3((unsigned)levels, (unsigned)Z), dim3(1024), 0,
+                       stream, coords, ord, g, make_bins(g.N, g, levels), W1, tiles_x, ntiles);
+    const int st = dxr::launch_status();
+    if (st != DXR_OK) return st;
+    hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 3, true>), grid, dim3(256), 0,
+                       stream, f1, coords, out, g, W1, tiles_x, ord);
+    return dxr::launch_status();
+  }
   hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 3>), grid, dim3(256), 0, stream, f1,
                      coords, out, g, W1, tiles_x, nullptr);
   return dxr::launch_status();
@@ -576,18 +785,20 @@ int launch_alt_r(const float* f1, const float* coords, float* out, const AltGeom
 }
 
 int launch_alt(const float* f1, const float* coords, float* out, const AltGeom& g, int levels,
-               int Z, int radius, bool vec, hipStream_t stream, int W1 = 0) {
+               int Z, int radius, bool vec, hipStream_t stream, int W1 = 0,
+               int4* ord = nullptr) {
   // MFMA form: C a multiple of 16 (k16 steps) up to 256, 16-byte aligned rows;
-  // the per-query VALU form otherwise.
+  // the per-query VALU form otherwise.  With a workspace (`ord`) the queries are
+  // ordered first (alt_order_kernel).
   if (vec && W1 > 0 && g.C % 16 == 0 && g.C <= 256) {
     switch (radius) {
-      case 0: return launch_alt_mfma_r<0, 1>(f1, coords, out, g, levels, Z, W1, stream);
-      case 1: return launch_alt_mfma_r<1, 1>(f1, coords, out, g, levels, Z, W1, stream);
-      case 2: return launch_alt_mfma_r<2, 1>(f1, coords, out, g, levels, Z, W1, stream);
-      case 3: return launch_alt_mfma_r<3, 1>(f1, coords, out, g, levels, Z, W1, stream);
-      case 4: return launch_alt_mfma_r<4, 1>(f1, coords, out, g, levels, Z, W1, stream);
-      case 5: return launch_alt_mfma_r<5, 1>(f1, coords, out, g, levels, Z, W1, stream);
-      case 6: return launch_alt_mfma_r<6, 1>(f1, coords, out, g, levels, Z, W1, stream);
+      case 0: return launch_alt_mfma_r<0, 1>(f1, coords, out, g, levels, Z, W1, stream, ord);
+      case 1: return launch_alt_mfma_r<1, 1>(f1, coords, out, g, levels, Z, W1, stream, ord);
+      case 2: return launch_alt_mfma_r<2, 1>(f1, coords, out, g, levels, Z, W1, stream, ord);
+      case 3: return launch_alt_mfma_r<3, 1>(f1, coords, out, g, levels, Z, W1, stream, ord);
+      case 4: return launch_alt_mfma_r<4, 1>(f1, coords, out, g, levels, Z, W1, stream, ord);
+      case 5: return launch_alt_mfma_r<5, 1>(f1, coords, out, g, levels, Z, W1, stream, ord);
+      case 6: return launch_alt_mfma_r<6, 1>(f1, coords, out, g, levels, Z, W1, stream, ord);
       default: return DXR_EUNSUPPORTED;
     }
   }
@@ -929,10 +1140,10 @@ extern "C" int dxr_avg_pool2x2_nhwc(const float* in, float* out, int64_t B, int6
   return dxr::launch_status();
 }
 
-extern "C" int dxr_alt_corr_lookup(const float* fmap1, const float* const* fmap2_levels,
-                                   const float* coords, float* out, int64_t B, int64_t H,
-                                   int64_t W, int64_t C, int num_levels, int radius,
-                                   float divisor, hipStream_t stream) {
+namespace {
+int alt_lookup(const float* fmap1, const float* const* fmap2_levels, const float* coords, float* out,
+               int64_t B, int64_t H, int64_t W, int64_t C, int num_levels, int radius,
+               float divisor, void* workspace, int64_t workspace_bytes, hipStream_t stream) {
   dxr::Levels L;
   if (!dxr::make_levels(B, H, W, num_levels, &L)) return DXR_EINVAL;
   if (C < 1 || radius < 0 || !(divisor == divisor) || divisor == 0.f) return DXR_EINVAL;
@@ -958,6 +1169,34 @@ extern "C" int dxr_alt_corr_lookup(const float* fmap1, const float* const* fmap2
     vec = vec && aligned16(fmap2_levels[l]);
     g.lv[l] = AltLevel{fmap2_levels[l], L.h[l], L.w[l], 1.f / (float)(1 << l), l * rd * rd};
   }
-  return launch_alt(fmap1, coords, out, g, num_levels, (int)B, radius, vec, stream, (int)W);
+  int4* ord = nullptr;
+  if (workspace != nullptr && aligned16(workspace) &&
+      workspace_bytes >= 16 * (long long)B * num_levels * alt_order_entries(H, W))
+    ord = static_cast<int4*>(workspace);
+  return launch_alt(fmap1, coords, out, g, num_levels, (int)B, radius, vec, stream, (int)W, ord);
+}
+}  // namespace
+
+extern "C" int dxr_alt_corr_lookup(const float* fmap1, const float* const* fmap2_levels,
+                                   const float* coords, float* out, int64_t B, int64_t H,
+                                   int64_t W, int64_t C, int num_levels, int radius,
+                                   float divisor, hipStream_t stream) {
+  return alt_lookup(fmap1, fmap2_levels, coords, out, B, H, W, C, num_levels, radius, divisor,
+                    nullptr, 0, stream);
+}
+
+extern "C" int64_t dxr_alt_workspace_bytes(int64_t B, int64_t H, int64_t W, int num_levels) {
+  if (B < 0 || H < 1 || W < 1 || num_levels < 1 || num_levels > 8 || H * W > (1LL << 30))
+    return -1;
+  return 16 * B * num_levels * alt_order_entries(H, W);
+}
+
+extern "C" int dxr_alt_corr_lookup_ws(const float* fmap1, const float* const* fmap2_levels,
+                                      const float* coords, float* out, int64_t B, int64_t H,
+                                      int64_t W, int64_t C, int num_levels, int radius,
+                                      float divisor, void* workspace, int64_t workspace_bytes,
+                                      hipStream_t stream) {
+  return alt_lookup(fmap1, fmap2_levels, coords, out, B, H, W, C, num_levels, radius, divisor,
+                    workspace, workspace_bytes, stream);
 }
 

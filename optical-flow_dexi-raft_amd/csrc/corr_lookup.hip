@@ -102,7 +102,7 @@ __device__ __forceinline__ float sample_coord(float c, float sm1, float half_sm1
 // instructions per wave, 1.7 waves per SIMD, 8.8 of 11.6 us left with gathers
 // and stores removed) was bound by its per-thread instruction chains.
 // ---------------------------------------------------------------------------
-template <int R, int NT_ = 512>
+template <int R, int NT_ = 512, int QB_ = 0>
 struct WideCfg {
   static constexpr int RD = 2 * R + 1;
   static constexpr int WD = RD + 2;                      // window side (cells)
@@ -111,7 +111,7 @@ struct WideCfg {
   static constexpr int QS = WD * RS + 4;                 // LDS cells per query (bank skew)
   static constexpr int K = RD * RD;                      // outputs per query and level
   static constexpr int NT = NT_;
-  static constexpr int QB = R <= 4 ? 32 : 16;            // queries per workgroup
+  static constexpr int QB = QB_ ? QB_ : (R <= 4 ? 32 : 16);   // queries per workgroup
   static constexpr int LG = RD <= 2 ? 1 : RD <= 4 ? 2 : RD <= 8 ? 3 : RD <= 16 ? 4 : 5;
   static constexpr int G = 1 << LG;                      // lanes per query in phase 0
   static constexpr int VSLOTS = QB * WD * NQ;            // 4-cell vectors per workgroup
@@ -154,9 +154,9 @@ __device__ __forceinline__ void load_vec(const PT* p, float* v) {
 // wave instruction reads the same window piece of 32 consecutive queries —
 // on levels 2/3, whose pages interleave queries at 32 / 8 B per tile, those
 // are neighbours in one or a few lines instead of 64 separate lines.
-template <int R, int NT_, bool QMAJ>
+template <int R, int NT_, bool QMAJ, int QB_ = 0>
 __device__ __forceinline__ void gather_slot(int s, int& qq, int& rem) {
-  using C = WideCfg<R, NT_>;
+  using C = WideCfg<R, NT_, QB_>;
   if constexpr (QMAJ) {
     qq = s % C::QB;
     rem = s / C::QB;
@@ -166,16 +166,16 @@ __device__ __forceinline__ void gather_slot(int s, int& qq, int& rem) {
   }
 }
 
-template <int R, int NT_, int V, typename PT, bool QMAJ = false>
+template <int R, int NT_, int V, typename PT, bool QMAJ = false, int QB_ = 0>
 __device__ __forceinline__ void gather_load(const PT* __restrict__ base, int qb0, const LevelAddr& A,
                                             const int2* org, int q0, int N, int tid,
-                                            float4 (&v)[WideCfg<R, NT_>::VIT]) {
-  using C = WideCfg<R, NT_>;
+                                            float4 (&v)[WideCfg<R, NT_, QB_>::VIT]) {
+  using C = WideCfg<R, NT_, QB_>;
 #pragma unroll
   for (int i = 0; i < C::VIT; ++i) {
     const int s = tid + i * C::NT;
     int qq, rem;
-    gather_slot<R, NT_, QMAJ>(s, qq, rem);
+    gather_slot<R, NT_, QMAJ, QB_>(s, qq, rem);
     const int r = rem / C::NQ, k = rem - r * C::NQ;
     float c[4] = {0.f, 0.f, 0.f, 0.f};
     if (s < C::VSLOTS && q0 + qq < N) {
@@ -201,38 +201,38 @@ __device__ __forceinline__ void gather_load(const PT* __restrict__ base, int qb0
   }
 }
 
-template <int R, int NT_, bool QMAJ = false>
-__device__ __forceinline__ void gather_store(const float4 (&v)[WideCfg<R, NT_>::VIT], float* cells,
+template <int R, int NT_, bool QMAJ = false, int QB_ = 0>
+__device__ __forceinline__ void gather_store(const float4 (&v)[WideCfg<R, NT_, QB_>::VIT], float* cells,
                                              int tid) {
-  using C = WideCfg<R, NT_>;
+  using C = WideCfg<R, NT_, QB_>;
 #pragma unroll
   for (int i = 0; i < C::VIT; ++i) {
     const int s = tid + i * C::NT;
     if (s < C::VSLOTS) {
       int qq, rem;
-      gather_slot<R, NT_, QMAJ>(s, qq, rem);
+      gather_slot<R, NT_, QMAJ, QB_>(s, qq, rem);
       *reinterpret_cast<float4*>(cells + qq * C::QS + rem * 4) = v[i];
     }
   }
 }
 
-template <int R, int NT_, int V, typename PT, bool QMAJ = false>
+template <int R, int NT_, int V, typename PT, bool QMAJ = false, int QB_ = 0>
 __device__ __forceinline__ void gather_windows(const PT* __restrict__ base, int qb0, const LevelAddr& A,
                                                const int2* org, float* cells, int q0, int N,
                                                int tid) {
-  float4 v[WideCfg<R, NT_>::VIT];
-  gather_load<R, NT_, V, PT, QMAJ>(base, qb0, A, org, q0, N, tid, v);
-  gather_store<R, NT_, QMAJ>(v, cells, tid);
+  float4 v[WideCfg<R, NT_, QB_>::VIT];
+  gather_load<R, NT_, V, PT, QMAJ, QB_>(base, qb0, A, org, q0, N, tid, v);
+  gather_store<R, NT_, QMAJ, QB_>(v, cells, tid);
 }
 
 // Phase 0 of the wide lookup (forward and backward): per (query, sample) the
 // coordinate round trip, floor and fractions; per query the window origin and
 // the far flag.  Tap data goes to xs / ys, origins to org.
-template <int R, int NT_>
+template <int R, int NT_, int QB_ = 0>
 __device__ __forceinline__ void wide_phase0(const float* __restrict__ coords, const LookupGeom& g,
                                             const LevelAddr& A, int b, int l, int q0, int tid,
                                             float4* xs, float4* ys, int2* org) {
-  using C = WideCfg<R, NT_>;
+  using C = WideCfg<R, NT_, QB_>;
   constexpr int RD = C::RD, WD = C::WD, RS = C::RS, QB = C::QB, G = C::G;
   const int Hl = A.h, Wl = A.w;
 #pragma unroll
@@ -279,11 +279,11 @@ __device__ __forceinline__ void wide_phase0(const float* __restrict__ coords, co
 
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
-template <int R, typename PT, int NT_ = 512>
+template <int R, typename PT, int NT_ = 512, int QB_ = 0>
 __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
     const PT* __restrict__ pyr, const float* __restrict__ coords, float* __restrict__ out,
     LookupGeom g) {
-  using C = WideCfg<R, NT_>;
+  using C = WideCfg<R, NT_, QB_>;
   constexpr int RD = C::RD, RS = C::RS, K = C::K, QB = C::QB;
   __shared__ __attribute__((aligned(16))) float cells[QB * C::QS];
   __shared__ float4 xs[RD * QB];   // {column in the LDS row (int bits), fx, 1-fx, -}
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
   const LevelAddr A = g.lv[l];
 
   // ---- phase 0
-  wide_phase0<R, NT_>(coords, g, A, b, l, q0, tid, xs, ys, org);
+  wide_phase0<R, NT_, QB_>(coords, g, A, b, l, q0, tid, xs, ys, org);
   __syncthreads();
 
   // ---- phase 1 (zeros off the level and for far queries)
@@ -306,15 +306,15 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
     // levels 2/3 (tile rows of 4 / 2 cells): query-major slots (round 3: Sintel
     // B=8 51.5 -> 50.1 us, KITTI B=8 bf16 54.1 -> 51.6 us, bit-identical)
     if (A.lth == 30)
-      gather_windows<R, NT_, 1, PT>(base, qb0, A, org, cells, q0, g.N, tid);
+      gather_windows<R, NT_, 1, PT, false, QB_>(base, qb0, A, org, cells, q0, g.N, tid);
     else if (A.tw >= 8)
-      gather_windows<R, NT_, 4, PT>(base, qb0, A, org, cells, q0, g.N, tid);
+      gather_windows<R, NT_, 4, PT, false, QB_>(base, qb0, A, org, cells, q0, g.N, tid);
     else if (A.tw == 4)
-      gather_windows<R, NT_, 4, PT, true>(base, qb0, A, org, cells, q0, g.N, tid);
+      gather_windows<R, NT_, 4, PT, true, QB_>(base, qb0, A, org, cells, q0, g.N, tid);
     else if (A.tw == 2)
-      gather_windows<R, NT_, 2, PT, true>(base, qb0, A, org, cells, q0, g.N, tid);
+      gather_windows<R, NT_, 2, PT, true, QB_>(base, qb0, A, org, cells, q0, g.N, tid);
     else
-      gather_windows<R, NT_, 1, PT>(base, qb0, A, org, cells, q0, g.N, tid);
+      gather_windows<R, NT_, 1, PT, false, QB_>(base, qb0, A, org, cells, q0, g.N, tid);
   }
   __syncthreads();
 
@@ -463,10 +463,25 @@ int launch_lookup_backward_r(const float* coords, const float* gout, float* gpyr
   return dxr::launch_status();
 }
 
+// Workgroup shape: 512 threads x 32 queries (4 resident per CU), or — when that
+// grid fits in one dispatch round (<= 1024 workgroups: Sintel / Chairs B=1) —
+// 256 threads x 16 queries, the same 16 threads per query in twice the
+// workgroups, so the per-CU load evens out (3.44 -> 6.9 workgroups per CU at
+// Sintel B=1: one CU in four no longer runs a fourth workgroup after the rest).
+// Round 3, same-process A/B (bit-identical): Sintel B=1 8.0 -> 7.4 us, Chairs
+// 5.6 -> 5.2 us; multi-round grids keep 512 x 32 (Sintel B=8 50.4 vs 53.3 us).
 template <int R, typename PT>
 int launch_lookup_r(const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
                     hipStream_t stream) {
   using W = WideCfg<R>;
+  const long long wg32 = (long long)((g.N + W::QB - 1) / W::QB) * g.levels * B;
+  if (R <= 4 && wg32 <= 1024) {
+    using S = WideCfg<R, 256, 16>;
+    const dim3 grid((unsigned)((g.N + S::QB - 1) / S::QB), (unsigned)g.levels, (unsigned)B);
+    hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT, 256, 16>), grid, dim3(256), 0, stream, pyr,
+                       coords, out, g);
+    return dxr::launch_status();
+  }
   const dim3 grid((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
   hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT>), grid, dim3(W::NT), 0, stream, pyr, coords,
                      out, g);

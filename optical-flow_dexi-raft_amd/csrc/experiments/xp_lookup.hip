@@ -7,7 +7,8 @@ namespace {
 
 // XP bits: 0 skip the window gathers, 1 skip phase 2 (return after the gather),
 // 2 return after phase 0, 3 synthetic coordinates (the grid: no coords loads),
-// 5 query-major gather slots on levels 2/3 (gather_slot QMAJ),
+// 5 query-major gather slots on levels 2/3 (gather_slot QMAJ; now the product's),
+// 64 / 128: the product kernel at 256 threads x 16 queries / 1024 x 64,
 // 8 record a per-workgroup timeline (s_memrealtime at start, after phase 0,
 // after the gather, at the end; plus the hardware id) into `trace`.
 template <int R, typename PT, int XP>
@@ -192,10 +193,23 @@ int xp_launch(const PT* pyr, const float* coords, float* out, const LookupGeom& 
   return dxr::launch_status();
 }
 
+// The product kernel with another workgroup shape: NT threads x QB queries
+// (the same 16 threads per query as the product's 512 x 32).
+template <int NT, int QB, typename PT>
+int xp_shape(const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
+             hipStream_t stream) {
+  const dim3 grid((unsigned)((g.N + QB - 1) / QB), (unsigned)g.levels, (unsigned)B);
+  hipLaunchKernelGGL((corr_lookup_wide_kernel<4, PT, NT, QB>), grid, dim3(NT), 0, stream, pyr, coords,
+                     out, g);
+  return dxr::launch_status();
+}
+
 template <typename PT>
 int xp_dispatch(int xp, const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
                 unsigned long long* trace, hipStream_t stream) {
   switch (xp) {
+    case 64: return xp_shape<256, 16>(pyr, coords, out, g, B, stream);
+    case 128: return xp_shape<1024, 64>(pyr, coords, out, g, B, stream);
     case 0: return xp_launch<0>(pyr, coords, out, g, B, trace, stream);
     case 1: return xp_launch<1>(pyr, coords, out, g, B, trace, stream);
     case 2: return xp_launch<2>(pyr, coords, out, g, B, trace, stream);

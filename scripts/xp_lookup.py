@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--hw", type=int, nargs=2, default=[55, 128])
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
-    ap.add_argument("--xp", type=int, nargs="+", default=[0, 32, 4, 1, 2, 8])
+    ap.add_argument("--xp", type=int, nargs="+", default=[0, 32, 64, 128, 4, 1])
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--trace", action="store_true")
@@ -68,7 +68,7 @@ def main():
                                out.data_ptr(), xp, trace.data_ptr(), stream)
         assert st == 0, st
 
-    for x in (0, 16, 32):
+    for x in (0, 16, 32, 64, 128):
         out.zero_()
         launch(x)
         torch.cuda.synchronize()
@@ -91,7 +91,7 @@ def main():
                       "us_per_launch": {x: [round(min(v), 2), round(float(np.median(v)), 2)]
                                         for x, v in res.items()}}))
     if a.trace:
-        for x in (256, 288, 260, 258):
+        for x in (256, 260, 258):
             for _ in range(50):
                 launch(0)
             launch(x)

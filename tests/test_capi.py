@@ -42,7 +42,8 @@ def test_header_declares_the_documented_entry_points():
         "dxr_pyramid_unpack", "dxr_pyramid_pack",
         "dxr_corr_lookup_backward", "dxr_pyramid_backward", "dxr_alt_corr_backward",
         "dxr_conv1x1_packed_bytes", "dxr_conv1x1_pack_weight", "dxr_corr_lookup_conv1x1",
-        "dxr_transpose", "dxr_avg_pool2x2_nhwc"}
+        "dxr_transpose", "dxr_avg_pool2x2_nhwc", "dxr_alt_workspace_bytes",
+        "dxr_alt_corr_lookup_ws"}
 
 
 def test_library_exports_every_declared_symbol(nat):
@@ -216,3 +217,21 @@ def test_build_workspace_bytes(nat):
     # validation is the plain build's: same statuses before any launch
     assert bw(P, P, 0, 0, 1, 0, 8, 8, 4, 16.0, P, 0, 0, P, 1 << 20, None) == nat.DXR_EINVAL
     assert bw(P, P, 0, 0, 0, 256, 8, 8, 4, 16.0, None, 0, 0, None, 0, None) == nat.DXR_OK
+
+
+def test_alt_workspace_bytes(nat):
+    """The on-the-fly lookup's query-order workspace: one 16-byte entry per query
+    slot of every 4 x 8 query tile, per level and coordinate set."""
+    lib = nat.load()
+    for B, H, W, L in ((1, 136, 240, 4), (2, 55, 128, 4), (3, 17, 19, 2)):
+        tiles = -(-H // 4) * -(-W // 8)
+        assert lib.dxr_alt_workspace_bytes(B, H, W, L) == 16 * B * L * tiles * 32
+    assert lib.dxr_alt_workspace_bytes(1, 0, 8, 4) == -1
+    assert lib.dxr_alt_workspace_bytes(1, 8, 8, 9) == -1
+    P = 1 << 12
+    aw = lib.dxr_alt_corr_lookup_ws
+    ptrs = (ctypes.c_void_p * 4)(P, P, P, P)
+    # validation as the workspace-less entry point, before any launch
+    assert aw(P, ptrs, P, P, 1, 16, 16, 64, 4, 4, 0.0, P, 1 << 20, None) == nat.DXR_EINVAL
+    assert aw(P, ptrs, P, P, 1, 16, 16, 64, 4, 9, 16.0, P, 1 << 20, None) == nat.DXR_EUNSUPPORTED
+    assert aw(None, None, None, None, 0, 16, 16, 64, 4, 4, 16.0, None, 0, None) == nat.DXR_OK

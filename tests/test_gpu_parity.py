@@ -305,6 +305,54 @@ def test_alternate_block_overflow_fallback(dx):
     assert (np.abs(got[fin] - ref[fin]) <= 1e-4 * scale[fin] + 1e-30).all()
 
 
+@pytest.mark.parametrize("flow", ["iid", "smooth", "far"])
+@pytest.mark.parametrize("shape", [(1, 256, 55, 128, 4), (2, 64, 30, 44, 3)])
+def test_alt_lookup_query_order_is_bit_identical(dx, flow, shape):
+    """dxr_alt_corr_lookup_ws (AlternateCorrBlock's entry point) orders each
+    level's queries first — by window position for flows that vary pixel to
+    pixel, in 4 x 8 tile order for smooth ones — and must give the workspace-less
+    spatial form's outputs bit for bit: the per-(cell, query) sums do not depend
+    on which queries share a workgroup.  'far' mixes NaN / inf / off-image
+    coordinates (the far bin) into i.i.d. flows."""
+    from dexiraft_amd import _native as nat
+    lib = nat.load()
+    B, D, H, W, r = shape
+    f1 = _t(dg.fmap(71, B, D, H, W, "fnet"))
+    f2 = _t(dg.fmap(72, B, D, H, W, "fnet"))
+    ys, xs = np.meshgrid(np.arange(H, dtype=np.float32), np.arange(W, dtype=np.float32),
+                         indexing="ij")
+    grid = np.stack([xs, ys])[None].repeat(B, 0)
+    rng = np.random.default_rng(73)
+    if flow == "smooth":
+        u = rng.normal(0, 4, size=(B, 2, 1, 1)) + 2 * np.sin(grid / 9.0)
+        c = (grid + u).astype(np.float32)
+    else:
+        c = (grid + rng.normal(0, 4, size=grid.shape)).astype(np.float32)
+        if flow == "far":
+            c[:, 0, 3, 5] = np.nan
+            c[:, 1, 7, 9] = np.inf
+            c[:, :, 10, 2:30:3] = -40.0
+            c[:, 0, 12, :20] = 3.0e9
+    ab = dx.AlternateCorrBlock(f1, f2, radius=r)
+    ct = _t(np.ascontiguousarray(c))
+    outs = []
+    for ws in (False, True):
+        out = torch.full((B, 4 * (2 * r + 1) ** 2, H, W), float("nan"), device=DEV)
+        n = lib.dxr_alt_workspace_bytes(B, H, W, 4)
+        buf = torch.empty(n, dtype=torch.uint8, device=DEV)
+        args = (ab._f1_nhwc.data_ptr(), ab._f2_ptrs, ct.data_ptr(), out.data_ptr(), B, H, W, D, 4,
+                r, float(np.sqrt(np.float32(D))))
+        st = (lib.dxr_alt_corr_lookup_ws(*args, buf.data_ptr(), n, nat.stream_of(ct)) if ws
+              else lib.dxr_alt_corr_lookup(*args, nat.stream_of(ct)))
+        assert st == 0
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.isnan(outs[0]), torch.isnan(outs[1]))
+    fin = ~torch.isnan(outs[0])
+    assert torch.equal(outs[0][fin], outs[1][fin])
+    assert torch.equal(ab(ct)[fin], outs[0][fin])
+
+
 def test_alt_cuda_corr_forward_ffi(dx):
     """Reference FFI form: NHWC fmaps, [B, N, H, W, 2] coords, H2 != H1."""
     B, H1, W1, H2, W2, C, N, r = 2, 9, 13, 7, 11, 64, 2, 3
