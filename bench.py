@@ -90,19 +90,22 @@ def lookup_bytes(B, H, W, s_pyr=4):
 
 
 def build_kernel(dtype, H, W):
-    """The build kernel the library runs for this workload (csrc/corr_build.hip
-    launch_build_f32 / launch_build_bf16) and the ceiling of the arithmetic it
-    runs: the split f32 build issues three f16 MFMA products per f32 product
-    (f16 pair split x = hi + 2^-11 lo, products hi*hi and hi*lo + lo*hi into two
-    f32 accumulators), so its binding ceiling is 2.5 PF / 3 = 833 TF
-    f32-equivalent; the f32 peak (157.3 TF) is §8(d)'s."""
+    """The build kernel the library runs for this workload (csrc/corr_build.hip:
+    CorrBlock passes a workspace, so dxr_corr_pyramid_build_ws takes its LDS-DMA
+    builds) and the ceiling of the arithmetic it runs: the f32 build issues three
+    f16 MFMA products per f32 product (operands pre-split into per-pixel
+    power-of-two scaled f16 pairs hi + lo; lo*hi + hi*lo + hi*hi into one f32
+    accumulator), so its binding ceiling is 2.5 PF / 3 = 833 TF f32-equivalent;
+    the f32 peak (157.3 TF) is §8(d)'s.  bf16 fmaps run one bf16 MFMA product."""
     if dtype == "bf16":
-        if W % 4 == 0:   # the two-query-block form (float4-aligned rows)
-            return "corr_build_bf16_q2_kernel", 1, PEAK_BF16_TFLOPS, "bf16"
-        return "corr_build_bf16_kernel", 1, PEAK_BF16_TFLOPS, "bf16"
-    if D % 16 == 0 and W % 2 == 0:
+        if D % 32 == 0:
+            return ("corr_build_dma_kernel (bf16 operand records by LDS-DMA: channels-last fmaps "
+                    "in place, NCHW fmaps after a pack pass; f32 accumulate)", 1,
+                    PEAK_BF16_TFLOPS, "bf16")
+        return "corr_build_bf16_q2_kernel", 1, PEAK_BF16_TFLOPS, "bf16"
+    if D % 16 == 0:
         return ("corr_build_dma_kernel (after split_pairs_kernel: f32 operands pre-split into "
-                "per-pixel power-of-two scaled f16 pairs hi + 2^-11 lo; LDS-DMA ring, "
+                "per-pixel power-of-two scaled f16 pairs hi + lo; LDS-DMA ring, "
                 "3 f16 MFMA products, f32 accumulate)", SPLIT_PRODUCTS, PEAK_BF16_TFLOPS,
                 "f16 MFMA, f32 accumulate")
     return "corr_build_f32_kernel", 1, PEAK_F32_TFLOPS, "f32"

@@ -331,8 +331,9 @@ int dxr_alt_corr_lookup(const float* fmap1, const float* const* fmap2_levels,
 
 /*
  * Bytes of device workspace dxr_alt_corr_lookup_ws uses for B coordinate sets
- * of H x W queries over num_levels levels (one 16-byte entry per query slot of
- * every 4 x 8 query tile and level; -1: bad geometry).  ABI 6.
+ * of H x W queries over num_levels levels (per level and set: the ordered list,
+ * 16 B per query slot of every 4 x 8 query tile, 4-B bin ids, 64 blocks'
+ * histograms of up to 4097 bins; -1: bad geometry).  ABI 6.
  */
 int64_t dxr_alt_workspace_bytes(int64_t B, int64_t H, int64_t W, int num_levels);
 
@@ -342,9 +343,10 @@ int64_t dxr_alt_workspace_bytes(int64_t B, int64_t H, int64_t W, int num_levels)
  * each level's queries before the lookup: grouped by window position (bins of
  * ~32 queries) when the 4 x 8 query tiles' union boxes would be larger than
  * 1.5x a bin group's (flows that vary pixel to pixel), else in tile order.  The
- * outputs are the workspace-less call's, bit for bit.  Falls back to
- * dxr_alt_corr_lookup when the workspace is NULL or short, or an image has
- * more than 1024 query tiles.  Replaces core/corr.py:74-91 as above.  ABI 6.
+ * outputs are the workspace-less call's, bit for bit.  Three small launches
+ * (count, scan, scatter) precede the lookup.  Falls back to
+ * dxr_alt_corr_lookup when the workspace is NULL or short.  Replaces
+ * core/corr.py:74-91 as above.  ABI 6.
  */
 int dxr_alt_corr_lookup_ws(const float* fmap1, const float* const* fmap2_levels,
                            const float* coords, float* out,

@@ -20,6 +20,7 @@
 // butterfly transpose (each lane ends with one cell's sum), cell sums go to LDS,
 // and after one barrier every thread emits outputs for one query with coalesced
 // 256-byte wave stores along the query dimension.
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 
@@ -255,7 +256,7 @@ __device__ __forceinline__ void alt_split8h(const float (&x)[8], uint4& h, uint4
 // the query operand split from fmap1 in registers.
 // BIN: the workgroup's 32 queries are not a 4 x 8 pixel tile but 32 consecutive
 // entries of `ord` — this coordinate set's and level's query list in the order
-// alt_order_kernel chose (grouped by window position, or the tile order), each
+// alt_bin_*_kernel chose (grouped by window position, or the tile order), each
 // entry {query, x, y, -} carrying the query's coordinates, so a workgroup's
 // first global read gives it both.
 // PF: k steps of cell-vector loads kept in flight (a ring of PF register stages).
@@ -264,7 +265,8 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
                                                                const float* __restrict__ coords,
                                                                float* __restrict__ out,
                                                                AltGeom g, int W1, int tiles_x,
-                                                               const int4* __restrict__ ord) {
+                                                               const int4* __restrict__ ord,
+                                                               long long ord_stride) {
   constexpr int RD = 2 * R + 1, RD1 = RD + 1, NCELL = RD1 * RD1;
   constexpr int CHUNK = 4 * 32 * NRB;                       // box cells per chunk
   constexpr int KB = CMAX / 8;                              // 8-channel blocks
@@ -307,8 +309,7 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
   if constexpr (BIN) {
     if (tid < TQ) {
       // per (coordinate set, level) gridDim.x * 32 entries, query -1 = padding
-      const int4 e = ord[((long long)z * gridDim.y + blockIdx.y) * ((long long)gridDim.x * TQ) +
-                         tile * TQ + tid];
+      const int4 e = ord[((long long)z * gridDim.y + blockIdx.y) * ord_stride + tile * TQ + tid];
       qlist[tid] = e.x;
       qxy[tid] = make_float2(__int_as_float(e.y), __int_as_float(e.z));
     }
@@ -573,22 +574,27 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
 // level 0 for flows that vary pixel to pixel (the bench's i.i.d. N(0, 4^2)
 // model): neighbouring queries' windows are unrelated.  Grouping the queries by
 // window position instead keeps every box near one window whatever the flow.
-// One workgroup per (coordinate set, level), 1024 threads, one launch:
-//   pass 1  thread = 4 x 8 query tile(s): load the tile's coordinates, bin every
-//           query by its window origin (bins of ~32 queries: 2^by x 2^bx origin
-//           cells, snake order over bin rows; non-finite coordinates last), LDS
-//           histogram, and the tile's union box area (the cells the tile order
-//           would multiply);
-//   scan    exclusive prefix of the histogram (wave scans + one LDS pass);
-//   choose  the bin order when the tiles' boxes average more than 1.5x a bin
-//           chunk's estimated box ((2^by + 2r + 1) x (2^bx + 2r + 1)), else the
-//           tile order (then the lookup multiplies exactly the spatial form's
-//           boxes: smooth flows lose nothing but this launch);
-//   pass 2  write the list: entry {query, x, y, 0}, queries of a bin in any
-//           order (the box GEMM's per-(cell, query) sums do not depend on which
-//           queries share a workgroup: outputs are bit-identical either way).
+// Three launches over OB blocks of whole tiles per (coordinate set, level):
+//   K1 alt_bin_count_kernel   thread = query (tile-major): bin by window origin
+//      (bins of ~32 queries: 2^by x 2^bx origin cells, snake order over bin
+//      rows; non-finite coordinates in a last bin), bin ids to the workspace,
+//      the block's histogram (LDS) to cnt[block][bin], and the block's tiles'
+//      union box areas (the cells the tile order would multiply) to cost[block];
+//   K2 alt_bin_scan_kernel    thread = bin: its exclusive prefix over the
+//      blocks (in place) and its total;
+//   K3 alt_bin_scatter_kernel chooses the bin order when the tiles' boxes
+//      average more than 1.5x a bin group's estimated box ((2^by + 2r + 1) x
+//      (2^bx + 2r + 1)), else the tile order (then the lookup multiplies exactly
+//      the spatial form's boxes); in bin order each block scans the bins' totals
+//      itself and writes its queries' entries {query, x, y, 0} at bin base +
+//      block prefix + an LDS rank, in tile order at their tile slots.
+// Queries of a bin land in any order: the box GEMM's per-(cell, query) sums do
+// not depend on which queries share a workgroup, so the lookup's outputs are
+// bit-identical to the tile order's.  (A one-workgroup-per-list form ran the
+// whole job on 4 CUs: 76 us per 1080p lookup.)
 // ---------------------------------------------------------------------------
 constexpr int BIN_MAX = 4096;
+constexpr int OB = 64;            // blocks per list
 
 struct BinGeom {
   int bsx[8], bsy[8], nbx[8], nby[8];
@@ -613,163 +619,252 @@ BinGeom make_bins(int N, const AltGeom& g, int levels) {
   return b;
 }
 
+// Workspace of one list (coordinate set, level): entries int4[NP] | bin ids
+// int[NP] | cnt int[OB][BIN_MAX + 1] | tot int[BIN_MAX + 1] | cost float[OB]
+// (16-B aligned).
+struct OrderWs {
+  long long np, ents, ids, cnt, tot, cost, bytes;   // byte offsets within a list
+};
+__host__ __device__ inline OrderWs order_ws(long long np) {
+  OrderWs w;
+  w.np = np;
+  w.ents = 0;
+  w.ids = w.ents + 16 * np;
+  w.cnt = w.ids + 4 * np;
+  w.tot = w.cnt + 4LL * OB * (BIN_MAX + 1);
+  w.cost = w.tot + 4LL * (BIN_MAX + 1);
+  w.bytes = (w.cost + 4LL * OB + 15) & ~15LL;
+  return w;
+}
+
+struct OrderArgs {
+  unsigned char* ws;   // lists [Z][L] of OrderWs.bytes each
+  long long list_bytes, np;
+  int W1, tiles_x, ntiles, tpb;   // tiles per block
+};
+
+// slot i of a block -> (tile, slot within the 4 x 8 tile) -> query (or -1)
+__device__ __forceinline__ int order_query(int blk, int i, const OrderArgs& o, int H1, int& tile,
+                                           int& slot) {
+  tile = blk * o.tpb + i / TQ;
+  slot = i % TQ;
+  const int qy = (tile / o.tiles_x) * TQY + slot / TQX, qx = (tile % o.tiles_x) * TQX + slot % TQX;
+  return (tile < o.ntiles && qy < H1 && qx < o.W1) ? qy * o.W1 + qx : -1;
+}
+
 template <int R>
-__global__ __launch_bounds__(1024) void alt_order_kernel(const float* __restrict__ coords,
-                                                         int4* __restrict__ ord, AltGeom g,
-                                                         BinGeom bg, int W1, int tiles_x,
-                                                         int ntiles) {
+__global__ __launch_bounds__(256) void alt_bin_count_kernel(const float* __restrict__ coords,
+                                                            AltGeom g, BinGeom bg, OrderArgs o) {
   constexpr int RD1 = 2 * R + 2;
-  __shared__ int cnt[BIN_MAX + 1];
-  __shared__ int wsum[16];
-  __shared__ float wcost[16];
-  __shared__ int use_bins;
+  __shared__ int hist[BIN_MAX + 1];
+  __shared__ float wcost[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int l = blockIdx.x, z = blockIdx.y;
+  const int blk = blockIdx.x, l = blockIdx.y, z = blockIdx.z;
   const AltLevel lv = g.lv[l];
   const int nbx = bg.nbx[l], nb = nbx * bg.nby[l], bsx = bg.bsx[l], bsy = bg.bsy[l];
   const float* cz = coords + (long long)z * g.coord_zstride;
-  const int H1 = g.N / W1;
-  const long long NP = (long long)ntiles * TQ;
-  int4* oz = ord + ((long long)z * gridDim.x + l) * NP;
-  for (int i = tid; i <= nb; i += 1024) cnt[i] = 0;
+  const int H1 = g.N / o.W1;
+  unsigned char* lw = o.ws + ((long long)z * gridDim.y + l) * o.list_bytes;
+  const OrderWs w = order_ws(o.np);
+  int* ids = reinterpret_cast<int*>(lw + w.ids);
+  for (int i = tid; i <= nb; i += 256) hist[i] = 0;
   __syncthreads();
-
-  // pass 1: thread = tile tid; the bins of its 32 queries stay in registers
-  // (two 16-bit bins per register)
-  uint32_t bins[TQ / 2];
   float cost = 0.f;
-  const int t = tid;
-  {
+  // 32 consecutive lanes = one tile: its union box by a 32-lane reduction
+  for (int i = tid; i < o.tpb * TQ; i += 256) {
+    int tile, slot;
+    const int q = order_query(blk, i, o, H1, tile, slot);
+    const int qc = max(q, 0);
+    const float x = cz[(long long)qc * g.coord_qstride] * lv.inv;
+    const float y = cz[(long long)qc * g.coord_qstride + g.coord_cstride] * lv.inv;
+    const float xf = floorf(x), yf = floorf(y);
+    int bin = nb;
     int lx0 = 0x7fffffff, ly0 = 0x7fffffff, lx1 = -1, ly1 = -1;
-    float cx_[TQ], cy_[TQ];
-#pragma unroll
-    for (int s = 0; s < TQ; ++s) {   // all 64 loads in flight
-      const int qy = (t / tiles_x) * TQY + s / TQX, qx = (t % tiles_x) * TQX + s % TQX;
-      const bool in = t < ntiles && qy < H1 && qx < W1;
-      const int q = in ? qy * W1 + qx : 0;
-      cx_[s] = in ? cz[(long long)q * g.coord_qstride] : __builtin_nanf("");
-      cy_[s] = in ? cz[(long long)q * g.coord_qstride + g.coord_cstride] : __builtin_nanf("");
-    }
-#pragma unroll
-    for (int s = 0; s < TQ; ++s) {
-      const int qy = (t / tiles_x) * TQY + s / TQX, qx = (t % tiles_x) * TQX + s % TQX;
-      const bool in = t < ntiles && qy < H1 && qx < W1;
-      const float x = cx_[s] * lv.inv, y = cy_[s] * lv.inv;
-      const float xf = floorf(x), yf = floorf(y);
-      int bin = nb;
-      if (fabsf(xf) < 1.0e8f && fabsf(yf) < 1.0e8f) {
-        const int cx = min(max((int)xf, 0), lv.W2 - 1), cy = min(max((int)yf, 0), lv.H2 - 1);
-        const int byi = cy >> bsy;
-        int bxi = cx >> bsx;
-        if (byi & 1) bxi = nbx - 1 - bxi;
-        bin = byi * nbx + bxi;
-        const int x0 = (int)xf - R, y0 = (int)yf - R;
-        if (x0 + RD1 > 0 && x0 < lv.W2 && y0 + RD1 > 0 && y0 < lv.H2) {   // live window
-          lx0 = min(lx0, max(x0, 0));
-          ly0 = min(ly0, max(y0, 0));
-          lx1 = max(lx1, min(x0 + RD1, lv.W2));
-          ly1 = max(ly1, min(y0 + RD1, lv.H2));
-        }
+    if (q >= 0 && fabsf(xf) < 1.0e8f && fabsf(yf) < 1.0e8f) {
+      const int cx = min(max((int)xf, 0), lv.W2 - 1), cy = min(max((int)yf, 0), lv.H2 - 1);
+      const int byi = cy >> bsy;
+      int bxi = cx >> bsx;
+      if (byi & 1) bxi = nbx - 1 - bxi;
+      bin = byi * nbx + bxi;
+      const int x0 = (int)xf - R, y0 = (int)yf - R;
+      if (x0 + RD1 > 0 && x0 < lv.W2 && y0 + RD1 > 0 && y0 < lv.H2) {   // live window
+        lx0 = max(x0, 0);
+        ly0 = max(y0, 0);
+        lx1 = min(x0 + RD1, lv.W2);
+        ly1 = min(y0 + RD1, lv.H2);
       }
-      if (in) atomicAdd(&cnt[bin], 1);
-      const uint32_t bv = in ? (uint32_t)bin : 0xffffu;
-      if (s & 1) bins[s >> 1] |= bv << 16;
-      else bins[s >> 1] = bv;
     }
-    if (lx1 > lx0) cost += (float)(lx1 - lx0) * (float)(ly1 - ly0);
-  }
-  // the tiles' box area, summed over the workgroup
+    if (q >= 0) {
+      atomicAdd(&hist[bin], 1);
+      ids[(long long)blk * o.tpb * TQ + i] = bin;
+    }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) cost += __shfl_xor(cost, o);
+    for (int d = 1; d < TQ; d <<= 1) {
+      lx0 = min(lx0, __shfl_xor(lx0, d));
+      ly0 = min(ly0, __shfl_xor(ly0, d));
+      lx1 = max(lx1, __shfl_xor(lx1, d));
+      ly1 = max(ly1, __shfl_xor(ly1, d));
+    }
+    if ((lane & 31) == 0 && lx1 > lx0) cost += (float)(lx1 - lx0) * (float)(ly1 - ly0);
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) cost += __shfl_xor(cost, d);
   if (lane == 0) wcost[wave] = cost;
   __syncthreads();
+  int* cnt = reinterpret_cast<int*>(lw + w.cnt) + (long long)blk * (BIN_MAX + 1);
+  for (int i = tid; i <= nb; i += 256) cnt[i] = hist[i];
+  if (tid == 0)
+    reinterpret_cast<float*>(lw + w.cost)[blk] = wcost[0] + wcost[1] + wcost[2] + wcost[3];
+}
 
-  // exclusive scan of cnt[0..nb]: thread t owns a run of `per` bins
-  const int per = (nb + 1 + 1023) / 1024;
-  int loc = 0;
-  for (int k = 0; k < per; ++k) {
-    const int b = tid * per + k;
-    if (b <= nb) loc += cnt[b];
-  }
-  int v = loc;
+// K2: thread = bin: exclusive prefix of its count over the OB blocks, in place
+// (64 loads in flight), and the bin's total.  Grid (ceil(bins / 256), L, Z).
+__global__ __launch_bounds__(256) void alt_bin_scan_kernel(BinGeom bg, OrderArgs o) {
+  const int l = blockIdx.y, z = blockIdx.z;
+  const int bin = blockIdx.x * 256 + threadIdx.x;
+  const int nb = bg.nbx[l] * bg.nby[l];
+  if (bin > nb) return;
+  unsigned char* lw = o.ws + ((long long)z * gridDim.y + l) * o.list_bytes;
+  const OrderWs w = order_ws(o.np);
+  int* cnt = reinterpret_cast<int*>(lw + w.cnt) + bin;
+  int c[OB];
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(v, o);
-    if (lane >= o) v += t;
+  for (int b = 0; b < OB; ++b) c[b] = cnt[(long long)b * (BIN_MAX + 1)];
+  int run = 0;
+#pragma unroll
+  for (int b = 0; b < OB; ++b) {
+    const int t = c[b];
+    cnt[(long long)b * (BIN_MAX + 1)] = run;
+    run += t;
   }
-  if (lane == 63) wsum[wave] = v;
-  __syncthreads();
+  reinterpret_cast<int*>(lw + w.tot)[bin] = run;
+}
+
+// K3: every block scans the bins' totals itself (<= 4097 values from L2) into
+// LDS bases, decides the order from the blocks' box costs (the same decision in
+// every block), then writes its queries' entries: at base[bin] + its block
+// prefix + an LDS rank (bin order), or at their tile slots (tile order).
+template <int R>
+__global__ __launch_bounds__(256) void alt_bin_scatter_kernel(const float* __restrict__ coords,
+                                                              AltGeom g, BinGeom bg, OrderArgs o) {
+  constexpr int RD1 = 2 * R + 2;
+  __shared__ int off[BIN_MAX + 1];
+  __shared__ int wsum[4];
+  __shared__ int binned_s;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int blk = blockIdx.x, l = blockIdx.y, z = blockIdx.z;
+  const int nb = bg.nbx[l] * bg.nby[l];
+  const float* cz = coords + (long long)z * g.coord_zstride;
+  const int H1 = g.N / o.W1;
+  unsigned char* lw = o.ws + ((long long)z * gridDim.y + l) * o.list_bytes;
+  const OrderWs w = order_ws(o.np);
+  int4* ents = reinterpret_cast<int4*>(lw + w.ents);
+  const int* ids = reinterpret_cast<const int*>(lw + w.ids);
   if (tid == 0) {
-    int acc = 0;
-    float tot = 0.f;
-    for (int w = 0; w < 16; ++w) {
-      const int t = wsum[w];
-      wsum[w] = acc;
-      acc += t;
-      tot += wcost[w];
-    }
-    const float chunk = (float)((1 << bsy) + RD1 - 1) * (float)((1 << bsx) + RD1 - 1);
-    use_bins = tot > 1.5f * chunk * (float)ntiles ? 1 : 0;
+    float c = 0.f;
+    const float* cost = reinterpret_cast<const float*>(lw + w.cost);
+    for (int b = 0; b < OB; ++b) c += cost[b];
+    const float chunk = (float)((1 << bg.bsy[l]) + RD1 - 1) * (float)((1 << bg.bsx[l]) + RD1 - 1);
+    binned_s = c > 1.5f * chunk * (float)o.ntiles ? 1 : 0;
   }
   __syncthreads();
-  int run = wsum[wave] + v - loc;
-  for (int k = 0; k < per; ++k) {
-    const int b = tid * per + k;
-    if (b <= nb) {
-      const int c = cnt[b];
-      cnt[b] = run;
-      run += c;
+  const bool binned = binned_s != 0;
+  if (binned) {
+    // exclusive scan of the totals: thread t owns bins [t * per, t * per + per)
+    const int* tot = reinterpret_cast<const int*>(lw + w.tot);
+    const int per = (nb + 1 + 255) / 256;    // <= 17
+    int loc = 0;
+    for (int k = 0; k < per; ++k) {
+      const int b = tid * per + k;
+      if (b <= nb) loc += tot[b];
     }
-  }
-  __syncthreads();
-
-  // pass 2: the list
-  const bool binned = use_bins != 0;
-  if (t < ntiles) {
+    int v = loc;
 #pragma unroll
-    for (int s = 0; s < TQ; ++s) {
-      const int qy = (t / tiles_x) * TQY + s / TQX, qx = (t % tiles_x) * TQX + s % TQX;
-      const bool in = qy < H1 && qx < W1;
-      const int q = in ? qy * W1 + qx : -1;
-      int4 e = make_int4(-1, 0, 0, 0);
-      if (in) e = make_int4(q, __float_as_int(cz[(long long)q * g.coord_qstride]),
-                            __float_as_int(cz[(long long)q * g.coord_qstride + g.coord_cstride]), 0);
-      if (binned) {
-        const int bin = (int)((bins[s >> 1] >> (16 * (s & 1))) & 0xffffu);
-        if (in) oz[atomicAdd(&cnt[bin], 1)] = e;
-      } else {
-        oz[(long long)t * TQ + s] = e;
+    for (int d = 1; d < 64; d <<= 1) {
+      const int t = __shfl_up(v, d);
+      if (lane >= d) v += t;
+    }
+    if (lane == 63) wsum[wave] = v;
+    __syncthreads();
+    int base = v - loc;
+    for (int i = 0; i < wave; ++i) base += wsum[i];
+    const int* cnt = reinterpret_cast<const int*>(lw + w.cnt) + (long long)blk * (BIN_MAX + 1);
+    for (int k = 0; k < per; ++k) {
+      const int b = tid * per + k;
+      if (b <= nb) {
+        off[b] = base + cnt[b];
+        base += tot[b];
       }
     }
+    __syncthreads();
   }
-  if (binned)   // entries past the queries: padding
-    for (long long i = g.N + tid; i < NP; i += 1024) oz[i] = make_int4(-1, 0, 0, 0);
+  for (int i = tid; i < o.tpb * TQ; i += 256) {
+    int tile, slot;
+    const int q = order_query(blk, i, o, H1, tile, slot);
+    if (tile >= o.ntiles) break;
+    int4 e = make_int4(-1, 0, 0, 0);
+    if (q >= 0)
+      e = make_int4(q, __float_as_int(cz[(long long)q * g.coord_qstride]),
+                    __float_as_int(cz[(long long)q * g.coord_qstride + g.coord_cstride]), 0);
+    if (!binned)
+      ents[(long long)tile * TQ + slot] = e;
+    else if (q >= 0)
+      ents[atomicAdd(&off[ids[(long long)blk * o.tpb * TQ + i]], 1)] = e;
+  }
+  if (binned && blk == 0)   // entries past the queries: padding
+    for (long long i = g.N + tid; i < o.np; i += 256) ents[i] = make_int4(-1, 0, 0, 0);
 }
 
 long long alt_order_entries(long long H, long long W) {
   return ((W + TQX - 1) / TQX) * ((H + TQY - 1) / TQY) * (long long)TQ;
 }
 
+long long alt_order_bytes(long long H, long long W) {
+  return order_ws(alt_order_entries(H, W)).bytes;
+}
+
 template <int R, int NRB>
 int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const AltGeom& g,
-                      int levels, int Z, int W1, hipStream_t stream, int4* ord = nullptr) {
+                      int levels, int Z, int W1, hipStream_t stream, void* ws = nullptr) {
   const int H1 = g.N / W1;
   const int tiles_x = (W1 + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
   const int ntiles = tiles_x * tiles_y;
   const dim3 grid((unsigned)ntiles, (unsigned)levels, (unsigned)Z);
   if (g.C > 256) return DXR_EUNSUPPORTED;
   // f16 pair split (r02, 1080p: 227 vs 275 us for the 3-way bf16 split), 3 workgroups/CU
-  if (ord != nullptr && ntiles <= 1024 && Z <= 65535) {   // one tile per order thread
-    hipLaunchKernelGGL((alt_order_kernel<R>), dim3((unsigned)levels, (unsigned)Z), dim3(1024), 0,
-                       stream, coords, ord, g, make_bins(g.N, g, levels), W1, tiles_x, ntiles);
-    const int st = dxr::launch_status();
+  if (ws != nullptr && Z <= 65535) {
+    OrderArgs o;
+    o.ws = static_cast<unsigned char*>(ws);
+    o.np = (long long)ntiles * TQ;
+    o.list_bytes = order_ws(o.np).bytes;
+    o.W1 = W1;
+    o.tiles_x = tiles_x;
+    o.ntiles = ntiles;
+    o.tpb = (ntiles + OB - 1) / OB;
+    const BinGeom bg = make_bins(g.N, g, levels);
+    const dim3 bgrid(OB, (unsigned)levels, (unsigned)Z);
+    hipLaunchKernelGGL((alt_bin_count_kernel<R>), bgrid, dim3(256), 0, stream, coords, g, bg, o);
+    int st = dxr::launch_status();
     if (st != DXR_OK) return st;
+    int nbmax = 0;
+    for (int l = 0; l < levels; ++l) nbmax = std::max(nbmax, bg.nbx[l] * bg.nby[l]);
+    hipLaunchKernelGGL(alt_bin_scan_kernel, dim3((unsigned)((nbmax + 1 + 255) / 256),
+                       (unsigned)levels, (unsigned)Z), dim3(256), 0, stream, bg, o);
+    st = dxr::launch_status();
+    if (st != DXR_OK) return st;
+    hipLaunchKernelGGL((alt_bin_scatter_kernel<R>), bgrid, dim3(256), 0, stream, coords, g, bg, o);
+    st = dxr::launch_status();
+    if (st != DXR_OK) return st;
+    // entries of list (z, l) start at list (z * levels + l) * list_bytes: the kernel
+    // indexes int4 entries by ((z * levels + l) * np + i), so lists are laid out
+    // with a stride of list_bytes / 16 entries
     hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 3, true>), grid, dim3(256), 0,
-                       stream, f1, coords, out, g, W1, tiles_x, ord);
+                       stream, f1, coords, out, g, W1, tiles_x, reinterpret_cast<const int4*>(ws),
+                       o.list_bytes / 16);
     return dxr::launch_status();
   }
   hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 3>), grid, dim3(256), 0, stream, f1,
-                     coords, out, g, W1, tiles_x, nullptr);
+                     coords, out, g, W1, tiles_x, nullptr, 0);
   return dxr::launch_status();
 }
 
@@ -786,10 +881,10 @@ int launch_alt_r(const float* f1, const float* coords, float* out, const AltGeom
 
 int launch_alt(const float* f1, const float* coords, float* out, const AltGeom& g, int levels,
                int Z, int radius, bool vec, hipStream_t stream, int W1 = 0,
-               int4* ord = nullptr) {
+               void* ord = nullptr) {
   // MFMA form: C a multiple of 16 (k16 steps) up to 256, 16-byte aligned rows;
   // the per-query VALU form otherwise.  With a workspace (`ord`) the queries are
-  // ordered first (alt_order_kernel).
+  // ordered first (alt_bin_*_kernel).
   if (vec && W1 > 0 && g.C % 16 == 0 && g.C <= 256) {
     switch (radius) {
       case 0: return launch_alt_mfma_r<0, 1>(f1, coords, out, g, levels, Z, W1, stream, ord);
@@ -1169,10 +1264,10 @@ int alt_lookup(const float* fmap1, const float* const* fmap2_levels, const float
     vec = vec && aligned16(fmap2_levels[l]);
     g.lv[l] = AltLevel{fmap2_levels[l], L.h[l], L.w[l], 1.f / (float)(1 << l), l * rd * rd};
   }
-  int4* ord = nullptr;
+  void* ord = nullptr;
   if (workspace != nullptr && aligned16(workspace) &&
-      workspace_bytes >= 16 * (long long)B * num_levels * alt_order_entries(H, W))
-    ord = static_cast<int4*>(workspace);
+      workspace_bytes >= (long long)B * num_levels * alt_order_bytes(H, W))
+    ord = workspace;
   return launch_alt(fmap1, coords, out, g, num_levels, (int)B, radius, vec, stream, (int)W, ord);
 }
 }  // namespace
@@ -1188,7 +1283,7 @@ extern "C" int dxr_alt_corr_lookup(const float* fmap1, const float* const* fmap2
 extern "C" int64_t dxr_alt_workspace_bytes(int64_t B, int64_t H, int64_t W, int num_levels) {
   if (B < 0 || H < 1 || W < 1 || num_levels < 1 || num_levels > 8 || H * W > (1LL << 30))
     return -1;
-  return 16 * B * num_levels * alt_order_entries(H, W);
+  return B * num_levels * alt_order_bytes(H, W);
 }
 
 extern "C" int dxr_alt_corr_lookup_ws(const float* fmap1, const float* const* fmap2_levels,

@@ -220,12 +220,15 @@ def test_build_workspace_bytes(nat):
 
 
 def test_alt_workspace_bytes(nat):
-    """The on-the-fly lookup's query-order workspace: one 16-byte entry per query
-    slot of every 4 x 8 query tile, per level and coordinate set."""
+    """The on-the-fly lookup's query-order workspace, per level and coordinate
+    set: a 16-byte entry and a bin id per query slot of every 4 x 8 query tile,
+    64 blocks' histograms of 4097 bins, the bins' totals and the blocks' box
+    costs, 16-byte aligned."""
     lib = nat.load()
     for B, H, W, L in ((1, 136, 240, 4), (2, 55, 128, 4), (3, 17, 19, 2)):
-        tiles = -(-H // 4) * -(-W // 8)
-        assert lib.dxr_alt_workspace_bytes(B, H, W, L) == 16 * B * L * tiles * 32
+        np_ = -(-H // 4) * -(-W // 8) * 32
+        per_list = (20 * np_ + 4 * 64 * 4097 + 4 * 4097 + 4 * 64 + 15) // 16 * 16
+        assert lib.dxr_alt_workspace_bytes(B, H, W, L) == B * L * per_list
     assert lib.dxr_alt_workspace_bytes(1, 0, 8, 4) == -1
     assert lib.dxr_alt_workspace_bytes(1, 8, 8, 9) == -1
     P = 1 << 12
