@@ -30,6 +30,8 @@
 
 namespace {
 
+typedef __attribute__((address_space(3))) void lds_void_t;
+
 struct AltLevel {
   const float* f2;        // [Bf, H2, W2, C]
   int H2, W2;
@@ -260,7 +262,8 @@ __device__ __forceinline__ void alt_split8h(const float (&x)[8], uint4& h, uint4
 // entry {query, x, y, -} carrying the query's coordinates, so a workgroup's
 // first global read gives it both.
 // PF: k steps of cell-vector loads kept in flight (a ring of PF register stages).
-template <int R, int NRB, int CMAX, bool H2 = false, int MINW = 2, bool BIN = false, int PF = 1>
+template <int R, int NRB, int CMAX, bool H2 = false, int MINW = 2, bool BIN = false, int PF = 1,
+          bool DMA = false>
 __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* __restrict__ f1,
                                                                const float* __restrict__ coords,
                                                                float* __restrict__ out,
@@ -277,6 +280,8 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
   __shared__ int box[4];                                    // bx0, by0, bw, bh
   __shared__ int qlist[TQ];                                 // BIN: query index or -1
   __shared__ float2 qxy[TQ];                                // BIN: its coordinates
+  // DMA: per wave two 4 KB buffers of 32 cells x 128 B (two k steps), swizzled 16-B slots
+  __shared__ __attribute__((aligned(16))) unsigned char cbuf[DMA ? 4 * 2 * 4096 : 16];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // Workgroups are dealt round-robin to the 8 XCDs; XCD k takes the k-th
@@ -408,6 +413,71 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
       const int cy = divbw(c), cx = c - cy * bw;
       src[rb] = f2b + ((long long)(by0 + cy) * lv.W2 + bx0 + cx) * g.C + 8 * kh;
     }
+    // DMA (f16 pair form): the wave's 32 cell vectors move by LDS-DMA, two k steps (128 B per cell)
+    // per batch into a double-buffered wave region: an instruction covers 8 cells x 128 B (8 lanes
+    // per cell: 8 line segments instead of the 32 cells x 32 B of a register load), and slot
+    // s of cell row r holds logical 16-B piece s ^ ((r >> 1) & 7), so the operand reads below
+    // (row j, pieces 4 step + 2 kh, + 1) are conflict-free ds_read_b128.  Same operands, same
+    // split, same products in the same order: bit-identical to the register form.
+    auto kloop_dma = [&]() {
+      static_assert(NRB == 1, "the DMA form stages one 32-cell block per wave");
+      af16 acc2 = {};
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[0][r] = 0.f;
+      const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(f2b), (short)0, lv.H2 * lv.W2 * g.C * 4, 0x00020000);
+      uint32_t voff[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = 8 * i + (lane >> 3), slot = lane & 7;
+        const int c = min(c0 + wave * 32 + row, ncells - 1);
+        const int cy = divbw(c), cx = c - cy * bw;
+        const int piece = slot ^ ((row >> 1) & 7);
+        voff[i] = (uint32_t)(((by0 + cy) * lv.W2 + bx0 + cx) * g.C) * 4u + 16u * piece;
+      }
+      // readfirstlane: the DMA's LDS destination must be wave-uniform (an SGPR)
+      unsigned char* wreg = cbuf + __builtin_amdgcn_readfirstlane(wave) * 8192;
+      auto issue = [&](int bt) {
+        unsigned char* dst = wreg + (bt & 1) * 4096;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rf, (lds_void_t*)(dst + i * 1024), 16, voff[i],
+                                                   bt * 128, 0, 0);
+      };
+      const int nbt = nkb / 4;                     // batches of two k16 steps
+      const int sw = (j >> 1) & 7;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      issue(0);
+      for (int bt = 0; bt < nbt; ++bt) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads of the buffer refilled next
+        if (bt + 1 < nbt) {
+          issue(bt + 1);
+          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const unsigned char* rb0 = wreg + (bt & 1) * 4096 + j * 128;
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const int ks = 2 * bt + st;
+          const int p0 = 4 * st + 2 * kh;
+          const float4 a = *reinterpret_cast<const float4*>(rb0 + 16 * (p0 ^ sw));
+          const float4 b = *reinterpret_cast<const float4*>(rb0 + 16 * ((p0 + 1) ^ sw));
+          const ah8 qh = __builtin_bit_cast(ah8, qplanes[(0 * KB + 2 * ks + kh) * TQ + j]);
+          const ah8 ql = __builtin_bit_cast(ah8, qplanes[(1 * KB + 2 * ks + kh) * TQ + j]);
+          const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+          uint4 h, l;
+          alt_split8h(x, h, l);
+          const ah8 th = __builtin_bit_cast(ah8, h), tl = __builtin_bit_cast(ah8, l);
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc2, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc2, 0, 0, 0);
+          acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qh, acc[0], 0, 0, 0);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[0][r] = __builtin_fmaf(acc2[r], 0x1p-11f, acc[0][r]);
+    };
     // cell vectors one k step ahead in registers
     auto kloop = [&](auto h2tag) {
       constexpr bool M2 = decltype(h2tag)::value;
@@ -510,7 +580,12 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
       }
     };
     if constexpr (H2) {
-      kloop(std::integral_constant<bool, true>{});
+      if constexpr (DMA && NRB == 1) {
+        if (nkb % 4 == 0) kloop_dma();
+        else kloop(std::integral_constant<bool, true>{});
+      } else {
+        kloop(std::integral_constant<bool, true>{});
+      }
       bool bad = false;
 #pragma unroll
       for (int rb = 0; rb < NRB; ++rb)
@@ -823,7 +898,7 @@ long long alt_order_bytes(long long H, long long W) {
   return order_ws(alt_order_entries(H, W)).bytes;
 }
 
-template <int R, int NRB>
+template <int R, int NRB, bool DMA = false>
 int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const AltGeom& g,
                       int levels, int Z, int W1, hipStream_t stream, void* ws = nullptr) {
   const int H1 = g.N / W1;
@@ -858,9 +933,14 @@ int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const Al
     // entries of list (z, l) start at list (z * levels + l) * list_bytes: the kernel
     // indexes int4 entries by ((z * levels + l) * np + i), so lists are laid out
     // with a stride of list_bytes / 16 entries
-    hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 3, true>), grid, dim3(256), 0,
-                       stream, f1, coords, out, g, W1, tiles_x, reinterpret_cast<const int4*>(ws),
-                       o.list_bytes / 16);
+    if constexpr (DMA)
+      hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 2, true, 1, true>), grid,
+                         dim3(256), 0, stream, f1, coords, out, g, W1, tiles_x,
+                         reinterpret_cast<const int4*>(ws), o.list_bytes / 16);
+    else
+      hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 3, true>), grid, dim3(256), 0,
+                         stream, f1, coords, out, g, W1, tiles_x,
+                         reinterpret_cast<const int4*>(ws), o.list_bytes / 16);
     return dxr::launch_status();
   }
   hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 3>), grid, dim3(256), 0, stream, f1,

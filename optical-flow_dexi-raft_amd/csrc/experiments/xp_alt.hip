@@ -1,0 +1,36 @@
+// Experiments target only (libdexiraft_corr_exp.so, build.py --experiments):
+// variants of the ordered on-the-fly lookup (csrc/alt_corr.hip).  Never loaded
+// by the package.
+#include "../alt_corr.hip"
+
+// variant 0: the product's ordered lookup (register cell loads, 3 workgroups per
+// CU); 1: cell vectors by LDS-DMA into per-wave swizzled buffers (2 per CU).
+// Radius 4, C % 32 == 0, 16-byte aligned NHWC fmaps; ws as dxr_alt_corr_lookup_ws.
+extern "C" int dxr_xp_alt_lookup(const float* fmap1, const float* const* fmap2_levels,
+                                 const float* coords, float* out, int64_t B, int64_t H,
+                                 int64_t W, int64_t C, int num_levels, float divisor, void* ws,
+                                 int variant, hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, num_levels, &L) || C % 32 != 0 || C > 256 || !ws)
+    return DXR_EINVAL;
+  AltGeom g;
+  g.N = (int)(H * W);
+  g.C = (int)C;
+  g.Nc = 1;
+  g.cout = num_levels * 81;
+  g.divisor = divisor;
+  g.div_recip = pow2_recip(divisor);
+  g.f1_bstride = H * W * C;
+  g.coord_zstride = 2 * H * W;
+  g.coord_cstride = H * W;
+  g.coord_qstride = 1;
+  for (int l = 0; l < num_levels; ++l)
+    g.lv[l] = AltLevel{fmap2_levels[l], L.h[l], L.w[l], 1.f / (float)(1 << l), l * 81};
+  if (variant == 0)
+    return launch_alt_mfma_r<4, 1, false>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+                                          stream, ws);
+  if (variant == 1)
+    return launch_alt_mfma_r<4, 1, true>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+                                         stream, ws);
+  return DXR_EINVAL;
+}

@@ -10,8 +10,9 @@ and times interleaved rounds of replays (HIP events, after a clock warm-up):
   --block corr  build (product CorrBlock) + 12 lookups by dxr_xp_lookup variant
                 (libdexiraft_corr_exp.so: 0 spatial level-2/3 gathers, 32 query-major,
                 64 the 256 x 16 shape, 128 1024 x 64) or the product's (-1);
-  --block alt   12 on-the-fly lookups: dxr_alt_corr_lookup (-1, tile order) or
-                dxr_alt_corr_lookup_ws (-2, queries ordered first).
+  --block alt   12 on-the-fly lookups: dxr_alt_corr_lookup (-1, tile order),
+                dxr_alt_corr_lookup_ws (-2, queries ordered first) or dxr_xp_alt_lookup
+                variant v - 100 (100 the product's ordered form, 101 LDS-DMA cell staging).
 
 Usage: python scripts/ab_step.py [--workload sintel] [--batch 1] [--variants -1 32 64]
 """
@@ -51,6 +52,9 @@ def main():
     vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
     xp.dxr_xp_lookup.restype = i32
     xp.dxr_xp_lookup.argtypes = [vp, i32, i64, i64, i64, i32, vp, vp, i32, vp, vp]
+    xp.dxr_xp_alt_lookup.restype = i32
+    xp.dxr_xp_alt_lookup.argtypes = [vp, ctypes.POINTER(vp), vp, vp, i64, i64, i64, i64, i32,
+                                     ctypes.c_float, vp, i32, vp]
     dev = torch.device("cuda", 0)
     B, (H, W), D = a.batch, SHAPES[a.workload], 256
     g = torch.Generator(device=dev)
@@ -95,8 +99,10 @@ def main():
                             W, D, 4, 4, 16.0)
                     if v == -1:
                         st = lib.dxr_alt_corr_lookup(*args, s)
-                    else:
+                    elif v == -2:
                         st = lib.dxr_alt_corr_lookup_ws(*args, ws.data_ptr(), nws, s)
+                    else:   # experiments: dxr_xp_alt_lookup variant v - 100
+                        st = xp.dxr_xp_alt_lookup(*args[:9], args[10], ws.data_ptr(), v - 100, s)
                     assert st == 0
 
         graphs = {}
