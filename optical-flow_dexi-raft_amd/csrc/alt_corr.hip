@@ -898,7 +898,10 @@ long long alt_order_bytes(long long H, long long W) {
   return order_ws(alt_order_entries(H, W)).bytes;
 }
 
-template <int R, int NRB, bool DMA = false>
+// PF: cell loads of the ordered form kept 4 k steps ahead (round 3: with compact boxes the
+// waves wait on L2 latency, 62 % of wave cycles at PF = 1; 1080p 12 lookups 2,033 -> 1,972 us,
+// Sintel 626 -> 612 us in the step).  The tile-order form stays at 1 (its boxes are L1/TA-bound).
+template <int R, int NRB, bool DMA = false, int PF = 4>
 int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const AltGeom& g,
                       int levels, int Z, int W1, hipStream_t stream, void* ws = nullptr) {
   const int H1 = g.N / W1;
@@ -938,8 +941,8 @@ int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const Al
                          dim3(256), 0, stream, f1, coords, out, g, W1, tiles_x,
                          reinterpret_cast<const int4*>(ws), o.list_bytes / 16);
     else
-      hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 3, true>), grid, dim3(256), 0,
-                         stream, f1, coords, out, g, W1, tiles_x,
+      hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 3, true, PF>), grid, dim3(256),
+                         0, stream, f1, coords, out, g, W1, tiles_x,
                          reinterpret_cast<const int4*>(ws), o.list_bytes / 16);
     return dxr::launch_status();
   }

@@ -3,8 +3,9 @@
 // by the package.
 #include "../alt_corr.hip"
 
-// variant 0: the product's ordered lookup (register cell loads, 3 workgroups per
-// CU); 1: cell vectors by LDS-DMA into per-wave swizzled buffers (2 per CU).
+// variant 0: the ordered lookup with cell loads 1 k step ahead (3 workgroups per
+// CU; the product keeps 4 ahead = variant 3); 1: cell vectors by LDS-DMA into per-wave swizzled buffers (2 per CU);
+// 2 / 3: cell loads 2 / 4 k steps ahead (register ring).
 // Radius 4, C % 32 == 0, 16-byte aligned NHWC fmaps; ws as dxr_alt_corr_lookup_ws.
 extern "C" int dxr_xp_alt_lookup(const float* fmap1, const float* const* fmap2_levels,
                                  const float* coords, float* out, int64_t B, int64_t H,
@@ -27,10 +28,16 @@ extern "C" int dxr_xp_alt_lookup(const float* fmap1, const float* const* fmap2_l
   for (int l = 0; l < num_levels; ++l)
     g.lv[l] = AltLevel{fmap2_levels[l], L.h[l], L.w[l], 1.f / (float)(1 << l), l * 81};
   if (variant == 0)
-    return launch_alt_mfma_r<4, 1, false>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+    return launch_alt_mfma_r<4, 1, false, 1>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
                                           stream, ws);
   if (variant == 1)
     return launch_alt_mfma_r<4, 1, true>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
                                          stream, ws);
+  if (variant == 2)
+    return launch_alt_mfma_r<4, 1, false, 2>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+                                             stream, ws);
+  if (variant == 3)
+    return launch_alt_mfma_r<4, 1, false, 4>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+                                             stream, ws);
   return DXR_EINVAL;
 }
