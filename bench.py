@@ -504,11 +504,15 @@ def main():
             achieved = aflops / (look_ms * 1e-3) / 1e12
             akern = "alt_corr_mfma_kernel"
             a_traffic, a_src = pmc_traffic(wl_key, akern + "<")
+            pipe = PEAK_BF16_TFLOPS / SPLIT_PRODUCTS   # the f16-pair split's own ceiling (833 TF)
             res["roofline"] = {
-                "kernel": akern + " (f16-pair split MFMA over query-tile window boxes, f32 "
-                                  "accumulate; stage d, per lookup)",
+                "kernel": akern + " (f16-pair split MFMA over the window boxes of 32 queries "
+                                  "grouped by window position (alt_bin_*_kernel order) or by "
+                                  "4 x 8 tile, f32 accumulate; stage d; avg_launch_us = one "
+                                  "lookup incl. its three ordering launches)",
                 "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F32_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_TFLOPS, 4),
+                "frac_pipe_ceiling": round(achieved / pipe, 4), "pipe_ceiling_tflops": round(pipe, 1),
                 "traffic": a_traffic, "traffic_source": a_src,
                 "algorithmic_flops_per_launch": aflops,
                 "avg_launch_us": round(look_ms * 1e3, 2),

@@ -1944,22 +1944,26 @@ int launch_dma_bf16_nhwc(const uint16_t* f1, const uint16_t* f2, OT* pyr, const 
 
 // Pack pass of the bf16 DMA build for NCHW fmaps: [D][N] bf16 -> blocked
 // records [D/32][N][32 k] (64 B per pixel and 32-channel block, the layout a
-// channels-last fmap already has per pixel).  Thread = 4 pixels x 8 channels:
-// eight 8-byte loads along pixels (a wave reads 512 contiguous bytes per
-// channel row; VEC: N % 4 == 0 and 8-byte aligned rows), a register transpose,
-// four 16-byte write-through stores (the build reads them from every XCD).
-// Grid (ceil(N / 256), D / 32, 2 B).
+// channels-last fmap already has per pixel).  Workgroup = 256 pixels x one
+// 32-channel block; thread = 4 pixels x 8 channels: eight 8-byte loads along
+// pixels (a wave reads 512 contiguous bytes per channel row; VEC: N % 4 == 0
+// and 8-byte aligned rows), a register transpose, then the workgroup's 16 KB
+// of records go through LDS so that every 16-byte write-through store
+// instruction covers 1 KB of contiguous records (per-lane record pieces were
+// partial-line write-throughs: 65 us at KITTI B=8).  Grid (ceil(N / 256), D / 32, 2 B).
 template <bool VEC>
 __global__ __launch_bounds__(256) void pack_bf16_kernel(const uint16_t* __restrict__ f1,
                                                         const uint16_t* __restrict__ f2,
                                                         uint8_t* __restrict__ o1,
                                                         uint8_t* __restrict__ o2, int D, int N) {
+  __shared__ __attribute__((aligned(16))) uint4 rec[256 * 4];   // [pixel][4 x 16 B]
   const int tid = threadIdx.x, quad = tid & 63, cg = tid >> 6;
   const int kb = blockIdx.y, b = blockIdx.z >> 1, which = blockIdx.z & 1;
   const long long pbase = (long long)b * D * N;
   const uint16_t* src = (which ? f2 : f1) + pbase + (long long)(kb * 32 + cg * 8) * N;
   uint8_t* dst = (which ? o2 : o1) + pbase * 2;
-  const int p0 = blockIdx.x * 256 + quad * 4;
+  const int pw = blockIdx.x * 256;                 // first pixel of the workgroup
+  const int p0 = pw + quad * 4;
   uint16_t v[8][4];
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
@@ -1973,17 +1977,22 @@ __global__ __launch_bounds__(256) void pack_bf16_kernel(const uint16_t* __restri
       for (int i = 0; i < 4; ++i) v[c][i] = p0 + i < N ? src[(long long)c * N + p0 + i] : (uint16_t)0;
     }
   }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    rec[(quad * 4 + i) * 4 + cg] = make_uint4((uint32_t)v[0][i] | ((uint32_t)v[1][i] << 16),
+                                              (uint32_t)v[2][i] | ((uint32_t)v[3][i] << 16),
+                                              (uint32_t)v[4][i] | ((uint32_t)v[5][i] << 16),
+                                              (uint32_t)v[6][i] | ((uint32_t)v[7][i] << 16));
+  __syncthreads();
   const __amdgpu_buffer_rsrc_t r =
       __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 0x7fffffff, 0x00020000);
+  const unsigned base = (unsigned)(((long long)kb * N + pw) * 64);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    if (p0 + i >= N) break;
-    const u32x4v w = {(uint32_t)v[0][i] | ((uint32_t)v[1][i] << 16),
-                      (uint32_t)v[2][i] | ((uint32_t)v[3][i] << 16),
-                      (uint32_t)v[4][i] | ((uint32_t)v[5][i] << 16),
-                      (uint32_t)v[6][i] | ((uint32_t)v[7][i] << 16)};
-    const unsigned off = (unsigned)(((long long)kb * N + p0 + i) * 64 + cg * 16);
-    __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 16);
+    const int e = i * 256 + tid;                   // 16-B piece of the workgroup's records
+    if (pw + (e >> 2) < N)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, rec[e]), r,
+                                             base + (unsigned)e * 16u, 0, 16);
   }
 }
 

@@ -27,19 +27,24 @@ def main(path: str) -> None:
             name = r.get("Kernel_Name", "")
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
     rows.sort()
-    prod = ("corr_build", "split_pairs", "pool", "transpose")
+    prod = ("corr_build", "split_pairs", "pack_bf16", "pool", "transpose")
     is_look = [("corr_lookup_wide_kernel" in n or "alt_corr_mfma_kernel" in n) for _, _, n in rows]
-    is_prep = [any(p in n for p in prod) and not is_look[i] for i, (_, _, n) in enumerate(rows)]
+    # the ordered on-the-fly lookup's three ordering launches belong to its lookup
+    is_aux = [("alt_bin_" in n) for _, _, n in rows]
+    is_prep = [any(p in n for p in prod) and not is_look[i] and not is_aux[i]
+               for i, (_, _, n) in enumerate(rows)]
     # step starts: a build-side kernel right after a lookup (or first in the trace)
     starts = [i for i in range(len(rows)) if is_prep[i] and (i == 0 or is_look[i - 1])]
-    b_us, l_us, span_us, idle_us = [], [], [], []
+    b_us, l_us, x_us, span_us, idle_us = [], [], [], [], []
     for a, b in zip(starts, starts[1:]):
         looks = [i for i in range(a, b) if is_look[i]]
+        aux = [i for i in range(a, b) if is_aux[i]]
         prep = [i for i in range(a, b) if is_prep[i]]
-        if len(looks) != 12 or len(looks) + len(prep) != b - a:
+        if len(looks) != 12 or len(looks) + len(aux) + len(prep) != b - a:
             continue
         b_us.append(sum(rows[i][1] - rows[i][0] for i in prep) / 1e3)
         l_us.extend((rows[i][1] - rows[i][0]) / 1e3 for i in looks)
+        x_us.append(sum(rows[i][1] - rows[i][0] for i in aux) / 1e3 / 12)
         span = (rows[b][0] - rows[a][0]) / 1e3
         busy = sum((rows[i][1] - rows[i][0]) for i in range(a, b)) / 1e3
         span_us.append(span)
@@ -51,9 +56,11 @@ def main(path: str) -> None:
     print(json.dumps({
         "steps": len(b_us),
         "build_us_median": med(b_us), "lookup_us_median": med(l_us),
+        "lookup_order_us_median": med(x_us),
         "step_span_us_median": med(span_us), "idle_us_per_step_median": med(idle_us),
         "what": "back-to-back steps of the bench's step graph: build + 12 lookups, from the "
-                "rocprofv3 kernel trace of the same command (durations are kernel begin-end)",
+                "rocprofv3 kernel trace of the same command (durations are kernel begin-end; "
+                "lookup_order_us: the on-the-fly lookup's ordering launches per lookup)",
     }))
 
 
