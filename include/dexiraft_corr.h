@@ -127,7 +127,11 @@ int64_t dxr_pyramid_level_offset(int64_t B, int64_t H, int64_t W, int level);
  * pair x = hi + 2^-11 lo and three f16 x f16 MFMA products per f32 product are
  * accumulated in two f32 accumulators (the lo*lo term, <= 2^-22 |x y|, dropped);
  * a page whose sums are not finite (an operand beyond the f16 range, or inf/NaN)
- * is recomputed on an exact three-way bf16 split (six products).  With
+ * is recomputed on an exact three-way bf16 split (six products).  The pair is
+ * unscaled here: where |x| < 2^-14, hi falls on f16's subnormal grid and the
+ * pair's error stays ~2^-36 absolute, so relative accuracy drops for tiny fmaps
+ * (~1e-4 at |x| ~ 1e-7); dxr_corr_pyramid_build_ws (per-pixel power-of-two
+ * scaling, what CorrBlock calls) has no such bound.  With
  * D % 16 != 0, odd W or DXR_BUILD_EXACT_F32 the exact-f32 MFMA
  * v_mfma_f32_32x32x2_f32 is used.  Pyramid stores are write-through (sc1).
  * DXR_BF16 inputs use bf16 MFMA with f32 accumulation.  NHWC and NCHW inputs

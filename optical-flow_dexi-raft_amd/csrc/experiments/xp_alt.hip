@@ -5,7 +5,7 @@
 
 // variant 0: the ordered lookup with cell loads 1 k step ahead (3 workgroups per
 // CU; the product keeps 4 ahead = variant 3); 1: cell vectors by LDS-DMA into per-wave swizzled buffers (2 per CU);
-// 2 / 3: cell loads 2 / 4 k steps ahead (register ring).
+// 2 / 3 / 4 / 5: cell loads 2 / 4 / 6 / 8 k steps ahead (register ring).
 // Radius 4, C % 32 == 0, 16-byte aligned NHWC fmaps; ws as dxr_alt_corr_lookup_ws.
 extern "C" int dxr_xp_alt_lookup(const float* fmap1, const float* const* fmap2_levels,
                                  const float* coords, float* out, int64_t B, int64_t H,
@@ -38,6 +38,12 @@ extern "C" int dxr_xp_alt_lookup(const float* fmap1, const float* const* fmap2_l
                                              stream, ws);
   if (variant == 3)
     return launch_alt_mfma_r<4, 1, false, 4>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+                                             stream, ws);
+  if (variant == 4)
+    return launch_alt_mfma_r<4, 1, false, 6>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+                                             stream, ws);
+  if (variant == 5)
+    return launch_alt_mfma_r<4, 1, false, 8>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
                                              stream, ws);
   return DXR_EINVAL;
 }
