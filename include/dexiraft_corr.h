@@ -23,6 +23,8 @@
  *                            (autograd of CorrBlock.__call__, train.py:175-178)
  *   dxr_pyramid_backward     core/corr.py:25-27,58-60 avg_pool2d + division
  *                            backward (autograd of CorrBlock.__init__)
+ *   dxr_fmap_grads           core/corr.py:13-27,52-60 the whole CorrBlock.__init__
+ *                            backward (pooling + division + matmul) to d fmap1/2
  *   dxr_avg_pool2x2          core/corr.py:69-71  F.avg_pool2d(fmap, 2, stride=2)
  *                            in AlternateCorrBlock.__init__
  *   dxr_avg_pool2x2_nhwc     core/corr.py:70-71 the same pool on channels-last fmaps
@@ -74,7 +76,7 @@ extern "C" {
 /* HIP's own definition; repeating an identical typedef is legal in C11/C++. */
 typedef struct ihipStream_t* hipStream_t;
 
-#define DXR_ABI_VERSION 6
+#define DXR_ABI_VERSION 7
 
 enum dxr_status {
   DXR_OK = 0,
@@ -264,6 +266,29 @@ int dxr_corr_lookup_conv1x1(const void* pyramid, int pyr_dtype,
 int dxr_pyramid_backward(const void* grad_pyramid, int grad_dtype,
                          int64_t B, int64_t H, int64_t W, int num_levels,
                          float divisor, float* grad_volume, hipStream_t stream);
+
+/*
+ * Backward of stages (a)+(b) straight to the fmap gradients, without the
+ * [B, H*W, H*W] volume gradient (core/corr.py:13-27,52-60 under autograd,
+ * train.py:175-178): the gradient pyramid is folded down the pooling chain
+ * inside the two GEMMs' operand loads,
+ *   grad_fmap1 = fmap2 . dV^T,  grad_fmap2 = fmap1 . dV   (dV as above),
+ * on MFMA with a three-way bf16 split of both operands (six products, f32
+ * accumulation: f32-class).  Deterministic (fixed summation order).
+ *   grad_pyramid : float32, the paged layout of dxr_corr_pyramid_build
+ *   fmap1, fmap2 : [B, D, H, W] float32, NCHW contiguous
+ *   grad_fmap1/2 : [B, D, H, W] float32 outputs, either may be NULL (skipped)
+ *   workspace    : >= dxr_fmap_grads_workspace_bytes(B, D, H, W, num_levels)
+ * Supported: D a multiple of 32, num_levels <= 4 (other valid requests return
+ * DXR_EUNSUPPORTED; dxr_pyramid_backward + two GEMMs covers them).
+ * dxr_fmap_grads_workspace_bytes returns -1 for unsupported shapes.
+ */
+int64_t dxr_fmap_grads_workspace_bytes(int64_t B, int64_t D, int64_t H, int64_t W,
+                                       int num_levels);
+int dxr_fmap_grads(const void* grad_pyramid, int grad_dtype, const float* fmap1,
+                   const float* fmap2, int64_t B, int64_t D, int64_t H, int64_t W,
+                   int num_levels, float divisor, float* grad_fmap1, float* grad_fmap2,
+                   void* workspace, int64_t workspace_bytes, hipStream_t stream);
 
 /*
  * 2x2 / stride-2 average pool, floor mode, of [planes, H, W] float32 into

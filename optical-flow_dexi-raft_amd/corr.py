@@ -12,8 +12,10 @@ differentiable with respect to the fmaps, as the reference is through matmul /
 avg_pool2d / grid_sample (train.py:175-178).  Each lookup's backward adds its
 bilinear transpose into one gradient pyramid owned by the block
 (``dxr_corr_lookup_backward``); the build's backward runs once after all of
-them, folds that pyramid down the pooling chain (``dxr_pyramid_backward``) and
-takes the fmap gradients as two plain GEMMs (torch.bmm: rocBLAS).
+them and takes the fmap gradients as two MFMA GEMMs that fold that pyramid down
+the pooling chain in their operand loads (``dxr_fmap_grads``: no [B, N, N]
+volume gradient).  Shapes it does not cover (D % 32 != 0, more than 4 levels)
+form dV (``dxr_pyramid_backward``) and run two torch.bmm (rocBLAS).
 
 Differences from the reference, all loud:
   * host (CPU) tensors raise ``RuntimeError`` instead of running on the CPU;
@@ -107,8 +109,24 @@ class _BuildGrad(torch.autograd.Function):
             return None, None, None
         f1, f2 = ctx.saved_tensors
         B, D, H, W = gs.geom
-        dv = torch.empty((B, H * W, H * W), dtype=torch.float32, device=f1.device)
         lib = nat.load()
+        wsb = lib.dxr_fmap_grads_workspace_bytes(B, D, H, W, gs.num_levels)
+        if wsb >= 0:   # the fused MFMA backward: no [B, N, N] dV
+            need1, need2 = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+            c1 = f1.contiguous() if need2 else None
+            c2 = f2.contiguous() if need1 else None
+            df1 = torch.empty((B, D, H, W), dtype=torch.float32, device=f1.device) if need1 else None
+            df2 = torch.empty((B, D, H, W), dtype=torch.float32, device=f1.device) if need2 else None
+            ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=f1.device)
+            with _Launch(gs.device):
+                st = lib.dxr_fmap_grads(gp.data_ptr(), nat.DXR_F32, nat.ptr(c1), nat.ptr(c2),
+                                        B, D, H, W, gs.num_levels, _sqrt_dim(D), nat.ptr(df1),
+                                        nat.ptr(df2),
+                                        ws.data_ptr(), wsb, nat.stream_of(ws))
+            nat.check(st, "CorrBlock backward (dxr_fmap_grads)")
+            return df1, df2, None
+        # D % 32 != 0 or more than 4 levels: dV, then two GEMMs
+        dv = torch.empty((B, H * W, H * W), dtype=torch.float32, device=f1.device)
         with _Launch(gs.device):
             st = lib.dxr_pyramid_backward(gp.data_ptr(), nat.DXR_F32, B, H, W, gs.num_levels,
                                           _sqrt_dim(D), dv.data_ptr(), nat.stream_of(dv))

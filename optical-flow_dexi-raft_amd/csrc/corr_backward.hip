@@ -1,0 +1,464 @@
+// Fmap gradients of the correlation pyramid on MFMA, with no [N x N] dV.
+//
+// Training backpropagates through matmul -> / sqrt(D) -> avg_pool2d chain ->
+// grid_sample (train.py:175-178, core/corr.py:13-27,52-60).  The lookups'
+// backwards leave one gradient pyramid G (paged like the pyramid, dxr_common.h).
+// Folding it down the pooling chain gives
+//   dV[q][t] = (G0 + (G1 + (G2 + G3/4)/4)/4)[q][t] / sqrt(D)   (floor-mode masks)
+// and the fmap gradients are two GEMMs against dV:
+//   dF1[d][q] = sum_t F2[d][t] dV[q][t]      (kernel KT: K runs over targets)
+//   dF2[d][t] = sum_q F1[d][q] dV[q][t]      (kernel !KT: K runs over queries)
+// (r02 formed dV in HBM with dxr_pyramid_backward — 189 MB per Sintel pair —
+// and ran the two GEMMs on rocBLAS f32.)
+//
+// Here a workgroup owns 256 channels x one n-block of 128 (a query block for
+// dF1, a level-0 target tile for dF2) and walks a chunk of k-blocks.  A k-block
+// is one page of each level: 128 queries x one 8 x 16 target tile (and its 4 x 8,
+// 2 x 4, 1 x 2 pooled tiles), all contiguous.  Per k-block the workgroup folds
+// the four pages into the dV tile, splits it three ways into bf16 (hi, mid, lo)
+// MFMA B-operand records in LDS, and runs 8 k-steps of v_mfma_f32_32x32x16_bf16
+// with six products (the f32-class split of dxr_common.h split8); the fmap
+// operand comes pre-split from a pack pass, one 1 KiB-contiguous record block
+// per wave and k-step.  The next k-block's pages are loaded into registers while
+// the MFMAs run.  Chunks of k-blocks (split K, so ~256 workgroups fill the chip)
+// write partial sums that a last pass adds in a fixed order: deterministic.
+#include <cmath>
+
+#include "dxr_common.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
+
+constexpr int PQ = dxr::PAGE_Q;           // queries per page
+constexpr int TH = dxr::PAGE_H;           // level-0 tile rows
+constexpr int TW = dxr::PAGE_W;           // level-0 tile cols
+constexpr int NB = 128;                   // n per workgroup
+constexpr int KSTEPS = 8;                 // 16-k steps per k-block (128)
+constexpr int DS = 256;                   // channels per workgroup (8 waves x 32)
+constexpr int NTHR = 512;
+constexpr int REC = KSTEPS * NB * 2;      // 16-B records per split part in LDS
+static_assert(PQ == NB && TH * TW == NB, "a k-block is one page");
+
+struct GradGeom {
+  int B, D, H, W, N;
+  int qt, tyn, txn;       // query blocks, tile rows, tile cols per pair
+  int nlev;               // tiled levels in the pyramid (1..4)
+  int lh[4], lw[4];
+  long long loff[4];
+  float divisor, recip;   // recip = 1/divisor when exact, else 0
+  int nblk, kbt, S;       // n blocks, k blocks, k chunks
+  int nslab;              // 256-channel slabs
+  long long ks;           // k steps of the packed operand
+};
+
+__device__ __forceinline__ uint4 ld4(const float* p) {
+  const float4 v = *reinterpret_cast<const float4*>(p);
+  return make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
+                    __float_as_uint(v.w));
+}
+
+// Page element offsets of (pair b, query block qb, tile (ty, tx)) at each level.
+__device__ __forceinline__ void page_bases(const GradGeom& g, int b, int qb, int ty, int tx,
+                                           long long (&base)[4]) {
+  const long long page = (((long long)b * g.qt + qb) * g.tyn + ty) * g.txn + tx;
+#pragma unroll
+  for (int l = 0; l < 4; ++l) base[l] = g.loff[l] + page * PQ * (NB >> (2 * l));
+}
+
+// One dV element from its four level gradients (pyramid_backward_kernel's order:
+// from the coarsest level down, t = g_l + t/4; masked levels contribute 0).
+__device__ __forceinline__ float fold(const GradGeom& g, int y, int x, bool qok, float g0, float g1,
+                                      float g2, float g3) {
+  float t = 0.f;
+  if (g.nlev > 3 && (y >> 3) < g.lh[3] && (x >> 3) < g.lw[3]) t = g3;
+  if (g.nlev > 2) t = (((y >> 2) < g.lh[2] && (x >> 2) < g.lw[2]) ? g2 : 0.f) + 0.25f * t;
+  if (g.nlev > 1) t = (((y >> 1) < g.lh[1] && (x >> 1) < g.lw[1]) ? g1 : 0.f) + 0.25f * t;
+  t = ((y < g.H && x < g.W && qok) ? g0 : 0.f) + 0.25f * t;
+  return g.recip != 0.f ? t * g.recip : t / g.divisor;
+}
+
+// Raw page values one thread folds.  KT (dF1, n = query, k = target): thread
+// (query tid&127, tile rows 2(tid>>7), +1, all 16 cols).  !KT (dF2, n = target,
+// k = query): thread (8 queries 8(tid>>5).., 4 targets 4(tid&31)..).
+template <bool KT>
+struct Raw;
+
+template <>
+struct Raw<true> {
+  uint4 g0[8];
+  uint4 g1[2];
+  uint4 g2;
+  float g3[2];
+};
+
+template <>
+struct Raw<false> {
+  uint4 g0[8];
+  float g1[8][2];
+  float g2[8];
+  float g3[8];
+};
+
+template <bool KT>
+__device__ __forceinline__ void load_raw(const GradGeom& g, const float* __restrict__ gp, int b,
+                                         int qb, int tile, Raw<KT>& r) {
+  const int tid = threadIdx.x;
+  long long base[4];
+  page_bases(g, b, qb, tile / g.txn, tile % g.txn, base);
+  if constexpr (KT) {
+    const int q = tid & 127, k = tid >> 7;
+    const float* p0 = gp + base[0] + q * 128 + k * 32;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.g0[i] = ld4(p0 + 4 * i);
+    r.g1[0] = r.g1[1] = make_uint4(0, 0, 0, 0);
+    r.g2 = make_uint4(0, 0, 0, 0);
+    r.g3[0] = r.g3[1] = 0.f;
+    if (g.nlev > 1) {
+      const float* p1 = gp + base[1] + q * 32 + k * 8;
+      r.g1[0] = ld4(p1);
+      r.g1[1] = ld4(p1 + 4);
+    }
+    if (g.nlev > 2) r.g2 = ld4(gp + base[2] + q * 8 + (k >> 1) * 4);
+    if (g.nlev > 3) {
+      const float2 v = *reinterpret_cast<const float2*>(gp + base[3] + q * 2);
+      r.g3[0] = v.x;
+      r.g3[1] = v.y;
+    }
+  } else {
+    const int tg = tid & 31, q0 = (tid >> 5) * 8, rr = tg >> 2, cq = tg & 3;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int q = q0 + i;
+      r.g0[i] = ld4(gp + base[0] + q * 128 + 4 * tg);
+      r.g1[i][0] = r.g1[i][1] = r.g2[i] = r.g3[i] = 0.f;
+      if (g.nlev > 1) {
+        const float2 v = *reinterpret_cast<const float2*>(gp + base[1] + q * 32 + (rr >> 1) * 8 + 2 * cq);
+        r.g1[i][0] = v.x;
+        r.g1[i][1] = v.y;
+      }
+      if (g.nlev > 2) r.g2[i] = gp[base[2] + q * 8 + (rr >> 2) * 4 + cq];
+      if (g.nlev > 3) r.g3[i] = gp[base[3] + q * 2 + (cq >> 1)];
+    }
+  }
+}
+
+__device__ __forceinline__ float u2f(uint32_t u) { return __uint_as_float(u); }
+__device__ __forceinline__ float comp(const uint4& v, int e) {
+  return u2f(e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w);
+}
+
+// Fold the raw values of k-block (qb, tile) into dV, split, write the LDS records
+// (part p, k-step s, n, half h) at sb[((p*8 + s)*128 + n)*2 + h].
+template <bool KT>
+__device__ __forceinline__ void fold_store(const GradGeom& g, const Raw<KT>& r, int qb, int tile,
+                                           uint4* __restrict__ sb) {
+  const int tid = threadIdx.x;
+  const int y0 = (tile / g.txn) * TH, x0 = (tile % g.txn) * TW;
+  if constexpr (KT) {
+    const int q = tid & 127, k = tid >> 7;
+    const bool qok = qb * PQ + q < g.N;
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const int y = y0 + 2 * k + rr;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int c = 8 * h + e, i = rr * 16 + c;
+          v[e] = fold(g, y, x0 + c, qok, comp(r.g0[i >> 2], i & 3), comp(r.g1[c >> 3], (c >> 1) & 3),
+                      comp(r.g2, c >> 2), r.g3[c >> 3]);
+        }
+        uint4 hi, mi, lo;
+        dxr::split8(v, hi, mi, lo);
+        const int rec = ((2 * k + rr) * NB + q) * 2 + h;
+        sb[rec] = hi;
+        sb[REC + rec] = mi;
+        sb[2 * REC + rec] = lo;
+      }
+    }
+  } else {
+    const int tg = tid & 31, qg = tid >> 5, rr = tg >> 2, cq = tg & 3;
+    const int y = y0 + rr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = 4 * cq + j;
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const bool qok = qb * PQ + qg * 8 + i < g.N;
+        v[i] = fold(g, y, x0 + c, qok, comp(r.g0[i], j), r.g1[i][j >> 1], r.g2[i], r.g3[i]);
+      }
+      uint4 hi, mi, lo;
+      dxr::split8(v, hi, mi, lo);
+      const int rec = ((qg >> 1) * NB + j * 32 + tg) * 2 + (qg & 1);
+      sb[rec] = hi;
+      sb[REC + rec] = mi;
+      sb[2 * REC + rec] = lo;
+    }
+  }
+}
+
+// XCD-aware linear order (workgroup w runs on XCD w % 8): each XCD takes a
+// contiguous range of (pair, slab, chunk, n block), n block fastest, so the
+// workgroups an XCD holds share one chunk's fmap operand in its L2.
+__device__ __forceinline__ long long xcd_linear(long long w, long long nwg) {
+  const long long q8 = nwg / 8, r8 = nwg % 8, xcd = w % 8;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + w / 8;
+}
+
+template <bool KT>
+__global__ __launch_bounds__(NTHR) void fmap_grad_kernel(const float* __restrict__ gp,
+                                                         const uint4* __restrict__ fp,
+                                                         float* __restrict__ out, GradGeom g) {
+  __shared__ uint4 sb[3 * REC];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  long long wl = xcd_linear(blockIdx.x, gridDim.x);
+  const int nb = (int)(wl % g.nblk);
+  wl /= g.nblk;
+  const int chunk = (int)(wl % g.S);
+  wl /= g.S;
+  const int slab = (int)(wl % g.nslab);
+  const int b = (int)(wl / g.nslab);
+  const int kb0 = (int)((long long)chunk * g.kbt / g.S);
+  const int kb1 = (int)((long long)(chunk + 1) * g.kbt / g.S);
+  const int d0 = slab * DS + wave * 32;
+  const bool active = d0 < g.D;  // D % 32 == 0: whole waves
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[j][v] = 0.f;
+
+  // fmap operand records: (((b*3 + p)*ks + k-step)*D + d)*2 + half
+  const long long pstride = g.ks * g.D * 2, kstride = (long long)g.D * 2;
+  const uint4* fa = fp + (long long)b * 3 * pstride + (long long)(d0 + (lane & 31)) * 2 + (lane >> 5);
+  const uint4* bl = sb + (lane & 31) * 2 + (lane >> 5);
+
+  Raw<KT> raw;
+  if (kb0 < kb1) load_raw<KT>(g, gp, b, KT ? nb : kb0, KT ? kb0 : nb, raw);
+  for (int kb = kb0; kb < kb1; ++kb) {
+    const int qb = KT ? nb : kb, tile = KT ? kb : nb;
+    __syncthreads();  // the previous k-block's operand reads are done
+    fold_store<KT>(g, raw, qb, tile, sb);
+    __syncthreads();
+    if (kb + 1 < kb1) load_raw<KT>(g, gp, b, KT ? nb : kb + 1, KT ? kb + 1 : nb, raw);
+    if (active) {
+      const uint4* fk = fa + (long long)kb * KSTEPS * kstride;
+      uint4 ah = fk[0], am = fk[pstride], al = fk[2 * pstride];
+#pragma unroll 1
+      for (int s = 0; s < KSTEPS; ++s) {
+        uint4 nh = ah, nm = am, nl = al;
+        if (s + 1 < KSTEPS) {
+          const uint4* fn = fk + (s + 1) * kstride;
+          nh = fn[0];
+          nm = fn[pstride];
+          nl = fn[2 * pstride];
+        }
+        const bf8v qh = __builtin_bit_cast(bf8v, ah), qm = __builtin_bit_cast(bf8v, am),
+                   ql = __builtin_bit_cast(bf8v, al);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint4* bp = bl + (s * NB + 32 * j) * 2;
+          const bf8v th = __builtin_bit_cast(bf8v, bp[0]), tm = __builtin_bit_cast(bf8v, bp[REC]),
+                     tl = __builtin_bit_cast(bf8v, bp[2 * REC]);
+          // small terms first
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, tm, acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ql, th, acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, tl, acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, th, acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, tm, acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, th, acc[j], 0, 0, 0);
+        }
+        ah = nh;
+        am = nm;
+        al = nl;
+      }
+    }
+  }
+  if (!active) return;
+  // C/D map: column n = lane & 31 (+32 j), row d = (v&3) + 8(v>>2) + 4(lane>>5)
+  float* o = out + ((long long)chunk * g.B + b) * g.D * g.N;
+  const int ty = nb / g.txn, tx = nb % g.txn;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    int px;
+    if constexpr (KT) {
+      const int q = nb * PQ + 32 * j + (lane & 31);
+      px = q < g.N ? q : -1;
+    } else {
+      const int t = 4 * (lane & 31) + j, y = ty * TH + (t >> 4), x = tx * TW + (t & 15);
+      px = (y < g.H && x < g.W) ? y * g.W + x : -1;
+    }
+    if (px < 0) continue;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int d = d0 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
+      o[(long long)d * g.N + px] = acc[j][v];
+    }
+  }
+}
+
+// Fmap -> three-way bf16 split operand records in the GEMM's k order.
+// TORD: k = target in tile order (tile*128 + row*16 + col); else k = query.
+template <bool TORD>
+__global__ __launch_bounds__(256) void fmap_split_kernel(const float* __restrict__ f,
+                                                         uint4* __restrict__ fp, GradGeom g) {
+  const long long total = (long long)g.B * g.ks * g.D * 2;
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const int h = (int)(idx & 1);
+    long long r = idx >> 1;
+    const int d = (int)(r % g.D);
+    r /= g.D;
+    const long long s = r % g.ks;
+    const int b = (int)(r / g.ks);
+    const float* src = f + ((long long)b * g.D + d) * g.N;
+    float x[8];
+    if constexpr (TORD) {
+      const int tile = (int)(s / KSTEPS);
+      const int y = (tile / g.txn) * TH + (int)(s % KSTEPS), xx = (tile % g.txn) * TW + 8 * h;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = (y < g.H && xx + e < g.W) ? src[y * g.W + xx + e] : 0.f;
+    } else {
+      const long long q = s * 16 + 8 * h;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = q + e < g.N ? src[q + e] : 0.f;
+    }
+    uint4 hi, mi, lo;
+    dxr::split8(x, hi, mi, lo);
+    const long long rec = (((long long)b * 3 * g.ks + s) * g.D + d) * 2 + h;
+    const long long ps = g.ks * g.D * 2;
+    fp[rec] = hi;
+    fp[rec + ps] = mi;
+    fp[rec + 2 * ps] = lo;
+  }
+}
+
+// out[i] = sum over chunks s (ascending) of part[s][i].
+__global__ __launch_bounds__(256) void chunk_sum_kernel(const float* __restrict__ part,
+                                                        float* __restrict__ out, long long n, int S) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    float t = part[i];
+    for (int s = 1; s < S; ++s) t += part[s * n + i];
+    out[i] = t;
+  }
+}
+
+long long align256(long long x) { return (x + 255) / 256 * 256; }
+
+bool make_geom(int64_t B, int64_t D, int64_t H, int64_t W, int num_levels, float divisor,
+               GradGeom* g) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, num_levels, &L)) return false;
+  g->B = (int)B;
+  g->D = (int)D;
+  g->H = (int)H;
+  g->W = (int)W;
+  g->N = (int)(H * W);
+  g->qt = L.lay[0].qt;
+  g->tyn = L.lay[0].ty;
+  g->txn = L.lay[0].tx;
+  g->nlev = num_levels;
+  for (int l = 0; l < 4; ++l) {
+    const int k = l < num_levels ? l : 0;
+    g->lh[l] = L.lay[k].h;
+    g->lw[l] = L.lay[k].w;
+    g->loff[l] = L.lay[k].off;
+  }
+  g->divisor = divisor;
+  int e2 = 0;
+  g->recip = (std::frexp(divisor, &e2) == 0.5f) ? 1.f / divisor : 0.f;
+  g->nslab = (int)((D + DS - 1) / DS);
+  return true;
+}
+
+// KT: n blocks = query blocks, k blocks = tiles; else the other way round.
+void set_kernel(GradGeom* g, bool kt) {
+  const int tiles = g->tyn * g->txn;
+  g->nblk = kt ? g->qt : tiles;
+  g->kbt = kt ? tiles : g->qt;
+  g->ks = (long long)g->kbt * KSTEPS;
+  const long long units = (long long)g->nblk * g->B * g->nslab;
+  long long S = units >= 256 ? 1 : 256 / units;
+  if (S > g->kbt) S = g->kbt;
+  g->S = (int)S;
+}
+
+long long operand_bytes(const GradGeom& g) { return align256((long long)g.B * 3 * g.ks * g.D * 32); }
+long long partial_bytes(const GradGeom& g) {
+  return g.S > 1 ? align256((long long)g.S * g.B * g.D * g.N * 4) : 0;
+}
+
+bool grads_supported(int64_t D, int num_levels) {
+  return D > 0 && D % 32 == 0 && num_levels >= 1 && num_levels <= dxr::TILED_LEVELS;
+}
+
+unsigned grid_for(long long total) {
+  long long blocks = (total + 255) / 256;
+  if (blocks > 2048 * 8) blocks = 2048 * 8;
+  return (unsigned)(blocks < 1 ? 1 : blocks);
+}
+
+}  // namespace
+
+extern "C" int64_t dxr_fmap_grads_workspace_bytes(int64_t B, int64_t D, int64_t H, int64_t W,
+                                                  int num_levels) {
+  GradGeom g;
+  if (!grads_supported(D, num_levels) || !make_geom(B, D, H, W, num_levels, 1.f, &g)) return -1;
+  long long ws = 0;
+  for (int kt = 0; kt < 2; ++kt) {
+    set_kernel(&g, kt == 1);
+    const long long need = operand_bytes(g) + partial_bytes(g);
+    if (need > ws) ws = need;
+  }
+  return ws;
+}
+
+extern "C" int dxr_fmap_grads(const void* grad_pyramid, int grad_dtype, const float* fmap1,
+                              const float* fmap2, int64_t B, int64_t D, int64_t H, int64_t W,
+                              int num_levels, float divisor, float* grad_fmap1, float* grad_fmap2,
+                              void* workspace, int64_t workspace_bytes, hipStream_t stream) {
+  if (grad_dtype != DXR_F32) return grad_dtype == DXR_BF16 ? DXR_EUNSUPPORTED : DXR_EINVAL;
+  if (D < 1 || B < 0 || B > 65535 || !(divisor == divisor) || divisor == 0.f) return DXR_EINVAL;
+  if (!grads_supported(D, num_levels)) return DXR_EUNSUPPORTED;
+  GradGeom g;
+  if (!make_geom(B, D, H, W, num_levels, divisor, &g)) return DXR_EINVAL;
+  if (B == 0 || (!grad_fmap1 && !grad_fmap2)) return DXR_OK;
+  if (!grad_pyramid || !workspace) return DXR_EINVAL;
+  if (workspace_bytes < dxr_fmap_grads_workspace_bytes(B, D, H, W, num_levels)) return DXR_EINVAL;
+  const float* gp = static_cast<const float*>(grad_pyramid);
+  for (int kt = 1; kt >= 0; --kt) {
+    float* dst = kt ? grad_fmap1 : grad_fmap2;
+    const float* src = kt ? fmap2 : fmap1;
+    if (!dst) continue;
+    if (!src) return DXR_EINVAL;
+    set_kernel(&g, kt == 1);
+    uint4* fp = static_cast<uint4*>(workspace);
+    float* part = g.S > 1 ? reinterpret_cast<float*>(static_cast<char*>(workspace) + operand_bytes(g))
+                          : dst;
+    const long long nwg = (long long)g.nblk * g.S * g.nslab * g.B;
+    if (kt) {
+      hipLaunchKernelGGL(fmap_split_kernel<true>, dim3(grid_for(g.B * g.ks * g.D * 2)), dim3(256), 0,
+                         stream, src, fp, g);
+      hipLaunchKernelGGL(fmap_grad_kernel<true>, dim3((unsigned)nwg), dim3(NTHR), 0, stream, gp, fp,
+                         part, g);
+    } else {
+      hipLaunchKernelGGL(fmap_split_kernel<false>, dim3(grid_for(g.B * g.ks * g.D * 2)), dim3(256), 0,
+                         stream, src, fp, g);
+      hipLaunchKernelGGL(fmap_grad_kernel<false>, dim3((unsigned)nwg), dim3(NTHR), 0, stream, gp, fp,
+                         part, g);
+    }
+    if (g.S > 1) {
+      const long long n = (long long)g.B * g.D * g.N;
+      hipLaunchKernelGGL(chunk_sum_kernel, dim3(grid_for(n)), dim3(256), 0, stream, part, dst, n, g.S);
+    }
+    const int st = dxr::launch_status();
+    if (st != DXR_OK) return st;
+  }
+  return DXR_OK;
+}

@@ -4,8 +4,9 @@
 One training step of the correlation path = CorrBlock(fmap1, fmap2) with fmaps
 that require grad + 12 lookups + backward of sum_k <w_k, lookup_k> (train.py:175-178
 backpropagates through the same ops).  Times the forward, the whole step, and the
-backward's pieces (12 dxr_corr_lookup_backward, dxr_pyramid_backward, the two
-fmap GEMMs) with HIP events, and reports the peak memory of the step.
+backward's pieces (12 dxr_corr_lookup_backward, then dxr_fmap_grads: two fused
+fmap GEMMs that fold the gradient pyramid in their operand loads) with HIP events,
+and reports the peak memory of the step.
 
 Usage: python scripts/time_backward.py [--workload sintel|chairs] [--reps 10]
 """
@@ -42,12 +43,18 @@ def main():
     coords = [grid + 4.0 * torch.randn(grid.shape, generator=g, device=dev) for _ in range(12)]
     wts = [torch.randn((B, 324, H, W), generator=g, device=dev) for _ in range(12)]
 
-    def step(backward=True):
-        a1, a2 = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
+    def forward_loss(a1, a2):
+        # the block is a local of the forward pass, as corr_fn in RAFT.forward
+        # (core/raft.py:101,147): it is gone when loss.backward() runs
         cb = dexiraft_amd.CorrBlock(a1, a2)
         loss = 0.0
         for c, w in zip(coords, wts):
             loss = loss + (cb(c) * w).sum()
+        return loss
+
+    def step(backward=True):
+        a1, a2 = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
+        loss = forward_loss(a1, a2)
         if backward:
             loss.backward()
         return a1, a2
@@ -81,8 +88,9 @@ def main():
     kern = {}
     for ev in prof.key_averages():
         name = ev.key
-        for key in ("corr_lookup_backward", "pyramid_backward", "corr_build_split", "corr_lookup_wide",
-                    "Cijk", "gemm", "elementwise", "reduce"):
+        for key in ("corr_lookup_backward", "pyramid_backward", "fmap_grad_kernel", "fmap_split",
+                    "chunk_sum", "corr_build", "split_pairs", "corr_lookup_wide", "Cijk", "gemm",
+                    "elementwise", "reduce", "fill"):
             if key in name:
                 t = getattr(ev, "device_time_total", None)
                 if t is None:

@@ -43,7 +43,7 @@ def test_header_declares_the_documented_entry_points():
         "dxr_corr_lookup_backward", "dxr_pyramid_backward", "dxr_alt_corr_backward",
         "dxr_conv1x1_packed_bytes", "dxr_conv1x1_pack_weight", "dxr_corr_lookup_conv1x1",
         "dxr_transpose", "dxr_avg_pool2x2_nhwc", "dxr_alt_workspace_bytes",
-        "dxr_alt_corr_lookup_ws"}
+        "dxr_alt_corr_lookup_ws", "dxr_fmap_grads_workspace_bytes", "dxr_fmap_grads"}
 
 
 def test_library_exports_every_declared_symbol(nat):
@@ -67,7 +67,7 @@ def test_library_is_gfx950_code(nat):
 
 def test_abi_version_and_status_strings(nat):
     lib = nat.load()
-    assert lib.dxr_abi_version() == nat.ABI_VERSION == 6
+    assert lib.dxr_abi_version() == nat.ABI_VERSION == 7
     assert lib.dxr_status_string(0) == b"ok"
     assert lib.dxr_status_string(1) == b"invalid argument"
     assert lib.dxr_status_string(2) == b"unsupported by this build"
@@ -238,3 +238,42 @@ def test_alt_workspace_bytes(nat):
     assert aw(P, ptrs, P, P, 1, 16, 16, 64, 4, 4, 0.0, P, 1 << 20, None) == nat.DXR_EINVAL
     assert aw(P, ptrs, P, P, 1, 16, 16, 64, 4, 9, 16.0, P, 1 << 20, None) == nat.DXR_EUNSUPPORTED
     assert aw(None, None, None, None, 0, 16, 16, 64, 4, 4, 16.0, None, 0, None) == nat.DXR_OK
+
+
+def _fmap_grads_ws(B, D, H, W):
+    """dxr_fmap_grads' workspace: the larger of its two GEMMs' needs, each the
+    three-way split fmap operand (3 x 16 bit per element, k padded to whole
+    k-blocks of 128) plus, when K is split into S > 1 chunks (~256 workgroups),
+    S partial [B, D, H*W] f32 sums."""
+    al = lambda x: (x + 255) // 256 * 256   # noqa: E731
+    N = H * W
+    qt, tiles = -(-N // 128), -(-H // 8) * -(-W // 16)
+    slabs = -(-D // 256)
+    need = 0
+    for nblk, kbt in ((qt, tiles), (tiles, qt)):
+        units = nblk * B * slabs
+        S = 1 if units >= 256 else min(256 // units, kbt)
+        op = al(B * 3 * kbt * 8 * D * 32)
+        need = max(need, op + (al(S * B * D * N * 4) if S > 1 else 0))
+    return need
+
+
+def test_fmap_grads_workspace_and_validation(nat):
+    lib = nat.load()
+    for B, D, H, W in ((1, 256, 55, 128), (2, 64, 23, 37), (8, 256, 47, 156), (1, 288, 46, 62)):
+        assert lib.dxr_fmap_grads_workspace_bytes(B, D, H, W, 4) == _fmap_grads_ws(B, D, H, W)
+    assert lib.dxr_fmap_grads_workspace_bytes(1, 48, 55, 128, 4) == -1   # D % 32
+    assert lib.dxr_fmap_grads_workspace_bytes(1, 256, 55, 128, 5) == -1  # row-major level
+    assert lib.dxr_fmap_grads_workspace_bytes(1, 256, 0, 128, 4) == -1
+    P = 1 << 12
+    fg = lib.dxr_fmap_grads
+    ws = _fmap_grads_ws(1, 256, 16, 16)
+    # statuses before any launch
+    assert fg(P, 0, P, P, 1, 256, 16, 16, 4, 0.0, P, P, P, ws, None) == nat.DXR_EINVAL
+    assert fg(P, 1, P, P, 1, 256, 16, 16, 4, 16.0, P, P, P, ws, None) == nat.DXR_EUNSUPPORTED
+    assert fg(P, 0, P, P, 1, 48, 16, 16, 4, 16.0, P, P, P, ws, None) == nat.DXR_EUNSUPPORTED
+    assert fg(P, 0, P, P, 1, 256, 16, 16, 5, 16.0, P, P, P, ws, None) == nat.DXR_EUNSUPPORTED
+    assert fg(P, 0, P, P, 1, 256, 16, 16, 4, 16.0, P, P, P, ws - 1, None) == nat.DXR_EINVAL
+    assert fg(P, 0, P, P, 1, 256, 16, 16, 4, 16.0, P, P, None, ws, None) == nat.DXR_EINVAL
+    assert fg(None, 0, None, None, 0, 256, 16, 16, 4, 16.0, None, None, None, 0, None) == nat.DXR_OK
+    assert fg(P, 0, P, P, 1, 256, 16, 16, 4, 16.0, None, None, None, 0, None) == nat.DXR_OK

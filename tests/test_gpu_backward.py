@@ -1,0 +1,174 @@
+"""GPU parity of the fused fmap-gradient backward (``dxr_fmap_grads``).
+
+The reference trains through matmul -> / sqrt(D) -> avg_pool2d -> grid_sample
+(train.py:175-178, core/corr.py:13-27,52-60).  Given a gradient pyramid G (what
+the lookups' backwards leave), d fmap1 = F2 dV^T and d fmap2 = F1 dV with dV the
+pooling-chain fold of G / sqrt(D).  The check: ``dxr_fmap_grads`` (dV folded
+inside the MFMA operand loads, never stored) against ``dxr_pyramid_backward``
+(dV in HBM, itself pinned by the reference autograd goldens) followed by float64
+GEMMs, and against the same dV through float32 rocBLAS (the round-2 path): the
+fused GEMMs must be at least as close to float64 as float32 BLAS is (f32 class),
+and within 1e-5 of max|grad|.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+import datagen as dg
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def dx():
+    import dexiraft_amd
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    dexiraft_amd.load_native()
+    return dexiraft_amd
+
+
+def _nat():
+    from dexiraft_amd import _native
+    return _native
+
+
+def _grad_pyramid(nat, B, H, W, L, seed, nan_at=None):
+    """A paged gradient pyramid with N(0, 1) cells on every level (zero padding)."""
+    lib = nat.load()
+    numel = lib.dxr_pyramid_numel(B, H, W, L)
+    gp = torch.zeros(numel, dtype=torch.float32, device=DEV)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(seed)
+    h, w = H, W
+    for lvl in range(L):
+        if lvl:
+            h, w = h // 2, w // 2
+        ref = torch.randn((B * H * W, h, w), generator=g, device=DEV)
+        if lvl == 0 and nan_at is not None:
+            ref[nan_at] = float("nan")
+        st = lib.dxr_pyramid_pack(ref.data_ptr(), B, H, W, L, lvl, gp.data_ptr(), nat.DXR_F32,
+                                  nat.stream_of(ref))
+        nat.check(st, "pack")
+    return gp
+
+
+def _fused(nat, gp, f1, f2, L, div, want=(True, True)):
+    lib = nat.load()
+    B, D, H, W = f1.shape
+    wsb = lib.dxr_fmap_grads_workspace_bytes(B, D, H, W, L)
+    assert wsb > 0
+    ws = torch.empty(wsb, dtype=torch.uint8, device=DEV)
+    df1 = torch.full_like(f1, float("nan")) if want[0] else None
+    df2 = torch.full_like(f2, float("nan")) if want[1] else None
+    st = lib.dxr_fmap_grads(gp.data_ptr(), nat.DXR_F32, f1.data_ptr(), f2.data_ptr(), B, D, H, W,
+                            L, div, nat.ptr(df1), nat.ptr(df2), ws.data_ptr(), wsb,
+                            nat.stream_of(f1))
+    nat.check(st, "dxr_fmap_grads")
+    return df1, df2
+
+
+def _volume_grad(nat, gp, B, H, W, L, div):
+    lib = nat.load()
+    dv = torch.empty((B, H * W, H * W), dtype=torch.float32, device=DEV)
+    st = lib.dxr_pyramid_backward(gp.data_ptr(), nat.DXR_F32, B, H, W, L, div, dv.data_ptr(),
+                                  nat.stream_of(dv))
+    nat.check(st, "dxr_pyramid_backward")
+    return dv
+
+
+SHAPES = [
+    (1, 256, 55, 128, 4),   # Sintel (C2): K split in 4 chunks
+    (1, 256, 46, 62, 4),    # Chairs (C1): ragged tiles and query block
+    (2, 64, 23, 37, 3),
+    (1, 32, 9, 17, 1),      # one level, one ragged tile
+    (3, 96, 16, 16, 2),
+    (1, 512, 20, 30, 4),    # two 256-channel slabs
+    (6, 256, 55, 128, 4),   # 330 n blocks: no K split
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_fmap_grads_match_volume_gradient_gemms(dx, shape):
+    nat = _nat()
+    B, D, H, W, L = shape
+    f1 = torch.from_numpy(dg.fmap(900 + D, B, D, H, W, "fnet")).to(DEV)
+    f2 = torch.from_numpy(dg.fmap(901 + D, B, D, H, W, "fnet")).to(DEV)
+    div = float(np.sqrt(np.float32(D), dtype=np.float32))
+    gp = _grad_pyramid(nat, B, H, W, L, seed=B * 1000 + H)
+    g1, g2 = _fused(nat, gp, f1, f2, L, div)
+    dv = _volume_grad(nat, gp, B, H, W, L, div)
+    N = H * W
+    r1 = torch.bmm(f2.reshape(B, D, N).double(), dv.double().transpose(1, 2)).reshape(B, D, H, W)
+    r2 = torch.bmm(f1.reshape(B, D, N).double(), dv.double()).reshape(B, D, H, W)
+    b1 = torch.bmm(f2.reshape(B, D, N), dv.transpose(1, 2)).reshape(B, D, H, W)
+    b2 = torch.bmm(f1.reshape(B, D, N), dv).reshape(B, D, H, W)
+    del dv
+    for name, got, ref, blas in (("dfmap1", g1, r1, b1), ("dfmap2", g2, r2, b2)):
+        assert torch.isfinite(got).all(), name
+        scale = ref.abs().max().item()
+        err = (got.double() - ref).abs().max().item()
+        err_blas = (blas.double() - ref).abs().max().item()
+        print(f"{shape} {name}: max|err| {err:.3e} (f32 BLAS {err_blas:.3e}) of max {scale:.3e}")
+        assert err <= 1e-5 * scale
+        assert err <= 2 * err_blas + 1e-7 * scale
+
+
+def test_fmap_grads_deterministic_and_one_sided(dx):
+    """Same inputs -> bit-identical gradients; a NULL output is skipped and the
+    other is unchanged by it."""
+    nat = _nat()
+    B, D, H, W, L = 1, 128, 30, 44, 4
+    f1 = torch.from_numpy(dg.fmap(911, B, D, H, W)).to(DEV)
+    f2 = torch.from_numpy(dg.fmap(912, B, D, H, W)).to(DEV)
+    gp = _grad_pyramid(nat, B, H, W, L, seed=913)
+    a1, a2 = _fused(nat, gp, f1, f2, L, 11.3137)
+    b1, b2 = _fused(nat, gp, f1, f2, L, 11.3137)
+    assert torch.equal(a1, b1) and torch.equal(a2, b2)
+    c1, none2 = _fused(nat, gp, f1, f2, L, 11.3137, want=(True, False))
+    none1, c2 = _fused(nat, gp, f1, f2, L, 11.3137, want=(False, True))
+    assert none1 is None and none2 is None
+    assert torch.equal(a1, c1) and torch.equal(a2, c2)
+
+
+def test_fmap_grads_propagate_nan_like_the_gemms(dx):
+    """A NaN gradient cell poisons exactly the query's dfmap1 column and the
+    target's dfmap2 column, as the dense GEMMs do."""
+    nat = _nat()
+    B, D, H, W, L = 1, 64, 24, 40, 4
+    f1 = torch.from_numpy(dg.fmap(921, B, D, H, W)).to(DEV)
+    f2 = torch.from_numpy(dg.fmap(922, B, D, H, W)).to(DEV)
+    q, ty, tx = 37, 5, 17
+    gp = _grad_pyramid(nat, B, H, W, L, seed=923, nan_at=(q, ty, tx))
+    g1, g2 = _fused(nat, gp, f1, f2, L, 8.0)
+    dv = _volume_grad(nat, gp, B, H, W, L, 8.0)
+    r1 = torch.bmm(f2.reshape(B, D, -1), dv.transpose(1, 2)).reshape(B, D, H, W)
+    r2 = torch.bmm(f1.reshape(B, D, -1), dv).reshape(B, D, H, W)
+    assert torch.equal(torch.isnan(g1), torch.isnan(r1))
+    assert torch.equal(torch.isnan(g2), torch.isnan(r2))
+    assert torch.isnan(g1[0, :, q // W, q % W]).all() and torch.isnan(g2[0, :, ty, tx]).all()
+    assert torch.isnan(g1).sum().item() == D and torch.isnan(g2).sum().item() == D
+
+
+@pytest.mark.parametrize("D", [48, 64])
+def test_corr_block_backward_fused_and_fallback_agree_with_torch(dx, D):
+    """D = 64 takes dxr_fmap_grads, D = 48 the dV + rocBLAS fallback; both match
+    torch autograd of the PyTorch restatement (tests/torch_ref.py)."""
+    from torch_ref import TorchCorrBlock
+    B, H, W = 1, 20, 36
+    f1 = torch.from_numpy(dg.fmap(931, B, D, H, W, "fnet")).to(DEV)
+    f2 = torch.from_numpy(dg.fmap(932, B, D, H, W, "fnet")).to(DEV)
+    cs = [torch.from_numpy(dg.coords(933 + k, B, H, W, "normal", 3.0)).to(DEV) for k in range(4)]
+    ws = [torch.from_numpy(dg.fmap(940 + k, B, 4 * 81, H, W)).to(DEV) for k in range(4)]
+
+    def run(cls):
+        a1, a2 = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
+        cb = cls(a1, a2)
+        sum((cb(c) * w).sum() for c, w in zip(cs, ws)).backward()
+        return a1.grad, a2.grad
+
+    for got, ref in zip(run(dx.CorrBlock), run(TorchCorrBlock)):
+        assert (got - ref).abs().max().item() <= 1e-4 * ref.abs().max().item()
