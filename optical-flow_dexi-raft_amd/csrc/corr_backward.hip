@@ -14,15 +14,16 @@
 // Here a workgroup owns 256 channels x one n-block of 128 (a query block for
 // dF1, a level-0 target tile for dF2) and walks a chunk of k-blocks.  A k-block
 // is one page of each level: 128 queries x one 8 x 16 target tile (and its 4 x 8,
-// 2 x 4, 1 x 2 pooled tiles), all contiguous.  Per k-block the workgroup folds
-// the four pages into the dV tile, splits it three ways into bf16 (hi, mid, lo)
-// MFMA B-operand records in LDS, and runs 8 k-steps of v_mfma_f32_32x32x16_bf16
-// with six products (the f32-class split of dxr_common.h split8); the fmap
-// operand comes pre-split from a pack pass, one 1 KiB-contiguous record block
-// per wave and k-step.  The next k-block's pages are loaded into registers while
-// the MFMAs run.  Chunks of k-blocks (split K, so ~256 workgroups fill the chip)
-// write partial sums that a last pass adds in a fixed order: deterministic.
+// 2 x 4, 1 x 2 pooled tiles), all contiguous.  Four fold waves turn the pages,
+// half a k-block per stage, into the dV operand: folded, split three ways into
+// bf16 (hi, mid, lo) MFMA B-operand records in LDS, one stage ahead of eight
+// MFMA waves that run v_mfma_f32_32x32x16_bf16 with six products (the f32-class
+// split of dxr_common.h split8) against the fmap operand, which comes pre-split
+// from a pack pass, one 1 KiB-contiguous record block per wave and k-step.
+// Chunks of k-blocks (split K, so ~256 workgroups fill the chip) write partial
+// sums that a last pass adds in a fixed order: deterministic.
 #include <cmath>
+#include <type_traits>
 
 #include "dxr_common.h"
 
@@ -37,8 +38,11 @@ constexpr int TW = dxr::PAGE_W;           // level-0 tile cols
 constexpr int NB = 128;                   // n per workgroup
 constexpr int KSTEPS = 8;                 // 16-k steps per k-block (128)
 constexpr int DS = 256;                   // channels per workgroup (8 waves x 32)
-constexpr int NTHR = 512;
-constexpr int REC = KSTEPS * NB * 2;      // 16-B records per split part in LDS
+constexpr int MW = 8;                     // MFMA waves (32 channels each)
+constexpr int LW = 4;                     // fold waves
+constexpr int NTHR = (MW + LW) * 64;
+constexpr int HK = 4;                     // k-steps per stage (half a k-block)
+constexpr int REC = HK * NB * 2;          // 16-B records per split part per stage
 static_assert(PQ == NB && TH * TW == NB, "a k-block is one page");
 
 struct GradGeom {
@@ -69,6 +73,7 @@ __device__ __forceinline__ void page_bases(const GradGeom& g, int b, int qb, int
 
 // One dV element from its four level gradients (pyramid_backward_kernel's order:
 // from the coarsest level down, t = g_l + t/4; masked levels contribute 0).
+template <bool DIV>
 __device__ __forceinline__ float fold(const GradGeom& g, int y, int x, bool qok, float g0, float g1,
                                       float g2, float g3) {
   float t = 0.f;
@@ -76,12 +81,13 @@ __device__ __forceinline__ float fold(const GradGeom& g, int y, int x, bool qok,
   if (g.nlev > 2) t = (((y >> 2) < g.lh[2] && (x >> 2) < g.lw[2]) ? g2 : 0.f) + 0.25f * t;
   if (g.nlev > 1) t = (((y >> 1) < g.lh[1] && (x >> 1) < g.lw[1]) ? g1 : 0.f) + 0.25f * t;
   t = ((y < g.H && x < g.W && qok) ? g0 : 0.f) + 0.25f * t;
-  return g.recip != 0.f ? t * g.recip : t / g.divisor;
+  return DIV ? t / g.divisor : t * g.recip;
 }
 
-// Raw page values one thread folds.  KT (dF1, n = query, k = target): thread
-// (query tid&127, tile rows 2(tid>>7), +1, all 16 cols).  !KT (dF2, n = target,
-// k = query): thread (8 queries 8(tid>>5).., 4 targets 4(tid&31)..).
+// Raw page values one fold thread (lt = 0..255) folds for a stage (half a
+// k-block).  KT (dF1, n = query, k = target): query lt&127, tile rows
+// 4*half + 2(lt>>7), +1, all 16 cols.  !KT (dF2, n = target, k = query): queries
+// 64*half + 8(lt>>5).. +7, targets 4(lt&31).. +3.
 template <bool KT>
 struct Raw;
 
@@ -103,12 +109,11 @@ struct Raw<false> {
 
 template <bool KT>
 __device__ __forceinline__ void load_raw(const GradGeom& g, const float* __restrict__ gp, int b,
-                                         int qb, int tile, Raw<KT>& r) {
-  const int tid = threadIdx.x;
+                                         int qb, int tile, int half, int lt, Raw<KT>& r) {
   long long base[4];
   page_bases(g, b, qb, tile / g.txn, tile % g.txn, base);
   if constexpr (KT) {
-    const int q = tid & 127, k = tid >> 7;
+    const int q = lt & 127, k = 2 * half + (lt >> 7);   // level-1 row of the pair of rows
     const float* p0 = gp + base[0] + q * 128 + k * 32;
 #pragma unroll
     for (int i = 0; i < 8; ++i) r.g0[i] = ld4(p0 + 4 * i);
@@ -120,14 +125,14 @@ __device__ __forceinline__ void load_raw(const GradGeom& g, const float* __restr
       r.g1[0] = ld4(p1);
       r.g1[1] = ld4(p1 + 4);
     }
-    if (g.nlev > 2) r.g2 = ld4(gp + base[2] + q * 8 + (k >> 1) * 4);
+    if (g.nlev > 2) r.g2 = ld4(gp + base[2] + q * 8 + half * 4);
     if (g.nlev > 3) {
       const float2 v = *reinterpret_cast<const float2*>(gp + base[3] + q * 2);
       r.g3[0] = v.x;
       r.g3[1] = v.y;
     }
   } else {
-    const int tg = tid & 31, q0 = (tid >> 5) * 8, rr = tg >> 2, cq = tg & 3;
+    const int tg = lt & 31, q0 = 64 * half + (lt >> 5) * 8, rr = tg >> 2, cq = tg & 3;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int q = q0 + i;
@@ -149,55 +154,104 @@ __device__ __forceinline__ float comp(const uint4& v, int e) {
   return u2f(e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w);
 }
 
-// Fold the raw values of k-block (qb, tile) into dV, split, write the LDS records
-// (part p, k-step s, n, half h) at sb[((p*8 + s)*128 + n)*2 + h].
-template <bool KT>
+// Is every cell of k-block (qb, tile) inside every level (no floor-mode mask,
+// no padding query)?  Then the fold needs no masks, and the coarse levels fold
+// once per level-1 cell instead of once per dV element.
+__device__ __forceinline__ bool interior(const GradGeom& g, int qb, int tile) {
+  const int y1 = (tile / g.txn) * TH + TH - 1, x1 = (tile % g.txn) * TW + TW - 1;
+  bool in = (qb + 1) * PQ <= g.N && y1 < g.H && x1 < g.W;
+#pragma unroll
+  for (int l = 1; l < 4; ++l)
+    if (l < g.nlev) in = in && (y1 >> l) < g.lh[l] && (x1 >> l) < g.lw[l];
+  return in;
+}
+
+__device__ __forceinline__ void store_split(const float (&v)[8], int rec, uint4* __restrict__ sb) {
+  uint4 hi, mi, lo;
+  dxr::split8(v, hi, mi, lo);
+  sb[rec] = hi;
+  sb[REC + rec] = mi;
+  sb[2 * REC + rec] = lo;
+}
+
+// Fold a stage's raw values into dV, split, write the stage's LDS records
+// (part p, k-step s of the stage, half h of the k-step, n) at
+// sb[p*REC + (s*2 + h)*128 + n]: an MFMA operand read is two 512-B runs and a
+// fold thread's store is lane-contiguous, both free of bank conflicts
+// (the [n][h] order, 32-B lane stride, spent half the LDS cycles in conflicts).  Interior k-blocks: the same arithmetic in the
+// same order (levels absent beyond nlev were loaded as 0, and x + 0.25*0 = x).
+template <bool KT, bool DIV>
 __device__ __forceinline__ void fold_store(const GradGeom& g, const Raw<KT>& r, int qb, int tile,
-                                           uint4* __restrict__ sb) {
-  const int tid = threadIdx.x;
+                                           int half, int lt, uint4* __restrict__ sb) {
   const int y0 = (tile / g.txn) * TH, x0 = (tile % g.txn) * TW;
+  const bool inner = interior(g, qb, tile);
+  auto scale = [&](float t) { return DIV ? t / g.divisor : t * g.recip; };
   if constexpr (KT) {
-    const int q = tid & 127, k = tid >> 7;
+    const int q = lt & 127, k = lt >> 7;
     const bool qok = qb * PQ + q < g.N;
+    float p1[8];  // this thread's level-1 row, coarser levels folded in
 #pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
-      const int y = y0 + 2 * k + rr;
+    for (int c1 = 0; c1 < 8; ++c1) {
+      const float p2 = comp(r.g2, c1 >> 1) + 0.25f * r.g3[c1 >> 2];
+      p1[c1] = comp(r.g1[c1 >> 2], c1 & 3) + 0.25f * p2;
+    }
+    auto body = [&](auto in_c) {
+      constexpr bool IN = decltype(in_c)::value;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int rr = 0; rr < 2; ++rr) {
+        const int y = y0 + 4 * half + 2 * k + rr;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int c = 8 * h + e, i = rr * 16 + c;
+            if constexpr (IN)
+              v[e] = scale(comp(r.g0[i >> 2], i & 3) + 0.25f * p1[c >> 1]);
+            else
+              v[e] = fold<DIV>(g, y, x0 + c, qok, comp(r.g0[i >> 2], i & 3),
+                               comp(r.g1[c >> 3], (c >> 1) & 3), comp(r.g2, c >> 2), r.g3[c >> 3]);
+          }
+          store_split(v, ((2 * k + rr) * 2 + h) * NB + q, sb);
+        }
+      }
+    };
+    if (inner)
+      body(std::true_type{});
+    else
+      body(std::false_type{});
+  } else {
+    const int tg = lt & 31, qg = lt >> 5, rr = tg >> 2, cq = tg & 3;
+    const int y = y0 + rr;
+    float p1[8][2];  // per query: its two level-1 cells, coarser levels folded in
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float p2 = r.g2[i] + 0.25f * r.g3[i];
+      p1[i][0] = r.g1[i][0] + 0.25f * p2;
+      p1[i][1] = r.g1[i][1] + 0.25f * p2;
+    }
+    auto body = [&](auto in_c) {
+      constexpr bool IN = decltype(in_c)::value;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = 4 * cq + j;
         float v[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int c = 8 * h + e, i = rr * 16 + c;
-          v[e] = fold(g, y, x0 + c, qok, comp(r.g0[i >> 2], i & 3), comp(r.g1[c >> 3], (c >> 1) & 3),
-                      comp(r.g2, c >> 2), r.g3[c >> 3]);
+        for (int i = 0; i < 8; ++i) {
+          if constexpr (IN) {
+            v[i] = scale(comp(r.g0[i], j) + 0.25f * p1[i][j >> 1]);
+          } else {
+            const bool qok = qb * PQ + 64 * half + qg * 8 + i < g.N;
+            v[i] = fold<DIV>(g, y, x0 + c, qok, comp(r.g0[i], j), r.g1[i][j >> 1], r.g2[i], r.g3[i]);
+          }
         }
-        uint4 hi, mi, lo;
-        dxr::split8(v, hi, mi, lo);
-        const int rec = ((2 * k + rr) * NB + q) * 2 + h;
-        sb[rec] = hi;
-        sb[REC + rec] = mi;
-        sb[2 * REC + rec] = lo;
+        store_split(v, qg * NB + j * 32 + tg, sb);
       }
-    }
-  } else {
-    const int tg = tid & 31, qg = tid >> 5, rr = tg >> 2, cq = tg & 3;
-    const int y = y0 + rr;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = 4 * cq + j;
-      float v[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const bool qok = qb * PQ + qg * 8 + i < g.N;
-        v[i] = fold(g, y, x0 + c, qok, comp(r.g0[i], j), r.g1[i][j >> 1], r.g2[i], r.g3[i]);
-      }
-      uint4 hi, mi, lo;
-      dxr::split8(v, hi, mi, lo);
-      const int rec = ((qg >> 1) * NB + j * 32 + tg) * 2 + (qg & 1);
-      sb[rec] = hi;
-      sb[REC + rec] = mi;
-      sb[2 * REC + rec] = lo;
-    }
+    };
+    if (inner)
+      body(std::true_type{});
+    else
+      body(std::false_type{});
   }
 }
 
@@ -209,11 +263,18 @@ __device__ __forceinline__ long long xcd_linear(long long w, long long nwg) {
   return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + w / 8;
 }
 
-template <bool KT>
+// Warp-specialised: LW fold waves turn gradient pages into dV operand stages
+// (two LDS buffers, one stage ahead), MW MFMA waves stream the fmap operand
+// from L2 and multiply.  The fold waves' page loads never sit in front of the
+// MFMA waves' operand loads in a vmcnt queue, and their VALU work overlaps the
+// MFMAs.  One barrier per stage: at barrier st the fold waves have published
+// stage st and the MFMA waves have finished stage st-1, whose buffer the fold
+// waves fill next.
+template <bool KT, bool DIV>
 __global__ __launch_bounds__(NTHR) void fmap_grad_kernel(const float* __restrict__ gp,
                                                          const uint4* __restrict__ fp,
                                                          float* __restrict__ out, GradGeom g) {
-  __shared__ uint4 sb[3 * REC];
+  __shared__ uint4 sb[2][3 * REC];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   long long wl = xcd_linear(blockIdx.x, gridDim.x);
   const int nb = (int)(wl % g.nblk);
@@ -224,9 +285,45 @@ __global__ __launch_bounds__(NTHR) void fmap_grad_kernel(const float* __restrict
   const int b = (int)(wl / g.nslab);
   const int kb0 = (int)((long long)chunk * g.kbt / g.S);
   const int kb1 = (int)((long long)(chunk + 1) * g.kbt / g.S);
+  const int nst = 2 * (kb1 - kb0);
+
+  if (wave >= MW) {  // fold waves
+    // KT: two register sets, stage st+1's pages are in flight while stage st
+    // folds and the MFMA waves finish stage st-1 (stage st = k-block kb0 + st/2,
+    // half st%2)
+    const int lt = tid - MW * 64;
+    auto load = [&](int st, Raw<KT>& r) {
+      const int kb = kb0 + (st >> 1);
+      load_raw<KT>(g, gp, b, KT ? nb : kb, KT ? kb : nb, st & 1, lt, r);
+    };
+    auto fold = [&](int st, const Raw<KT>& r) {
+      const int kb = kb0 + (st >> 1);
+      fold_store<KT, DIV>(g, r, KT ? nb : kb, KT ? kb : nb, st & 1, lt, sb[st & 1]);
+    };
+    Raw<KT> r0;
+    if (nst > 0) load(0, r0);
+    if constexpr (KT) {
+      Raw<KT> r1;
+      for (int st = 0; st < nst; st += 2) {  // nst is even
+        load(st + 1, r1);
+        fold(st, r0);
+        __syncthreads();
+        if (st + 2 < nst) load(st + 2, r0);
+        fold(st + 1, r1);
+        __syncthreads();
+      }
+    } else {  // 64 raw values a thread: one set (two would spill)
+      for (int st = 0; st < nst; ++st) {
+        fold(st, r0);
+        if (st + 1 < nst) load(st + 1, r0);
+        __syncthreads();
+      }
+    }
+    return;
+  }
+
   const int d0 = slab * DS + wave * 32;
   const bool active = d0 < g.D;  // D % 32 == 0: whole waves
-
   f32x16 acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -235,48 +332,54 @@ __global__ __launch_bounds__(NTHR) void fmap_grad_kernel(const float* __restrict
 
   // fmap operand records: (((b*3 + p)*ks + k-step)*D + d)*2 + half
   const long long pstride = g.ks * g.D * 2, kstride = (long long)g.D * 2;
-  const uint4* fa = fp + (long long)b * 3 * pstride + (long long)(d0 + (lane & 31)) * 2 + (lane >> 5);
-  const uint4* bl = sb + (lane & 31) * 2 + (lane >> 5);
-
-  Raw<KT> raw;
-  if (kb0 < kb1) load_raw<KT>(g, gp, b, KT ? nb : kb0, KT ? kb0 : nb, raw);
-  for (int kb = kb0; kb < kb1; ++kb) {
-    const int qb = KT ? nb : kb, tile = KT ? kb : nb;
-    __syncthreads();  // the previous k-block's operand reads are done
-    fold_store<KT>(g, raw, qb, tile, sb);
-    __syncthreads();
-    if (kb + 1 < kb1) load_raw<KT>(g, gp, b, KT ? nb : kb + 1, KT ? kb + 1 : nb, raw);
-    if (active) {
-      const uint4* fk = fa + (long long)kb * KSTEPS * kstride;
-      uint4 ah = fk[0], am = fk[pstride], al = fk[2 * pstride];
-#pragma unroll 1
-      for (int s = 0; s < KSTEPS; ++s) {
-        uint4 nh = ah, nm = am, nl = al;
-        if (s + 1 < KSTEPS) {
-          const uint4* fn = fk + (s + 1) * kstride;
-          nh = fn[0];
-          nm = fn[pstride];
-          nl = fn[2 * pstride];
-        }
-        const bf8v qh = __builtin_bit_cast(bf8v, ah), qm = __builtin_bit_cast(bf8v, am),
-                   ql = __builtin_bit_cast(bf8v, al);
+  const uint4* fa = fp + (long long)b * 3 * pstride + (long long)(d0 + (lane & 31)) * 2 +
+                    (lane >> 5) + (long long)kb0 * KSTEPS * kstride;
+  const int bl = (lane >> 5) * NB + (lane & 31);
+  // fmap operand: a stage's four k-steps in registers; each k-step's slot is
+  // reloaded with the next stage's k-step as soon as its MFMAs have issued (a
+  // stage of cover; no register rotation, so no wait for a load in flight)
+  uint4 A[HK][3];
+  auto load_a = [&](int st, int s, uint4 (&a)[3]) {
+    const uint4* f = fa + (long long)(st * HK + s) * kstride;
+    a[0] = f[0];
+    a[1] = f[pstride];
+    a[2] = f[2 * pstride];
+  };
+  if (active && nst > 0) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint4* bp = bl + (s * NB + 32 * j) * 2;
-          const bf8v th = __builtin_bit_cast(bf8v, bp[0]), tm = __builtin_bit_cast(bf8v, bp[REC]),
-                     tl = __builtin_bit_cast(bf8v, bp[2 * REC]);
-          // small terms first
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, tm, acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ql, th, acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, tl, acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, th, acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, tm, acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, th, acc[j], 0, 0, 0);
-        }
-        ah = nh;
-        am = nm;
-        al = nl;
+    for (int s = 0; s < HK; ++s) load_a(0, s, A[s]);
+  }
+  for (int st = 0; st < nst; ++st) {
+    __syncthreads();  // stage st published
+    if (!active) continue;
+    const uint4* sp = sb[st & 1] + bl;
+#pragma unroll
+    for (int s = 0; s < HK; ++s) {
+      const bf8v qh = __builtin_bit_cast(bf8v, A[s][0]), qm = __builtin_bit_cast(bf8v, A[s][1]),
+                 ql = __builtin_bit_cast(bf8v, A[s][2]);
+      bf8v th[4], tm[4], tl[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint4* bp = sp + s * 2 * NB + 32 * j;
+        th[j] = __builtin_bit_cast(bf8v, bp[0]);
+        tm[j] = __builtin_bit_cast(bf8v, bp[REC]);
+        tl[j] = __builtin_bit_cast(bf8v, bp[2 * REC]);
       }
+      // per accumulator small terms first; the four tiles interleaved so no
+      // MFMA waits on the one before it
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, tm[j], acc[j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ql, th[j], acc[j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, tl[j], acc[j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, th[j], acc[j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, tm[j], acc[j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, th[j], acc[j], 0, 0, 0);
+      if (st + 1 < nst) load_a(st + 1, s, A[s]);
     }
   }
   if (!active) return;
@@ -442,16 +545,20 @@ extern "C" int dxr_fmap_grads(const void* grad_pyramid, int grad_dtype, const fl
     float* part = g.S > 1 ? reinterpret_cast<float*>(static_cast<char*>(workspace) + operand_bytes(g))
                           : dst;
     const long long nwg = (long long)g.nblk * g.S * g.nslab * g.B;
+    const dim3 pg(grid_for(g.B * g.ks * g.D * 2)), gg((unsigned)nwg);
+    const bool div = g.recip == 0.f;
     if (kt) {
-      hipLaunchKernelGGL(fmap_split_kernel<true>, dim3(grid_for(g.B * g.ks * g.D * 2)), dim3(256), 0,
-                         stream, src, fp, g);
-      hipLaunchKernelGGL(fmap_grad_kernel<true>, dim3((unsigned)nwg), dim3(NTHR), 0, stream, gp, fp,
-                         part, g);
+      hipLaunchKernelGGL(fmap_split_kernel<true>, pg, dim3(256), 0, stream, src, fp, g);
+      if (div)
+        hipLaunchKernelGGL((fmap_grad_kernel<true, true>), gg, dim3(NTHR), 0, stream, gp, fp, part, g);
+      else
+        hipLaunchKernelGGL((fmap_grad_kernel<true, false>), gg, dim3(NTHR), 0, stream, gp, fp, part, g);
     } else {
-      hipLaunchKernelGGL(fmap_split_kernel<false>, dim3(grid_for(g.B * g.ks * g.D * 2)), dim3(256), 0,
-                         stream, src, fp, g);
-      hipLaunchKernelGGL(fmap_grad_kernel<false>, dim3((unsigned)nwg), dim3(NTHR), 0, stream, gp, fp,
-                         part, g);
+      hipLaunchKernelGGL(fmap_split_kernel<false>, pg, dim3(256), 0, stream, src, fp, g);
+      if (div)
+        hipLaunchKernelGGL((fmap_grad_kernel<false, true>), gg, dim3(NTHR), 0, stream, gp, fp, part, g);
+      else
+        hipLaunchKernelGGL((fmap_grad_kernel<false, false>), gg, dim3(NTHR), 0, stream, gp, fp, part, g);
     }
     if (g.S > 1) {
       const long long n = (long long)g.B * g.D * g.N;
