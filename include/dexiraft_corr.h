@@ -20,7 +20,8 @@
  *                            core/utils/utils.py:57-71 bilinear_sampler
  *                            (F.grid_sample, align_corners=True, zero padding)
  *   dxr_corr_lookup_backward core/utils/utils.py:65 grid_sample backward
- *                            (autograd of CorrBlock.__call__, train.py:175-178)
+ *                            (autograd of CorrBlock.__call__, train.py:175-178);
+ *                            _multi: several lookups' backwards in one launch
  *   dxr_pyramid_backward     core/corr.py:25-27,58-60 avg_pool2d + division
  *                            backward (autograd of CorrBlock.__init__)
  *   dxr_fmap_grads           core/corr.py:13-27,52-60 the whole CorrBlock.__init__
@@ -228,6 +229,17 @@ int dxr_corr_lookup_backward(const float* coords, const float* grad_out,
                              int64_t B, int64_t H, int64_t W, int num_levels,
                              int radius, void* grad_pyramid, int grad_dtype,
                              hipStream_t stream);
+
+/*
+ * The same for n_sets lookups of one block at once (coords[i], grad_out[i]),
+ * added in the order given — the result equals n_sets single calls in that
+ * order bit for bit — in one launch, so each workgroup's window lines stay in
+ * L2 across the sets.  n_sets <= 16 (more: DXR_EUNSUPPORTED).
+ */
+int dxr_corr_lookup_backward_multi(const float* const* coords, const float* const* grad_out,
+                                   int n_sets, int64_t B, int64_t H, int64_t W,
+                                   int num_levels, int radius, void* grad_pyramid,
+                                   int grad_dtype, hipStream_t stream);
 
 /*
  * Stage (c) fused with the motion encoder's 1x1 convolution (SURVEY.md §8(f)

@@ -44,6 +44,8 @@ SIGNATURES: dict[str, tuple[object, list[object]]] = {
     "dxr_corr_lookup": (_int, [_vp, _int, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp]),
     "dxr_avg_pool2x2": (_int, [_vp, _vp, _i64, _i64, _i64, _vp]),
     "dxr_corr_lookup_backward": (_int, [_vp, _vp, _i64, _i64, _i64, _int, _int, _vp, _int, _vp]),
+    "dxr_corr_lookup_backward_multi": (_int, [ctypes.POINTER(_vp), ctypes.POINTER(_vp), _int, _i64,
+                                              _i64, _i64, _int, _int, _vp, _int, _vp]),
     "dxr_pyramid_backward": (_int, [_vp, _int, _i64, _i64, _i64, _int, _f32, _vp, _vp]),
     "dxr_fmap_grads_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64, _int]),
     "dxr_fmap_grads": (_int, [_vp, _int, _vp, _vp, _i64, _i64, _i64, _i64, _int, _f32, _vp, _vp,

@@ -11,8 +11,8 @@ Training: with float32 fmaps that require grad (under grad mode), the block is
 differentiable with respect to the fmaps, as the reference is through matmul /
 avg_pool2d / grid_sample (train.py:175-178).  Each lookup's backward adds its
 bilinear transpose into one gradient pyramid owned by the block
-(``dxr_corr_lookup_backward``); the build's backward runs once after all of
-them and takes the fmap gradients as two MFMA GEMMs that fold that pyramid down
+(``dxr_corr_lookup_backward_multi``, a few lookups per launch); the build's
+backward runs once after all of them and takes the fmap gradients as two MFMA GEMMs that fold that pyramid down
 the pooling chain in their operand loads (``dxr_fmap_grads``: no [B, N, N]
 volume gradient).  Shapes it does not cover (D % 32 != 0, more than 4 levels)
 form dV (``dxr_pyramid_backward``) and run two torch.bmm (rocBLAS).
@@ -82,12 +82,38 @@ class _GradState:
     so no reference cycle keeps the pyramid (``block._buf``) or the gradient
     pyramid alive after the step: both are freed by refcount."""
 
-    __slots__ = ("geom", "num_levels", "radius", "device", "numel", "grad_pyr")
+    __slots__ = ("geom", "num_levels", "radius", "device", "numel", "grad_pyr", "pending")
 
     def __init__(self, geom, num_levels, radius, device, numel):
         self.geom, self.num_levels, self.radius = geom, num_levels, radius
         self.device, self.numel = device, numel
         self.grad_pyr = None
+        self.pending = []   # (coords, grad_out) of lookups whose backward is not applied yet
+
+    def flush(self):
+        """Add the pending lookups' backwards into the gradient pyramid, in the
+        order autograd delivered them, with one launch per _BW_SETS lookups
+        (dxr_corr_lookup_backward_multi: bit-identical to one launch each)."""
+        if not self.pending:
+            return
+        if self.grad_pyr is None:
+            self.grad_pyr = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        B, D, H, W = self.geom
+        n = len(self.pending)
+        cs = (ctypes.c_void_p * n)(*[c.data_ptr() for c, _ in self.pending])
+        gs = (ctypes.c_void_p * n)(*[g.data_ptr() for _, g in self.pending])
+        lib = nat.load()
+        with _Launch(self.device):
+            st = lib.dxr_corr_lookup_backward_multi(cs, gs, n, B, H, W, self.num_levels, self.radius,
+                                                    self.grad_pyr.data_ptr(), nat.DXR_F32,
+                                                    nat.stream_of(self.grad_pyr))
+        nat.check(st, "CorrBlock lookup backward (dxr_corr_lookup_backward_multi)")
+        self.pending = []
+
+
+# Lookup backwards applied per launch: their window lines stay in L2 across the
+# sets; the pending grad_out tensors ([B, L*(2r+1)^2, H, W] each) live until then.
+_BW_SETS = 4
 
 
 class _BuildGrad(torch.autograd.Function):
@@ -104,6 +130,7 @@ class _BuildGrad(torch.autograd.Function):
     @staticmethod
     def backward(ctx, _gtoken):
         gs = ctx.gs
+        gs.flush()
         gp, gs.grad_pyr = gs.grad_pyr, None
         if gp is None:
             return None, None, None
@@ -149,16 +176,9 @@ class _LookupGrad(torch.autograd.Function):
     def backward(ctx, gout):
         gs = ctx.gs
         (coords,) = ctx.saved_tensors
-        B, D, H, W = gs.geom
-        if gs.grad_pyr is None:
-            gs.grad_pyr = torch.zeros(gs.numel, dtype=torch.float32, device=gs.device)
-        g = gout.contiguous().float()
-        lib = nat.load()
-        with _Launch(gs.device):
-            st = lib.dxr_corr_lookup_backward(coords.data_ptr(), g.data_ptr(), B, H, W,
-                                              gs.num_levels, gs.radius, gs.grad_pyr.data_ptr(),
-                                              nat.DXR_F32, nat.stream_of(g))
-        nat.check(st, "CorrBlock lookup backward (dxr_corr_lookup_backward)")
+        gs.pending.append((coords, gout.contiguous().float()))
+        if len(gs.pending) >= _BW_SETS:
+            gs.flush()
         return gout.new_zeros(()), None, None
 
 

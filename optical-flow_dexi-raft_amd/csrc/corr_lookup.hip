@@ -355,9 +355,19 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
 // a deterministic order (no LDS atomics).  Taps off the level get no gradient
 // (zero padding); far and non-finite queries contribute nothing.
 // ---------------------------------------------------------------------------
+// Several lookups' backwards in one launch (round 3): a workgroup applies the
+// sets in the given order, one read-modify-write pass each, so the result is
+// the one-set launches' bit for bit; its window lines stay in L2 between passes
+// instead of making a round trip to HBM per lookup.
+constexpr int BW_MAX_SETS = 16;
+struct BwSets {
+  const float* coords[BW_MAX_SETS];
+  const float* gout[BW_MAX_SETS];
+  int n;
+};
+
 template <int R>
-__global__ __launch_bounds__(512) void corr_lookup_backward_kernel(const float* __restrict__ coords,
-                                                                   const float* __restrict__ gout,
+__global__ __launch_bounds__(512) void corr_lookup_backward_kernel(BwSets sets,
                                                                    float* __restrict__ gpyr,
                                                                    LookupGeom g) {
   using C = WideCfg<R, 512>;
@@ -372,6 +382,21 @@ __global__ __launch_bounds__(512) void corr_lookup_backward_kernel(const float* 
   const int l = blockIdx.y, b = blockIdx.z;
   const int q0 = blockIdx.x * QB;
   const LevelAddr A = g.lv[l];
+  for (int set = 0; set < sets.n; ++set) {
+  if (set > 0) {
+    // the previous pass's stores are complete before any wave of the workgroup
+    // reads them back (one CU, one L1: workgroup scope; an agent-scope fence
+    // writes the XCD's L2 back and cost 5x the kernel)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+  const float* __restrict__ coords = sets.coords[set];
+  const float* __restrict__ gout = sets.gout[set];
+  // thread-index arithmetic stays inside the pass (hoisted out of the set loop
+  // it would hold ~100 VGPRs across passes and halve the resident workgroups)
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
   wide_phase0<R, 512>(coords, g, A, b, l, q0, tid, xs, ys, org);
   for (int i = tid; i < K * QB; i += NT) {
     const int k = i / QB, qq = i - k * QB, q = q0 + qq;
@@ -451,15 +476,15 @@ __global__ __launch_bounds__(512) void corr_lookup_backward_kernel(const float* 
 #pragma unroll
   for (int i = 0; i < ITER; ++i)
     if (okv[i]) base[offv[i]] = old[i] + accv[i];
+  }
 }
 
 template <int R>
-int launch_lookup_backward_r(const float* coords, const float* gout, float* gpyr,
-                             const LookupGeom& g, int B, hipStream_t stream) {
+int launch_lookup_backward_r(const BwSets& sets, float* gpyr, const LookupGeom& g, int B,
+                             hipStream_t stream) {
   using W = WideCfg<R, 512>;
   const dim3 grid((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
-  hipLaunchKernelGGL((corr_lookup_backward_kernel<R>), grid, dim3(512), 0, stream, coords, gout,
-                     gpyr, g);
+  hipLaunchKernelGGL((corr_lookup_backward_kernel<R>), grid, dim3(512), 0, stream, sets, gpyr, g);
   return dxr::launch_status();
 }
 
@@ -858,17 +883,19 @@ extern "C" int dxr_corr_lookup(const void* pyramid, int pyr_dtype, int64_t B, in
   return DXR_EINVAL;
 }
 
-extern "C" int dxr_corr_lookup_backward(const float* coords, const float* grad_out, int64_t B,
-                                        int64_t H, int64_t W, int num_levels, int radius,
-                                        void* grad_pyramid, int grad_dtype, hipStream_t stream) {
+namespace {
+int lookup_backward(const BwSets& sets, int64_t B, int64_t H, int64_t W, int num_levels, int radius,
+                    void* grad_pyramid, int grad_dtype, hipStream_t stream) {
   dxr::Levels L;
   if (!dxr::make_levels(B, H, W, num_levels, &L)) return DXR_EINVAL;
   if (radius < 0) return DXR_EINVAL;
   if (radius > 8) return DXR_EUNSUPPORTED;
   if (grad_dtype != DXR_F32) return grad_dtype == DXR_BF16 ? DXR_EUNSUPPORTED : DXR_EINVAL;
   if (B > 65535 || H * W > (1LL << 30)) return DXR_EINVAL;
-  if (B == 0) return DXR_OK;
-  if (!coords || !grad_out || !grad_pyramid) return DXR_EINVAL;
+  if (B == 0 || sets.n == 0) return DXR_OK;
+  if (!grad_pyramid) return DXR_EINVAL;
+  for (int i = 0; i < sets.n; ++i)
+    if (!sets.coords[i] || !sets.gout[i]) return DXR_EINVAL;
   const int rd = 2 * radius + 1;
   LookupGeom g;
   g.N = (int)(H * W);
@@ -877,16 +904,43 @@ extern "C" int dxr_corr_lookup_backward(const float* coords, const float* grad_o
   for (int l = 0; l < L.n; ++l) g.lv[l] = level_addr(L.lay[l]);
   float* gp = static_cast<float*>(grad_pyramid);
   switch (radius) {
-    case 0: return launch_lookup_backward_r<0>(coords, grad_out, gp, g, (int)B, stream);
-    case 1: return launch_lookup_backward_r<1>(coords, grad_out, gp, g, (int)B, stream);
-    case 2: return launch_lookup_backward_r<2>(coords, grad_out, gp, g, (int)B, stream);
-    case 3: return launch_lookup_backward_r<3>(coords, grad_out, gp, g, (int)B, stream);
-    case 4: return launch_lookup_backward_r<4>(coords, grad_out, gp, g, (int)B, stream);
-    case 5: return launch_lookup_backward_r<5>(coords, grad_out, gp, g, (int)B, stream);
-    case 6: return launch_lookup_backward_r<6>(coords, grad_out, gp, g, (int)B, stream);
-    case 7: return launch_lookup_backward_r<7>(coords, grad_out, gp, g, (int)B, stream);
-    default: return launch_lookup_backward_r<8>(coords, grad_out, gp, g, (int)B, stream);
+    case 0: return launch_lookup_backward_r<0>(sets, gp, g, (int)B, stream);
+    case 1: return launch_lookup_backward_r<1>(sets, gp, g, (int)B, stream);
+    case 2: return launch_lookup_backward_r<2>(sets, gp, g, (int)B, stream);
+    case 3: return launch_lookup_backward_r<3>(sets, gp, g, (int)B, stream);
+    case 4: return launch_lookup_backward_r<4>(sets, gp, g, (int)B, stream);
+    case 5: return launch_lookup_backward_r<5>(sets, gp, g, (int)B, stream);
+    case 6: return launch_lookup_backward_r<6>(sets, gp, g, (int)B, stream);
+    case 7: return launch_lookup_backward_r<7>(sets, gp, g, (int)B, stream);
+    default: return launch_lookup_backward_r<8>(sets, gp, g, (int)B, stream);
   }
+}
+}  // namespace
+
+extern "C" int dxr_corr_lookup_backward(const float* coords, const float* grad_out, int64_t B,
+                                        int64_t H, int64_t W, int num_levels, int radius,
+                                        void* grad_pyramid, int grad_dtype, hipStream_t stream) {
+  BwSets sets{};
+  sets.coords[0] = coords;
+  sets.gout[0] = grad_out;
+  sets.n = 1;
+  return lookup_backward(sets, B, H, W, num_levels, radius, grad_pyramid, grad_dtype, stream);
+}
+
+extern "C" int dxr_corr_lookup_backward_multi(const float* const* coords, const float* const* grad_out,
+                                              int n_sets, int64_t B, int64_t H, int64_t W,
+                                              int num_levels, int radius, void* grad_pyramid,
+                                              int grad_dtype, hipStream_t stream) {
+  if (n_sets < 0) return DXR_EINVAL;
+  if (n_sets > BW_MAX_SETS) return DXR_EUNSUPPORTED;
+  if (n_sets > 0 && (!coords || !grad_out)) return DXR_EINVAL;
+  BwSets sets{};
+  for (int i = 0; i < n_sets; ++i) {
+    sets.coords[i] = coords[i];
+    sets.gout[i] = grad_out[i];
+  }
+  sets.n = n_sets;
+  return lookup_backward(sets, B, H, W, num_levels, radius, grad_pyramid, grad_dtype, stream);
 }
 
 extern "C" int64_t dxr_conv1x1_packed_bytes(int64_t cout, int64_t cin) {

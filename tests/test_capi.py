@@ -43,7 +43,8 @@ def test_header_declares_the_documented_entry_points():
         "dxr_corr_lookup_backward", "dxr_pyramid_backward", "dxr_alt_corr_backward",
         "dxr_conv1x1_packed_bytes", "dxr_conv1x1_pack_weight", "dxr_corr_lookup_conv1x1",
         "dxr_transpose", "dxr_avg_pool2x2_nhwc", "dxr_alt_workspace_bytes",
-        "dxr_alt_corr_lookup_ws", "dxr_fmap_grads_workspace_bytes", "dxr_fmap_grads"}
+        "dxr_alt_corr_lookup_ws", "dxr_fmap_grads_workspace_bytes", "dxr_fmap_grads",
+        "dxr_corr_lookup_backward_multi"}
 
 
 def test_library_exports_every_declared_symbol(nat):
@@ -277,3 +278,18 @@ def test_fmap_grads_workspace_and_validation(nat):
     assert fg(P, 0, P, P, 1, 256, 16, 16, 4, 16.0, P, P, None, ws, None) == nat.DXR_EINVAL
     assert fg(None, 0, None, None, 0, 256, 16, 16, 4, 16.0, None, None, None, 0, None) == nat.DXR_OK
     assert fg(P, 0, P, P, 1, 256, 16, 16, 4, 16.0, None, None, None, 0, None) == nat.DXR_OK
+
+
+def test_lookup_backward_multi_validation(nat):
+    lib = nat.load()
+    P = 1 << 12
+    arr = (ctypes.c_void_p * 17)(*([P] * 17))
+    fn = lib.dxr_corr_lookup_backward_multi
+    assert fn(arr, arr, 17, 1, 16, 16, 4, 4, P, nat.DXR_F32, None) == nat.DXR_EUNSUPPORTED
+    assert fn(arr, arr, -1, 1, 16, 16, 4, 4, P, nat.DXR_F32, None) == nat.DXR_EINVAL
+    assert fn(arr, arr, 2, 1, 16, 16, 4, 9, P, nat.DXR_F32, None) == nat.DXR_EUNSUPPORTED
+    assert fn(arr, arr, 2, 1, 16, 16, 4, 4, None, nat.DXR_F32, None) == nat.DXR_EINVAL
+    nul = (ctypes.c_void_p * 2)(P, None)
+    assert fn(arr, nul, 2, 1, 16, 16, 4, 4, P, nat.DXR_F32, None) == nat.DXR_EINVAL
+    assert fn(None, None, 0, 1, 16, 16, 4, 4, P, nat.DXR_F32, None) == nat.DXR_OK
+    assert fn(arr, arr, 2, 0, 16, 16, 4, 4, P, nat.DXR_F32, None) == nat.DXR_OK

@@ -172,3 +172,31 @@ def test_corr_block_backward_fused_and_fallback_agree_with_torch(dx, D):
 
     for got, ref in zip(run(dx.CorrBlock), run(TorchCorrBlock)):
         assert (got - ref).abs().max().item() <= 1e-4 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("r", [4, 3])
+def test_lookup_backward_multi_equals_sequential_calls(dx, r):
+    """dxr_corr_lookup_backward_multi over n coordinate sets == n single calls
+    in the same order, bit for bit (what the deferred autograd path relies on)."""
+    import ctypes
+    nat = _nat()
+    lib = nat.load()
+    B, H, W, L = 2, 30, 44, 4
+    n = 5
+    K = L * (2 * r + 1) ** 2
+    cs = [torch.from_numpy(dg.coords(960 + k, B, H, W, "normal", 3.0 + k)).to(DEV) for k in range(n)]
+    gs = [torch.from_numpy(dg.fmap(970 + k, B, K, H, W)).to(DEV) for k in range(n)]
+    numel = lib.dxr_pyramid_numel(B, H, W, L)
+    seq = torch.zeros(numel, device=DEV)
+    s = nat.stream_of(seq)
+    for c, g in zip(cs, gs):
+        assert lib.dxr_corr_lookup_backward(c.data_ptr(), g.data_ptr(), B, H, W, L, r,
+                                            seq.data_ptr(), nat.DXR_F32, s) == 0
+    multi = torch.zeros(numel, device=DEV)
+    cp = (ctypes.c_void_p * n)(*[c.data_ptr() for c in cs])
+    gp = (ctypes.c_void_p * n)(*[g.data_ptr() for g in gs])
+    assert lib.dxr_corr_lookup_backward_multi(cp, gp, n, B, H, W, L, r, multi.data_ptr(),
+                                              nat.DXR_F32, s) == 0
+    torch.cuda.synchronize()
+    assert seq.abs().sum().item() > 0
+    assert torch.equal(seq, multi)
