@@ -227,11 +227,35 @@ __device__ __forceinline__ void gather_windows(const PT* __restrict__ base, int 
 
 // Phase 0 of the wide lookup (forward and backward): per (query, sample) the
 // coordinate round trip, floor and fractions; per query the window origin and
-// the far flag.  Tap data goes to xs / ys, origins to org.
+// the far flag.  Tap data goes to xs / ys, origins to org.  Split into the
+// coordinate loads and the rest so the multi-set backward can load the next
+// set's coordinates a pass ahead.
 template <int R, int NT_, int QB_ = 0>
-__device__ __forceinline__ void wide_phase0(const float* __restrict__ coords, const LookupGeom& g,
-                                            const LevelAddr& A, int b, int l, int q0, int tid,
-                                            float4* xs, float4* ys, int2* org) {
+struct Phase0Coords {
+  float x[WideCfg<R, NT_, QB_>::SIT], y[WideCfg<R, NT_, QB_>::SIT];
+};
+
+template <int R, int NT_, int QB_ = 0>
+__device__ __forceinline__ void wide_phase0_load(const float* __restrict__ coords, const LookupGeom& g,
+                                                 int b, int q0, int tid, Phase0Coords<R, NT_, QB_>& c) {
+  using C = WideCfg<R, NT_, QB_>;
+  constexpr int QB = C::QB, G = C::G;
+#pragma unroll
+  for (int it = 0; it < C::SIT; ++it) {
+    const int slot = tid + it * C::NT;
+    c.x[it] = c.y[it] = 0.f;
+    if (slot >= QB * G) break;   // whole waves
+    const int q = q0 + (slot >> C::LG);
+    if (q < g.N) {
+      c.x[it] = coords[((long long)b * 2 + 0) * g.N + q];
+      c.y[it] = coords[((long long)b * 2 + 1) * g.N + q];
+    }
+  }
+}
+
+template <int R, int NT_, int QB_ = 0>
+__device__ __forceinline__ void wide_phase0_taps(const Phase0Coords<R, NT_, QB_>& c, const LevelAddr& A,
+                                                 int l, int tid, float4* xs, float4* ys, int2* org) {
   using C = WideCfg<R, NT_, QB_>;
   constexpr int RD = C::RD, WD = C::WD, RS = C::RS, QB = C::QB, G = C::G;
   const int Hl = A.h, Wl = A.w;
@@ -240,12 +264,7 @@ __device__ __forceinline__ void wide_phase0(const float* __restrict__ coords, co
     const int slot = tid + it * C::NT;
     if (slot >= QB * G) break;   // whole waves
     const int j = slot & (G - 1), qq = slot >> C::LG;
-    const int q = q0 + qq;
-    float cx = 0.f, cy = 0.f;
-    if (q < g.N) {
-      cx = coords[((long long)b * 2 + 0) * g.N + q];
-      cy = coords[((long long)b * 2 + 1) * g.N + q];
-    }
+    const float cx = c.x[it], cy = c.y[it];
     const float inv = 1.f / (float)(1 << l);  // exact power of two
     const float wm1 = (float)(Wl - 1), hm1 = (float)(Hl - 1);
     const float ux = sample_coord(__fadd_rn(cx * inv, (float)(j - R)), wm1, wm1 / 2.f);
@@ -275,6 +294,15 @@ __device__ __forceinline__ void wide_phase0(const float* __restrict__ coords, co
       ys[j * QB + qq] = make_float4(__int_as_float(row), fy, __fsub_rn(1.f, fy), 0.f);
     }
   }
+}
+
+template <int R, int NT_, int QB_ = 0>
+__device__ __forceinline__ void wide_phase0(const float* __restrict__ coords, const LookupGeom& g,
+                                            const LevelAddr& A, int b, int l, int q0, int tid,
+                                            float4* xs, float4* ys, int2* org) {
+  Phase0Coords<R, NT_, QB_> c;
+  wide_phase0_load<R, NT_, QB_>(coords, g, b, q0, tid, c);
+  wide_phase0_taps<R, NT_, QB_>(c, A, l, tid, xs, ys, org);
 }
 
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
@@ -357,8 +385,11 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
 // ---------------------------------------------------------------------------
 // Several lookups' backwards in one launch (round 3): a workgroup applies the
 // sets in the given order, one read-modify-write pass each, so the result is
-// the one-set launches' bit for bit; its window lines stay in L2 between passes
-// instead of making a round trip to HBM per lookup.
+// the one-set launches' bit for bit; its window lines stay in L2 between passes,
+// and the next set's coordinates and output gradient load during this pass's
+// sums and stores.  Eight waves per SIMD (four workgroups per CU) beat six with
+// no spill: 0.323 vs 0.337 ms for Sintel's 12 lookups (0.373 without the
+// prefetch; scripts/ab_lookup_backward.sh).
 constexpr int BW_MAX_SETS = 16;
 struct BwSets {
   const float* coords[BW_MAX_SETS];
@@ -367,7 +398,7 @@ struct BwSets {
 };
 
 template <int R>
-__global__ __launch_bounds__(512) void corr_lookup_backward_kernel(BwSets sets,
+__global__ __launch_bounds__(512, 8) void corr_lookup_backward_kernel(BwSets sets,
                                                                    float* __restrict__ gpyr,
                                                                    LookupGeom g) {
   using C = WideCfg<R, 512>;
@@ -379,10 +410,25 @@ __global__ __launch_bounds__(512) void corr_lookup_backward_kernel(BwSets sets,
   __shared__ float T[QB * WD * RD];        // [qq][cy][ox]
   __shared__ float4 xq[QB * RD];           // xs query-major
 
-  const int tid = threadIdx.x;
   const int l = blockIdx.y, b = blockIdx.z;
   const int q0 = blockIdx.x * QB;
   const LevelAddr A = g.lv[l];
+  // a set's coordinates and output gradient, loaded a pass ahead
+  constexpr int GIT = (K * QB + NT - 1) / NT;
+  Phase0Coords<R, 512> cc;
+  float gv[GIT];
+  auto load_set = [&](int set) {
+    const int t0 = threadIdx.x;
+    wide_phase0_load<R, 512>(sets.coords[set], g, b, q0, t0, cc);
+    const float* __restrict__ gout = sets.gout[set];
+#pragma unroll
+    for (int it = 0; it < GIT; ++it) {
+      const int i = t0 + it * NT, k = i / QB, qq = i - k * QB, q = q0 + qq;
+      gv[it] = (i < K * QB && q < g.N) ? gout[((long long)b * g.cout + (long long)l * K + k) * g.N + q]
+                                       : 0.f;
+    }
+  };
+  load_set(0);
   for (int set = 0; set < sets.n; ++set) {
   if (set > 0) {
     // the previous pass's stores are complete before any wave of the workgroup
@@ -392,18 +438,18 @@ __global__ __launch_bounds__(512) void corr_lookup_backward_kernel(BwSets sets,
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
-  const float* __restrict__ coords = sets.coords[set];
-  const float* __restrict__ gout = sets.gout[set];
   // thread-index arithmetic stays inside the pass (hoisted out of the set loop
   // it would hold ~100 VGPRs across passes and halve the resident workgroups)
   int tid = threadIdx.x;
   asm volatile("" : "+v"(tid));
-  wide_phase0<R, 512>(coords, g, A, b, l, q0, tid, xs, ys, org);
-  for (int i = tid; i < K * QB; i += NT) {
-    const int k = i / QB, qq = i - k * QB, q = q0 + qq;
-    G[i] = q < g.N ? gout[((long long)b * g.cout + (long long)l * K + k) * g.N + q] : 0.f;
+  wide_phase0_taps<R, 512>(cc, A, l, tid, xs, ys, org);
+#pragma unroll
+  for (int it = 0; it < GIT; ++it) {
+    const int i = tid + it * NT;
+    if (i < K * QB) G[i] = gv[it];
   }
   __syncthreads();
+  if (set + 1 < sets.n) load_set(set + 1);  // in flight during this pass's sums and stores
 
   // Sample oy's taps sit on window rows row(oy) and row(oy)+1 with row(oy) in
   // {oy, oy+1} (row = floor_oy - min_j(floor_j - j)), so row cy hears only from
