@@ -200,3 +200,22 @@ def test_lookup_backward_multi_equals_sequential_calls(dx, r):
     torch.cuda.synchronize()
     assert seq.abs().sum().item() > 0
     assert torch.equal(seq, multi)
+
+
+def test_deferred_lookup_backwards_flush_per_backward_pass(dx):
+    """Six lookups (one batch of four, then the last two at the build's backward),
+    backpropagated twice through a retained graph: the second pass starts from a
+    fresh gradient pyramid, so the fmap gradients exactly double."""
+    B, D, H, W = 1, 64, 24, 40
+    f1 = torch.from_numpy(dg.fmap(981, B, D, H, W, "fnet")).to(DEV)
+    f2 = torch.from_numpy(dg.fmap(982, B, D, H, W, "fnet")).to(DEV)
+    cs = [torch.from_numpy(dg.coords(983 + k, B, H, W, "normal", 3.0)).to(DEV) for k in range(6)]
+    ws = [torch.from_numpy(dg.fmap(990 + k, B, 4 * 81, H, W)).to(DEV) for k in range(6)]
+    a1, a2 = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
+    cb = dx.CorrBlock(a1, a2)
+    loss = sum((cb(c) * w).sum() for c, w in zip(cs, ws))
+    loss.backward(retain_graph=True)
+    g1, g2 = a1.grad.clone(), a2.grad.clone()
+    assert cb._gs.pending == [] and cb._gs.grad_pyr is None
+    loss.backward()
+    assert torch.equal(a1.grad, 2 * g1) and torch.equal(a2.grad, 2 * g2)
