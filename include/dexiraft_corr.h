@@ -234,7 +234,7 @@ int dxr_corr_lookup_backward(const float* coords, const float* grad_out,
  * The same for n_sets lookups of one block at once (coords[i], grad_out[i]),
  * added in the order given — the result equals n_sets single calls in that
  * order bit for bit — in one launch, so each workgroup's window lines stay in
- * L2 across the sets.  n_sets <= 16 (more: DXR_EUNSUPPORTED).
+ * L2 across the sets.  n_sets <= 16 (more: DXR_EUNSUPPORTED).  ABI 7.
  */
 int dxr_corr_lookup_backward_multi(const float* const* coords, const float* const* grad_out,
                                    int n_sets, int64_t B, int64_t H, int64_t W,
@@ -293,7 +293,7 @@ int dxr_pyramid_backward(const void* grad_pyramid, int grad_dtype,
  *   workspace    : >= dxr_fmap_grads_workspace_bytes(B, D, H, W, num_levels)
  * Supported: D a multiple of 32, num_levels <= 4 (other valid requests return
  * DXR_EUNSUPPORTED; dxr_pyramid_backward + two GEMMs covers them).
- * dxr_fmap_grads_workspace_bytes returns -1 for unsupported shapes.
+ * dxr_fmap_grads_workspace_bytes returns -1 for unsupported shapes.  ABI 7.
  */
 int64_t dxr_fmap_grads_workspace_bytes(int64_t B, int64_t D, int64_t H, int64_t W,
                                        int num_levels);
