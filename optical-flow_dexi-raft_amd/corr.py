@@ -82,13 +82,15 @@ class _GradState:
     so no reference cycle keeps the pyramid (``block._buf``) or the gradient
     pyramid alive after the step: both are freed by refcount."""
 
-    __slots__ = ("geom", "num_levels", "radius", "device", "numel", "grad_pyr", "pending")
+    __slots__ = ("geom", "num_levels", "radius", "device", "numel", "grad_pyr", "pending",
+                 "end_hook")
 
     def __init__(self, geom, num_levels, radius, device, numel):
         self.geom, self.num_levels, self.radius = geom, num_levels, radius
         self.device, self.numel = device, numel
         self.grad_pyr = None
         self.pending = []   # (coords, grad_out) of lookups whose backward is not applied yet
+        self.end_hook = False   # an end-of-backward-pass callback is queued
 
     def flush(self):
         """Add the pending lookups' backwards into the gradient pyramid, in the
@@ -103,12 +105,37 @@ class _GradState:
         cs = (ctypes.c_void_p * n)(*[c.data_ptr() for c, _ in self.pending])
         gs = (ctypes.c_void_p * n)(*[g.data_ptr() for _, g in self.pending])
         lib = nat.load()
-        with _Launch(self.device):
-            st = lib.dxr_corr_lookup_backward_multi(cs, gs, n, B, H, W, self.num_levels, self.radius,
-                                                    self.grad_pyr.data_ptr(), nat.DXR_F32,
-                                                    nat.stream_of(self.grad_pyr))
+        try:
+            with _Launch(self.device):
+                st = lib.dxr_corr_lookup_backward_multi(cs, gs, n, B, H, W, self.num_levels,
+                                                        self.radius, self.grad_pyr.data_ptr(),
+                                                        nat.DXR_F32, nat.stream_of(self.grad_pyr))
+        finally:
+            # never carry (coords, grad_out) entries into another flush, even if
+            # the launch failed: a stale entry would be added twice
+            self.pending = []
         nat.check(st, "CorrBlock lookup backward (dxr_corr_lookup_backward_multi)")
+
+    def reset(self):
+        """Drop pending lookups and the partial gradient pyramid (a backward pass
+        that ended before the build's backward ran, e.g. an exception part-way or
+        ``autograd.grad`` with inputs that stop before the build)."""
         self.pending = []
+        self.grad_pyr = None
+
+    def arm_end_of_pass(self):
+        """Queue (once per backward pass) a callback that runs when autograd's
+        pass ends: whatever the build's backward did not consume by then belongs
+        to a partial pass and is dropped, so it cannot leak into the next one."""
+        if self.end_hook:
+            return
+        self.end_hook = True
+
+        def _end():
+            self.end_hook = False
+            if self.pending or self.grad_pyr is not None:
+                self.reset()
+        torch.autograd.Variable._execution_engine.queue_callback(_end)
 
 
 # Lookup backwards applied per launch: their window lines stay in L2 across the
@@ -130,7 +157,11 @@ class _BuildGrad(torch.autograd.Function):
     @staticmethod
     def backward(ctx, _gtoken):
         gs = ctx.gs
-        gs.flush()
+        try:
+            gs.flush()
+        except BaseException:
+            gs.reset()
+            raise
         gp, gs.grad_pyr = gs.grad_pyr, None
         if gp is None:
             return None, None, None
@@ -176,6 +207,7 @@ class _LookupGrad(torch.autograd.Function):
     def backward(ctx, gout):
         gs = ctx.gs
         (coords,) = ctx.saved_tensors
+        gs.arm_end_of_pass()
         gs.pending.append((coords, gout.contiguous().float()))
         if len(gs.pending) >= _BW_SETS:
             gs.flush()
@@ -343,19 +375,22 @@ def _packed_weight(weight: torch.Tensor, device: torch.device) -> torch.Tensor:
 class CorrBlock:
     """All-pairs correlation pyramid + radius-r lookup (reference core/corr.py:12-60).
 
-    ``CorrBlock(fmap1, fmap2, num_levels=4, radius=4)`` builds the 4-level
-    pyramid of ``fmap1^T fmap2 / sqrt(D)`` in one fused MFMA launch
-    (``dxr_corr_pyramid_build``); each ``__call__(coords)`` is one lookup launch
+    ``CorrBlock(fmap1, fmap2, num_levels=4, radius=4)`` builds the pyramid of
+    ``fmap1^T fmap2 / sqrt(D)`` with its avg-pool levels fused into the GEMM's
+    epilogue (``dxr_corr_pyramid_build_ws``, with a workspace from torch's
+    caching allocator); each ``__call__(coords)`` is one lookup launch
     (``dxr_corr_lookup``) returning a new contiguous float32
     ``[B, num_levels*(2r+1)^2, H, W]`` tensor in the reference's channel order.
 
     fp32 fmaps (the reference's dtype, core/raft.py:139-142) compute in f32
-    class (every operand split into an f16 pair hi + 2^-11 lo, three f16 MFMA
-    products per f32 product into two f32 accumulators, with an in-kernel
-    fallback to an exact three-way bf16 split for operands beyond the f16 range)
-    and store an f32 pyramid; bf16 fmaps build a bf16 pyramid on bf16 MFMA.  The
-    pyramid lives in one paged buffer (``_buf``); ``corr_pyramid`` gives the
-    reference-layout levels on demand.
+    class: a split pass scales every pixel's channel vector by a power of two
+    and stores it as an f16 pair hi + lo, then the LDS-DMA build runs three f16
+    MFMA products per f32 product (lo*hi, hi*lo, hi*hi) into one f32
+    accumulator and undoes the scales exactly in the epilogue.  A workgroup
+    whose sums are not finite (inf/NaN operands) recomputes its pages on the
+    exact-f32 MFMA.  The pyramid is stored in f32; bf16 fmaps build a bf16
+    pyramid on bf16 MFMA.  It lives in one paged buffer (``_buf``);
+    ``corr_pyramid`` gives the reference-layout levels on demand.
     """
 
     def __init__(self, fmap1, fmap2, num_levels=4, radius=4):
@@ -386,7 +421,7 @@ class CorrBlock:
         grad = _wants_grad(fmap1, fmap2)
         self._in_dt = in_dt
         f1, f2, st = self._launch_build(fmap1, fmap2, grad)
-        nat.check(st, "CorrBlock build (dxr_corr_pyramid_build)")
+        nat.check(st, "CorrBlock build (dxr_corr_pyramid_build_ws)")
         self._level_sizes = sizes
         self._ref_pyramid = None
         if grad:
@@ -403,24 +438,26 @@ class CorrBlock:
         once, then moved by LDS-DMA)."""
         B, D, H, W = self._geom
         lib = nat.load()
-        nbytes = lib.dxr_build_workspace_bytes(self._in_dt, B, D, H, W)
-        ws = torch.empty(max(nbytes, 0), dtype=torch.uint8, device=self._device) \
-            if nbytes > 0 else None
+        nbytes = max(lib.dxr_build_workspace_bytes(self._in_dt, B, D, H, W), 0)
 
-        def launch(f1, f2, layout):
+        def launch(f1, f2, layout, with_ws=True):
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=self._device) \
+                if with_ws and nbytes > 0 else None
             with _Launch(self._device):
                 return lib.dxr_corr_pyramid_build_ws(
                     f1.data_ptr(), f2.data_ptr(), self._in_dt, layout, B, D, H, W,
                     self.num_levels, _sqrt_dim(D), self._buf.data_ptr(), self._pyr_dt,
-                    nat.DXR_BUILD_AUTO, nat.ptr(ws), max(nbytes, 0), nat.stream_of(f1))
+                    nat.DXR_BUILD_AUTO, nat.ptr(ws), nbytes if ws is not None else 0,
+                    nat.stream_of(f1))
 
         st = nat.DXR_EUNSUPPORTED
         if not grad and _channels_last(fmap1) and _channels_last(fmap2):
             # channels-last fmaps (SURVEY §8(f) row 4): read in place by the
-            # build's NHWC operand loads (f32: the pre-split pass, bf16: the
-            # two-block bf16 build), no layout pass
+            # build's NHWC operand loads (f32: the pre-split pass, into the
+            # workspace; bf16: the DMA build reads the rows directly and needs no
+            # workspace), no layout pass
             f1, f2 = fmap1, fmap2
-            st = launch(f1, f2, nat.DXR_NHWC)
+            st = launch(f1, f2, nat.DXR_NHWC, with_ws=self._in_dt != nat.DXR_BF16)
         if st == nat.DXR_EUNSUPPORTED:
             if grad:
                 f1, f2 = fmap1.contiguous(), fmap2.contiguous()   # tracked by autograd

@@ -219,3 +219,33 @@ def test_deferred_lookup_backwards_flush_per_backward_pass(dx):
     assert cb._gs.pending == [] and cb._gs.grad_pyr is None
     loss.backward()
     assert torch.equal(a1.grad, 2 * g1) and torch.equal(a2.grad, 2 * g2)
+
+
+def test_partial_backward_pass_does_not_leak(dx):
+    """A backward pass that stops before the build (autograd.grad with respect to
+    the build's token) leaves pending lookup gradients behind; the
+    end-of-pass callback drops them, so a following full pass gives exactly the
+    gradients of a fresh block."""
+    B, D, H, W = 1, 64, 24, 40
+    f1 = torch.from_numpy(dg.fmap(1081, B, D, H, W, "fnet")).to(DEV)
+    f2 = torch.from_numpy(dg.fmap(1082, B, D, H, W, "fnet")).to(DEV)
+    cs = [torch.from_numpy(dg.coords(1083 + k, B, H, W, "normal", 3.0)).to(DEV) for k in range(3)]
+    ws = [torch.from_numpy(dg.fmap(1090 + k, B, 4 * 81, H, W)).to(DEV) for k in range(3)]
+
+    def run(partial):
+        a1, a2 = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
+        cb = dx.CorrBlock(a1, a2)
+        loss = sum((cb(c) * w).sum() for c, w in zip(cs, ws))
+        if partial:
+            # a pass that runs the lookups' backward nodes but not the build's:
+            # gradients with respect to the build's token only
+            outs = [cb(c) for c in cs]
+            l2 = sum((o * w).sum() for o, w in zip(outs, ws))
+            torch.autograd.grad(l2, [cb._token], retain_graph=True, allow_unused=True)
+            assert cb._gs.pending == [] and cb._gs.grad_pyr is None
+        loss.backward()
+        return a1.grad.clone(), a2.grad.clone()
+
+    g1, g2 = run(False)
+    p1, p2 = run(True)
+    assert torch.equal(g1, p1) and torch.equal(g2, p2)

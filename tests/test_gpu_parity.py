@@ -127,8 +127,8 @@ def test_large_shapes_against_reference_checksums(dx, name):
         # Bias guard: a systematic error shows up linearly in a 10^7-cell sum,
         # random rounding only as sqrt(n).  MFMAs align and truncate their addends
         # inside the f32 accumulator: r01's 3-way bf16 split showed a mean error of
-        # -2.7e-9 max|ref| at Sintel (GPU diag, scripts/diag_bias.py), i.e. 3.7e4x
-        # under the 1e-4 per-cell tolerance; bound it at 1e-8 max|ref| per cell.
+        # -2.7e-9 max|ref| at Sintel (a round-1 GPU diagnostic, retired since), i.e.
+        # 3.7e4x under the 1e-4 per-cell tolerance; bound it at 1e-8 max|ref| per cell.
         # (The bias is per cell of level 0 and pooling keeps it: scale by level 0's max.)
         assert abs(s - ref_s) <= 1e-6 * abs(ref_s) + 1e-8 * a.numel() * float(d["pyr0_maxabs"])
         assert abs(s2 - ref_s2) <= 1e-5 * ref_s2
