@@ -25,8 +25,10 @@ after some milliseconds of load, and 30 timed steps behind 3 warmups read 11 %
 below the steady rate (round 2: 3,936 vs 4,414-4,454 pairs/s at 300-2,000 steps).
 Kernel durations for the rooflines: lookup = HIP events on the launch stream
 around back-to-back replays of a graph of the step's 12 lookups, / 12 (one
-lookup plus its same-stream kernel boundary); build = the timed step time minus
-12 lookups (the build plus its boundary and the graph launch).
+lookup plus its same-stream kernel boundary); build = the same around a graph
+of 10 back-to-back builds, / 10 (the split pass, the build and their
+boundaries); what the timed step spends beyond 12 lookups + one build (the
+graph launch, the build -> lookup boundary) is reported as step_boundary_us.
 ``--mode eager`` times plain Python calls instead.
 """
 from __future__ import annotations
@@ -61,6 +63,7 @@ WORKLOADS = {
     "1080p": ((1088, 1920), (136, 240), 1, "f32"),
 }
 D, RADIUS, LEVELS, ITERS = 256, 4, 4, 12
+BUILDS_PER_GRAPH = 10        # back-to-back builds per graph in the build-timing pass
 
 
 def level_sizes(H, W, L=LEVELS):
@@ -338,7 +341,9 @@ def main():
         lookups()
 
     timing = ("lookup = hip events around back-to-back replays of a graph of the step's 12 "
-              "lookups / 12 (kernel + its same-stream boundary); build = timed step - 12 lookups")
+              "lookups / 12; build = hip events around back-to-back replays of a graph of "
+              f"{BUILDS_PER_GRAPH} builds / {BUILDS_PER_GRAPH} (each incl. its same-stream "
+              "boundaries); boundary = timed step - 12 lookups - build")
     with torch.no_grad(), torch.cuda.stream(stream):
         for _ in range(max(min(args.warmup, 3), 1)):  # eager warmup (also a JIT-free check)
             step()
@@ -395,19 +400,31 @@ def main():
             g_look = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_look, stream=stream, pool=g_step.pool()):
                 [cb(c) for c in coords]
+            # the build alone, as a graph of back-to-back builds (each block freed
+            # before the next is built, as in the step)
+            g_build = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_build, stream=stream):
+                for _ in range(BUILDS_PER_GRAPH):
+                    block_cls(f1, f2, radius=RADIUS)
             for _ in range(5):
                 g_look.replay()
+                g_build.replay()
             torch.cuda.synchronize()
             reps = max(20, min(args.steps, 100))
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            for _ in range(reps):
-                g_look.replay()
-            e1.record(stream)
-            torch.cuda.synchronize()
-            look_ms = e0.elapsed_time(e1) / reps / ITERS
-            build_ms = elapsed / args.steps * 1e3 - ITERS * look_ms
-            del keep
+
+            def events(graph, n):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(n):
+                    graph.replay()
+                e1.record(stream)
+                torch.cuda.synchronize()
+                return e0.elapsed_time(e1) / n
+
+            look_ms = events(g_look, reps) / ITERS
+            build_ms = events(g_build, max(5, reps // 4)) / BUILDS_PER_GRAPH
+            boundary_ms = elapsed / args.steps * 1e3 - ITERS * look_ms - build_ms
+            del keep, g_build
         else:
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             ev[0].record(stream)
@@ -417,6 +434,7 @@ def main():
             ev[2].record(stream)
             torch.cuda.synchronize()
             build_ms, look_ms = ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]) / ITERS
+            boundary_ms = elapsed / args.steps * 1e3 - ITERS * look_ms - build_ms
 
     elapsed = max_over_ranks(elapsed, device=dev)
     if not finite:
@@ -486,6 +504,7 @@ def main():
                 "algorithmic_bytes_per_launch": bb,
                 "hbm_frac": round(bb / (build_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
                 "avg_launch_us": round(build_ms * 1e3, 2),
+                "step_boundary_us": round(boundary_ms * 1e3, 2),
             }
             res["lookup_roofline"] = {
                 "kernel": "corr_lookup_wide_kernel (stage c)",
@@ -517,6 +536,7 @@ def main():
                 "algorithmic_flops_per_launch": aflops,
                 "avg_launch_us": round(look_ms * 1e3, 2),
                 "pool_and_layout_us_per_step": round(build_ms * 1e3, 2),
+                "step_boundary_us": round(boundary_ms * 1e3, 2),
             }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(H, W, args.cpu_seconds, args.cpu_impl)

@@ -139,6 +139,21 @@ int64_t dxr_pyramid_level_offset(int64_t B, int64_t H, int64_t W, int level);
  * v_mfma_f32_32x32x2_f32 is used.  Pyramid stores are write-through (sc1).
  * DXR_BF16 inputs use bf16 MFMA with f32 accumulation.  NHWC and NCHW inputs
  * of the same values give bit-identical pyramids.
+ *
+ * Kernels by request (both build entry points; tests/test_gpu_parity.py
+ * test_build_kernel_by_request runs each one by name against the oracle):
+ *   f32, workspace, AUTO, D % 16 == 0   split_pairs_kernel + corr_build_dma_kernel
+ *                                        (CorrBlock's path; NCHW or NHWC)
+ *   f32, no workspace, AUTO, D % 16 == 0, even W
+ *                                        corr_build_split_kernel (round-2 register
+ *                                        split; the documented fallback for callers
+ *                                        that cannot provide a workspace)
+ *   f32, EXACT_F32 or D % 16 != 0 (or odd W without a workspace)
+ *                                        corr_build_f32_kernel (exact-f32 MFMA)
+ *   bf16 NCHW, workspace, D % 32 == 0   pack_bf16_kernel + corr_build_dma_kernel
+ *   bf16 NHWC, D % 32 == 0              corr_build_dma_kernel (rows read in place)
+ *   bf16 NCHW, no workspace, W % 4 == 0 corr_build_bf16_q2_kernel
+ *   bf16 otherwise                      corr_build_bf16_kernel (one query block)
  */
 int dxr_corr_pyramid_build(const void* fmap1, const void* fmap2, int in_dtype,
                            int fmap_layout, int64_t B, int64_t D, int64_t H,

@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
                                                                float* __restrict__ out,
                                                                AltGeom g, int W1, int tiles_x,
                                                                const int4* __restrict__ ord,
-                                                               long long ord_stride) {
+                                                               long long ord_stride, int XL) {
   constexpr int RD = 2 * R + 1, RD1 = RD + 1, NCELL = RD1 * RD1;
   constexpr int CHUNK = 4 * 32 * NRB;                       // box cells per chunk
   constexpr int KB = CMAX / 8;                              // 8-channel blocks
@@ -287,14 +287,27 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
   // Workgroups are dealt round-robin to the 8 XCDs; XCD k takes the k-th
   // contiguous band of tiles instead, so neighbouring tiles (whose boxes overlap)
   // share one L2 (the bijection of csrc/corr_build.hip's page_coord; r01 1080p:
-  // FETCH 424 -> 162 MB per lookup).
-  int tile = blockIdx.x;
-  {
+  // FETCH 424 -> 162 MB per lookup).  XL (levels dividing 8, levels x tiles a
+  // multiple of 8): the XCDs are shared out by level too — 8 / levels XCDs per
+  // level, each taking a contiguous band of that level's list — so one output
+  // line (32 pixels of one channel, written by the workgroups holding those
+  // pixels' queries) is written from one or two XCDs' L2s: with queries ordered
+  // by window position a line's 32 queries sit in bins of several bands, and
+  // partial dirty lines written back from several L2s multiplied the output's
+  // write traffic (r03 1080p: WRITE 137 MB per lookup for a 42 MB output).
+  int tile = blockIdx.x, lvl = blockIdx.y;
+  if (XL) {
+    const int T = gridDim.x, L = gridDim.y;
+    const int lin = blockIdx.x + T * blockIdx.y, xcd = lin % 8, k = lin / 8;
+    const int xpl = 8 / L;
+    lvl = xcd / xpl;
+    tile = (xcd % xpl) * (T / xpl) + k;
+  } else {
     const int n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = tile % 8;
     tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + tile / 8;
   }
   const int tx = tile % tiles_x, ty = tile / tiles_x;
-  const AltLevel lv = g.lv[blockIdx.y];
+  const AltLevel lv = g.lv[lvl];
   const int z = blockIdx.z, bf = z / g.Nc;
   const float* cz = coords + (long long)z * g.coord_zstride;
   const float* f1b = f1 + (long long)bf * g.f1_bstride;
@@ -314,7 +327,7 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
   if constexpr (BIN) {
     if (tid < TQ) {
       // per (coordinate set, level) gridDim.x * 32 entries, query -1 = padding
-      const int4 e = ord[((long long)z * gridDim.y + blockIdx.y) * ord_stride + tile * TQ + tid];
+      const int4 e = ord[((long long)z * gridDim.y + lvl) * ord_stride + tile * TQ + tid];
       qlist[tid] = e.x;
       qxy[tid] = make_float2(__int_as_float(e.y), __int_as_float(e.z));
     }
@@ -903,10 +916,14 @@ long long alt_order_bytes(long long H, long long W) {
 // Sintel 626 -> 612 us in the step).  The tile-order form stays at 1 (its boxes are L1/TA-bound).
 template <int R, int NRB, bool DMA = false, int PF = 4>
 int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const AltGeom& g,
-                      int levels, int Z, int W1, hipStream_t stream, void* ws = nullptr) {
+                      int levels, int Z, int W1, hipStream_t stream, void* ws = nullptr,
+                      int xl = -1) {
   const int H1 = g.N / W1;
   const int tiles_x = (W1 + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
   const int ntiles = tiles_x * tiles_y;
+  // XCDs shared out by level (alt_corr_mfma_kernel XL) where the split is exact
+  const int xl_ok = (8 % levels == 0 && ((long long)levels * ntiles) % 8 == 0) ? 1 : 0;
+  const int XL = xl < 0 ? xl_ok : (xl & xl_ok);
   const dim3 grid((unsigned)ntiles, (unsigned)levels, (unsigned)Z);
   if (g.C > 256) return DXR_EUNSUPPORTED;
   // f16 pair split (r02, 1080p: 227 vs 275 us for the 3-way bf16 split), 3 workgroups/CU
@@ -939,15 +956,15 @@ int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const Al
     if constexpr (DMA)
       hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 2, true, 1, true>), grid,
                          dim3(256), 0, stream, f1, coords, out, g, W1, tiles_x,
-                         reinterpret_cast<const int4*>(ws), o.list_bytes / 16);
+                         reinterpret_cast<const int4*>(ws), o.list_bytes / 16, XL);
     else
       hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 3, true, PF>), grid, dim3(256),
                          0, stream, f1, coords, out, g, W1, tiles_x,
-                         reinterpret_cast<const int4*>(ws), o.list_bytes / 16);
+                         reinterpret_cast<const int4*>(ws), o.list_bytes / 16, XL);
     return dxr::launch_status();
   }
   hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 3>), grid, dim3(256), 0, stream, f1,
-                     coords, out, g, W1, tiles_x, nullptr, 0);
+                     coords, out, g, W1, tiles_x, nullptr, 0, 0);
   return dxr::launch_status();
 }
 

@@ -48,6 +48,7 @@ struct BuildGeom {
   int levels;           // fused levels (1..4)
   int tiles_w, tiles_h; // tiles per image (TX, TY)
   int qt;               // query blocks (pages along queries) per pair
+  int strip;            // target tiles per strip of the XCD-banded page order
   float divisor;        // sqrt(D) in the reference
   float recip;          // 1/divisor when that is exact (power of two), else 0
   int lh[4], lw[4];     // level sizes
@@ -66,46 +67,58 @@ struct PageCoord {
   long long page;
 };
 
-constexpr int STRIP = 8;
+constexpr int STRIP = 8;          // default strip width (BuildGeom::strip)
 
-// QB: query blocks per workgroup (the grid walks groups of QB blocks; qblk is
-// the group's first block, page its first page).
-template <bool REMAP, int QB = 1>
-__device__ __forceinline__ PageCoord page_coord(const BuildGeom& g) {
+// Position wl of the linear (strip-walking) order -> page coordinates.  QB:
+// query blocks per workgroup (the order walks groups of QB blocks; qblk is the
+// group's first block, page its first page).
+template <int QB>
+__device__ __forceinline__ PageCoord unit_coord(const BuildGeom& g, long long wl) {
   PageCoord c;
   const int T = g.tiles_w * g.tiles_h;
   const int qtq = (g.qt + QB - 1) / QB;
-  if constexpr (!REMAP) {
-    c.txi = blockIdx.x % g.tiles_w;
-    c.tyi = blockIdx.x / g.tiles_w;
-    c.qblk = blockIdx.y * QB;
-    c.b = blockIdx.z;
-  } else {
-    const long long per_pair = (long long)qtq * T;
-    const long long nwg = (long long)gridDim.x;
-    const long long w = blockIdx.x;
-    const long long q8 = nwg / 8, r8 = nwg % 8, xcd = w % 8;
-    const long long wl = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + w / 8;
+  const long long per_pair = (long long)qtq * T;
+  {
     c.b = (int)(wl / per_pair);
     long long rem = wl - c.b * per_pair;
-    const int nfull = T / STRIP;
+    const int S = g.strip;
+    const int nfull = T / S;
     int tile;
-    if (rem < (long long)nfull * qtq * STRIP) {
-      const int st = (int)(rem / ((long long)qtq * STRIP));
-      const int in = (int)(rem - (long long)st * qtq * STRIP);
-      c.qblk = in / STRIP * QB;
-      tile = st * STRIP + in % STRIP;
+    if (rem < (long long)nfull * qtq * S) {
+      const int st = (int)(rem / ((long long)qtq * S));
+      const int in = (int)(rem - (long long)st * qtq * S);
+      c.qblk = in / S * QB;
+      tile = st * S + in % S;
     } else {
-      const int nl = T - nfull * STRIP;
-      const int in = (int)(rem - (long long)nfull * qtq * STRIP);
+      const int nl = T - nfull * S;
+      const int in = (int)(rem - (long long)nfull * qtq * S);
       c.qblk = in / nl * QB;
-      tile = nfull * STRIP + in % nl;
+      tile = nfull * S + in % nl;
     }
     c.txi = tile % g.tiles_w;
     c.tyi = tile / g.tiles_w;
   }
   c.page = (((long long)c.b * g.qt + c.qblk) * g.tiles_h + c.tyi) * g.tiles_w + c.txi;
   return c;
+}
+
+template <bool REMAP, int QB = 1>
+__device__ __forceinline__ PageCoord page_coord(const BuildGeom& g) {
+  if constexpr (REMAP) {
+    const long long nwg = (long long)gridDim.x;
+    const long long w = blockIdx.x;
+    const long long q8 = nwg / 8, r8 = nwg % 8, xcd = w % 8;
+    const long long wl = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + w / 8;
+    return unit_coord<QB>(g, wl);
+  } else {
+    PageCoord c;
+    c.txi = blockIdx.x % g.tiles_w;
+    c.tyi = blockIdx.x / g.tiles_w;
+    c.qblk = blockIdx.y * QB;
+    c.b = blockIdx.z;
+    c.page = (((long long)c.b * g.qt + c.qblk) * g.tiles_h + c.tyi) * g.tiles_w + c.txi;
+    return c;
+  }
 }
 
 // Global -> register staging of one BK slice of the query panel (A: [BK][BM])
@@ -2048,6 +2061,7 @@ BuildGeom make_geom(int64_t D, int64_t H, int64_t W, float divisor, const dxr::L
   g.tiles_w = (int)((W + TW - 1) / TW);
   g.tiles_h = (int)((H + TH - 1) / TH);
   g.qt = (int)((H * W + BM - 1) / BM);
+  g.strip = STRIP;
   g.divisor = divisor;
   int e2 = 0;
   g.recip = (std::frexp(divisor, &e2) == 0.5f) ? 1.f / divisor : 0.f;  // exact iff 2^k

@@ -171,14 +171,20 @@ __global__ __launch_bounds__(2 * NT, 4) void xp_build_dma_kernel(
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if constexpr ((XP & 8) == 0) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (ks + 2 < nk && (XP & 4) == 0) dma(ks + 2);
+    if constexpr ((XP & 16) == 0)
+      if (ks + 2 < nk && (XP & 4) == 0) dma(ks + 2);
     const unsigned char* st = smem + ((XP & 4) ? (ks & 1) : (ks % DMA_RING)) * DMA_STAGE;
     const h8v qh = *reinterpret_cast<const h8v*>(st + qh_off);
     const h8v ql = *reinterpret_cast<const h8v*>(st + ql_off);
+    h8v thv[4], tlv[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const h8v th = *reinterpret_cast<const h8v*>(st + th_off + t * 2048);
-      const h8v tl = *reinterpret_cast<const h8v*>(st + tl_off + t * 2048);
+      thv[t] = *reinterpret_cast<const h8v*>(st + th_off + t * 2048);
+      tlv[t] = *reinterpret_cast<const h8v*>(st + tl_off + t * 2048);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const h8v th = thv[t], tl = tlv[t];
       // small terms first
       if constexpr ((XP & 2) != 0) {
         acc[t][0] += (float)(th[0] + tl[1] + qh[2] + ql[3]);
@@ -187,6 +193,14 @@ __global__ __launch_bounds__(2 * NT, 4) void xp_build_dma_kernel(
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc[t], 0, 0, 0);
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qh, acc[t], 0, 0, 0);
       }
+      // XP bit 4: the next DMAs issue behind the first tile's MFMAs (their issue
+      // cost then overlaps the matrix pipe instead of delaying the fragment reads)
+      if constexpr ((XP & 16) != 0)
+        if (t == 0 && ks + 2 < nk && (XP & 4) == 0) {
+          __builtin_amdgcn_sched_barrier(0);
+          dma(ks + 2);
+          __builtin_amdgcn_sched_barrier(0);
+        }
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -326,6 +340,184 @@ __global__ __launch_bounds__(PX * 16) void xp_split_px_kernel(const float* __res
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, rec[c]), rs, off + 16 * c, 0, 16);
 }
 
+// Persistent form of the DMA build (round 4 experiment): gridDim.x workgroups
+// (a multiple of 8) walk the units (two query blocks x one tile) of the linear
+// order; XCD k's workgroups take XCD k's contiguous range of units, local slot
+// i taking units i, i + G/8, ...  XP bit 1: workgroups of the upper half of each
+// XCD's slots first sleep `stagger` real-time ticks (10 ns), so that the two
+// workgroups of a CU run out of phase (one in its K loop while the other
+// stores).  Bit 8: per-unit s_memrealtime stamps {start, K loop done, stores
+// done, hw id} at trace[4 * unit].  Finite data only (no recompute path).
+template <typename OT, int XP>
+__global__ __launch_bounds__(2 * NT, 4) void xp_build_persist_kernel(
+    const uint8_t* __restrict__ sp1, const uint8_t* __restrict__ sp2, const int* __restrict__ ex1,
+    const int* __restrict__ ex2, OT* __restrict__ pyr, BuildGeom g, long long nunits, int stagger,
+    unsigned long long* __restrict__ trace) {
+  constexpr int LDS_RING = DMA_RING * DMA_STAGE;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_RING + NTGT * 4 + 16];
+  int* const sexp = reinterpret_cast<int*>(smem + LDS_RING);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int half = wave >> 2, w4 = wave & 3;
+  const int j = lane & 31, kh = lane >> 5;
+  const long long spstride = (long long)g.D * g.N * 4;
+  const int per_xcd = gridDim.x / 8, xcd = blockIdx.x % 8, local = blockIdx.x / 8;
+  const long long q8 = nunits / 8, r8 = nunits % 8;
+  const long long ustart = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const long long ucount = q8 + (xcd < r8 ? 1 : 0);
+  if constexpr ((XP & 2) != 0) {
+    if (local >= per_xcd / 2) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)stagger)
+        __builtin_amdgcn_s_sleep(8);
+    }
+  }
+  const int kq = (j >> 2) & 3;
+  const int qh_off = wave * 2048 + j * 64 + 16 * (kh ^ kq);
+  const int ql_off = wave * 2048 + j * 64 + 16 * ((2 + kh) ^ kq);
+  const int trow0 = ((j >> 2) & 1) * 16 + (j & 3) + 4 * (j >> 3);
+  const int kt = ((trow0 >> 2) & 1) | ((trow0 >> 3) & 2);
+  const int th_off = DMA_TILE + trow0 * 64 + 16 * (kh ^ kt);
+  const int tl_off = DMA_TILE + trow0 * 64 + 16 * ((2 + kh) ^ kt);
+  const int nk = g.D / BKS;
+
+  for (long long u = local; u < ucount; u += per_xcd) {
+    const long long wl = ustart + u;
+    const unsigned long long xt0 = (XP & 256) ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const PageCoord pc = unit_coord<2>(g, wl);
+    const int th0 = pc.tyi * TH, tw0 = pc.txi * TW;
+    const int q0 = pc.qblk * BM;
+    const int b = pc.b;
+    __syncthreads();   // the previous unit's epilogue is done with the LDS
+    const int qj = q0 + wave * 32 + j;
+    const int sq = qj < g.N ? ex1[(long long)b * g.N + qj] : 0;
+    if (tid < NTGT) {
+      const int r = tid >> 4, c = tid & 15;
+      const bool in = th0 + r < g.H && tw0 + c < g.W;
+      sexp[tid] = in ? ex2[(long long)b * g.N + (th0 + r) * g.W + tw0 + c] : 0;
+    }
+    const __amdgpu_buffer_rsrc_t rq =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sp1 + b * spstride), (short)0,
+                                          (int)spstride, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rt =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sp2 + b * spstride), (short)0,
+                                          (int)spstride, 0x00020000);
+    uint32_t vq[2], vt;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = 16 * i + (lane >> 2), ps = lane & 3;
+      const int q = q0 + wave * 32 + row;
+      const int cq = ps ^ ((row >> 2) & 3);
+      vq[i] = q < g.N ? (uint32_t)(q * 64 + 16 * cq) : 0x80000000u;
+    }
+    {
+      const int ps = lane & 3, r = wave, col = lane >> 2, trow = r * 16 + col;
+      const int ct = ps ^ (((trow >> 2) & 1) | ((trow >> 3) & 2));
+      const int hh = th0 + r, ww = tw0 + col;
+      vt = (hh < g.H && ww < g.W) ? (uint32_t)((hh * g.W + ww) * 64 + 16 * ct) : 0x80000000u;
+    }
+    auto dma = [&](int ks) {
+      unsigned char* st = smem + (ks % DMA_RING) * DMA_STAGE;
+      const int so = ks * g.N * 64;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rq, (lds_void_t*)(st + wave * 2048 + i * 1024), 16, vq[i], so, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (lds_void_t*)(st + DMA_TILE + wave * 1024), 16,
+                                               vt, so, 0, 0);
+    };
+    f32x16 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    dma(0);
+    if (nk > 1) dma(1);
+    for (int ks = 0; ks < nk; ++ks) {
+      if (ks + 1 < nk) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((XP & 16) == 0)
+        if (ks + 2 < nk) dma(ks + 2);
+      const unsigned char* st = smem + (ks % DMA_RING) * DMA_STAGE;
+      const h8v qh = *reinterpret_cast<const h8v*>(st + qh_off);
+      const h8v ql = *reinterpret_cast<const h8v*>(st + ql_off);
+      h8v thv[4], tlv[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        thv[t] = *reinterpret_cast<const h8v*>(st + th_off + t * 2048);
+        tlv[t] = *reinterpret_cast<const h8v*>(st + tl_off + t * 2048);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tlv[t], qh, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(thv[t], ql, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(thv[t], qh, acc[t], 0, 0, 0);
+        if constexpr ((XP & 16) != 0)
+          if (t == 0 && ks + 2 < nk) {
+            __builtin_amdgcn_sched_barrier(0);
+            dma(ks + 2);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const unsigned long long xt1 = (XP & 256) ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const bool live = pc.qblk + half < g.qt;
+    const long long page = pc.page + (live ? (long long)half * g.tiles_h * g.tiles_w : 0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int4* se = reinterpret_cast<const int4*>(sexp + (2 * t + kh) * 16);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int4 s4 = se[v];
+        acc[t][4 * v + 0] = __builtin_ldexpf(acc[t][4 * v + 0], -(sq + s4.x));
+        acc[t][4 * v + 1] = __builtin_ldexpf(acc[t][4 * v + 1], -(sq + s4.y));
+        acc[t][4 * v + 2] = __builtin_ldexpf(acc[t][4 * v + 2], -(sq + s4.z));
+        acc[t][4 * v + 3] = __builtin_ldexpf(acc[t][4 * v + 3], -(sq + s4.w));
+      }
+    }
+    if (live) {
+      scale_acc<false>(acc, g);
+      paged_epilogue<OT, 1 | 4>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0, pyr,
+                                g, page, w4, lane);
+    }
+    if constexpr ((XP & 256) != 0) {
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      const unsigned long long xt2 = __builtin_amdgcn_s_memrealtime();
+      if (tid < 4) {
+        const unsigned long long hw = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+                                      ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(20 | (15 << 11)) << 32);
+        trace[wl * 4 + tid] = tid == 0 ? xt0 : tid == 1 ? xt1 : tid == 2 ? xt2 : hw;
+      }
+    }
+  }
+}
+
+template <int XP>
+int xp_persist(const float* f1, const float* f2, float* pyr, const BuildGeom& g, int B, void* ws,
+               int nwg, int stagger, unsigned long long* trace, hipStream_t stream) {
+  const long long N = g.N, spb = align256((long long)B * g.D * N * 4), eb = align256((long long)B * N * 4);
+  uint8_t* w = static_cast<uint8_t*>(ws);
+  int* e1 = reinterpret_cast<int*>(w + 2 * spb);
+  int* e2 = reinterpret_cast<int*>(w + 2 * spb + eb);
+  hipLaunchKernelGGL((split_pairs_kernel<false>), dim3((unsigned)((N + 63) / 64), (unsigned)B, 2),
+                     dim3(1024), 0, stream, f1, f2, reinterpret_cast<uint4*>(w),
+                     reinterpret_cast<uint4*>(w + spb), e1, e2, g.D, g.N);
+  const long long nunits = (long long)B * ((g.qt + 1) / 2) * g.tiles_h * g.tiles_w;
+  long long grid = std::min<long long>(nwg, nunits);
+  grid = std::max<long long>(8, grid / 8 * 8);
+  hipLaunchKernelGGL((xp_build_persist_kernel<float, XP>), dim3((unsigned)grid), dim3(2 * NT), 0,
+                     stream, w, w + spb, e1, e2, pyr, g, nunits, stagger, trace);
+  return dxr::launch_status();
+}
+
 }  // namespace
 
 // Variant xp of the pre-split build (f32 NCHW fmaps, W % 4 == 0, D % 16 == 0,
@@ -352,6 +544,8 @@ extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t
     case 257: return xp_dma<257>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     case 32: return xp_dma<32>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     case 33: return xp_dma<33>(f1, f2, pyr, g, (int)B, ws, trace, stream);
+    case 16: return xp_dma<16>(f1, f2, pyr, g, (int)B, ws, trace, stream);
+    case 272: return xp_dma<272>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     default: return DXR_EINVAL;
   }
 }
@@ -377,4 +571,40 @@ extern "C" int dxr_xp_split(const float* f1, const float* f2, int64_t B, int64_t
     default: return DXR_EINVAL;
   }
   return dxr::launch_status();
+}
+
+// Persistent build variant xp (0 plain, 2 stagger, +256 trace) over nwg workgroups.
+extern "C" int dxr_xp_build_persist(const float* f1, const float* f2, int64_t B, int64_t D,
+                                    int64_t H, int64_t W, float* pyr, void* ws, int xp, int nwg,
+                                    int stagger, unsigned long long* trace, hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, 4, &L) || W % 4 || D % 16) return DXR_EINVAL;
+  const BuildGeom g = make_geom(D, H, W, std::sqrt((float)D), L);
+  if (g.recip == 0.f || nwg < 8) return DXR_EINVAL;
+  switch (xp) {
+    case 0: return xp_persist<0>(f1, f2, pyr, g, (int)B, ws, nwg, stagger, trace, stream);
+    case 2: return xp_persist<2>(f1, f2, pyr, g, (int)B, ws, nwg, stagger, trace, stream);
+    case 256: return xp_persist<256>(f1, f2, pyr, g, (int)B, ws, nwg, stagger, trace, stream);
+    case 258: return xp_persist<258>(f1, f2, pyr, g, (int)B, ws, nwg, stagger, trace, stream);
+    case 16: return xp_persist<16>(f1, f2, pyr, g, (int)B, ws, nwg, stagger, trace, stream);
+    case 18: return xp_persist<18>(f1, f2, pyr, g, (int)B, ws, nwg, stagger, trace, stream);
+    default: return DXR_EINVAL;
+  }
+}
+
+// The product's DMA builds with another strip width of the XCD-banded page
+// order (BuildGeom::strip, product 8): f32 NCHW (ws as dxr_corr_pyramid_build_ws)
+// or bf16 channels-last (no workspace).  Same pages bit for bit.
+extern "C" int dxr_xp_build_strip(const void* f1, const void* f2, int in_dtype, int64_t B,
+                                  int64_t D, int64_t H, int64_t W, void* pyr, void* ws, int strip,
+                                  hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, 4, &L) || strip < 1) return DXR_EINVAL;
+  BuildGeom g = make_geom(D, H, W, std::sqrt((float)D), L);
+  g.strip = strip;
+  if (in_dtype == DXR_F32)
+    return launch_dma<float, false>(static_cast<const float*>(f1), static_cast<const float*>(f2),
+                                    static_cast<float*>(pyr), g, (int)B, ws, stream);
+  return launch_dma_bf16_nhwc(static_cast<const uint16_t*>(f1), static_cast<const uint16_t*>(f2),
+                              static_cast<uint16_t*>(pyr), g, (int)B, stream);
 }

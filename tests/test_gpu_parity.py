@@ -844,3 +844,67 @@ def test_backward_only_flows_to_fmaps_that_require_grad(dx):
     assert out.grad_fn is None
     with pytest.raises(NotImplementedError, match="coords"):
         cb(c.clone().requires_grad_(True))
+
+
+# Every build kernel the library can run, by the request that selects it
+# (include/dexiraft_corr.h, "Kernels by request"): the kernel's name is the
+# test id.  Each runs through the C-ABI and is checked against the float64
+# oracle at the dtype's tolerance (f32 1e-4 of max per level, bf16 1e-2).
+_BUILD_PATHS = [
+    # id, in dtype, layout, workspace, algo, (B, D, H, W)
+    ("split_pairs_kernel+corr_build_dma_kernel", "f32", "nchw", True, "auto", (1, 64, 23, 31)),
+    ("split_pairs_kernel+corr_build_dma_kernel-nhwc", "f32", "nhwc", True, "auto", (1, 64, 23, 32)),
+    ("corr_build_split_kernel", "f32", "nchw", False, "auto", (1, 64, 23, 32)),
+    ("corr_build_split_kernel-nhwc", "f32", "nhwc", False, "auto", (1, 64, 23, 32)),
+    ("corr_build_f32_kernel-exact", "f32", "nchw", False, "exact", (1, 64, 23, 32)),
+    ("corr_build_f32_kernel-exact-ws", "f32", "nchw", True, "exact", (1, 64, 23, 32)),
+    ("corr_build_f32_kernel-d24", "f32", "nchw", True, "auto", (1, 24, 23, 31)),
+    ("pack_bf16_kernel+corr_build_dma_kernel", "bf16", "nchw", True, "auto", (1, 64, 23, 32)),
+    ("corr_build_dma_kernel-bf16-nhwc", "bf16", "nhwc", False, "auto", (1, 64, 23, 32)),
+    ("corr_build_bf16_q2_kernel", "bf16", "nchw", False, "auto", (1, 64, 23, 32)),
+    ("corr_build_bf16_kernel-w31", "bf16", "nchw", False, "auto", (1, 64, 23, 31)),
+]
+
+
+@pytest.mark.parametrize("path", _BUILD_PATHS, ids=[p[0] for p in _BUILD_PATHS])
+def test_build_kernel_by_request(dx, path):
+    from dexiraft_amd import _native as nat
+    _, dt, layout, with_ws, algo, (B, D, H, W) = path
+    lib = nat.load()
+    a = dg.fmap(881, B, D, H, W, "fnet")
+    b = dg.fmap(882, B, D, H, W, "fnet")
+    ref = oracle.corr_pyramid(a, b, 4, np.float64)
+    f1, f2 = _t(a), _t(b)
+    code = nat.DXR_F32
+    if dt == "bf16":
+        f1, f2, code = f1.bfloat16(), f2.bfloat16(), nat.DXR_BF16
+        ref = oracle.corr_pyramid(f1.float().cpu().numpy(), f2.float().cpu().numpy(), 4, np.float64)
+    lay = nat.DXR_NCHW
+    if layout == "nhwc":
+        f1 = f1.contiguous(memory_format=torch.channels_last)
+        f2 = f2.contiguous(memory_format=torch.channels_last)
+        lay = nat.DXR_NHWC
+    buf = torch.empty(lib.dxr_pyramid_numel(B, H, W, 4), device=DEV,
+                      dtype=torch.float32 if dt == "f32" else torch.bfloat16)
+    al = nat.DXR_BUILD_EXACT_F32 if algo == "exact" else nat.DXR_BUILD_AUTO
+    div = float(np.sqrt(np.float32(D)))
+    s = nat.stream_of(f1)
+    if with_ws:
+        nb = max(lib.dxr_build_workspace_bytes(code, B, D, H, W), 0)
+        ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=DEV)
+        st = lib.dxr_corr_pyramid_build_ws(f1.data_ptr(), f2.data_ptr(), code, lay, B, D, H, W, 4,
+                                           div, buf.data_ptr(), code, al, ws.data_ptr(), nb, s)
+    else:
+        st = lib.dxr_corr_pyramid_build(f1.data_ptr(), f2.data_ptr(), code, lay, B, D, H, W, 4, div,
+                                        buf.data_ptr(), code, al, s)
+    assert st == 0
+    tol = 1e-4 if dt == "f32" else 1e-2
+    h, w = H, W
+    for lvl in range(4):
+        if lvl:
+            h, w = h // 2, w // 2
+        t = torch.empty((B * H * W, h, w), device=DEV)
+        assert lib.dxr_pyramid_unpack(buf.data_ptr(), code, B, H, W, 4, lvl, t.data_ptr(), s) == 0
+        got = t.cpu().numpy()
+        m = np.abs(ref[lvl]).max()
+        assert np.abs(got - ref[lvl].reshape(got.shape)).max() <= tol * m, lvl
