@@ -406,11 +406,17 @@ def main():
             with torch.cuda.graph(g_build, stream=stream):
                 for _ in range(BUILDS_PER_GRAPH):
                     block_cls(f1, f2, radius=RADIUS)
+            # the captures left the GPU idle: bring the clocks back up first
+            t_w = time.perf_counter()
+            while time.perf_counter() - t_w < min(args.clock_warmup_s, 0.25):
+                for _ in range(10):
+                    g_step.replay()
+                torch.cuda.synchronize()
             for _ in range(5):
                 g_look.replay()
                 g_build.replay()
             torch.cuda.synchronize()
-            reps = max(20, min(args.steps, 100))
+            reps = max(50, min(args.steps, 100))
 
             def events(graph, n):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -295,6 +295,7 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
   // by window position a line's 32 queries sit in bins of several bands, and
   // partial dirty lines written back from several L2s multiplied the output's
   // write traffic (r03 1080p: WRITE 137 MB per lookup for a 42 MB output).
+  // Measured slower (the levels cost different amounts): experiments only.
   int tile = blockIdx.x, lvl = blockIdx.y;
   if (XL) {
     const int T = gridDim.x, L = gridDim.y;
@@ -921,9 +922,12 @@ int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const Al
   const int H1 = g.N / W1;
   const int tiles_x = (W1 + TQX - 1) / TQX, tiles_y = (H1 + TQY - 1) / TQY;
   const int ntiles = tiles_x * tiles_y;
-  // XCDs shared out by level (alt_corr_mfma_kernel XL) where the split is exact
+  // XCDs shared out by level (alt_corr_mfma_kernel XL) where the split is exact:
+  // experiments only — round 4, 1080p i.i.d. flows, 12 ordered lookups in the
+  // step: 2,567 us with it against 1,990 us without (the levels' lists cost
+  // different amounts, so the XCDs of the cheap levels idle)
   const int xl_ok = (8 % levels == 0 && ((long long)levels * ntiles) % 8 == 0) ? 1 : 0;
-  const int XL = xl < 0 ? xl_ok : (xl & xl_ok);
+  const int XL = xl < 0 ? 0 : (xl & xl_ok);
   const dim3 grid((unsigned)ntiles, (unsigned)levels, (unsigned)Z);
   if (g.C > 256) return DXR_EUNSUPPORTED;
   // f16 pair split (r02, 1080p: 227 vs 275 us for the 3-way bf16 split), 3 workgroups/CU

@@ -253,6 +253,20 @@ __device__ __forceinline__ void wide_phase0_load(const float* __restrict__ coord
   }
 }
 
+// min over the aligned group of G lanes (G = 2, 4, 8, 16: DPP within a row of
+// 16 lanes, no LDS round trip; 32: cross-row shuffles).  Order-free, so the same
+// value as any other reduction order.
+template <int G>
+__device__ __forceinline__ int group_min(int v) {
+  if constexpr (G >= 2) v = min(v, __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false));  // quad [1,0,3,2]
+  if constexpr (G >= 4) v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false));  // quad [2,3,0,1]
+  if constexpr (G >= 8) v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false)); // row_half_mirror
+  if constexpr (G >= 16) v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false)); // row_mirror
+  if constexpr (G >= 32) v = min(v, __shfl_xor(v, 16));
+  if constexpr (G >= 64) v = min(v, __shfl_xor(v, 32));
+  return v;
+}
+
 template <int R, int NT_, int QB_ = 0>
 __device__ __forceinline__ void wide_phase0_taps(const Phase0Coords<R, NT_, QB_>& c, const LevelAddr& A,
                                                  int l, int tid, float4* xs, float4* ys, int2* org) {
@@ -265,7 +279,7 @@ __device__ __forceinline__ void wide_phase0_taps(const Phase0Coords<R, NT_, QB_>
     if (slot >= QB * G) break;   // whole waves
     const int j = slot & (G - 1), qq = slot >> C::LG;
     const float cx = c.x[it], cy = c.y[it];
-    const float inv = 1.f / (float)(1 << l);  // exact power of two
+    const float inv = __builtin_ldexpf(1.f, -l);  // 2^-l, exact (no division)
     const float wm1 = (float)(Wl - 1), hm1 = (float)(Hl - 1);
     const float ux = sample_coord(__fadd_rn(cx * inv, (float)(j - R)), wm1, wm1 / 2.f);
     const float uy = sample_coord(__fadd_rn(cy * inv, (float)(j - R)), hm1, hm1 / 2.f);
@@ -278,11 +292,8 @@ __device__ __forceinline__ void wide_phase0_taps(const Phase0Coords<R, NT_, QB_>
       mx = bad ? FAR_ORIGIN : (int)flx - j;
       my = bad ? FAR_ORIGIN : (int)fly - j;
     }
-#pragma unroll
-    for (int o = 1; o < G; o <<= 1) {
-      mx = min(mx, __shfl_xor(mx, o));
-      my = min(my, __shfl_xor(my, o));
-    }
+    mx = group_min<G>(mx);
+    my = group_min<G>(my);
     // windows entirely off the level hold only zeros: no loads
     const bool far = mx + WD <= 0 || mx >= Wl || my + WD <= 0 || my >= Hl;
     if (j == 0) org[qq] = far ? make_int2(FAR_ORIGIN, FAR_ORIGIN) : make_int2(mx, my);
@@ -307,7 +318,10 @@ __device__ __forceinline__ void wide_phase0(const float* __restrict__ coords, co
 
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
-template <int R, typename PT, int NT_ = 512, int QB_ = 0>
+// TSTORE (experiments): the outputs go through LDS (aliasing the staged
+// windows) and leave as 16-byte write-through stores of 4 queries each instead
+// of one 4-byte store per output.
+template <int R, typename PT, int NT_ = 512, int QB_ = 0, bool TSTORE = false>
 __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
     const PT* __restrict__ pyr, const float* __restrict__ coords, float* __restrict__ out,
     LookupGeom g) {
@@ -348,6 +362,58 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
 
   // ---- phase 2
   const int qq = tid % QB, cls = tid / QB;
+  if constexpr (TSTORE) {
+    static_assert(K * QB <= QB * C::QS, "the outputs fit the window staging");
+    constexpr int NKT = (K + C::NCLS - 1) / C::NCLS;
+    float res[NKT];
+    const float* cq = cells + qq * C::QS;
+#pragma unroll
+    for (int i = 0; i < NKT; ++i) {
+      const int k = cls + i * C::NCLS;
+      res[i] = 0.f;
+      if (k < K) {
+        const int ox = k / RD, oy = k - ox * RD;
+        const float4 xd = xs[ox * QB + qq], yd = ys[oy * QB + qq];
+        const float* p = cq + __float_as_int(yd.x) + __float_as_int(xd.x);
+        const float v00 = p[0], v01 = p[1], v10 = p[RS], v11 = p[RS + 1];
+        const float nw = __fmul_rn(yd.z, xd.z), ne = __fmul_rn(yd.z, xd.y);
+        const float sw = __fmul_rn(yd.y, xd.z), se = __fmul_rn(yd.y, xd.y);
+        float r = __fmul_rn(nw, v00);
+        r = __builtin_fmaf(ne, v01, r);
+        r = __builtin_fmaf(sw, v10, r);
+        res[i] = __builtin_fmaf(se, v11, r);
+      }
+    }
+    __syncthreads();   // every tap read: the staging becomes the output tile [K][QB]
+#pragma unroll
+    for (int i = 0; i < NKT; ++i) {
+      const int k = cls + i * C::NCLS;
+      if (k < K) cells[k * QB + qq] = res[i];
+    }
+    __syncthreads();
+    float* ob0 = out + ((long long)b * g.cout + (long long)l * K) * g.N;
+    const bool vec = (g.N & 3) == 0 && q0 + QB <= g.N;
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        ob0, (short)0, 0x7fffffff, 0x00020000);
+    for (int e = tid; e < K * QB / 4; e += NT_) {
+      const int k = e / (QB / 4), c4 = e - k * (QB / 4);
+      const float4 v = *reinterpret_cast<const float4*>(cells + k * QB + 4 * c4);
+      if (vec) {
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u32x4_t, f4v{v.x, v.y, v.z, v.w}), ro,
+            (unsigned)(((long long)k * g.N + q0 + 4 * c4) * 4), 0, 16);
+      } else {
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (q0 + 4 * c4 + u < g.N)
+            __hip_atomic_store(ob0 + (long long)k * g.N + q0 + 4 * c4 + u, vv[u], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    return;
+  }
   if (q0 + qq >= g.N) return;
   const float* cq = cells + qq * C::QS;
   float* ob = out + ((long long)b * g.cout + (long long)l * K) * g.N + q0 + qq;
@@ -397,8 +463,13 @@ struct BwSets {
   int n;
 };
 
+// Minimum waves per SIMD by radius: 8 (<= 64 VGPRs) holds r <= 5 without
+// scratch; r = 6 spilled 44 B/lane at that bound and r = 7 / 8 need 86 / 109
+// VGPRs, so r >= 6 asks for 4 (<= 128 VGPRs, no spill).
+constexpr int bw_min_waves(int r) { return r <= 5 ? 8 : 4; }
+
 template <int R>
-__global__ __launch_bounds__(512, 8) void corr_lookup_backward_kernel(BwSets sets,
+__global__ __launch_bounds__(512, bw_min_waves(R)) void corr_lookup_backward_kernel(BwSets sets,
                                                                    float* __restrict__ gpyr,
                                                                    LookupGeom g) {
   using C = WideCfg<R, 512>;

@@ -243,6 +243,12 @@ __global__ __launch_bounds__(2 * NT, 4) void xp_build_dma_kernel(
 #pragma unroll
           for (int r = 0; r < 16; ++r) sum += acc[t][r];
         if (sum == 1234.5f) pyr[tid] = to_out<OT>(sum);  // keeps the K loop live
+      } else if constexpr ((XP & 64) != 0) {   // non-temporal instead of write-through stores
+        paged_epilogue<OT, 1 | 2>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0,
+                                  pyr, g, page, w4, lane);
+      } else if constexpr ((XP & 128) != 0) {  // plain (write-back) stores
+        paged_epilogue<OT, 1>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0,
+                              pyr, g, page, w4, lane);
       } else {
         paged_epilogue<OT, 1 | 4>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0,
                                   pyr, g, page, w4, lane);
@@ -545,6 +551,8 @@ extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t
     case 32: return xp_dma<32>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     case 33: return xp_dma<33>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     case 16: return xp_dma<16>(f1, f2, pyr, g, (int)B, ws, trace, stream);
+    case 64: return xp_dma<64>(f1, f2, pyr, g, (int)B, ws, trace, stream);
+    case 128: return xp_dma<128>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     case 272: return xp_dma<272>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     default: return DXR_EINVAL;
   }
@@ -607,4 +615,20 @@ extern "C" int dxr_xp_build_strip(const void* f1, const void* f2, int in_dtype, 
                                     static_cast<float*>(pyr), g, (int)B, ws, stream);
   return launch_dma_bf16_nhwc(static_cast<const uint16_t*>(f1), static_cast<const uint16_t*>(f2),
                               static_cast<uint16_t*>(pyr), g, (int)B, stream);
+}
+
+// The software-pipelined build (corr_build_pipe_kernel) for A/B against the
+// product: f32 NCHW with its split pass (ws as dxr_corr_pyramid_build_ws) or
+// bf16 channels-last (no workspace); D = 256.
+extern "C" int dxr_xp_build_pipe(const void* f1, const void* f2, int in_dtype, int64_t B,
+                                 int64_t D, int64_t H, int64_t W, void* pyr, void* ws,
+                                 hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, 4, &L) || D != 256) return DXR_EINVAL;
+  const BuildGeom g = make_geom(D, H, W, std::sqrt((float)D), L);
+  if (in_dtype == DXR_F32)
+    return launch_pipe<float, false>(static_cast<const float*>(f1), static_cast<const float*>(f2),
+                                     static_cast<float*>(pyr), g, (int)B, ws, stream);
+  return launch_pipe_bf16_nhwc(static_cast<const uint16_t*>(f1), static_cast<const uint16_t*>(f2),
+                               static_cast<uint16_t*>(pyr), g, (int)B, stream);
 }

@@ -174,7 +174,7 @@ def test_corr_block_backward_fused_and_fallback_agree_with_torch(dx, D):
         assert (got - ref).abs().max().item() <= 1e-4 * ref.abs().max().item()
 
 
-@pytest.mark.parametrize("r", [4, 3])
+@pytest.mark.parametrize("r", [4, 3, 6, 8])
 def test_lookup_backward_multi_equals_sequential_calls(dx, r):
     """dxr_corr_lookup_backward_multi over n coordinate sets == n single calls
     in the same order, bit for bit (what the deferred autograd path relies on)."""
