@@ -318,10 +318,7 @@ __device__ __forceinline__ void wide_phase0(const float* __restrict__ coords, co
 
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
-// TSTORE (experiments): the outputs go through LDS (aliasing the staged
-// windows) and leave as 16-byte write-through stores of 4 queries each instead
-// of one 4-byte store per output.
-template <int R, typename PT, int NT_ = 512, int QB_ = 0, bool TSTORE = false>
+template <int R, typename PT, int NT_ = 512, int QB_ = 0>
 __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
     const PT* __restrict__ pyr, const float* __restrict__ coords, float* __restrict__ out,
     LookupGeom g) {
@@ -362,58 +359,6 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
 
   // ---- phase 2
   const int qq = tid % QB, cls = tid / QB;
-  if constexpr (TSTORE) {
-    static_assert(K * QB <= QB * C::QS, "the outputs fit the window staging");
-    constexpr int NKT = (K + C::NCLS - 1) / C::NCLS;
-    float res[NKT];
-    const float* cq = cells + qq * C::QS;
-#pragma unroll
-    for (int i = 0; i < NKT; ++i) {
-      const int k = cls + i * C::NCLS;
-      res[i] = 0.f;
-      if (k < K) {
-        const int ox = k / RD, oy = k - ox * RD;
-        const float4 xd = xs[ox * QB + qq], yd = ys[oy * QB + qq];
-        const float* p = cq + __float_as_int(yd.x) + __float_as_int(xd.x);
-        const float v00 = p[0], v01 = p[1], v10 = p[RS], v11 = p[RS + 1];
-        const float nw = __fmul_rn(yd.z, xd.z), ne = __fmul_rn(yd.z, xd.y);
-        const float sw = __fmul_rn(yd.y, xd.z), se = __fmul_rn(yd.y, xd.y);
-        float r = __fmul_rn(nw, v00);
-        r = __builtin_fmaf(ne, v01, r);
-        r = __builtin_fmaf(sw, v10, r);
-        res[i] = __builtin_fmaf(se, v11, r);
-      }
-    }
-    __syncthreads();   // every tap read: the staging becomes the output tile [K][QB]
-#pragma unroll
-    for (int i = 0; i < NKT; ++i) {
-      const int k = cls + i * C::NCLS;
-      if (k < K) cells[k * QB + qq] = res[i];
-    }
-    __syncthreads();
-    float* ob0 = out + ((long long)b * g.cout + (long long)l * K) * g.N;
-    const bool vec = (g.N & 3) == 0 && q0 + QB <= g.N;
-    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-        ob0, (short)0, 0x7fffffff, 0x00020000);
-    for (int e = tid; e < K * QB / 4; e += NT_) {
-      const int k = e / (QB / 4), c4 = e - k * (QB / 4);
-      const float4 v = *reinterpret_cast<const float4*>(cells + k * QB + 4 * c4);
-      if (vec) {
-        typedef float f4v __attribute__((ext_vector_type(4)));
-        __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(u32x4_t, f4v{v.x, v.y, v.z, v.w}), ro,
-            (unsigned)(((long long)k * g.N + q0 + 4 * c4) * 4), 0, 16);
-      } else {
-        const float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (q0 + 4 * c4 + u < g.N)
-            __hip_atomic_store(ob0 + (long long)k * g.N + q0 + 4 * c4 + u, vv[u], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    return;
-  }
   if (q0 + qq >= g.N) return;
   const float* cq = cells + qq * C::QS;
   float* ob = out + ((long long)b * g.cout + (long long)l * K) * g.N + q0 + qq;
@@ -430,7 +375,10 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
     r = __builtin_fmaf(se, v11, r);
     // write-through (sc1) output stores (round 2): the outputs leave the XCD's
     // L2 while the kernel runs instead of as dirty lines the next kernel
-    // boundary writes back (Sintel B=1 9.5 -> 8.5 us, B=8 58.0 -> 54.6 us)
+    // boundary writes back (Sintel B=1 9.5 -> 8.5 us, B=8 58.0 -> 54.6 us).
+    // Round 4: routing them through LDS as 16-byte stores of 4 queries was
+    // slower in the step (Sintel B=1 237.9 vs 222.8 us, B=8 1,623 vs 1,583 us,
+    // KITTI B=8 bf16 1,268 vs 1,193 us).
     __hip_atomic_store(ob + (unsigned)(k * g.N), r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }

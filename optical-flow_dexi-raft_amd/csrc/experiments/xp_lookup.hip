@@ -195,11 +195,11 @@ int xp_launch(const PT* pyr, const float* coords, float* out, const LookupGeom& 
 
 // The product kernel with another workgroup shape: NT threads x QB queries
 // (the same 16 threads per query as the product's 512 x 32).
-template <int NT, int QB, bool TS = false, typename PT>
+template <int NT, int QB, typename PT>
 int xp_shape(const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
              hipStream_t stream) {
   const dim3 grid((unsigned)((g.N + QB - 1) / QB), (unsigned)g.levels, (unsigned)B);
-  hipLaunchKernelGGL((corr_lookup_wide_kernel<4, PT, NT, QB, TS>), grid, dim3(NT), 0, stream, pyr,
+  hipLaunchKernelGGL((corr_lookup_wide_kernel<4, PT, NT, QB>), grid, dim3(NT), 0, stream, pyr,
                      coords, out, g);
   return dxr::launch_status();
 }
@@ -210,8 +210,6 @@ int xp_dispatch(int xp, const PT* pyr, const float* coords, float* out, const Lo
   switch (xp) {
     case 64: return xp_shape<256, 16>(pyr, coords, out, g, B, stream);
     case 128: return xp_shape<1024, 64>(pyr, coords, out, g, B, stream);
-    case 512: return xp_shape<512, 32, true>(pyr, coords, out, g, B, stream);
-    case 576: return xp_shape<256, 16, true>(pyr, coords, out, g, B, stream);
     case 0: return xp_launch<0>(pyr, coords, out, g, B, trace, stream);
     case 1: return xp_launch<1>(pyr, coords, out, g, B, trace, stream);
     case 2: return xp_launch<2>(pyr, coords, out, g, B, trace, stream);

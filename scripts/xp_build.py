@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--split", type=int, nargs="*", default=[0, 1, 2, 3, 4],
                     help="split-pass variants timed alone (dxr_xp_split)")
+    ap.add_argument("--trace-xp", type=int, nargs="*", default=[256, 257],
+                    help="traced variants (bit 8 set): per-workgroup timeline summary")
     a = ap.parse_args()
     import dexiraft_amd
     from dexiraft_amd import _native as nat
@@ -122,7 +124,7 @@ def main():
                     sres[v].append(e0.elapsed_time(e1) * 1e3 / a.reps)
             print(json.dumps({"split_us_min_med": {v: [round(min(t), 2), round(float(np.median(t)), 2)]
                                                    for v, t in sres.items()}}), flush=True)
-        for x in (256, 257):
+        for x in a.trace_xp:
             for _ in range(3):
                 graphs[a.xp[0]].replay()
             launch(x)
@@ -138,6 +140,20 @@ def main():
                 "epilogue_p10_p50_p90": [round(float(np.percentile(ep, q)), 2) for q in (10, 50, 90)],
                 "first_round_end_p50": round(float(np.percentile(s[:512, 2], 50)), 2),
                 "distinct_hw_ids": int(len(np.unique(cu)))}), flush=True)
+            # co-residence of the first dispatch round: workgroups that started
+            # within 2 us of the first, grouped by CU (xcc, se, sh, cu of HW_ID)
+            hw = t[:, 3]
+            key = ((hw >> 32) & 7) * 4096 + ((hw >> 8) & 0xFF)
+            first = np.where(s[:, 0] < 2.0)[0]
+            groups = {}
+            for wg in first:
+                groups.setdefault(int(key[wg]), []).append(int(wg))
+            d = [g2[1] - g2[0] for g2 in groups.values() if len(g2) == 2]
+            print(json.dumps({"variant": x, "first_round_wgs": int(len(first)),
+                              "cus": len(groups),
+                              "pair_blockidx_delta_hist": {str(k): int(v) for k, v in
+                                                           zip(*np.unique(d, return_counts=True))}
+                              if d else {}}), flush=True)
 
 
 if __name__ == "__main__":
