@@ -20,14 +20,8 @@
 // MFMA waves that run v_mfma_f32_32x32x16_bf16 with six products (the f32-class
 // split of dxr_common.h split8) against the fmap operand, which comes pre-split
 // from a pack pass, one 1 KiB-contiguous record block per wave and k-step.
-// Chunks of k-blocks (split K, so ~256 workgroups fill the chip) add into the
-// output in chunk order inside the kernel (round 4): chunk 0 stores its sums,
-// chunk c waits for chunk c-1's flag, adds its sums to what is there and raises
-// its own flag — ((p0 + p1) + p2) + p3, the order of round 3's chunk_sum_kernel
-// over a partial-sum workspace (28.8 MB at Sintel), bit for bit, with no such
-// workspace.  Used only when every workgroup of the launch is resident at once
-// (one per CU: a waiting chunk never waits on one that cannot start); otherwise
-// the partial sums and chunk_sum_kernel remain.
+// Chunks of k-blocks (split K, so ~256 workgroups fill the chip) write partial
+// sums that a last pass adds in a fixed order: deterministic.
 #include <cmath>
 #include <type_traits>
 
@@ -276,20 +270,10 @@ __device__ __forceinline__ long long xcd_linear(long long w, long long nwg) {
 // MFMAs.  One barrier per stage: at barrier st the fold waves have published
 // stage st and the MFMA waves have finished stage st-1, whose buffer the fold
 // waves fill next.
-// CHAIN: `out` is the final gradient and chunks add into it in order, handing
-// over through flags[(b * nslab + slab) * nblk + nb] (zeroed by the split pass):
-// chunk c waits until its flag reads c, adds, then stores c + 1.  The producer
-// side is the guide's release pattern (every storing wave's vmcnt(0), the
-// workgroup barrier, one lane's agent release fence, a vmcnt(0) the compiler
-// cannot drop, a relaxed agent flag store); the consumer polls with relaxed
-// agent loads, then an agent acquire fence and a barrier before any load of the
-// output.  A poll that sees nothing for 200 ms gives up (the sums are then
-// wrong, never a hang).
-template <bool KT, bool DIV, bool CHAIN = false>
+template <bool KT, bool DIV>
 __global__ __launch_bounds__(NTHR) void fmap_grad_kernel(const float* __restrict__ gp,
                                                          const uint4* __restrict__ fp,
-                                                         float* __restrict__ out, GradGeom g,
-                                                         int* __restrict__ flags) {
+                                                         float* __restrict__ out, GradGeom g) {
   __shared__ uint4 sb[2][3 * REC];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   long long wl = xcd_linear(blockIdx.x, gridDim.x);
@@ -398,54 +382,25 @@ __global__ __launch_bounds__(NTHR) void fmap_grad_kernel(const float* __restrict
       if (st + 1 < nst) load_a(st + 1, s, A[s]);
     }
   }
-  int* const flag = flags + ((long long)b * g.nslab + slab) * g.nblk + nb;
-  if constexpr (CHAIN) {
-    // the MFMA waves (the fold waves have left) wait for chunk - 1's sums
-    if (chunk > 0) {
-      if (tid == 0) {
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != chunk &&
-               __builtin_amdgcn_s_memrealtime() - t0 < 20000000ull)
-          __builtin_amdgcn_s_sleep(2);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __syncthreads();
-    }
-  }
-  if (active) {
-    // C/D map: column n = lane & 31 (+32 j), row d = (v&3) + 8(v>>2) + 4(lane>>5)
-    float* o = out + ((long long)(CHAIN ? 0 : chunk) * g.B + b) * g.D * g.N;
-    const int ty = nb / g.txn, tx = nb % g.txn;
+  if (!active) return;
+  // C/D map: column n = lane & 31 (+32 j), row d = (v&3) + 8(v>>2) + 4(lane>>5)
+  float* o = out + ((long long)chunk * g.B + b) * g.D * g.N;
+  const int ty = nb / g.txn, tx = nb % g.txn;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int px;
-      if constexpr (KT) {
-        const int q = nb * PQ + 32 * j + (lane & 31);
-        px = q < g.N ? q : -1;
-      } else {
-        const int t = 4 * (lane & 31) + j, y = ty * TH + (t >> 4), x = tx * TW + (t & 15);
-        px = (y < g.H && x < g.W) ? y * g.W + x : -1;
-      }
-      if (px < 0) continue;
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int d = d0 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
-        float r = acc[j][v];
-        if (CHAIN && chunk > 0) r = o[(long long)d * g.N + px] + r;
-        o[(long long)d * g.N + px] = r;
-      }
+  for (int j = 0; j < 4; ++j) {
+    int px;
+    if constexpr (KT) {
+      const int q = nb * PQ + 32 * j + (lane & 31);
+      px = q < g.N ? q : -1;
+    } else {
+      const int t = 4 * (lane & 31) + j, y = ty * TH + (t >> 4), x = tx * TW + (t & 15);
+      px = (y < g.H && x < g.W) ? y * g.W + x : -1;
     }
-  }
-  if constexpr (CHAIN) {
-    if (chunk + 1 < g.S) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(flag, chunk + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+    if (px < 0) continue;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int d = d0 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
+      o[(long long)d * g.N + px] = acc[j][v];
     }
   }
 }
@@ -454,11 +409,7 @@ __global__ __launch_bounds__(NTHR) void fmap_grad_kernel(const float* __restrict
 // TORD: k = target in tile order (tile*128 + row*16 + col); else k = query.
 template <bool TORD>
 __global__ __launch_bounds__(256) void fmap_split_kernel(const float* __restrict__ f,
-                                                         uint4* __restrict__ fp, GradGeom g,
-                                                         int* __restrict__ flags, int nflags) {
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nflags;
-       i += (long long)gridDim.x * blockDim.x)
-    flags[i] = 0;   // the chained GEMM's hand-off flags (stream order publishes them)
+                                                         uint4* __restrict__ fp, GradGeom g) {
   const long long total = (long long)g.B * g.ks * g.D * 2;
   for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (long long)gridDim.x * blockDim.x) {
@@ -542,30 +493,8 @@ void set_kernel(GradGeom* g, bool kt) {
 }
 
 long long operand_bytes(const GradGeom& g) { return align256((long long)g.B * 3 * g.ks * g.D * 32); }
-
-// Compute units of the current device (the chained reduction needs every
-// workgroup resident: one per CU, its LDS takes the CU).
-int device_cus() {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      n = 0;
-    cus = n > 0 ? n : -1;
-  }
-  return cus;
-}
-
-long long grad_workgroups(const GradGeom& g) { return (long long)g.nblk * g.S * g.nslab * g.B; }
-bool chained(const GradGeom& g) { return g.S > 1 && grad_workgroups(g) <= device_cus(); }
-long long flag_count(const GradGeom& g) { return (long long)g.B * g.nslab * g.nblk; }
-
-// Workspace beyond the operand: hand-off flags (chained), or S partial sums.
 long long partial_bytes(const GradGeom& g) {
-  if (g.S <= 1) return 0;
-  if (chained(g)) return align256(flag_count(g) * 4);
-  return align256((long long)g.S * g.B * g.D * g.N * 4);
+  return g.S > 1 ? align256((long long)g.S * g.B * g.D * g.N * 4) : 0;
 }
 
 bool grads_supported(int64_t D, int num_levels) {
@@ -613,34 +542,25 @@ extern "C" int dxr_fmap_grads(const void* grad_pyramid, int grad_dtype, const fl
     if (!src) return DXR_EINVAL;
     set_kernel(&g, kt == 1);
     uint4* fp = static_cast<uint4*>(workspace);
-    const bool chain = chained(g);
-    char* after = static_cast<char*>(workspace) + operand_bytes(g);
-    float* part = g.S > 1 && !chain ? reinterpret_cast<float*>(after) : dst;
-    int* flags = chain ? reinterpret_cast<int*>(after) : nullptr;
-    const int nflags = chain ? (int)flag_count(g) : 0;
-    const long long nwg = grad_workgroups(g);
+    float* part = g.S > 1 ? reinterpret_cast<float*>(static_cast<char*>(workspace) + operand_bytes(g))
+                          : dst;
+    const long long nwg = (long long)g.nblk * g.S * g.nslab * g.B;
     const dim3 pg(grid_for(g.B * g.ks * g.D * 2)), gg((unsigned)nwg);
     const bool div = g.recip == 0.f;
-    auto gemm = [&](auto kt_c, auto div_c, auto chain_c) {
-      constexpr bool KT = decltype(kt_c)::value, DV = decltype(div_c)::value,
-                     CH = decltype(chain_c)::value;
-      hipLaunchKernelGGL((fmap_grad_kernel<KT, DV, CH>), gg, dim3(NTHR), 0, stream, gp, fp, part,
-                         g, flags);
-    };
-    using T = std::true_type;
-    using F = std::false_type;
-    if (kt)
-      hipLaunchKernelGGL(fmap_split_kernel<true>, pg, dim3(256), 0, stream, src, fp, g, flags, nflags);
-    else
-      hipLaunchKernelGGL(fmap_split_kernel<false>, pg, dim3(256), 0, stream, src, fp, g, flags, nflags);
     if (kt) {
-      if (div) { if (chain) gemm(T{}, T{}, T{}); else gemm(T{}, T{}, F{}); }
-      else { if (chain) gemm(T{}, F{}, T{}); else gemm(T{}, F{}, F{}); }
+      hipLaunchKernelGGL(fmap_split_kernel<true>, pg, dim3(256), 0, stream, src, fp, g);
+      if (div)
+        hipLaunchKernelGGL((fmap_grad_kernel<true, true>), gg, dim3(NTHR), 0, stream, gp, fp, part, g);
+      else
+        hipLaunchKernelGGL((fmap_grad_kernel<true, false>), gg, dim3(NTHR), 0, stream, gp, fp, part, g);
     } else {
-      if (div) { if (chain) gemm(F{}, T{}, T{}); else gemm(F{}, T{}, F{}); }
-      else { if (chain) gemm(F{}, F{}, T{}); else gemm(F{}, F{}, F{}); }
+      hipLaunchKernelGGL(fmap_split_kernel<false>, pg, dim3(256), 0, stream, src, fp, g);
+      if (div)
+        hipLaunchKernelGGL((fmap_grad_kernel<false, true>), gg, dim3(NTHR), 0, stream, gp, fp, part, g);
+      else
+        hipLaunchKernelGGL((fmap_grad_kernel<false, false>), gg, dim3(NTHR), 0, stream, gp, fp, part, g);
     }
-    if (g.S > 1 && !chain) {
+    if (g.S > 1) {
       const long long n = (long long)g.B * g.D * g.N;
       hipLaunchKernelGGL(chunk_sum_kernel, dim3(grid_for(n)), dim3(256), 0, stream, part, dst, n, g.S);
     }
