@@ -362,6 +362,10 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
   if (q0 + qq >= g.N) return;
   const float* cq = cells + qq * C::QS;
   float* ob = out + ((long long)b * g.cout + (long long)l * K) * g.N + q0 + qq;
+  // (round 4: unrolled and branch-free over the thread's outputs, every LDS read
+  // issued before the first sum, was slower in the step: Sintel B=1 207.3 vs
+  // 204.7 us, Chairs 102.9 vs 100.5, Sintel B=8 1,541 vs 1,519, KITTI B=8 bf16
+  // 1,136 vs 1,107 us)
   for (int k = cls; k < K; k += C::NCLS) {
     const int ox = k / RD, oy = k - ox * RD;
     const float4 xd = xs[ox * QB + qq], yd = ys[oy * QB + qq];

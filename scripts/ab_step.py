@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--variants", type=int, nargs="+", default=[-1, 32, 64])
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--prev-lib", default=str(REPO / "scripts" / "libdexiraft_corr_prev.so"),
+                    help="variant -3: dxr_corr_lookup of this earlier product library")
     a = ap.parse_args()
     import dexiraft_amd
     from dexiraft_amd import _native as nat
@@ -55,6 +57,11 @@ def main():
     xp.dxr_xp_alt_lookup.restype = i32
     xp.dxr_xp_alt_lookup.argtypes = [vp, ctypes.POINTER(vp), vp, vp, i64, i64, i64, i64, i32,
                                      ctypes.c_float, vp, i32, vp]
+    prev = None
+    if -3 in a.variants:
+        prev = ctypes.CDLL(a.prev_lib)
+        prev.dxr_corr_lookup.restype = i32
+        prev.dxr_corr_lookup.argtypes = [vp, i32, i64, i64, i64, i32, i32, vp, vp, vp]
     dev = torch.device("cuda", 0)
     B, (H, W), D = a.batch, SHAPES[a.workload], 256
     g = torch.Generator(device=dev)
@@ -86,9 +93,10 @@ def main():
                 f_1, f_2, st = cb._launch_build(f1, f2)
                 assert st == 0
                 for c, o in zip(coords, outs):
-                    if v == -1:
-                        st = lib.dxr_corr_lookup(cb._buf.data_ptr(), cb._pyr_dt, B, H, W, 4, 4,
-                                                 c.data_ptr(), o.data_ptr(), s)
+                    if v in (-1, -3):
+                        fn = lib.dxr_corr_lookup if v == -1 else prev.dxr_corr_lookup
+                        st = fn(cb._buf.data_ptr(), cb._pyr_dt, B, H, W, 4, 4, c.data_ptr(),
+                                o.data_ptr(), s)
                     else:
                         st = xp.dxr_xp_lookup(cb._buf.data_ptr(), cb._pyr_dt, B, H, W, 4,
                                               c.data_ptr(), o.data_ptr(), v, None, s)
