@@ -4,6 +4,7 @@
   ws   : dxr_corr_pyramid_build_ws (pre-split pass + LDS-DMA build, round 3)
   nows : dxr_corr_pyramid_build    (register-split build, round 2)
   exact: DXR_BUILD_EXACT_F32       (exact-f32 MFMA build)
+  prev : dxr_corr_pyramid_build_ws of an earlier product library (--prev-lib)
 
 Each variant is captured as a HIP graph of --reps back-to-back builds and the
 graphs are replayed in interleaved rounds after a clock warm-up (HIP events;
@@ -32,10 +33,19 @@ def main():
     ap.add_argument("--layout", default="nchw", choices=["nchw", "nhwc"])
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--prev-lib", default=str(REPO / "scripts" / "libdexiraft_corr_prev.so"))
     a = ap.parse_args()
     import dexiraft_amd
     from dexiraft_amd import _native as nat
     lib = dexiraft_amd.load_native()
+    prev = None
+    if "prev" in a.variants:
+        import ctypes
+        prev = ctypes.CDLL(a.prev_lib)
+        for name, (res, args) in nat.SIGNATURES.items():
+            if hasattr(prev, name):
+                getattr(prev, name).restype = res
+                getattr(prev, name).argtypes = args
     dev = torch.device("cuda", 0)
     D = 256
     stream = torch.cuda.Stream(device=dev)
@@ -58,8 +68,9 @@ def main():
 
         def build(v):
             s = stream.cuda_stream
-            if v == "ws":
-                st = lib.dxr_corr_pyramid_build_ws(f1.data_ptr(), f2.data_ptr(), nat.DXR_F32,
+            if v in ("ws", "prev"):
+                fn = lib if v == "ws" else prev
+                st = fn.dxr_corr_pyramid_build_ws(f1.data_ptr(), f2.data_ptr(), nat.DXR_F32,
                                                    layout, B, D, H, W, 4, div, pyr.data_ptr(),
                                                    nat.DXR_F32, nat.DXR_BUILD_AUTO, ws.data_ptr(),
                                                    wsb, s)
@@ -71,10 +82,15 @@ def main():
             assert st == 0, (v, st)
 
         graphs = {}
+        ref = None
         with torch.cuda.stream(stream):
             for v in a.variants:
                 build(v)
                 torch.cuda.synchronize()
+                if v in ("ws", "prev"):
+                    if ref is None:
+                        ref = pyr.clone()
+                    assert torch.equal(torch.nan_to_num(pyr, nan=3.0), torch.nan_to_num(ref, nan=3.0)), v
                 gr = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gr, stream=stream):
                     for _ in range(a.reps):
