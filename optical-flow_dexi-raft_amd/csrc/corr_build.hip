@@ -70,95 +70,47 @@ struct PageCoord {
 
 constexpr int STRIP = 8;          // default strip width (BuildGeom::strip)
 
-// Position rem of one pair's strip-walking order over its first qtq groups of
-// QB query blocks (strips of g.strip target tiles, query-group-major inside a
-// strip) -> (query block, tile).
-template <int QB>
-__device__ __forceinline__ void strip_coord(const BuildGeom& g, long long rem, int qtq, int& qblk,
-                                            int& tile) {
-  const int T = g.tiles_w * g.tiles_h;
-  const int S = g.strip;
-  const int nfull = T / S;
-  if (rem < (long long)nfull * qtq * S) {
-    const int st = (int)(rem / ((long long)qtq * S));
-    const int in = (int)(rem - (long long)st * qtq * S);
-    qblk = in / S * QB;
-    tile = st * S + in % S;
-  } else {
-    const int nl = T - nfull * S;
-    const int in = (int)(rem - (long long)nfull * qtq * S);
-    qblk = in / nl * QB;
-    tile = nfull * S + in % nl;
-  }
-}
-
-__device__ __forceinline__ PageCoord page_of(const BuildGeom& g, int b, int qblk, int tile) {
-  PageCoord c;
-  c.b = b;
-  c.qblk = qblk;
-  c.txi = tile % g.tiles_w;
-  c.tyi = tile / g.tiles_w;
-  c.page = (((long long)c.b * g.qt + c.qblk) * g.tiles_h + c.tyi) * g.tiles_w + c.txi;
-  return c;
-}
-
 // Position wl of the linear (strip-walking) order -> page coordinates.  QB:
 // query blocks per workgroup (the order walks groups of QB blocks; qblk is the
 // group's first block, page its first page).
 template <int QB>
 __device__ __forceinline__ PageCoord unit_coord(const BuildGeom& g, long long wl) {
+  PageCoord c;
   const int T = g.tiles_w * g.tiles_h;
   const int qtq = (g.qt + QB - 1) / QB;
   const long long per_pair = (long long)qtq * T;
-  const int b = (int)(wl / per_pair);
-  int qblk, tile;
-  strip_coord<QB>(g, wl - b * per_pair, qtq, qblk, tile);
-  return page_of(g, b, qblk, tile);
-}
-
-// The grid's units dealt to the XCDs: XCD k (workgroup w runs on XCD w % 8:
-// round-robin dispatch, used for speed only) takes the k-th contiguous range
-// of the linear order, its workgroups in dispatch order.  QB = 2 with an odd
-// number of query blocks (Sintel: 55): the last group of every target tile
-// holds one block — half the work of a unit — and those half units go last in
-// every XCD's range (round 4: the fourth dispatch round of 512 slots then runs
-// half units, not full ones: Sintel 1,568 units = 3 x 512 + 32).
-template <int QB>
-__device__ __forceinline__ PageCoord remap_coord(const BuildGeom& g) {
-  const long long nwg = (long long)gridDim.x;
-  const long long w = blockIdx.x;
-  const long long q8 = nwg / 8, r8 = nwg % 8, xcd = w % 8, local = w / 8;
-  const long long start = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
-  if constexpr (QB == 2) {
-    if (g.qt & 1) {
-      const int T = g.tiles_w * g.tiles_h;
-      const int qtq = (g.qt + 1) / 2;
-      const long long npairs = nwg / ((long long)qtq * T);
-      const long long H = npairs * T;                    // half units
-      const long long h8 = H / 8, hr = H % 8;
-      const long long hstart = xcd < hr ? xcd * (h8 + 1) : hr * (h8 + 1) + (xcd - hr) * h8;
-      const long long hx = h8 + (xcd < hr ? 1 : 0);
-      const long long count = q8 + (xcd < r8 ? 1 : 0);
-      const long long fx = count - hx;                  // full units of this XCD
-      if (local < fx) {
-        const long long f = (start - hstart) + local;   // full units before + this one
-        const long long per = (long long)(qtq - 1) * T;
-        const int b = (int)(f / per);
-        int qblk, tile;
-        strip_coord<2>(g, f - b * per, qtq - 1, qblk, tile);
-        return page_of(g, b, qblk, tile);
-      }
-      const long long h = hstart + (local - fx);
-      return page_of(g, (int)(h / T), 2 * (qtq - 1), (int)(h % T));
+  {
+    c.b = (int)(wl / per_pair);
+    long long rem = wl - c.b * per_pair;
+    const int S = g.strip;
+    const int nfull = T / S;
+    int tile;
+    if (rem < (long long)nfull * qtq * S) {
+      const int st = (int)(rem / ((long long)qtq * S));
+      const int in = (int)(rem - (long long)st * qtq * S);
+      c.qblk = in / S * QB;
+      tile = st * S + in % S;
+    } else {
+      const int nl = T - nfull * S;
+      const int in = (int)(rem - (long long)nfull * qtq * S);
+      c.qblk = in / nl * QB;
+      tile = nfull * S + in % nl;
     }
+    c.txi = tile % g.tiles_w;
+    c.tyi = tile / g.tiles_w;
   }
-  return unit_coord<QB>(g, start + local);
+  c.page = (((long long)c.b * g.qt + c.qblk) * g.tiles_h + c.tyi) * g.tiles_w + c.txi;
+  return c;
 }
 
 template <bool REMAP, int QB = 1>
 __device__ __forceinline__ PageCoord page_coord(const BuildGeom& g) {
   if constexpr (REMAP) {
-    return remap_coord<QB>(g);
+    const long long nwg = (long long)gridDim.x;
+    const long long w = blockIdx.x;
+    const long long q8 = nwg / 8, r8 = nwg % 8, xcd = w % 8;
+    const long long wl = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + w / 8;
+    return unit_coord<QB>(g, wl);
   } else {
     PageCoord c;
     c.txi = blockIdx.x % g.tiles_w;
