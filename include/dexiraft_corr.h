@@ -399,12 +399,13 @@ int64_t dxr_alt_workspace_bytes(int64_t B, int64_t H, int64_t W, int num_levels)
 
 /*
  * dxr_alt_corr_lookup with a caller-owned workspace (16-byte aligned, at least
- * dxr_alt_workspace_bytes; no initialisation needed).  One extra launch orders
- * each level's queries before the lookup: grouped by window position (bins of
- * ~32 queries) when the 4 x 8 query tiles' union boxes would be larger than
- * 1.5x a bin group's (flows that vary pixel to pixel), else in tile order.  The
- * outputs are the workspace-less call's, bit for bit.  Three small launches
- * (count, scan, scatter) precede the lookup.  Falls back to
+ * dxr_alt_workspace_bytes; no initialisation needed).  Three small launches
+ * (count, scan, scatter) order each level's queries before the lookup: grouped
+ * by window position (bins of ~32 queries) when the 4 x 8 query tiles' union
+ * boxes would be larger than 1.5x a bin group's (flows that vary pixel to
+ * pixel), else in tile order.  The scan always walks the fixed 64 x 4097-bin
+ * histogram, so the three launches cost a few microseconds even for small
+ * maps.  The outputs are the workspace-less call's, bit for bit.  Falls back to
  * dxr_alt_corr_lookup when the workspace is NULL or short.  Replaces
  * core/corr.py:74-91 as above.  ABI 6.
  */
