@@ -77,7 +77,7 @@ extern "C" {
 /* HIP's own definition; repeating an identical typedef is legal in C11/C++. */
 typedef struct ihipStream_t* hipStream_t;
 
-#define DXR_ABI_VERSION 7
+#define DXR_ABI_VERSION 8
 
 enum dxr_status {
   DXR_OK = 0,
@@ -257,6 +257,23 @@ int dxr_corr_lookup_backward_multi(const float* const* coords, const float* cons
                                    int grad_dtype, hipStream_t stream);
 
 /*
+ * dxr_corr_lookup_backward_multi that also records a magnitude bound of the
+ * gradient pyramid for dxr_fmap_grads_bounded: every workgroup keeps the largest
+ * |value| it writes (non-finite values count as +inf) in its own element of
+ * bound_slots, a float32 array of dxr_lookup_backward_bound_slots(B, H, W,
+ * num_levels, radius) elements that the caller zero-fills with the gradient
+ * pyramid (the slot keeps the maximum over calls).  The gradient pyramid is the
+ * one dxr_corr_lookup_backward_multi writes, bit for bit.  ABI 8.
+ */
+int64_t dxr_lookup_backward_bound_slots(int64_t B, int64_t H, int64_t W, int num_levels,
+                                        int radius);
+int dxr_corr_lookup_backward_multi_bound(const float* const* coords,
+                                         const float* const* grad_out, int n_sets,
+                                         int64_t B, int64_t H, int64_t W, int num_levels,
+                                         int radius, void* grad_pyramid, int grad_dtype,
+                                         float* bound_slots, hipStream_t stream);
+
+/*
  * Stage (c) fused with the motion encoder's 1x1 convolution (SURVEY.md §8(f)
  * row 2; inference):
  *   out[b,o,h,w] = act(bias[o] + sum_c weight[o,c] * lookup(coords)[b,c,h,w])
@@ -320,6 +337,28 @@ int dxr_fmap_grads(const void* grad_pyramid, int grad_dtype, const float* fmap1,
                    const float* fmap2, int64_t B, int64_t D, int64_t H, int64_t W,
                    int num_levels, float divisor, float* grad_fmap1, float* grad_fmap2,
                    void* workspace, int64_t workspace_bytes, hipStream_t stream);
+
+/*
+ * dxr_fmap_grads given a bound on the gradient pyramid: bound_slots[0..n_slots)
+ * (device float32, e.g. dxr_corr_lookup_backward_multi_bound's slots) hold
+ * values whose maximum is >= max |grad_pyramid|.  Both operands then run as
+ * power-of-two-scaled f16 pairs (x 2^s = hi + lo, |x 2^s| < 2^14; one scale per
+ * fmap channel, one for the folded dV) with three f16 MFMA products and f32
+ * accumulation — half the MFMA work of the six-product split, f32-class:
+ * per-operand error <= 2^-22 |x| + 2^-39 of its scale's bound.  A pair whose
+ * fmap holds inf/NaN, or a non-finite bound, runs the six-product arithmetic of
+ * dxr_fmap_grads (same IEEE propagation).  A bound below the true maximum gives
+ * wrong (overflowed) results.  workspace: >= dxr_fmap_grads_bounded_workspace_bytes
+ * (<= dxr_fmap_grads_workspace_bytes, which covers both forms).  Same outputs'
+ * layout, deterministic.  ABI 8.
+ */
+int64_t dxr_fmap_grads_bounded_workspace_bytes(int64_t B, int64_t D, int64_t H, int64_t W,
+                                               int num_levels);
+int dxr_fmap_grads_bounded(const void* grad_pyramid, int grad_dtype, const float* fmap1,
+                           const float* fmap2, int64_t B, int64_t D, int64_t H, int64_t W,
+                           int num_levels, float divisor, const float* bound_slots,
+                           int64_t n_slots, float* grad_fmap1, float* grad_fmap2,
+                           void* workspace, int64_t workspace_bytes, hipStream_t stream);
 
 /*
  * 2x2 / stride-2 average pool, floor mode, of [planes, H, W] float32 into

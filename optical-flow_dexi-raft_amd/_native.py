@@ -15,7 +15,7 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_PATH = Path(__file__).resolve().with_name("libdexiraft_corr.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 DXR_OK, DXR_EINVAL, DXR_EUNSUPPORTED, DXR_EHIP = 0, 1, 2, -1
 DXR_F32, DXR_BF16 = 0, 1
@@ -46,10 +46,17 @@ SIGNATURES: dict[str, tuple[object, list[object]]] = {
     "dxr_corr_lookup_backward": (_int, [_vp, _vp, _i64, _i64, _i64, _int, _int, _vp, _int, _vp]),
     "dxr_corr_lookup_backward_multi": (_int, [ctypes.POINTER(_vp), ctypes.POINTER(_vp), _int, _i64,
                                               _i64, _i64, _int, _int, _vp, _int, _vp]),
+    "dxr_lookup_backward_bound_slots": (_i64, [_i64, _i64, _i64, _int, _int]),
+    "dxr_corr_lookup_backward_multi_bound": (_int, [ctypes.POINTER(_vp), ctypes.POINTER(_vp), _int,
+                                                    _i64, _i64, _i64, _int, _int, _vp, _int, _vp,
+                                                    _vp]),
     "dxr_pyramid_backward": (_int, [_vp, _int, _i64, _i64, _i64, _int, _f32, _vp, _vp]),
     "dxr_fmap_grads_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64, _int]),
     "dxr_fmap_grads": (_int, [_vp, _int, _vp, _vp, _i64, _i64, _i64, _i64, _int, _f32, _vp, _vp,
                               _vp, _i64, _vp]),
+    "dxr_fmap_grads_bounded_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64, _int]),
+    "dxr_fmap_grads_bounded": (_int, [_vp, _int, _vp, _vp, _i64, _i64, _i64, _i64, _int, _f32, _vp,
+                                      _i64, _vp, _vp, _vp, _i64, _vp]),
     "dxr_alt_corr_forward": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64,
                                     _i64, _int, _vp]),
     "dxr_alt_corr_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64,

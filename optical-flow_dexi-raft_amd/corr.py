@@ -82,12 +82,17 @@ class _GradState:
     so no reference cycle keeps the pyramid (``block._buf``) or the gradient
     pyramid alive after the step: both are freed by refcount."""
 
-    __slots__ = ("geom", "num_levels", "radius", "device", "numel", "grad_pyr", "pending",
-                 "end_hook")
+    __slots__ = ("geom", "num_levels", "radius", "device", "numel", "nslots", "grad_pyr",
+                 "pending", "end_hook")
 
     def __init__(self, geom, num_levels, radius, device, numel):
         self.geom, self.num_levels, self.radius = geom, num_levels, radius
         self.device, self.numel = device, numel
+        B, _, H, W = geom
+        # the lookup backwards' magnitude bound (one float per workgroup), kept
+        # after the gradient pyramid in the same zero-filled buffer
+        self.nslots = max(int(nat.load().dxr_lookup_backward_bound_slots(B, H, W, num_levels,
+                                                                          radius)), 0)
         self.grad_pyr = None
         self.pending = []   # (coords, grad_out) of lookups whose backward is not applied yet
         self.end_hook = False   # an end-of-backward-pass callback is queued
@@ -99,7 +104,8 @@ class _GradState:
         if not self.pending:
             return
         if self.grad_pyr is None:
-            self.grad_pyr = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+            self.grad_pyr = torch.zeros(self.numel + self.nslots, dtype=torch.float32,
+                                        device=self.device)
         B, D, H, W = self.geom
         n = len(self.pending)
         cs = (ctypes.c_void_p * n)(*[c.data_ptr() for c, _ in self.pending])
@@ -107,14 +113,18 @@ class _GradState:
         lib = nat.load()
         try:
             with _Launch(self.device):
-                st = lib.dxr_corr_lookup_backward_multi(cs, gs, n, B, H, W, self.num_levels,
-                                                        self.radius, self.grad_pyr.data_ptr(),
-                                                        nat.DXR_F32, nat.stream_of(self.grad_pyr))
+                st = lib.dxr_corr_lookup_backward_multi_bound(
+                    cs, gs, n, B, H, W, self.num_levels, self.radius, self.grad_pyr.data_ptr(),
+                    nat.DXR_F32, self.slots_ptr(), nat.stream_of(self.grad_pyr))
         finally:
             # never carry (coords, grad_out) entries into another flush, even if
             # the launch failed: a stale entry would be added twice
             self.pending = []
-        nat.check(st, "CorrBlock lookup backward (dxr_corr_lookup_backward_multi)")
+        nat.check(st, "CorrBlock lookup backward (dxr_corr_lookup_backward_multi_bound)")
+
+    def slots_ptr(self):
+        """Device address of the bound slots behind the gradient pyramid."""
+        return self.grad_pyr.data_ptr() + 4 * self.numel
 
     def reset(self):
         """Drop pending lookups and the partial gradient pyramid (a backward pass
@@ -162,13 +172,14 @@ class _BuildGrad(torch.autograd.Function):
         except BaseException:
             gs.reset()
             raise
-        gp, gs.grad_pyr = gs.grad_pyr, None
-        if gp is None:
+        if gs.grad_pyr is None:
             return None, None, None
+        slots = gs.slots_ptr()
+        gp, gs.grad_pyr = gs.grad_pyr, None
         f1, f2 = ctx.saved_tensors
         B, D, H, W = gs.geom
         lib = nat.load()
-        wsb = lib.dxr_fmap_grads_workspace_bytes(B, D, H, W, gs.num_levels)
+        wsb = lib.dxr_fmap_grads_bounded_workspace_bytes(B, D, H, W, gs.num_levels)
         if wsb >= 0:   # the fused MFMA backward: no [B, N, N] dV
             need1, need2 = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
             c1 = f1.contiguous() if need2 else None
@@ -177,11 +188,13 @@ class _BuildGrad(torch.autograd.Function):
             df2 = torch.empty((B, D, H, W), dtype=torch.float32, device=f1.device) if need2 else None
             ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=f1.device)
             with _Launch(gs.device):
-                st = lib.dxr_fmap_grads(gp.data_ptr(), nat.DXR_F32, nat.ptr(c1), nat.ptr(c2),
-                                        B, D, H, W, gs.num_levels, _sqrt_dim(D), nat.ptr(df1),
-                                        nat.ptr(df2),
-                                        ws.data_ptr(), wsb, nat.stream_of(ws))
-            nat.check(st, "CorrBlock backward (dxr_fmap_grads)")
+                # f16 pair GEMMs scaled by the lookups' bound (three MFMA products)
+                st = lib.dxr_fmap_grads_bounded(gp.data_ptr(), nat.DXR_F32, nat.ptr(c1),
+                                                nat.ptr(c2), B, D, H, W, gs.num_levels,
+                                                _sqrt_dim(D), slots, gs.nslots, nat.ptr(df1),
+                                                nat.ptr(df2), ws.data_ptr(), wsb,
+                                                nat.stream_of(ws))
+            nat.check(st, "CorrBlock backward (dxr_fmap_grads_bounded)")
             return df1, df2, None
         # D % 32 != 0 or more than 4 levels: dV, then two GEMMs
         dv = torch.empty((B, H * W, H * W), dtype=torch.float32, device=f1.device)

@@ -22,6 +22,19 @@
 // from a pack pass, one 1 KiB-contiguous record block per wave and k-step.
 // Chunks of k-blocks (split K, so ~256 workgroups fill the chip) write partial
 // sums that a last pass adds in a fixed order: deterministic.
+//
+// Bounded form (round 4, dxr_fmap_grads_bounded): when the caller knows a bound
+// on |G| (the lookup backwards' per-workgroup maxima), both operands run as
+// power-of-two-scaled f16 pairs x = hi + lo (x 2^s < 2^14: hi = RNE_f16(x 2^s),
+// lo = RNE_f16(x 2^s - hi)) — one scale per fmap channel (the GEMM's M rows),
+// one for all of dV (its n columns and k rows) — and three f16 products
+// (lo*hi, hi*lo, hi*hi) replace the six bf16 ones: half the MFMA work and
+// two-thirds of the fold's records.  Error per element <= 2^-22 |x| + 2^-39 of
+// the scale's bound (f16 subnormals keep an absolute step); the scales are
+// undone exactly (ldexp) per output row.  A pair whose fmap has a non-finite
+// channel, or a non-finite bound, runs the six-product path inside the same
+// kernel, splitting the fmap operand from f32 in registers: IEEE propagation as
+// the unbounded form.
 #include <cmath>
 #include <type_traits>
 
@@ -154,6 +167,55 @@ __device__ __forceinline__ float comp(const uint4& v, int e) {
   return u2f(e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w);
 }
 
+// f16 pair of 8 values scaled by 2^e (|x 2^e| < 2^14 by the choice of e).
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split8h(const float (&v)[8], int e, uint4& hi, uint4& lo) {
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float a = __builtin_ldexpf(v[2 * i], e), b = __builtin_ldexpf(v[2 * i + 1], e);
+    const f2v ab = {a, b};
+    const h2v hv = __builtin_convertvector(ab, h2v);
+    const f2v r = {__builtin_fmaf((float)hv[0], -1.f, a), __builtin_fmaf((float)hv[1], -1.f, b)};
+    h[i] = __builtin_bit_cast(uint32_t, hv);
+    l[i] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, h2v));
+  }
+  hi = make_uint4(h[0], h[1], h[2], h[3]);
+  lo = make_uint4(l[0], l[1], l[2], l[3]);
+}
+
+// The 8 fmap values of operand record (k-step s, half h) of channel row `src`
+// (one channel's plane of a pair): TORD, k = target in tile order; else k = query.
+template <bool TORD>
+__device__ __forceinline__ void load_fmap8(const float* __restrict__ src, const GradGeom& g,
+                                           long long s, int h, float (&x)[8]) {
+  auto two4 = [&](const float* p) {   // 16-B aligned: two float4 loads
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+    x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+  };
+  if constexpr (TORD) {
+    const int tile = (int)(s / KSTEPS);
+    const int y = (tile / g.txn) * TH + (int)(s % KSTEPS), xx = (tile % g.txn) * TW + 8 * h;
+    if ((g.W & 3) == 0 && y < g.H && xx + 8 <= g.W) {   // plane and row bases 16-B aligned
+      two4(src + y * g.W + xx);
+      return;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = (y < g.H && xx + e < g.W) ? src[y * g.W + xx + e] : 0.f;
+  } else {
+    const long long q = s * 16 + 8 * h;
+    if ((g.N & 3) == 0 && q + 8 <= g.N) {
+      two4(src + q);
+      return;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = q + e < g.N ? src[q + e] : 0.f;
+  }
+}
+
 // Is every cell of k-block (qb, tile) inside every level (no floor-mode mask,
 // no padding query)?  Then the fold needs no masks, and the coarse levels fold
 // once per level-1 cell instead of once per dV element.
@@ -180,9 +242,24 @@ __device__ __forceinline__ void store_split(const float (&v)[8], int rec, uint4*
 // fold thread's store is lane-contiguous, both free of bank conflicts
 // (the [n][h] order, 32-B lane stride, spent half the LDS cycles in conflicts).  Interior k-blocks: the same arithmetic in the
 // same order (levels absent beyond nlev were loaded as 0, and x + 0.25*0 = x).
-template <bool KT, bool DIV>
+// F16: the records are the f16 pair of dV 2^ev (parts hi, lo) instead of the
+// three-way bf16 split.
+template <bool F16>
+__device__ __forceinline__ void store_rec(const float (&v)[8], int rec, uint4* __restrict__ sb,
+                                          int ev) {
+  if constexpr (F16) {
+    uint4 hi, lo;
+    split8h(v, ev, hi, lo);
+    sb[rec] = hi;
+    sb[REC + rec] = lo;
+  } else {
+    store_split(v, rec, sb);
+  }
+}
+
+template <bool KT, bool DIV, bool F16 = false>
 __device__ __forceinline__ void fold_store(const GradGeom& g, const Raw<KT>& r, int qb, int tile,
-                                           int half, int lt, uint4* __restrict__ sb) {
+                                           int half, int lt, uint4* __restrict__ sb, int ev = 0) {
   const int y0 = (tile / g.txn) * TH, x0 = (tile % g.txn) * TW;
   const bool inner = interior(g, qb, tile);
   auto scale = [&](float t) { return DIV ? t / g.divisor : t * g.recip; };
@@ -212,7 +289,7 @@ __device__ __forceinline__ void fold_store(const GradGeom& g, const Raw<KT>& r, 
               v[e] = fold<DIV>(g, y, x0 + c, qok, comp(r.g0[i >> 2], i & 3),
                                comp(r.g1[c >> 3], (c >> 1) & 3), comp(r.g2, c >> 2), r.g3[c >> 3]);
           }
-          store_split(v, ((2 * k + rr) * 2 + h) * NB + q, sb);
+          store_rec<F16>(v, ((2 * k + rr) * 2 + h) * NB + q, sb, ev);
         }
       }
     };
@@ -245,7 +322,7 @@ __device__ __forceinline__ void fold_store(const GradGeom& g, const Raw<KT>& r, 
             v[i] = fold<DIV>(g, y, x0 + c, qok, comp(r.g0[i], j), r.g1[i][j >> 1], r.g2[i], r.g3[i]);
           }
         }
-        store_split(v, qg * NB + j * 32 + tg, sb);
+        store_rec<F16>(v, qg * NB + j * 32 + tg, sb, ev);
       }
     };
     if (inner)
@@ -405,6 +482,322 @@ __global__ __launch_bounds__(NTHR) void fmap_grad_kernel(const float* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------
+// Bounded form: f16 pair operands, three products (see the file comment).
+// Scales (workspace, int32): [0] dV's exponent ev, [1] 1 when the bound is
+// finite, [2 + b D + d] the exponent of channel d of pair b, or SCALE_BAD when
+// that channel holds a non-finite value.
+constexpr int SCALE_BAD = -2147483647 - 1;
+constexpr int SCALE_TOP = 14;     // |x 2^s| < 2^SCALE_TOP for every |x| <= m
+
+__device__ __forceinline__ int scale_for(float m) {   // m finite, >= 0
+  if (!(m > 0.f)) return 0;
+  int e;
+  (void)__builtin_frexpf(m, &e);
+  const int s = SCALE_TOP - e;
+  return s < -125 ? -125 : (s > 125 ? 125 : s);
+}
+
+// One kernel body for both arithmetics (F16: f16 pairs from the pre-split
+// records `fp`, three products; else the six-product bf16 split with the fmap
+// operand split from f32 (`fsrc`) in registers — the non-finite path).
+template <bool KT, bool DIV, bool F16>
+__device__ __forceinline__ void grad_body(const float* __restrict__ gp, const uint4* __restrict__ fp,
+                                          const float* __restrict__ fsrc,
+                                          const int* __restrict__ scales, float* __restrict__ out,
+                                          const GradGeom& g, uint4* __restrict__ sbase, int nb,
+                                          int chunk, int slab, int b, int ev) {
+  constexpr int NP = F16 ? 2 : 3;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kb0 = (int)((long long)chunk * g.kbt / g.S);
+  const int kb1 = (int)((long long)(chunk + 1) * g.kbt / g.S);
+  const int nst = 2 * (kb1 - kb0);
+  auto stage = [&](int st) { return sbase + (st & 1) * (3 * REC); };
+
+  if (wave >= MW) {  // fold waves (as fmap_grad_kernel)
+    const int lt = tid - MW * 64;
+    auto load = [&](int st, Raw<KT>& r) {
+      const int kb = kb0 + (st >> 1);
+      load_raw<KT>(g, gp, b, KT ? nb : kb, KT ? kb : nb, st & 1, lt, r);
+    };
+    auto fold = [&](int st, const Raw<KT>& r) {
+      const int kb = kb0 + (st >> 1);
+      fold_store<KT, DIV, F16>(g, r, KT ? nb : kb, KT ? kb : nb, st & 1, lt, stage(st), ev);
+    };
+    Raw<KT> r0;
+    if (nst > 0) load(0, r0);
+    if constexpr (KT) {
+      Raw<KT> r1;
+      for (int st = 0; st < nst; st += 2) {
+        load(st + 1, r1);
+        fold(st, r0);
+        __syncthreads();
+        if (st + 2 < nst) load(st + 2, r0);
+        fold(st + 1, r1);
+        __syncthreads();
+      }
+    } else {
+      for (int st = 0; st < nst; ++st) {
+        fold(st, r0);
+        if (st + 1 < nst) load(st + 1, r0);
+        __syncthreads();
+      }
+    }
+    return;
+  }
+
+  const int d0 = slab * DS + wave * 32;
+  const bool active = d0 < g.D;
+  f32x16 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[j][v] = 0.f;
+
+  // F16 records: (((b*2 + p)*ks + k-step)*D + d)*2 + half
+  const long long pstride = g.ks * g.D * 2, kstride = (long long)g.D * 2;
+  const int dl = active ? d0 + (lane & 31) : 0, hl = lane >> 5;
+  const uint4* fa = fp + (long long)b * 2 * pstride + (long long)dl * 2 + hl +
+                    (long long)kb0 * KSTEPS * kstride;
+  const float* plane = fsrc + ((long long)b * g.D + dl) * g.N;
+  const int bl = hl * NB + (lane & 31);
+  uint4 A[HK][NP];
+  auto load_a = [&](int st, int s, uint4 (&a)[NP]) {
+    if constexpr (F16) {
+      const uint4* f = fa + (long long)(st * HK + s) * kstride;
+      a[0] = f[0];
+      a[1] = f[pstride];
+    } else {
+      float x[8];
+      load_fmap8<KT>(plane, g, (long long)kb0 * KSTEPS + st * HK + s, hl, x);
+      dxr::split8(x, a[0], a[1], a[NP - 1]);
+    }
+  };
+  if (active && nst > 0) {
+#pragma unroll
+    for (int s = 0; s < HK; ++s) load_a(0, s, A[s]);
+  }
+  for (int st = 0; st < nst; ++st) {
+    __syncthreads();  // stage st published
+    if (!active) continue;
+    const uint4* sp = stage(st) + bl;
+#pragma unroll
+    for (int s = 0; s < HK; ++s) {
+      if constexpr (F16) {
+        const h8v ah = __builtin_bit_cast(h8v, A[s][0]), al = __builtin_bit_cast(h8v, A[s][1]);
+        h8v th[4], tl[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint4* bp = sp + s * 2 * NB + 32 * j;
+          th[j] = __builtin_bit_cast(h8v, bp[0]);
+          tl[j] = __builtin_bit_cast(h8v, bp[REC]);
+        }
+        // small terms first, the four tiles interleaved
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, th[j], acc[j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, tl[j], acc[j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, th[j], acc[j], 0, 0, 0);
+      } else {
+        const bf8v qh = __builtin_bit_cast(bf8v, A[s][0]), qm = __builtin_bit_cast(bf8v, A[s][1]),
+                   ql = __builtin_bit_cast(bf8v, A[s][NP - 1]);
+        bf8v th[4], tm[4], tl[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint4* bp = sp + s * 2 * NB + 32 * j;
+          th[j] = __builtin_bit_cast(bf8v, bp[0]);
+          tm[j] = __builtin_bit_cast(bf8v, bp[REC]);
+          tl[j] = __builtin_bit_cast(bf8v, bp[2 * REC]);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, tm[j], acc[j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ql, th[j], acc[j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, tl[j], acc[j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, th[j], acc[j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, tm[j], acc[j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, th[j], acc[j], 0, 0, 0);
+      }
+      if (st + 1 < nst) load_a(st + 1, s, A[s]);
+    }
+  }
+  if (!active) return;
+  // undo the scales: row d's exponent + dV's
+  int un[16];
+#pragma unroll
+  for (int v = 0; v < 16; ++v)
+    un[v] = F16 ? -(scales[2 + b * g.D + d0 + (v & 3) + 8 * (v >> 2) + 4 * hl] + ev) : 0;
+  float* o = out + ((long long)chunk * g.B + b) * g.D * g.N;
+  const int ty = nb / g.txn, tx = nb % g.txn;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    int px;
+    if constexpr (KT) {
+      const int q = nb * PQ + 32 * j + (lane & 31);
+      px = q < g.N ? q : -1;
+    } else {
+      const int t = 4 * (lane & 31) + j, y = ty * TH + (t >> 4), x = tx * TW + (t & 15);
+      px = (y < g.H && x < g.W) ? y * g.W + x : -1;
+    }
+    if (px < 0) continue;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int d = d0 + (v & 3) + 8 * (v >> 2) + 4 * hl;
+      o[(long long)d * g.N + px] = F16 ? __builtin_ldexpf(acc[j][v], un[v]) : acc[j][v];
+    }
+  }
+}
+
+template <bool KT, bool DIV>
+__global__ __launch_bounds__(NTHR) void fmap_grad_bounded_kernel(const float* __restrict__ gp,
+                                                                 const uint4* __restrict__ fp,
+                                                                 const float* __restrict__ fsrc,
+                                                                 const int* __restrict__ scales,
+                                                                 float* __restrict__ out, GradGeom g) {
+  __shared__ uint4 sb[2 * 3 * REC];
+  __shared__ int s_ok;
+  const int tid = threadIdx.x;
+  long long wl = xcd_linear(blockIdx.x, gridDim.x);
+  const int nb = (int)(wl % g.nblk);
+  wl /= g.nblk;
+  const int chunk = (int)(wl % g.S);
+  wl /= g.S;
+  const int slab = (int)(wl % g.nslab);
+  const int b = (int)(wl / g.nslab);
+  if (tid == 0) s_ok = scales[1];
+  __syncthreads();
+  for (int i = tid; i < g.D; i += NTHR)
+    if (scales[2 + b * g.D + i] == SCALE_BAD) s_ok = 0;   // same value from every writer
+  __syncthreads();
+  const int ev = scales[0];
+  if (s_ok)
+    grad_body<KT, DIV, true>(gp, fp, fsrc, scales, out, g, sb, nb, chunk, slab, b, ev);
+  else
+    grad_body<KT, DIV, false>(gp, fp, fsrc, scales, out, g, sb, nb, chunk, slab, b, ev);
+}
+
+// Fmap -> f16 pair records of the bounded form, grid (ceil(D / 4), B, slices),
+// 1024 threads: four waves per channel find its max |x| (its scale; float4
+// loads, four in flight per lane), then the workgroup writes its slice of the
+// four channels' records, eight threads per 128-B line.  Workgroup (0, 0) also
+// reduces the bound slots to dV's scale: |dV| <= vfac max|G|.
+template <bool TORD>
+__global__ __launch_bounds__(1024) void fmap_split16_kernel(const float* __restrict__ f,
+                                                            uint4* __restrict__ fp,
+                                                            int* __restrict__ scales,
+                                                            const float* __restrict__ slots,
+                                                            long long n_slots, float vfac, GradGeom g) {
+  __shared__ float pm[16];
+  __shared__ int pbad[16];
+  __shared__ int se[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.y, dbase = blockIdx.x * 4;
+  const int slice = blockIdx.z, nslice = gridDim.z;   // this workgroup's share of the records
+  auto wave_reduce = [&](float m, bool bad) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = __builtin_fmaxf(m, __shfl_xor(m, o));
+    bad = __any(bad);
+    if (lane == 0) {
+      pm[w] = m;
+      pbad[w] = bad;
+    }
+  };
+  auto absmax = [&](float v, float& m, bool& bad) {
+    const float a = __builtin_fabsf(v);
+    if (a <= 3.40282347e38f) m = __builtin_fmaxf(m, a);
+    else bad = true;
+  };
+  {
+    const int d = dbase + (w >> 2), part = w & 3;
+    float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;
+    bool bad = false;
+    if (d < g.D) {
+      const float* src = f + ((long long)b * g.D + d) * g.N;
+      if ((g.N & 3) == 0) {   // 16-B aligned planes: float4 loads, four in flight
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        const int n4 = g.N >> 2;
+        int q = part * 64 + lane;
+        for (; q + 768 < n4; q += 1024) {
+          const float4 a = s4[q], c = s4[q + 256], e = s4[q + 512], h = s4[q + 768];
+          absmax(a.x, m0, bad); absmax(a.y, m1, bad); absmax(a.z, m2, bad); absmax(a.w, m3, bad);
+          absmax(c.x, m0, bad); absmax(c.y, m1, bad); absmax(c.z, m2, bad); absmax(c.w, m3, bad);
+          absmax(e.x, m0, bad); absmax(e.y, m1, bad); absmax(e.z, m2, bad); absmax(e.w, m3, bad);
+          absmax(h.x, m0, bad); absmax(h.y, m1, bad); absmax(h.z, m2, bad); absmax(h.w, m3, bad);
+        }
+        for (; q < n4; q += 256) {
+          const float4 a = s4[q];
+          absmax(a.x, m0, bad); absmax(a.y, m1, bad); absmax(a.z, m2, bad); absmax(a.w, m3, bad);
+        }
+      } else {
+        int p = part * 64 + lane;
+        for (; p + 768 < g.N; p += 1024) {   // four independent loads per step
+          const float v0 = src[p], v1 = src[p + 256], v2 = src[p + 512], v3 = src[p + 768];
+          absmax(v0, m0, bad);
+          absmax(v1, m1, bad);
+          absmax(v2, m2, bad);
+          absmax(v3, m3, bad);
+        }
+        for (; p < g.N; p += 256) absmax(src[p], m0, bad);
+      }
+    }
+    wave_reduce(__builtin_fmaxf(__builtin_fmaxf(m0, m1), __builtin_fmaxf(m2, m3)), bad);
+  }
+  __syncthreads();
+  if (tid < 4) {
+    const float m = __builtin_fmaxf(__builtin_fmaxf(pm[4 * tid], pm[4 * tid + 1]),
+                                    __builtin_fmaxf(pm[4 * tid + 2], pm[4 * tid + 3]));
+    const bool bad = pbad[4 * tid] | pbad[4 * tid + 1] | pbad[4 * tid + 2] | pbad[4 * tid + 3];
+    se[tid] = bad ? SCALE_BAD : scale_for(m);
+    if (slice == 0 && dbase + tid < g.D) scales[2 + b * g.D + dbase + tid] = se[tid];
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && slice == 0) {
+    __syncthreads();   // pm / pbad reused
+    float m = 0.f;
+    bool bad = false;
+    for (long long i = tid; i < n_slots; i += 1024) {
+      const float v = slots[i];
+      if (v <= 3.40282347e38f) m = __builtin_fmaxf(m, v);
+      else bad = true;
+    }
+    wave_reduce(m, bad);
+    __syncthreads();
+    if (tid == 0) {   // (slice-0 workgroup (0, 0) only)
+      float mm = 0.f;
+      bool bb = false;
+      for (int i = 0; i < 16; ++i) {
+        mm = __builtin_fmaxf(mm, pm[i]);
+        bb |= pbad[i] != 0;
+      }
+      const float bound = mm * vfac;
+      const bool ok = !bb && bound <= 3.40282347e38f;
+      scales[0] = ok ? scale_for(bound) : 0;
+      scales[1] = ok ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  const long long pstride = g.ks * g.D * 2;
+  const long long items = g.ks * 8;
+  const long long i0 = items * slice / nslice, i1 = items * (slice + 1) / nslice;
+  for (long long it = i0 + tid; it < i1; it += 1024) {
+    const int h = (int)(it & 1), dd = (int)((it >> 1) & 3);
+    const long long s = it >> 3;
+    const int d = dbase + dd;
+    if (d >= g.D || se[dd] == SCALE_BAD) continue;
+    float x[8];
+    load_fmap8<TORD>(f + ((long long)b * g.D + d) * g.N, g, s, h, x);
+    uint4 hi, lo;
+    split8h(x, se[dd], hi, lo);
+    const long long rec = (((long long)b * 2 * g.ks + s) * g.D + d) * 2 + h;
+    fp[rec] = hi;
+    fp[rec + pstride] = lo;
+  }
+}
+
 // Fmap -> three-way bf16 split operand records in the GEMM's k order.
 // TORD: k = target in tile order (tile*128 + row*16 + col); else k = query.
 template <bool TORD>
@@ -507,19 +900,103 @@ unsigned grid_for(long long total) {
   return (unsigned)(blocks < 1 ? 1 : blocks);
 }
 
+long long scales_bytes(const GradGeom& g) { return align256((2 + (long long)g.B * g.D) * 4); }
+long long operand16_bytes(const GradGeom& g) { return align256((long long)g.B * 2 * g.ks * g.D * 32); }
+
 }  // namespace
 
-extern "C" int64_t dxr_fmap_grads_workspace_bytes(int64_t B, int64_t D, int64_t H, int64_t W,
-                                                  int num_levels) {
+namespace {
+// form 0: dxr_fmap_grads (three-part operand); 1: the bounded form (scales +
+// two-part operand); either adds the chunks' partial sums
+long long grads_workspace(int64_t B, int64_t D, int64_t H, int64_t W, int num_levels, int form) {
   GradGeom g;
   if (!grads_supported(D, num_levels) || !make_geom(B, D, H, W, num_levels, 1.f, &g)) return -1;
   long long ws = 0;
   for (int kt = 0; kt < 2; ++kt) {
     set_kernel(&g, kt == 1);
-    const long long need = operand_bytes(g) + partial_bytes(g);
+    const long long need = (form ? scales_bytes(g) + operand16_bytes(g) : operand_bytes(g)) +
+                           partial_bytes(g);
     if (need > ws) ws = need;
   }
   return ws;
+}
+}  // namespace
+
+// The larger of both forms' workspace (the bounded form needs less: its own query below).
+extern "C" int64_t dxr_fmap_grads_workspace_bytes(int64_t B, int64_t D, int64_t H, int64_t W,
+                                                  int num_levels) {
+  const long long a = grads_workspace(B, D, H, W, num_levels, 0);
+  const long long b = grads_workspace(B, D, H, W, num_levels, 1);
+  return a < b ? b : a;
+}
+
+extern "C" int64_t dxr_fmap_grads_bounded_workspace_bytes(int64_t B, int64_t D, int64_t H,
+                                                          int64_t W, int num_levels) {
+  return grads_workspace(B, D, H, W, num_levels, 1);
+}
+
+extern "C" int dxr_fmap_grads_bounded(const void* grad_pyramid, int grad_dtype, const float* fmap1,
+                                      const float* fmap2, int64_t B, int64_t D, int64_t H, int64_t W,
+                                      int num_levels, float divisor, const float* bound_slots,
+                                      int64_t n_slots, float* grad_fmap1, float* grad_fmap2,
+                                      void* workspace, int64_t workspace_bytes, hipStream_t stream) {
+  if (grad_dtype != DXR_F32) return grad_dtype == DXR_BF16 ? DXR_EUNSUPPORTED : DXR_EINVAL;
+  if (D < 1 || B < 0 || B > 65535 || !(divisor == divisor) || divisor == 0.f) return DXR_EINVAL;
+  if (!grads_supported(D, num_levels)) return DXR_EUNSUPPORTED;
+  GradGeom g;
+  if (!make_geom(B, D, H, W, num_levels, divisor, &g)) return DXR_EINVAL;
+  if (B == 0 || (!grad_fmap1 && !grad_fmap2)) return DXR_OK;
+  if (!grad_pyramid || !workspace || !bound_slots || n_slots < 1) return DXR_EINVAL;
+  if (workspace_bytes < grads_workspace(B, D, H, W, num_levels, 1)) return DXR_EINVAL;
+  const float* gp = static_cast<const float*>(grad_pyramid);
+  // |dV| <= (1 + 1/4 + 1/16 + 1/64) max|G| / divisor (the fold), with headroom
+  const float vfac = 1.34f / __builtin_fabsf(divisor);
+  for (int kt = 1; kt >= 0; --kt) {
+    float* dst = kt ? grad_fmap1 : grad_fmap2;
+    const float* src = kt ? fmap2 : fmap1;
+    if (!dst) continue;
+    if (!src) return DXR_EINVAL;
+    set_kernel(&g, kt == 1);
+    char* w = static_cast<char*>(workspace);
+    int* scales = reinterpret_cast<int*>(w);
+    uint4* fp = reinterpret_cast<uint4*>(w + scales_bytes(g));
+    float* part = g.S > 1 ? reinterpret_cast<float*>(w + scales_bytes(g) + operand16_bytes(g)) : dst;
+    const long long nwg = (long long)g.nblk * g.S * g.nslab * g.B;
+    // ~256 split workgroups: the four channels' records in slices (each slice
+    // recomputes the four maxima, L2 hits after the first)
+    const long long cwg = (g.D + 3) / 4 * (long long)g.B;
+    const unsigned nsl = (unsigned)(cwg >= 256 ? 1 : (256 + cwg - 1) / cwg);
+    const dim3 sg((unsigned)((g.D + 3) / 4), (unsigned)g.B, nsl), gg((unsigned)nwg);
+    const bool div = g.recip == 0.f;
+    if (kt)
+      hipLaunchKernelGGL(fmap_split16_kernel<true>, sg, dim3(1024), 0, stream, src, fp, scales,
+                         bound_slots, (long long)n_slots, vfac, g);
+    else
+      hipLaunchKernelGGL(fmap_split16_kernel<false>, sg, dim3(1024), 0, stream, src, fp, scales,
+                         bound_slots, (long long)n_slots, vfac, g);
+    if (kt) {
+      if (div)
+        hipLaunchKernelGGL((fmap_grad_bounded_kernel<true, true>), gg, dim3(NTHR), 0, stream, gp, fp,
+                           src, scales, part, g);
+      else
+        hipLaunchKernelGGL((fmap_grad_bounded_kernel<true, false>), gg, dim3(NTHR), 0, stream, gp,
+                           fp, src, scales, part, g);
+    } else {
+      if (div)
+        hipLaunchKernelGGL((fmap_grad_bounded_kernel<false, true>), gg, dim3(NTHR), 0, stream, gp,
+                           fp, src, scales, part, g);
+      else
+        hipLaunchKernelGGL((fmap_grad_bounded_kernel<false, false>), gg, dim3(NTHR), 0, stream, gp,
+                           fp, src, scales, part, g);
+    }
+    if (g.S > 1) {
+      const long long n = (long long)g.B * g.D * g.N;
+      hipLaunchKernelGGL(chunk_sum_kernel, dim3(grid_for(n)), dim3(256), 0, stream, part, dst, n, g.S);
+    }
+    const int st = dxr::launch_status();
+    if (st != DXR_OK) return st;
+  }
+  return DXR_OK;
 }
 
 extern "C" int dxr_fmap_grads(const void* grad_pyramid, int grad_dtype, const float* fmap1,

@@ -415,15 +415,24 @@ struct BwSets {
   int n;
 };
 
-// Minimum waves per SIMD by radius: 8 (<= 64 VGPRs) holds r <= 5 without
-// scratch; r = 6 spilled 44 B/lane at that bound and r = 7 / 8 need 86 / 109
+// Minimum waves per SIMD by radius: 8 (<= 64 VGPRs) up to r = 5 — r = 4 then
+// keeps 44 B/lane in scratch (52 with the bound slots; r = 5: 0 / 12) and still
+// ran faster than six waves without a spill (0.323 vs 0.337 ms, Sintel's 12
+// lookups); r = 6 spilled 44 B/lane at that bound and r = 7 / 8 need 86 / 109
 // VGPRs, so r >= 6 asks for 4 (<= 128 VGPRs, no spill).
 constexpr int bw_min_waves(int r) { return r <= 5 ? 8 : 4; }
 
-template <int R>
+// BOUND: also keep, per workgroup, the largest |value| it wrote over all its
+// passes (non-finite values count as +inf) in bound_slots[workgroup] (a plain
+// read-max-write of the workgroup's own slot, so repeated launches over one
+// zero-initialised slot array leave the maximum of all of them): the gradient
+// pyramid's magnitude bound the f16 pair fmap-gradient GEMMs scale by
+// (dxr_fmap_grads_bounded).  Order-free, so deterministic.
+template <int R, bool BOUND = false>
 __global__ __launch_bounds__(512, bw_min_waves(R)) void corr_lookup_backward_kernel(BwSets sets,
                                                                    float* __restrict__ gpyr,
-                                                                   LookupGeom g) {
+                                                                   LookupGeom g,
+                                                                   float* __restrict__ bound_slots) {
   using C = WideCfg<R, 512>;
   constexpr int RD = C::RD, WD = C::WD, RS = C::RS, K = C::K, QB = C::QB, NT = C::NT;
   __shared__ float4 xs[RD * QB];
@@ -432,6 +441,7 @@ __global__ __launch_bounds__(512, bw_min_waves(R)) void corr_lookup_backward_ker
   __shared__ float G[K * QB];              // [k][qq]
   __shared__ float T[QB * WD * RD];        // [qq][cy][ox]
   __shared__ float4 xq[QB * RD];           // xs query-major
+  __shared__ unsigned wbound;              // BOUND: float bits of the running max
 
   const int l = blockIdx.y, b = blockIdx.z;
   const int q0 = blockIdx.x * QB;
@@ -451,6 +461,7 @@ __global__ __launch_bounds__(512, bw_min_waves(R)) void corr_lookup_backward_ker
                                        : 0.f;
     }
   };
+  if (BOUND && threadIdx.x == 0) wbound = 0u;   // published by the pass's first barrier
   load_set(0);
   for (int set = 0; set < sets.n; ++set) {
   if (set > 0) {
@@ -554,15 +565,45 @@ __global__ __launch_bounds__(512, bw_min_waves(R)) void corr_lookup_backward_ker
 #pragma unroll
   for (int i = 0; i < ITER; ++i)
     if (okv[i]) base[offv[i]] = old[i] + accv[i];
+  if constexpr (BOUND) {
+    float m = 0.f;
+#pragma unroll
+    for (int i = 0; i < ITER; ++i)
+      if (okv[i]) {
+        const float a = __builtin_fabsf(old[i] + accv[i]);
+        m = a <= 3.40282347e38f ? __builtin_fmaxf(m, a) : __builtin_inff();
+      }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = __builtin_fmaxf(m, __shfl_xor(m, o));
+    if ((tid & 63) == 0) __hip_atomic_fetch_max(&wbound, __float_as_uint(m), __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  }
+  if constexpr (BOUND) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const long long w = blockIdx.x + (long long)gridDim.x * (blockIdx.y + (long long)gridDim.y * blockIdx.z);
+      bound_slots[w] = __builtin_fmaxf(bound_slots[w], __uint_as_float(wbound));
+    }
   }
 }
 
 template <int R>
-int launch_lookup_backward_r(const BwSets& sets, float* gpyr, const LookupGeom& g, int B,
-                             hipStream_t stream) {
+dim3 lookup_backward_grid(const LookupGeom& g, int B) {
   using W = WideCfg<R, 512>;
-  const dim3 grid((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
-  hipLaunchKernelGGL((corr_lookup_backward_kernel<R>), grid, dim3(512), 0, stream, sets, gpyr, g);
+  return dim3((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
+}
+
+template <int R>
+int launch_lookup_backward_r(const BwSets& sets, float* gpyr, const LookupGeom& g, int B,
+                             float* bound_slots, hipStream_t stream) {
+  const dim3 grid = lookup_backward_grid<R>(g, B);
+  if (bound_slots)
+    hipLaunchKernelGGL((corr_lookup_backward_kernel<R, true>), grid, dim3(512), 0, stream, sets, gpyr,
+                       g, bound_slots);
+  else
+    hipLaunchKernelGGL((corr_lookup_backward_kernel<R, false>), grid, dim3(512), 0, stream, sets,
+                       gpyr, g, bound_slots);
   return dxr::launch_status();
 }
 
@@ -963,7 +1004,7 @@ extern "C" int dxr_corr_lookup(const void* pyramid, int pyr_dtype, int64_t B, in
 
 namespace {
 int lookup_backward(const BwSets& sets, int64_t B, int64_t H, int64_t W, int num_levels, int radius,
-                    void* grad_pyramid, int grad_dtype, hipStream_t stream) {
+                    void* grad_pyramid, int grad_dtype, float* bound_slots, hipStream_t stream) {
   dxr::Levels L;
   if (!dxr::make_levels(B, H, W, num_levels, &L)) return DXR_EINVAL;
   if (radius < 0) return DXR_EINVAL;
@@ -982,15 +1023,15 @@ int lookup_backward(const BwSets& sets, int64_t B, int64_t H, int64_t W, int num
   for (int l = 0; l < L.n; ++l) g.lv[l] = level_addr(L.lay[l]);
   float* gp = static_cast<float*>(grad_pyramid);
   switch (radius) {
-    case 0: return launch_lookup_backward_r<0>(sets, gp, g, (int)B, stream);
-    case 1: return launch_lookup_backward_r<1>(sets, gp, g, (int)B, stream);
-    case 2: return launch_lookup_backward_r<2>(sets, gp, g, (int)B, stream);
-    case 3: return launch_lookup_backward_r<3>(sets, gp, g, (int)B, stream);
-    case 4: return launch_lookup_backward_r<4>(sets, gp, g, (int)B, stream);
-    case 5: return launch_lookup_backward_r<5>(sets, gp, g, (int)B, stream);
-    case 6: return launch_lookup_backward_r<6>(sets, gp, g, (int)B, stream);
-    case 7: return launch_lookup_backward_r<7>(sets, gp, g, (int)B, stream);
-    default: return launch_lookup_backward_r<8>(sets, gp, g, (int)B, stream);
+    case 0: return launch_lookup_backward_r<0>(sets, gp, g, (int)B, bound_slots, stream);
+    case 1: return launch_lookup_backward_r<1>(sets, gp, g, (int)B, bound_slots, stream);
+    case 2: return launch_lookup_backward_r<2>(sets, gp, g, (int)B, bound_slots, stream);
+    case 3: return launch_lookup_backward_r<3>(sets, gp, g, (int)B, bound_slots, stream);
+    case 4: return launch_lookup_backward_r<4>(sets, gp, g, (int)B, bound_slots, stream);
+    case 5: return launch_lookup_backward_r<5>(sets, gp, g, (int)B, bound_slots, stream);
+    case 6: return launch_lookup_backward_r<6>(sets, gp, g, (int)B, bound_slots, stream);
+    case 7: return launch_lookup_backward_r<7>(sets, gp, g, (int)B, bound_slots, stream);
+    default: return launch_lookup_backward_r<8>(sets, gp, g, (int)B, bound_slots, stream);
   }
 }
 }  // namespace
@@ -1002,7 +1043,8 @@ extern "C" int dxr_corr_lookup_backward(const float* coords, const float* grad_o
   sets.coords[0] = coords;
   sets.gout[0] = grad_out;
   sets.n = 1;
-  return lookup_backward(sets, B, H, W, num_levels, radius, grad_pyramid, grad_dtype, stream);
+  return lookup_backward(sets, B, H, W, num_levels, radius, grad_pyramid, grad_dtype, nullptr,
+                         stream);
 }
 
 extern "C" int dxr_corr_lookup_backward_multi(const float* const* coords, const float* const* grad_out,
@@ -1018,7 +1060,50 @@ extern "C" int dxr_corr_lookup_backward_multi(const float* const* coords, const 
     sets.gout[i] = grad_out[i];
   }
   sets.n = n_sets;
-  return lookup_backward(sets, B, H, W, num_levels, radius, grad_pyramid, grad_dtype, stream);
+  return lookup_backward(sets, B, H, W, num_levels, radius, grad_pyramid, grad_dtype, nullptr,
+                         stream);
+}
+
+extern "C" int64_t dxr_lookup_backward_bound_slots(int64_t B, int64_t H, int64_t W, int num_levels,
+                                                   int radius) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, num_levels, &L) || radius < 0 || radius > 8) return -1;
+  if (B > 65535 || H * W > (1LL << 30)) return -1;
+  LookupGeom g;
+  g.N = (int)(H * W);
+  g.levels = num_levels;
+  dim3 d;
+  switch (radius) {
+    case 0: d = lookup_backward_grid<0>(g, (int)B); break;
+    case 1: d = lookup_backward_grid<1>(g, (int)B); break;
+    case 2: d = lookup_backward_grid<2>(g, (int)B); break;
+    case 3: d = lookup_backward_grid<3>(g, (int)B); break;
+    case 4: d = lookup_backward_grid<4>(g, (int)B); break;
+    case 5: d = lookup_backward_grid<5>(g, (int)B); break;
+    case 6: d = lookup_backward_grid<6>(g, (int)B); break;
+    case 7: d = lookup_backward_grid<7>(g, (int)B); break;
+    default: d = lookup_backward_grid<8>(g, (int)B); break;
+  }
+  return (int64_t)d.x * d.y * d.z;
+}
+
+extern "C" int dxr_corr_lookup_backward_multi_bound(const float* const* coords,
+                                                    const float* const* grad_out, int n_sets,
+                                                    int64_t B, int64_t H, int64_t W, int num_levels,
+                                                    int radius, void* grad_pyramid, int grad_dtype,
+                                                    float* bound_slots, hipStream_t stream) {
+  if (n_sets < 0) return DXR_EINVAL;
+  if (n_sets > BW_MAX_SETS) return DXR_EUNSUPPORTED;
+  if (n_sets > 0 && (!coords || !grad_out)) return DXR_EINVAL;
+  if (!bound_slots) return DXR_EINVAL;
+  BwSets sets{};
+  for (int i = 0; i < n_sets; ++i) {
+    sets.coords[i] = coords[i];
+    sets.gout[i] = grad_out[i];
+  }
+  sets.n = n_sets;
+  return lookup_backward(sets, B, H, W, num_levels, radius, grad_pyramid, grad_dtype, bound_slots,
+                         stream);
 }
 
 extern "C" int64_t dxr_conv1x1_packed_bytes(int64_t cout, int64_t cin) {

@@ -88,7 +88,7 @@ def main():
     kern = {}
     for ev in prof.key_averages():
         name = ev.key
-        for key in ("corr_lookup_backward", "pyramid_backward", "fmap_grad_kernel", "fmap_split",
+        for key in ("corr_lookup_backward", "pyramid_backward", "fmap_grad", "fmap_split",
                     "chunk_sum", "corr_build", "split_pairs", "corr_lookup_wide", "Cijk", "gemm",
                     "elementwise", "reduce", "fill"):
             if key in name:

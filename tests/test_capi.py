@@ -44,7 +44,9 @@ def test_header_declares_the_documented_entry_points():
         "dxr_conv1x1_packed_bytes", "dxr_conv1x1_pack_weight", "dxr_corr_lookup_conv1x1",
         "dxr_transpose", "dxr_avg_pool2x2_nhwc", "dxr_alt_workspace_bytes",
         "dxr_alt_corr_lookup_ws", "dxr_fmap_grads_workspace_bytes", "dxr_fmap_grads",
-        "dxr_corr_lookup_backward_multi"}
+        "dxr_corr_lookup_backward_multi", "dxr_lookup_backward_bound_slots",
+        "dxr_corr_lookup_backward_multi_bound", "dxr_fmap_grads_bounded",
+        "dxr_fmap_grads_bounded_workspace_bytes"}
 
 
 def test_library_exports_every_declared_symbol(nat):
@@ -68,7 +70,7 @@ def test_library_is_gfx950_code(nat):
 
 def test_abi_version_and_status_strings(nat):
     lib = nat.load()
-    assert lib.dxr_abi_version() == nat.ABI_VERSION == 7
+    assert lib.dxr_abi_version() == nat.ABI_VERSION == 8
     assert lib.dxr_status_string(0) == b"ok"
     assert lib.dxr_status_string(1) == b"invalid argument"
     assert lib.dxr_status_string(2) == b"unsupported by this build"
@@ -293,3 +295,35 @@ def test_lookup_backward_multi_validation(nat):
     assert fn(arr, nul, 2, 1, 16, 16, 4, 4, P, nat.DXR_F32, None) == nat.DXR_EINVAL
     assert fn(None, None, 0, 1, 16, 16, 4, 4, P, nat.DXR_F32, None) == nat.DXR_OK
     assert fn(arr, arr, 2, 0, 16, 16, 4, 4, P, nat.DXR_F32, None) == nat.DXR_OK
+
+
+def test_bounded_backward_entry_points_validation(nat):
+    lib = nat.load()
+    P = 1 << 12
+    # one slot per lookup-backward workgroup: 32 (r = 4) queries x level x pair
+    for B, H, W, L, r in ((1, 55, 128, 4, 4), (2, 23, 37, 3, 3), (1, 16, 16, 4, 8)):
+        n = lib.dxr_lookup_backward_bound_slots(B, H, W, L, r)
+        assert n > 0 and n % (L * B) == 0 and (n // (L * B)) * 64 >= H * W
+    assert lib.dxr_lookup_backward_bound_slots(1, 16, 16, 4, 9) == -1
+    assert lib.dxr_lookup_backward_bound_slots(1, 0, 16, 4, 4) == -1
+    arr = (ctypes.c_void_p * 17)(*([P] * 17))
+    fb = lib.dxr_corr_lookup_backward_multi_bound
+    assert fb(arr, arr, 2, 1, 16, 16, 4, 4, P, nat.DXR_F32, None, None) == nat.DXR_EINVAL  # no slots
+    assert fb(arr, arr, 17, 1, 16, 16, 4, 4, P, nat.DXR_F32, P, None) == nat.DXR_EUNSUPPORTED
+    assert fb(arr, arr, 2, 1, 16, 16, 4, 9, P, nat.DXR_F32, P, None) == nat.DXR_EUNSUPPORTED
+    assert fb(arr, arr, 2, 0, 16, 16, 4, 4, P, nat.DXR_F32, P, None) == nat.DXR_OK
+    fg = lib.dxr_fmap_grads_bounded
+    bw = lib.dxr_fmap_grads_bounded_workspace_bytes
+    for B, D, H, W in ((1, 256, 55, 128), (2, 64, 23, 37), (8, 256, 47, 156), (1, 288, 46, 62)):
+        assert 0 < bw(B, D, H, W, 4) < _fmap_grads_ws(B, D, H, W)
+        assert lib.dxr_fmap_grads_workspace_bytes(B, D, H, W, 4) == _fmap_grads_ws(B, D, H, W)
+    assert bw(1, 48, 55, 128, 4) == -1
+    ws = bw(1, 256, 16, 16, 4)
+    assert fg(P, 0, P, P, 1, 256, 16, 16, 4, 0.0, P, 1, P, P, P, ws, None) == nat.DXR_EINVAL
+    assert fg(P, 1, P, P, 1, 256, 16, 16, 4, 16.0, P, 1, P, P, P, ws, None) == nat.DXR_EUNSUPPORTED
+    assert fg(P, 0, P, P, 1, 48, 16, 16, 4, 16.0, P, 1, P, P, P, ws, None) == nat.DXR_EUNSUPPORTED
+    assert fg(P, 0, P, P, 1, 256, 16, 16, 4, 16.0, None, 1, P, P, P, ws, None) == nat.DXR_EINVAL
+    assert fg(P, 0, P, P, 1, 256, 16, 16, 4, 16.0, P, 0, P, P, P, ws, None) == nat.DXR_EINVAL
+    assert fg(P, 0, P, P, 1, 256, 16, 16, 4, 16.0, P, 1, P, P, P, ws - 1, None) == nat.DXR_EINVAL
+    assert fg(None, 0, None, None, 0, 256, 16, 16, 4, 16.0, None, 0, None, None, None, 0,
+              None) == nat.DXR_OK

@@ -249,3 +249,139 @@ def test_partial_backward_pass_does_not_leak(dx):
     g1, g2 = run(False)
     p1, p2 = run(True)
     assert torch.equal(g1, p1) and torch.equal(g2, p2)
+
+
+# ---------------------------------------------------------------------------
+# Bounded form (dxr_fmap_grads_bounded): f16 pair operands scaled by a bound on
+# |G|, three MFMA products; the six-product arithmetic for non-finite inputs.
+
+def _bounded(nat, gp, f1, f2, L, div, slots, want=(True, True)):
+    lib = nat.load()
+    B, D, H, W = f1.shape
+    wsb = lib.dxr_fmap_grads_bounded_workspace_bytes(B, D, H, W, L)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=DEV)
+    df1 = torch.full_like(f1, float("nan")) if want[0] else None
+    df2 = torch.full_like(f2, float("nan")) if want[1] else None
+    st = lib.dxr_fmap_grads_bounded(gp.data_ptr(), nat.DXR_F32, f1.data_ptr(), f2.data_ptr(), B, D,
+                                    H, W, L, div, slots.data_ptr(), slots.numel(), nat.ptr(df1),
+                                    nat.ptr(df2), ws.data_ptr(), wsb, nat.stream_of(f1))
+    nat.check(st, "dxr_fmap_grads_bounded")
+    return df1, df2
+
+
+def _slots(gp, factor=1.0, n=7):
+    """n bound slots whose max is factor * max|gp| (the rest smaller)."""
+    m = gp.abs().max().float() * factor
+    return torch.stack([m * (0.5 ** k) for k in range(n)][::-1]).contiguous()
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("factor", [1.0, 3000.0])
+def test_fmap_grads_bounded_match_volume_gradient_gemms(dx, shape, factor):
+    """f32 class: within 1e-5 of max|grad| of float64 and within 4x of what float32
+    BLAS on the same dV gets, for a tight bound and a 3000x loose one."""
+    nat = _nat()
+    B, D, H, W, L = shape
+    f1 = torch.from_numpy(dg.fmap(900 + D, B, D, H, W, "fnet")).to(DEV)
+    f2 = torch.from_numpy(dg.fmap(901 + D, B, D, H, W, "fnet")).to(DEV)
+    div = float(np.sqrt(np.float32(D), dtype=np.float32))
+    gp = _grad_pyramid(nat, B, H, W, L, seed=B * 1000 + H)
+    g1, g2 = _bounded(nat, gp, f1, f2, L, div, _slots(gp, factor))
+    dv = _volume_grad(nat, gp, B, H, W, L, div)
+    N = H * W
+    r1 = torch.bmm(f2.reshape(B, D, N).double(), dv.double().transpose(1, 2)).reshape(B, D, H, W)
+    r2 = torch.bmm(f1.reshape(B, D, N).double(), dv.double()).reshape(B, D, H, W)
+    b1 = torch.bmm(f2.reshape(B, D, N), dv.transpose(1, 2)).reshape(B, D, H, W)
+    b2 = torch.bmm(f1.reshape(B, D, N), dv).reshape(B, D, H, W)
+    del dv
+    for name, got, ref, blas in (("dfmap1", g1, r1, b1), ("dfmap2", g2, r2, b2)):
+        assert torch.isfinite(got).all(), name
+        scale = ref.abs().max().item()
+        err = (got.double() - ref).abs().max().item()
+        err_blas = (blas.double() - ref).abs().max().item()
+        print(f"{shape} x{factor} {name}: max|err| {err:.3e} (f32 BLAS {err_blas:.3e}) of max {scale:.3e}")
+        assert err <= 1e-5 * scale
+        assert err <= 4 * err_blas + 1e-7 * scale
+
+
+def test_fmap_grads_bounded_deterministic_and_one_sided(dx):
+    nat = _nat()
+    B, D, H, W, L = 1, 128, 30, 44, 4
+    f1 = torch.from_numpy(dg.fmap(911, B, D, H, W)).to(DEV)
+    f2 = torch.from_numpy(dg.fmap(912, B, D, H, W)).to(DEV)
+    gp = _grad_pyramid(nat, B, H, W, L, seed=913)
+    sl = _slots(gp)
+    a1, a2 = _bounded(nat, gp, f1, f2, L, 11.3137, sl)
+    b1, b2 = _bounded(nat, gp, f1, f2, L, 11.3137, sl)
+    assert torch.equal(a1, b1) and torch.equal(a2, b2)
+    c1, none2 = _bounded(nat, gp, f1, f2, L, 11.3137, sl, want=(True, False))
+    none1, c2 = _bounded(nat, gp, f1, f2, L, 11.3137, sl, want=(False, True))
+    assert none1 is None and none2 is None
+    assert torch.equal(a1, c1) and torch.equal(a2, c2)
+
+
+def test_fmap_grads_bounded_non_finite_takes_the_six_product_path(dx):
+    """A NaN gradient cell makes the bound NaN: the whole call runs the
+    six-product arithmetic, so the outputs equal dxr_fmap_grads' bit for bit
+    (NaN exactly in the query's and the target's columns).  An inf in one pair's
+    fmap sends only that pair there; the other pair keeps the f16 form."""
+    nat = _nat()
+    B, D, H, W, L = 1, 64, 24, 40, 4
+    f1 = torch.from_numpy(dg.fmap(921, B, D, H, W)).to(DEV)
+    f2 = torch.from_numpy(dg.fmap(922, B, D, H, W)).to(DEV)
+    q, ty, tx = 37, 5, 17
+    gp = _grad_pyramid(nat, B, H, W, L, seed=923, nan_at=(q, ty, tx))
+    sl = torch.full((3,), float("nan"), device=DEV)
+    g1, g2 = _bounded(nat, gp, f1, f2, L, 8.0, sl)
+    u1, u2 = _fused(nat, gp, f1, f2, L, 8.0)
+    assert torch.equal(torch.isnan(g1), torch.isnan(u1)) and torch.equal(torch.isnan(g2), torch.isnan(u2))
+    assert torch.isnan(g1).sum().item() == D and torch.isnan(g2).sum().item() == D
+    fin = ~torch.isnan(u1)
+    assert torch.equal(g1[fin], u1[fin]) and torch.equal(g2[~torch.isnan(u2)], u2[~torch.isnan(u2)])
+
+    B = 2
+    f1 = torch.from_numpy(dg.fmap(924, B, D, H, W)).to(DEV)
+    f2 = torch.from_numpy(dg.fmap(925, B, D, H, W)).to(DEV)
+    f2[1, 3, 4, 5] = float("inf")
+    gp = _grad_pyramid(nat, B, H, W, L, seed=926)
+    g1, _ = _bounded(nat, gp, f1, f2, L, 8.0, _slots(gp), want=(True, False))
+    u1, _ = _fused(nat, gp, f1, f2, L, 8.0, want=(True, False))
+    assert torch.equal(torch.isnan(g1[1]), torch.isnan(u1[1]))
+    assert torch.equal(torch.isinf(g1[1]), torch.isinf(u1[1]))
+    same = torch.isfinite(u1[1])
+    assert torch.equal(g1[1][same], u1[1][same])          # pair 1: six-product path
+    assert torch.isfinite(g1[0]).all() and not torch.equal(g1[0], u1[0])   # pair 0: f16 pairs
+    assert (g1[0] - u1[0]).abs().max().item() <= 1e-5 * u1[0].abs().max().item()
+
+
+@pytest.mark.parametrize("r", [4, 3])
+def test_lookup_backward_multi_bound_slots(dx, r):
+    """The bound form writes the same gradient pyramid bit for bit, and its slots'
+    maximum bounds max|G| (it is the largest value any pass wrote)."""
+    import ctypes
+    nat = _nat()
+    lib = nat.load()
+    B, H, W, L = 2, 30, 44, 4
+    n = 6
+    K = L * (2 * r + 1) ** 2
+    cs = [torch.from_numpy(dg.coords(1260 + k, B, H, W, "normal", 3.0 + k)).to(DEV) for k in range(n)]
+    gs = [torch.from_numpy(dg.fmap(1270 + k, B, K, H, W)).to(DEV) for k in range(n)]
+    numel = lib.dxr_pyramid_numel(B, H, W, L)
+    nsl = lib.dxr_lookup_backward_bound_slots(B, H, W, L, r)
+    ref = torch.zeros(numel, device=DEV)
+    got = torch.zeros(numel + nsl, device=DEV)
+    s = nat.stream_of(ref)
+    for lo, hi in ((0, 4), (4, 6)):
+        cp = (ctypes.c_void_p * (hi - lo))(*[c.data_ptr() for c in cs[lo:hi]])
+        gp = (ctypes.c_void_p * (hi - lo))(*[g.data_ptr() for g in gs[lo:hi]])
+        assert lib.dxr_corr_lookup_backward_multi(cp, gp, hi - lo, B, H, W, L, r, ref.data_ptr(),
+                                                  nat.DXR_F32, s) == 0
+        assert lib.dxr_corr_lookup_backward_multi_bound(cp, gp, hi - lo, B, H, W, L, r,
+                                                        got.data_ptr(), nat.DXR_F32,
+                                                        got.data_ptr() + 4 * numel, s) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(got[:numel], ref)
+    m = ref.abs().max().item()
+    bound = got[numel:].max().item()
+    assert m > 0 and m <= bound <= 4 * m
+    assert (got[numel:] >= 0).all()
