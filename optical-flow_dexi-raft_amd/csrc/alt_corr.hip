@@ -262,8 +262,11 @@ __device__ __forceinline__ void alt_split8h(const float (&x)[8], uint4& h, uint4
 // entry {query, x, y, -} carrying the query's coordinates, so a workgroup's
 // first global read gives it both.
 // PF: k steps of cell-vector loads kept in flight (a ring of PF register stages).
+// XP (experiments only; 0 in the product): bit 0 feeds the cell vectors' raw
+// bits to the f16 MFMAs instead of splitting them (and skips the non-finite
+// fallback) — a timing ablation of the split's VALU work, results meaningless.
 template <int R, int NRB, int CMAX, bool H2 = false, int MINW = 2, bool BIN = false, int PF = 1,
-          bool DMA = false>
+          bool DMA = false, int XP = 0>
 __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* __restrict__ f1,
                                                                const float* __restrict__ coords,
                                                                float* __restrict__ out,
@@ -544,9 +547,14 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
 #pragma unroll
           for (int rb = 0; rb < NRB; ++rb) {
             const float4 a = ca[rb], b = cb[rb];
-            const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
             uint4 h, l;
-            alt_split8h(x, h, l);
+            if constexpr ((XP & 1) != 0) {
+              h = __builtin_bit_cast(uint4, a);
+              l = __builtin_bit_cast(uint4, b);
+            } else {
+              const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+              alt_split8h(x, h, l);
+            }
             const ah8 th = __builtin_bit_cast(ah8, h), tl = __builtin_bit_cast(ah8, l);
             acc2[rb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc2[rb], 0, 0, 0);
             acc2[rb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc2[rb], 0, 0, 0);
@@ -605,7 +613,8 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
       for (int rb = 0; rb < NRB; ++rb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) bad |= !(__builtin_fabsf(acc[rb][r]) <= 3.40282347e38f);
-      if (__ballot(bad) != 0) kloop(std::integral_constant<bool, false>{});   // wave-uniform
+      if ((XP & 1) == 0 && __ballot(bad) != 0)
+        kloop(std::integral_constant<bool, false>{});   // wave-uniform
     } else {
       kloop(std::integral_constant<bool, false>{});
     }
@@ -915,7 +924,7 @@ long long alt_order_bytes(long long H, long long W) {
 // PF: cell loads of the ordered form kept 4 k steps ahead (round 3: with compact boxes the
 // waves wait on L2 latency, 62 % of wave cycles at PF = 1; 1080p 12 lookups 2,033 -> 1,972 us,
 // Sintel 626 -> 612 us in the step).  The tile-order form stays at 1 (its boxes are L1/TA-bound).
-template <int R, int NRB, bool DMA = false, int PF = 4>
+template <int R, int NRB, bool DMA = false, int PF = 4, int XP = 0>
 int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const AltGeom& g,
                       int levels, int Z, int W1, hipStream_t stream, void* ws = nullptr,
                       int xl = -1) {
@@ -962,7 +971,7 @@ int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const Al
                          dim3(256), 0, stream, f1, coords, out, g, W1, tiles_x,
                          reinterpret_cast<const int4*>(ws), o.list_bytes / 16, XL);
     else
-      hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 3, true, PF>), grid, dim3(256),
+      hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 3, true, PF, false, XP>), grid, dim3(256),
                          0, stream, f1, coords, out, g, W1, tiles_x,
                          reinterpret_cast<const int4*>(ws), o.list_bytes / 16, XL);
     return dxr::launch_status();

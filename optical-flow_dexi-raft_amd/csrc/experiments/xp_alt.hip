@@ -6,7 +6,8 @@
 // variant 0: the ordered lookup with cell loads 1 k step ahead (3 workgroups per
 // CU; the product keeps 4 ahead = variant 3); 1: cell vectors by LDS-DMA into per-wave swizzled buffers (2 per CU);
 // 2 / 3 / 4 / 5: cell loads 2 / 4 / 6 / 8 k steps ahead (register ring); 6 / 7: variant 3
-// with the level-by-XCD workgroup mapping off / on (3 = the product's choice).
+// with the level-by-XCD workgroup mapping off / on (3 = the product's choice); 8: variant 3
+// without the cell vectors' f16 split (a timing ablation).
 // Radius 4, C % 32 == 0, 16-byte aligned NHWC fmaps; ws as dxr_alt_corr_lookup_ws.
 extern "C" int dxr_xp_alt_lookup(const float* fmap1, const float* const* fmap2_levels,
                                  const float* coords, float* out, int64_t B, int64_t H,
@@ -46,6 +47,9 @@ extern "C" int dxr_xp_alt_lookup(const float* fmap1, const float* const* fmap2_l
   if (variant == 5)
     return launch_alt_mfma_r<4, 1, false, 8>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
                                              stream, ws);
+  if (variant == 8)   // variant 3 without the cell split (timing ablation)
+    return launch_alt_mfma_r<4, 1, false, 4, 1>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+                                                stream, ws);
   if (variant == 6 || variant == 7)
     return launch_alt_mfma_r<4, 1, false, 4>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
                                              stream, ws, variant - 6);

@@ -385,3 +385,36 @@ def test_lookup_backward_multi_bound_slots(dx, r):
     bound = got[numel:].max().item()
     assert m > 0 and m <= bound <= 4 * m
     assert (got[numel:] >= 0).all()
+
+
+def test_corr_block_backward_bounded_path_matches_six_products_on_nan(dx):
+    """Training through CorrBlock takes the bounded path; a NaN in one lookup's
+    output gradient makes its bound NaN, so the step falls back to the six-product
+    arithmetic: the fmap gradients equal dxr_fmap_grads' on the same gradient
+    pyramid bit for bit (NaN pattern included)."""
+    import ctypes
+    nat = _nat()
+    lib = nat.load()
+    B, D, H, W, L, r = 1, 64, 24, 40, 4, 4
+    f1 = torch.from_numpy(dg.fmap(1181, B, D, H, W, "fnet")).to(DEV)
+    f2 = torch.from_numpy(dg.fmap(1182, B, D, H, W, "fnet")).to(DEV)
+    cs = [torch.from_numpy(dg.coords(1183 + k, B, H, W, "normal", 3.0)).to(DEV) for k in range(3)]
+    ws = [torch.from_numpy(dg.fmap(1190 + k, B, L * 81, H, W)).to(DEV) for k in range(3)]
+    ws[1][0, 5, 7, 9] = float("nan")
+    a1, a2 = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
+    cb = dx.CorrBlock(a1, a2)
+    sum((cb(c) * w).sum() for c, w in zip(cs, ws)).backward()
+    # the same gradient pyramid by hand, then the unbounded (six-product) form
+    numel = lib.dxr_pyramid_numel(B, H, W, L)
+    gp = torch.zeros(numel, device=DEV)
+    # autograd delivers the lookups' backwards last-created first
+    cp = (ctypes.c_void_p * 3)(*[c.data_ptr() for c in cs[::-1]])
+    gq = (ctypes.c_void_p * 3)(*[w.data_ptr() for w in ws[::-1]])
+    assert lib.dxr_corr_lookup_backward_multi(cp, gq, 3, B, H, W, L, r, gp.data_ptr(), nat.DXR_F32,
+                                              nat.stream_of(gp)) == 0
+    u1, u2 = _fused(nat, gp, f1, f2, L, float(np.sqrt(np.float32(D))))
+    for got, ref in ((a1.grad, u1), (a2.grad, u2)):
+        assert torch.isnan(ref).any()
+        assert torch.equal(torch.isnan(got), torch.isnan(ref))
+        fin = ~torch.isnan(ref)
+        assert torch.equal(got[fin], ref[fin])
