@@ -258,12 +258,14 @@ int dxr_corr_lookup_backward_multi(const float* const* coords, const float* cons
 
 /*
  * dxr_corr_lookup_backward_multi that also records a magnitude bound of the
- * gradient pyramid for dxr_fmap_grads_bounded: every workgroup keeps the largest
- * |value| it writes (non-finite values count as +inf) in its own element of
- * bound_slots, a float32 array of dxr_lookup_backward_bound_slots(B, H, W,
- * num_levels, radius) elements that the caller zero-fills with the gradient
- * pyramid (the slot keeps the maximum over calls).  The gradient pyramid is the
- * one dxr_corr_lookup_backward_multi writes, bit for bit.  ABI 8.
+ * gradient pyramid for dxr_fmap_grads_bounded: every workgroup adds to its own
+ * element of bound_slots (a float32 array of dxr_lookup_backward_bound_slots(B,
+ * H, W, num_levels, radius) elements that the caller zero-fills with the
+ * gradient pyramid) 9 x the largest |grad_out| it reads per set (a cell hears
+ * from at most 3 x 3 samples, tap weights <= 1; non-finite values count as
+ * +inf), so after any number of calls max(bound_slots) >= max |grad_pyramid|.
+ * The gradient pyramid is the one dxr_corr_lookup_backward_multi writes, bit
+ * for bit.  ABI 8.
  */
 int64_t dxr_lookup_backward_bound_slots(int64_t B, int64_t H, int64_t W, int num_levels,
                                         int radius);

@@ -420,14 +420,22 @@ struct BwSets {
 // ran faster than six waves without a spill (0.323 vs 0.337 ms, Sintel's 12
 // lookups); r = 6 spilled 44 B/lane at that bound and r = 7 / 8 need 86 / 109
 // VGPRs, so r >= 6 asks for 4 (<= 128 VGPRs, no spill).
-constexpr int bw_min_waves(int r) { return r <= 5 ? 8 : 4; }
+// (BW_WAVES_SMALL_R: the experiments target rebuilds this file with another
+// value for the r <= 5 bound; the product keeps 8)
+#ifndef BW_WAVES_SMALL_R
+#define BW_WAVES_SMALL_R 8
+#endif
+constexpr int bw_min_waves(int r) { return r <= 5 ? BW_WAVES_SMALL_R : 4; }
 
-// BOUND: also keep, per workgroup, the largest |value| it wrote over all its
-// passes (non-finite values count as +inf) in bound_slots[workgroup] (a plain
-// read-max-write of the workgroup's own slot, so repeated launches over one
-// zero-initialised slot array leave the maximum of all of them): the gradient
-// pyramid's magnitude bound the f16 pair fmap-gradient GEMMs scale by
-// (dxr_fmap_grads_bounded).  Order-free, so deterministic.
+// BOUND: also add to bound_slots[workgroup] a bound on the magnitude of what this
+// launch adds to the workgroup's cells: a cell hears from at most three samples
+// per axis, each with a tap weight <= 1, so per set |added| <= 9 max|grad_out|
+// over the workgroup's queries at its level (non-finite -> +inf).  The sets'
+// maxima are summed in set order and the slot read-add-written (the workgroup
+// owns it), so over zero-initialised slots the slots' maximum bounds max|G|
+// after any number of launches: the gradient pyramid's magnitude bound the f16
+// pair fmap-gradient GEMMs scale by (dxr_fmap_grads_bounded).  Taken from the
+// output gradients as they arrive, off the read-modify-write path; deterministic.
 template <int R, bool BOUND = false>
 __global__ __launch_bounds__(512, bw_min_waves(R)) void corr_lookup_backward_kernel(BwSets sets,
                                                                    float* __restrict__ gpyr,
@@ -441,7 +449,7 @@ __global__ __launch_bounds__(512, bw_min_waves(R)) void corr_lookup_backward_ker
   __shared__ float G[K * QB];              // [k][qq]
   __shared__ float T[QB * WD * RD];        // [qq][cy][ox]
   __shared__ float4 xq[QB * RD];           // xs query-major
-  __shared__ unsigned wbound;              // BOUND: float bits of the running max
+  __shared__ unsigned wmax[BW_MAX_SETS];   // BOUND: float bits of each set's max |grad_out|
 
   const int l = blockIdx.y, b = blockIdx.z;
   const int q0 = blockIdx.x * QB;
@@ -461,7 +469,7 @@ __global__ __launch_bounds__(512, bw_min_waves(R)) void corr_lookup_backward_ker
                                        : 0.f;
     }
   };
-  if (BOUND && threadIdx.x == 0) wbound = 0u;   // published by the pass's first barrier
+  if (BOUND && threadIdx.x < BW_MAX_SETS) wmax[threadIdx.x] = 0u;   // published by the first barrier
   load_set(0);
   for (int set = 0; set < sets.n; ++set) {
   if (set > 0) {
@@ -481,6 +489,18 @@ __global__ __launch_bounds__(512, bw_min_waves(R)) void corr_lookup_backward_ker
   for (int it = 0; it < GIT; ++it) {
     const int i = tid + it * NT;
     if (i < K * QB) G[i] = gv[it];
+  }
+  if constexpr (BOUND) {
+    float m = 0.f;
+#pragma unroll
+    for (int it = 0; it < GIT; ++it) {
+      const float a = __builtin_fabsf(gv[it]);   // padding slots hold 0
+      m = a <= 3.40282347e38f ? __builtin_fmaxf(m, a) : __builtin_inff();
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = __builtin_fmaxf(m, __shfl_xor(m, o));
+    if ((tid & 63) == 0) __hip_atomic_fetch_max(&wmax[set], __float_as_uint(m), __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   __syncthreads();
   if (set + 1 < sets.n) load_set(set + 1);  // in flight during this pass's sums and stores
@@ -520,70 +540,102 @@ __global__ __launch_bounds__(512, bw_min_waves(R)) void corr_lookup_backward_ker
   // Every (query, cell) of the workgroup is a distinct gradient-pyramid element
   // (each query owns its images), so the read-modify-writes are independent:
   // all sums first, then all reads in flight together, then all writes
-  // (round 2; one dependent round trip per element before).
-  constexpr int NE = QB * WD * RS, ITER = (NE + NT - 1) / NT;
-  float accv[ITER];
-  unsigned offv[ITER];
-  bool okv[ITER];
+  // (round 2; one dependent round trip per element before).  Round 4: a thread
+  // takes V consecutive cells of a window row (V = 4 on levels 0-2, whose tile
+  // rows are >= 4 cells; 2 on level 3; 1 on row-major levels): one V-wide load
+  // and store, the V + 2 column candidates read from LDS once.  Cells of the
+  // vector outside the window or the level keep their old bits; each cell's sum
+  // is the one-cell form's, term for term.
+  auto colpass = [&](auto vtag) {
+    constexpr int V = decltype(vtag)::value;
+    constexpr int NGR = RS / V, NE = QB * WD * NGR, ITER = (NE + NT - 1) / NT;
+    typedef float vf __attribute__((ext_vector_type(V)));
+    vf accv[ITER];
+    unsigned offv[ITER], okm[ITER];
 #pragma unroll
-  for (int i = 0; i < ITER; ++i) {
-    const int e = tid + i * NT;
-    okv[i] = false;
-    accv[i] = 0.f;
-    offv[i] = 0u;
-    if (e >= NE) continue;
-    const int qq = e / (WD * RS), rem = e - qq * (WD * RS);
-    const int cy = rem / RS, cx = rem - cy * RS;
-    const int2 o = org[qq];
-    if (q0 + qq >= g.N || o.x == FAR_ORIGIN) continue;
-    // only the WD window columns from o.x can receive gradient (the LDS row starts
-    // at o.x & ~3): the rest would add zero
-    if (cx < (o.x & 3) || cx >= (o.x & 3) + WD) continue;
-    const int yy = o.y + cy, xx = (o.x & ~3) + cx;
-    if ((unsigned)yy >= (unsigned)A.h || (unsigned)xx >= (unsigned)A.w) continue;
-    float acc = 0.f;
-    const float* t = T + (qq * WD + cy) * RD;
-    // col(ox) - (o.x & 3) is ox or ox+1: column cx hears from ox in {c-2, c-1, c}
-    const int c = cx - (o.x & 3);
+    for (int i = 0; i < ITER; ++i) {
+      const int e = tid + i * NT;
+      okm[i] = 0u;
+      offv[i] = 0u;
 #pragma unroll
-    for (int d = 2; d >= 0; --d) {
-      const int ox = c - d;
-      if (ox < 0 || ox >= RD) continue;
-      const float4 xd = xq[qq * RD + ox];
-      const int col = __float_as_int(xd.x);
-      if (col == cx || col + 1 == cx) acc = __builtin_fmaf(t[ox], col == cx ? xd.z : xd.y, acc);
-    }
-    okv[i] = true;
-    accv[i] = acc;
-    offv[i] = (unsigned)(qb0 + qq) * (unsigned)A.S +
-              ((unsigned)((yy >> A.lth) * A.tx + (xx >> A.ltw))) * (unsigned)A.pageS +
-              (unsigned)((yy & A.mh) * A.tw + (xx & A.mw));
-  }
-  float old[ITER];
+      for (int v = 0; v < V; ++v) accv[i][v] = 0.f;
+      if (e >= NE) continue;
+      const int qq = e / (WD * NGR), rem = e - qq * (WD * NGR);
+      const int cy = rem / NGR, cx0 = (rem - cy * NGR) * V;
+      const int2 o = org[qq];
+      if (q0 + qq >= g.N || o.x == FAR_ORIGIN) continue;
+      const int s0 = o.x & 3, c0 = cx0 - s0;   // window column of the vector's first cell
+      const int yy = o.y + cy, xx0 = (o.x & ~3) + cx0;
+      // xx0 is V-aligned: a vector starting left of the level lies wholly off it
+      if ((unsigned)yy >= (unsigned)A.h || xx0 < 0 || xx0 >= A.w) continue;
+      if (c0 + V <= 0 || c0 >= WD) continue;    // no window column in the vector
+      const float* t = T + (qq * WD + cy) * RD;
+      // col(ox) - s0 is ox or ox+1: window column c hears from ox in {c-2, c-1, c}
+      float tk[V + 2];
+      float4 xk[V + 2];
 #pragma unroll
-  for (int i = 0; i < ITER; ++i) old[i] = okv[i] ? base[offv[i]] : 0.f;
-#pragma unroll
-  for (int i = 0; i < ITER; ++i)
-    if (okv[i]) base[offv[i]] = old[i] + accv[i];
-  if constexpr (BOUND) {
-    float m = 0.f;
-#pragma unroll
-    for (int i = 0; i < ITER; ++i)
-      if (okv[i]) {
-        const float a = __builtin_fabsf(old[i] + accv[i]);
-        m = a <= 3.40282347e38f ? __builtin_fmaxf(m, a) : __builtin_inff();
+      for (int k = 0; k < V + 2; ++k) {
+        const int ox = c0 - 2 + k;
+        const bool in = ox >= 0 && ox < RD;
+        tk[k] = in ? t[in ? ox : 0] : 0.f;
+        xk[k] = in ? xq[qq * RD + (in ? ox : 0)] : make_float4(__int_as_float(-100), 0.f, 0.f, 0.f);
       }
+      unsigned m = 0u;
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) m = __builtin_fmaxf(m, __shfl_xor(m, o));
-    if ((tid & 63) == 0) __hip_atomic_fetch_max(&wbound, __float_as_uint(m), __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
+      for (int v = 0; v < V; ++v) {
+        const int cx = cx0 + v, c = c0 + v;
+        if (c < 0 || c >= WD || xx0 + v >= A.w) continue;
+        float acc = 0.f;
+#pragma unroll
+        for (int d = 2; d >= 0; --d) {
+          const int ox = c - d;
+          if (ox < 0 || ox >= RD) continue;
+          const float4 xd = xk[v + 2 - d];
+          const int col = __float_as_int(xd.x);
+          if (col == cx || col + 1 == cx) acc = __builtin_fmaf(tk[v + 2 - d], col == cx ? xd.z : xd.y, acc);
+        }
+        accv[i][v] = acc;
+        m |= 1u << v;
+      }
+      okm[i] = m;
+      offv[i] = (unsigned)(qb0 + qq) * (unsigned)A.S +
+                ((unsigned)((yy >> A.lth) * A.tx + (xx0 >> A.ltw))) * (unsigned)A.pageS +
+                (unsigned)((yy & A.mh) * A.tw + (xx0 & A.mw));
+    }
+    vf old[ITER];
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+      if (okm[i]) {
+        if constexpr (V == 1) old[i][0] = base[offv[i]];
+        else old[i] = *reinterpret_cast<const vf*>(base + offv[i]);
+      } else {
+#pragma unroll
+        for (int v = 0; v < V; ++v) old[i][v] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+      if (!okm[i]) continue;
+      vf nv = old[i];
+#pragma unroll
+      for (int v = 0; v < V; ++v)
+        if (okm[i] & (1u << v)) nv[v] = old[i][v] + accv[i][v];
+      if constexpr (V == 1) base[offv[i]] = nv[0];
+      else *reinterpret_cast<vf*>(base + offv[i]) = nv;
+    }
+  };
+  if (A.lth == 30) colpass(std::integral_constant<int, 1>{});
+  else if (A.tw >= 4) colpass(std::integral_constant<int, 4>{});
+  else if (A.tw == 2) colpass(std::integral_constant<int, 2>{});
+  else colpass(std::integral_constant<int, 1>{});
   }
   if constexpr (BOUND) {
     __syncthreads();
     if (threadIdx.x == 0) {
       const long long w = blockIdx.x + (long long)gridDim.x * (blockIdx.y + (long long)gridDim.y * blockIdx.z);
-      bound_slots[w] = __builtin_fmaxf(bound_slots[w], __uint_as_float(wbound));
+      float t = bound_slots[w];
+      for (int k = 0; k < sets.n; ++k) t += 9.f * __uint_as_float(wmax[k]);
+      bound_slots[w] = t;
     }
   }
 }

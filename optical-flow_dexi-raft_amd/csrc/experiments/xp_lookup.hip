@@ -1,6 +1,9 @@
 // Experiments target only (libdexiraft_corr_exp.so, build.py --experiments):
 // timing ablations and layout variants of the lookup (csrc/corr_lookup.hip).
-// Never loaded by the package.
+// Never loaded by the package.  The lookup backward's r <= 5 launch bound is 6
+// waves per SIMD here (the product: 8), so this library's
+// dxr_corr_lookup_backward_multi[_bound] is that A/B variant.
+#define BW_WAVES_SMALL_R 6
 #include "../corr_lookup.hip"
 
 namespace {

@@ -357,7 +357,7 @@ def test_fmap_grads_bounded_non_finite_takes_the_six_product_path(dx):
 @pytest.mark.parametrize("r", [4, 3])
 def test_lookup_backward_multi_bound_slots(dx, r):
     """The bound form writes the same gradient pyramid bit for bit, and its slots'
-    maximum bounds max|G| (it is the largest value any pass wrote)."""
+    maximum bounds max|G|: each workgroup adds 9 x its largest |grad_out| per set."""
     import ctypes
     nat = _nat()
     lib = nat.load()
@@ -383,7 +383,8 @@ def test_lookup_backward_multi_bound_slots(dx, r):
     assert torch.equal(got[:numel], ref)
     m = ref.abs().max().item()
     bound = got[numel:].max().item()
-    assert m > 0 and m <= bound <= 4 * m
+    top = 9 * sum(g.abs().max().item() for g in gs)
+    assert m > 0 and m <= bound <= top * (1 + 1e-6)
     assert (got[numel:] >= 0).all()
 
 
