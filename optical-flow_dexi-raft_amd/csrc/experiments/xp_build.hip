@@ -175,6 +175,9 @@ __global__ __launch_bounds__(2 * NT, 4) void xp_build_dma_kernel(
   // exponent loads and LDS writes above must not count against the ring's vmcnt
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int nk = g.D / BKS;
+  // XP bit 10: the K loop at wave priority 1 (wins issue arbitration against the
+  // co-resident workgroup's epilogue waves); bit 11: the epilogue at priority 1
+  if constexpr ((XP & 1024) != 0) __builtin_amdgcn_s_setprio(1);
   dma(0);
   if (nk > 1) dma(1);
   for (int ks = 0; ks < nk; ++ks) {
@@ -224,6 +227,8 @@ __global__ __launch_bounds__(2 * NT, 4) void xp_build_dma_kernel(
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();   // ring reads done: the LDS is free for reuse
+  if constexpr ((XP & 1024) != 0) __builtin_amdgcn_s_setprio(0);
+  if constexpr ((XP & 2048) != 0) __builtin_amdgcn_s_setprio(1);
   const unsigned long long xt1 = (XP & 256) ? __builtin_amdgcn_s_memrealtime() : 0ull;
 
   // vote: a non-finite sum means an operand pixel was not finite; the
@@ -1053,6 +1058,8 @@ extern "C" int dxr_xp_build(const float* f1, const float* f2, int64_t B, int64_t
     case 768 + (8 << 12): return xp_dma<768 + (8 << 12)>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     case 768 + (12 << 12): return xp_dma<768 + (12 << 12)>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     case 128: return xp_dma<128>(f1, f2, pyr, g, (int)B, ws, trace, stream);
+    case 1024: return xp_dma<1024>(f1, f2, pyr, g, (int)B, ws, trace, stream);
+    case 2048: return xp_dma<2048>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     case 272: return xp_dma<272>(f1, f2, pyr, g, (int)B, ws, trace, stream);
     default: return DXR_EINVAL;
   }
