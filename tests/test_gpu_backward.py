@@ -419,3 +419,28 @@ def test_corr_block_backward_bounded_path_matches_six_products_on_nan(dx):
         assert torch.equal(torch.isnan(got), torch.isnan(ref))
         fin = ~torch.isnan(ref)
         assert torch.equal(got[fin], ref[fin])
+
+
+@pytest.mark.parametrize("levels,radius,D", [(5, 4, 64), (6, 3, 32), (3, 2, 64)])
+def test_corr_block_backward_other_levels_agree_with_torch(dx, levels, radius, D):
+    """Lookup backwards on row-major levels (>= 4: one-cell column pass) and on
+    fewer tiled levels, through CorrBlock (L > 4 takes the dV + GEMM fallback,
+    L <= 4 the bounded fused GEMMs): against torch autograd of the PyTorch
+    restatement (tests/torch_ref.py)."""
+    from torch_ref import TorchCorrBlock
+    B, H, W = 1, 36, 52
+    f1 = torch.from_numpy(dg.fmap(1331, B, D, H, W, "fnet")).to(DEV)
+    f2 = torch.from_numpy(dg.fmap(1332, B, D, H, W, "fnet")).to(DEV)
+    cs = [torch.from_numpy(dg.coords(1333 + k, B, H, W, "normal", 3.0)).to(DEV) for k in range(5)]
+    K = levels * (2 * radius + 1) ** 2
+    ws = [torch.from_numpy(dg.fmap(1340 + k, B, K, H, W)).to(DEV) for k in range(5)]
+
+    def run(cls):
+        a1, a2 = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
+        cb = cls(a1, a2, num_levels=levels, radius=radius)
+        sum((cb(c) * w).sum() for c, w in zip(cs, ws)).backward()
+        return a1.grad, a2.grad
+
+    for got, ref in zip(run(dx.CorrBlock), run(TorchCorrBlock)):
+        assert torch.isfinite(got).all()
+        assert (got - ref).abs().max().item() <= 1e-4 * ref.abs().max().item()
