@@ -217,10 +217,20 @@ __device__ __forceinline__ void st4(float* p, float a, float b, float c, float d
   *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
 }
 
+// f32 -> output element.  bf16: the hardware conversion (v_cvt_pk_bf16_f32, RNE,
+// NaN stays NaN) — the software RNE of dxr::f32_to_bf16 cost ~6 VALU per value
+// and left the bf16 build VALU-bound (round 4 PMC: 1,850 VALU per wave against
+// 64 MFMAs at KITTI B=8).
 template <typename OT>
 __device__ __forceinline__ OT to_out(float v) {
-  if constexpr (sizeof(OT) == 2) return dxr::f32_to_bf16(v);
+  if constexpr (sizeof(OT) == 2) return (OT)(dxr::cvt_pk_bf16(v, 0.f) & 0xffffu);
   else return v;
+}
+// Two values as one packed word (first in the low half).
+template <typename OT>
+__device__ __forceinline__ uint32_t to_out2(float a, float b) {
+  static_assert(sizeof(OT) == 2, "packed pairs are bf16");
+  return dxr::cvt_pk_bf16(a, b);
 }
 
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
@@ -279,10 +289,10 @@ __device__ __forceinline__ void store8(OT* ub, OT* dst, const float* src) {
   const float4 a = f4(src), c = f4(src + 4);
   if constexpr (sizeof(OT) == 2) {
     u32x4v u;
-    u.x = (uint32_t)to_out<OT>(a.x) | ((uint32_t)to_out<OT>(a.y) << 16);
-    u.y = (uint32_t)to_out<OT>(a.z) | ((uint32_t)to_out<OT>(a.w) << 16);
-    u.z = (uint32_t)to_out<OT>(c.x) | ((uint32_t)to_out<OT>(c.y) << 16);
-    u.w = (uint32_t)to_out<OT>(c.z) | ((uint32_t)to_out<OT>(c.w) << 16);
+    u.x = to_out2<OT>(a.x, a.y);
+    u.y = to_out2<OT>(a.z, a.w);
+    u.z = to_out2<OT>(c.x, c.y);
+    u.w = to_out2<OT>(c.z, c.w);
     epi_put<EX>(ub, dst, u);
   } else {
     epi_put<EX>(ub, dst, f32x4v{a.x, a.y, a.z, a.w});
@@ -393,8 +403,8 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
       epi_put<EX>(pb2, pg2, f32x4v{r0, r1, r2, r3});
     } else {
       u32x2v w;
-      w.x = (uint32_t)to_out<OT>(r0) | ((uint32_t)to_out<OT>(r1) << 16);
-      w.y = (uint32_t)to_out<OT>(r2) | ((uint32_t)to_out<OT>(r3) << 16);
+      w.x = to_out2<OT>(r0, r1);
+      w.y = to_out2<OT>(r2, r3);
       epi_put<EX>(pb2, pg2, w);
     }
   }

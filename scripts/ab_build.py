@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--shapes", nargs="+", default=["1x55x128", "8x55x128", "1x46x62"])
     ap.add_argument("--variants", nargs="+", default=["ws", "nows"])
     ap.add_argument("--layout", default="nchw", choices=["nchw", "nhwc"])
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"],
+                    help="bf16: bf16 fmaps -> bf16 pyramid (variants ws / prev)")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--prev-lib", default=str(REPO / "scripts" / "libdexiraft_corr_prev.so"))
@@ -55,25 +57,28 @@ def main():
         g.manual_seed(7)
         f1 = torch.randn((B, D, H, W), generator=g, device=dev)
         f2 = torch.randn((B, D, H, W), generator=g, device=dev)
+        dt = nat.DXR_F32
+        if a.dtype == "bf16":
+            f1, f2, dt = f1.bfloat16(), f2.bfloat16(), nat.DXR_BF16
         layout = nat.DXR_NCHW
         if a.layout == "nhwc":
             f1 = f1.contiguous(memory_format=torch.channels_last)
             f2 = f2.contiguous(memory_format=torch.channels_last)
             layout = nat.DXR_NHWC
         n = lib.dxr_pyramid_numel(B, H, W, 4)
-        pyr = torch.empty(n, device=dev)
-        wsb = lib.dxr_build_workspace_bytes(nat.DXR_F32, B, D, H, W)
-        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        pyr = torch.empty(n, device=dev, dtype=torch.float32 if dt == nat.DXR_F32 else torch.bfloat16)
+        wsb = lib.dxr_build_workspace_bytes(dt, B, D, H, W)
+        ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
         div = float(np.sqrt(np.float32(D)))
 
         def build(v):
             s = stream.cuda_stream
             if v in ("ws", "prev"):
                 fn = lib if v == "ws" else prev
-                st = fn.dxr_corr_pyramid_build_ws(f1.data_ptr(), f2.data_ptr(), nat.DXR_F32,
+                st = fn.dxr_corr_pyramid_build_ws(f1.data_ptr(), f2.data_ptr(), dt,
                                                    layout, B, D, H, W, 4, div, pyr.data_ptr(),
-                                                   nat.DXR_F32, nat.DXR_BUILD_AUTO, ws.data_ptr(),
-                                                   wsb, s)
+                                                   dt, nat.DXR_BUILD_AUTO, ws.data_ptr(),
+                                                   max(wsb, 0), s)
             else:
                 algo = nat.DXR_BUILD_EXACT_F32 if v == "exact" else nat.DXR_BUILD_AUTO
                 st = lib.dxr_corr_pyramid_build(f1.data_ptr(), f2.data_ptr(), nat.DXR_F32, layout,
@@ -90,7 +95,9 @@ def main():
                 if v in ("ws", "prev"):
                     if ref is None:
                         ref = pyr.clone()
-                    assert torch.equal(torch.nan_to_num(pyr, nan=3.0), torch.nan_to_num(ref, nan=3.0)), v
+                    same = torch.equal(torch.nan_to_num(pyr.float(), nan=3.0),
+                                       torch.nan_to_num(ref.float(), nan=3.0))
+                    assert same, v
                 gr = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gr, stream=stream):
                     for _ in range(a.reps):
@@ -109,7 +116,7 @@ def main():
                     e1.record(stream)
                     torch.cuda.synchronize()
                     res[v].append(e0.elapsed_time(e1) * 1e3 / a.reps)
-        print(json.dumps({"shape": [B, D, H, W], "layout": a.layout,
+        print(json.dumps({"shape": [B, D, H, W], "layout": a.layout, "dtype": a.dtype,
                           "us_per_build_min_med": {v: [round(min(x), 1), round(float(np.median(x)), 1)]
                                                    for v, x in res.items()}}), flush=True)
 
