@@ -356,14 +356,21 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
       const int t = 2 * u + s;
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
-        const float o0 = acc[t][2 * m], o1 = acc[t][2 * m + 1];
-        const float p0 = __shfl_xor(o0, 32), p1 = __shfl_xor(o1, 32);
-        const float t0 = h ? p0 : o0, t1 = h ? p1 : o1;
-        const float b0 = h ? o0 : p0, b1 = h ? o1 : p1;
+        // v_permlane32_swap of a value with itself gives every lane both halves'
+        // values: the lower (row 2t, kh = 0) and the upper (row 2t + 1) — no LDS
+        // shuffle, no selects (round 4; was __shfl_xor + four selects per pair)
+        const auto x0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[t][2 * m]),
+                                                         __float_as_uint(acc[t][2 * m]), false, false);
+        const auto x1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[t][2 * m + 1]),
+                                                         __float_as_uint(acc[t][2 * m + 1]), false, false);
+        const float t0 = __uint_as_float(x0[0]), t1 = __uint_as_float(x1[0]);
+        const float b0 = __uint_as_float(x0[1]), b1 = __uint_as_float(x1[1]);
         l1[s][m] = (((t0 + t1) + b0) + b1) * 0.25f;
       }
-      st4(wl + j * P1 + t * 8 + 4 * h, l1[s][4 * h], l1[s][4 * h + 1], l1[s][4 * h + 2],
-          l1[s][4 * h + 3]);
+      // the lane half's four values by selects (indexing l1 by the runtime h
+      // compiled to an 8-way compare/select chain per value)
+      st4(wl + j * P1 + t * 8 + 4 * h, h ? l1[s][4] : l1[s][0], h ? l1[s][5] : l1[s][1],
+          h ? l1[s][6] : l1[s][2], h ? l1[s][7] : l1[s][3]);
     }
 #pragma unroll
     for (int n = 0; n < 4; ++n)
