@@ -1482,9 +1482,11 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
   if constexpr (!BF) {
     sq = qj < g.N ? ex1[(long long)b * g.N + qj] : 0;
     if (tid < NTGT) {
+      // the target pixel's unscale factor 2^-s (exact: s in [-125, 125])
       const int r = tid >> 4, c = tid & 15;
       const bool in = th0 + r < g.H && tw0 + c < g.W;
-      sexp[tid] = in ? ex2[(long long)b * g.N + (th0 + r) * g.W + tw0 + c] : 0;
+      const int e = in ? ex2[(long long)b * g.N + (th0 + r) * g.W + tw0 + c] : 0;
+      sexp[tid] = __float_as_int(__builtin_ldexpf(1.f, -e));
     }
     if (tid == 0) *redo = 0;
   }
@@ -1604,21 +1606,27 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
     for (int r = 0; r < 16; ++r) bad |= !(__builtin_fabsf(acc[t][r]) <= 3.40282347e38f);
   if (bad) *redo = 1;
   __syncthreads();
-  // undo the pixel scales: acc[t][r] is query qj x tile pixel (row 2t + kh, col r)
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int4* se = reinterpret_cast<const int4*>(sexp + (2 * t + kh) * 16);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int4 s4 = se[u];
-      acc[t][4 * u + 0] = __builtin_ldexpf(acc[t][4 * u + 0], -(sq + s4.x));
-      acc[t][4 * u + 1] = __builtin_ldexpf(acc[t][4 * u + 1], -(sq + s4.y));
-      acc[t][4 * u + 2] = __builtin_ldexpf(acc[t][4 * u + 2], -(sq + s4.z));
-      acc[t][4 * u + 3] = __builtin_ldexpf(acc[t][4 * u + 3], -(sq + s4.w));
-    }
-  }
+  // undo the pixel scales and divide by sqrt(D): acc[t][r] is query qj x tile
+  // pixel (row 2t + kh, col r).  Two multiplies by powers of two (the query's
+  // 2^-sq, with an exact 1/sqrt(D) folded in, and the target's 2^-st from LDS):
+  // exact while the values stay normal, so the same pages as ldexp(acc,
+  // -(sq + st)) * (1/sqrt(D)) — two packed multiplies per pair instead of an
+  // exponent add, an ldexp and a multiply per value (round 4)
   if (live) {   // a half past the last query block has no page (epilogue syncs per wave)
-    scale_acc<DIV>(acc, g);
+    const float qs = DIV ? __builtin_ldexpf(1.f, -sq) : __builtin_ldexpf(g.recip, -sq);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float4* se = reinterpret_cast<const float4*>(sexp + (2 * t + kh) * 16);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 s4 = se[u];
+        acc[t][4 * u + 0] = (acc[t][4 * u + 0] * qs) * s4.x;
+        acc[t][4 * u + 1] = (acc[t][4 * u + 1] * qs) * s4.y;
+        acc[t][4 * u + 2] = (acc[t][4 * u + 2] * qs) * s4.z;
+        acc[t][4 * u + 3] = (acc[t][4 * u + 3] * qs) * s4.w;
+      }
+    }
+    if constexpr (DIV) scale_acc<DIV>(acc, g);
     paged_epilogue<OT, 1 | 4>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0, pyr,
                               g, page, w4, lane);
   }

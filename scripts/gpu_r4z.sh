@@ -3,7 +3,7 @@
 # spill in the f32 DMA build) — build tests, same-process A/B vs the previous
 # library (bit identity asserted), Sintel bench.
 set -u
-O=gpurun_out/r4z
+O=gpurun_out/${RUN_TAG:-r4z}
 mkdir -p "$O"
 export TMPDIR=/tmp
 step() {
