@@ -45,6 +45,7 @@ struct LevelAddr {
   int h, w;                 // true level size
   int lth, ltw, mh, mw;     // tile shifts / masks
   int tw, tx, lqb, qt;
+  int lS, lpS;              // paged levels: log2 S, log2 pageS (shifts, not multiplies)
   long long off, qstride, S, pageS;
 };
 
@@ -65,9 +66,12 @@ LevelAddr level_addr(const dxr::LevelLayout& y) {
     a.lqb = __builtin_ctz(y.qb);
     a.pageS = (long long)y.qb * a.S;
     a.qstride = (long long)y.ty * y.tx * a.pageS;
+    a.lS = __builtin_ctzll(a.S);
+    a.lpS = __builtin_ctzll(a.pageS);
   } else {         // row-major level
     a.lth = 30; a.ltw = 30; a.mh = 0x3fffffff; a.mw = 0x3fffffff;
     a.lqb = 0; a.pageS = 0; a.qstride = a.S;
+    a.lS = a.lpS = -1;
   }
   return a;
 }
@@ -182,13 +186,17 @@ __device__ __forceinline__ void gather_load(const PT* __restrict__ base, int qb0
       const int2 o = org[qq];
       const int yy = o.y + r, x0 = (o.x & ~3) + 4 * k;
       if (o.x != FAR_ORIGIN && (unsigned)yy < (unsigned)A.h && x0 >= 0 && x0 < A.w) {
-        const unsigned qoff = (unsigned)(qb0 + qq) * (unsigned)A.S;
-        const unsigned yoff = (unsigned)(yy >> A.lth) * (unsigned)A.tx;
-        const unsigned yin = (unsigned)((yy & A.mh) * A.tw);
+        // V > 1: a paged level (power-of-two S, pageS, tw): shifts and a 24-bit
+        // multiply instead of quarter-rate 32-bit ones (round 4)
+        const unsigned qoff = V > 1 ? (unsigned)(qb0 + qq) << A.lS : (unsigned)(qb0 + qq) * (unsigned)A.S;
+        const unsigned yoff = V > 1 ? __umul24((unsigned)(yy >> A.lth), (unsigned)A.tx)
+                                    : (unsigned)(yy >> A.lth) * (unsigned)A.tx;
+        const unsigned yin = V > 1 ? (unsigned)(yy & A.mh) << A.ltw : (unsigned)((yy & A.mh) * A.tw);
 #pragma unroll
         for (int h = 0; h < 4; h += V) {
           const int x = x0 + h;
-          const unsigned e = qoff + (yoff + (unsigned)(x >> A.ltw)) * (unsigned)A.pageS + yin +
+          const unsigned tl = yoff + (unsigned)(x >> A.ltw);
+          const unsigned e = qoff + (V > 1 ? tl << A.lpS : tl * (unsigned)A.pageS) + yin +
                              (unsigned)(x & A.mw);
           if (V == 4 || x < A.w) load_vec<V, PT>(base + e, c + h);
         }
@@ -362,6 +370,9 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
   if (q0 + qq >= g.N) return;
   const float* cq = cells + qq * C::QS;
   float* ob = out + ((long long)b * g.cout + (long long)l * K) * g.N + q0 + qq;
+  // output k at ob + k N: a pointer stepped by NCLS N (no per-store multiply)
+  float* op = ob + (long long)cls * g.N;
+  const long long ostep = (long long)C::NCLS * g.N;
   // (round 4: unrolled and branch-free over the thread's outputs, every LDS read
   // issued before the first sum, was slower in the step: Sintel B=1 207.3 vs
   // 204.7 us, Chairs 102.9 vs 100.5, Sintel B=8 1,541 vs 1,519, KITTI B=8 bf16
@@ -383,7 +394,8 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
     // Round 4: routing them through LDS as 16-byte stores of 4 queries was
     // slower in the step (Sintel B=1 237.9 vs 222.8 us, B=8 1,623 vs 1,583 us,
     // KITTI B=8 bf16 1,268 vs 1,193 us).
-    __hip_atomic_store(ob + (unsigned)(k * g.N), r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(op, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    op += ostep;
   }
 }
 
