@@ -1368,20 +1368,31 @@ __global__ __launch_bounds__(1024) void split_pairs_kernel(const float* __restri
         x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
       }
     } else {
+      // channel stride N by 32-bit adds (a pair's plane is < 2^31 elements): no
+      // quarter-rate 64-bit multiply in front of every load
+      unsigned o = (unsigned)(kb * 16) * (unsigned)N + (unsigned)p;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) x[i] = src[(long long)(kb * 16 + i) * N + p];
+      for (int i = 0; i < 16; ++i) {
+        x[i] = src[o];
+        o += (unsigned)N;
+      }
     }
   };
   float x[16];
+  // the pixel's max |x| over finite channels and whether any is not finite
+  // (-1 below): the same value as the one-select-chain form, two ops per channel
   float m = 0.f;
+  bool nonfin = false;
   for (int kb = kb0; kb < nkb && live; kb += 16) {
     load16(kb, x);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const float a = __builtin_fabsf(x[i]);
-      m = (m < 0.f || !(a <= 3.40282347e38f)) ? -1.f : (a > m ? a : m);
+      nonfin |= !(a <= 3.40282347e38f);
+      m = __builtin_fmaxf(m, a <= 3.40282347e38f ? a : 0.f);
     }
   }
+  if (nonfin) m = -1.f;
   red[kb0][pl] = m;
   __syncthreads();
   float mm = 0.f;
