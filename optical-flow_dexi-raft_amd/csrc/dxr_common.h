@@ -123,8 +123,15 @@ __device__ __forceinline__ void split8(const float (&x)[8], uint4& h, uint4& m, 
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const float a = x[2 * e], b = x[2 * e + 1];
-    const uint32_t hp = cvt_pk_bf16(a, b);
-    // an infinite hi keeps mid = lo = 0 (inf - inf would turn +-inf products into NaN)
+    uint32_t hp = cvt_pk_bf16(a, b);
+    // a finite value that rounds past bf16's largest finite (|x| > ~3.39e38)
+    // keeps its truncation as hi, so the pair stays finite and exact
+    if (__builtin_isinf(__uint_as_float(hp << 16)) && !__builtin_isinf(a))
+      hp = (hp & 0xffff0000u) | (__float_as_uint(a) >> 16);
+    if (__builtin_isinf(__uint_as_float(hp & 0xffff0000u)) && !__builtin_isinf(b))
+      hp = (hp & 0xffffu) | (__float_as_uint(b) & 0xffff0000u);
+    // an infinite hi (an infinite input) keeps mid = lo = 0 (inf - inf would
+    // turn +-inf products into NaN)
     const float ha = __uint_as_float(hp << 16), hb = __uint_as_float(hp & 0xffff0000u);
     const float ra = __builtin_isinf(ha) ? 0.f : a - ha, rb = __builtin_isinf(hb) ? 0.f : b - hb;
     const uint32_t mp = cvt_pk_bf16(ra, rb);

@@ -163,6 +163,23 @@ def test_fused_fewer_levels(dx, levels, r):
     tolerance_check(got, _ref64(cb(c), w, b).astype(np.float32), RTOL)
 
 
+def test_fused_weight_above_bf16_max_stays_finite(dx):
+    """A finite weight that rounds to inf in bf16 (3.4e38 > ~3.396e38) keeps a
+    finite hi/mid/lo split (hi = its truncation), so the contraction matches the
+    float64 product instead of turning into inf (dxr_common.h split8)."""
+    B, D, H, W = 1, 64, 16, 16
+    f1 = _t(dg.fmap(100, B, D, H, W) * np.float32(1e-3))
+    f2 = _t(dg.fmap(101, B, D, H, W) * np.float32(1e-3))
+    c = _t(dg.coords(102, B, H, W, "normal", 2.0))
+    w = _t(dg.fmap(103, 1, 1, 32, 324)[0, 0] / np.float32(18.0))
+    w[:, 7] = 3.4e38
+    w[::2, 7] = -3.4e38
+    cb = dx.CorrBlock(f1, f2)
+    got = cb.lookup_conv1x1(c, w, None, relu=False).cpu().numpy()
+    assert np.isfinite(got).all()
+    tolerance_check(got, _ref64(cb(c), w, None, relu=False).astype(np.float32), RTOL)
+
+
 def test_fused_far_and_nan_coords(dx):
     """Far coordinates give zero samples (bias only); a NaN coordinate makes that
     pixel's samples NaN, so its outputs are NaN exactly where the unfused path's are."""
