@@ -68,6 +68,7 @@ struct GradGeom {
   int nblk, kbt, S;       // n blocks, k blocks, k chunks
   int nslab;              // 256-channel slabs
   long long ks;           // k steps of the packed operand
+  float* out0;            // chunk 0's sums: the output itself (chunks >= 1: the workspace)
 };
 
 __device__ __forceinline__ uint4 ld4(const float* p) {
@@ -461,7 +462,8 @@ __global__ __launch_bounds__(NTHR) void fmap_grad_kernel(const float* __restrict
   }
   if (!active) return;
   // C/D map: column n = lane & 31 (+32 j), row d = (v&3) + 8(v>>2) + 4(lane>>5)
-  float* o = out + ((long long)chunk * g.B + b) * g.D * g.N;
+  float* o = chunk == 0 ? g.out0 + (long long)b * g.D * g.N
+                        : out + ((long long)(chunk - 1) * g.B + b) * g.D * g.N;
   const int ty = nb / g.txn, tx = nb % g.txn;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -632,7 +634,8 @@ __device__ __forceinline__ void grad_body(const float* __restrict__ gp, const ui
 #pragma unroll
   for (int v = 0; v < 16; ++v)
     un[v] = F16 ? -(scales[2 + b * g.D + d0 + (v & 3) + 8 * (v >> 2) + 4 * hl] + ev) : 0;
-  float* o = out + ((long long)chunk * g.B + b) * g.D * g.N;
+  float* o = chunk == 0 ? g.out0 + (long long)b * g.D * g.N
+                        : out + ((long long)(chunk - 1) * g.B + b) * g.D * g.N;
   const int ty = nb / g.txn, tx = nb % g.txn;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -834,13 +837,15 @@ __global__ __launch_bounds__(256) void fmap_split_kernel(const float* __restrict
   }
 }
 
-// out[i] = sum over chunks s (ascending) of part[s][i].
+// out[i] = sum over chunks s (ascending) of chunk s's sums: chunk 0's are out[i]
+// itself, chunk s >= 1's part[s - 1][i] (one [B, D, H*W] buffer fewer in the
+// workspace than S separate partials; the same additions in the same order).
 __global__ __launch_bounds__(256) void chunk_sum_kernel(const float* __restrict__ part,
                                                         float* __restrict__ out, long long n, int S) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
-    float t = part[i];
-    for (int s = 1; s < S; ++s) t += part[s * n + i];
+    float t = out[i];
+    for (int s = 1; s < S; ++s) t += part[(s - 1) * n + i];
     out[i] = t;
   }
 }
@@ -887,7 +892,7 @@ void set_kernel(GradGeom* g, bool kt) {
 
 long long operand_bytes(const GradGeom& g) { return align256((long long)g.B * 3 * g.ks * g.D * 32); }
 long long partial_bytes(const GradGeom& g) {
-  return g.S > 1 ? align256((long long)g.S * g.B * g.D * g.N * 4) : 0;
+  return g.S > 1 ? align256((long long)(g.S - 1) * g.B * g.D * g.N * 4) : 0;
 }
 
 bool grads_supported(int64_t D, int num_levels) {
@@ -957,6 +962,7 @@ extern "C" int dxr_fmap_grads_bounded(const void* grad_pyramid, int grad_dtype, 
     if (!dst) continue;
     if (!src) return DXR_EINVAL;
     set_kernel(&g, kt == 1);
+    g.out0 = dst;
     char* w = static_cast<char*>(workspace);
     int* scales = reinterpret_cast<int*>(w);
     uint4* fp = reinterpret_cast<uint4*>(w + scales_bytes(g));
@@ -1018,6 +1024,7 @@ extern "C" int dxr_fmap_grads(const void* grad_pyramid, int grad_dtype, const fl
     if (!dst) continue;
     if (!src) return DXR_EINVAL;
     set_kernel(&g, kt == 1);
+    g.out0 = dst;
     uint4* fp = static_cast<uint4*>(workspace);
     float* part = g.S > 1 ? reinterpret_cast<float*>(static_cast<char*>(workspace) + operand_bytes(g))
                           : dst;

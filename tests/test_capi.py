@@ -247,7 +247,7 @@ def _fmap_grads_ws(B, D, H, W):
     """dxr_fmap_grads' workspace: the larger of its two GEMMs' needs, each the
     three-way split fmap operand (3 x 16 bit per element, k padded to whole
     k-blocks of 128) plus, when K is split into S > 1 chunks (~256 workgroups),
-    S partial [B, D, H*W] f32 sums."""
+    S - 1 partial [B, D, H*W] f32 sums (chunk 0 sums into the output itself)."""
     al = lambda x: (x + 255) // 256 * 256   # noqa: E731
     N = H * W
     qt, tiles = -(-N // 128), -(-H // 8) * -(-W // 16)
@@ -257,7 +257,7 @@ def _fmap_grads_ws(B, D, H, W):
         units = nblk * B * slabs
         S = 1 if units >= 256 else min(256 // units, kbt)
         op = al(B * 3 * kbt * 8 * D * 32)
-        need = max(need, op + (al(S * B * D * N * 4) if S > 1 else 0))
+        need = max(need, op + (al((S - 1) * B * D * N * 4) if S > 1 else 0))
     return need
 
 
