@@ -1341,18 +1341,21 @@ __device__ __forceinline__ void split_record(const float (&x)[16], uint4 (&rec)[
 // records stored directly write every line in four partial pieces: 13.7 vs
 // 9.5 us at Sintel B=1 against plain stores, which in turn leave the build's
 // K loop evicting dirty lines.)
-template <bool NHWC, bool LO11 = false>
-__global__ __launch_bounds__(1024) void split_pairs_kernel(const float* __restrict__ f1,
-                                                           const float* __restrict__ f2,
-                                                           uint4* __restrict__ sp1,
-                                                           uint4* __restrict__ sp2,
-                                                           int* __restrict__ e1, int* __restrict__ e2,
-                                                           int D, int N) {
-  __shared__ float red[16][65];
-  __shared__ __attribute__((aligned(16))) uint4 tr[16][64 * 5];   // per wave: 64 records, 80-B pitch
+template <bool NHWC, bool LO11 = false, int PX = 64>
+__global__ __launch_bounds__(PX * 16) void split_pairs_kernel(const float* __restrict__ f1,
+                                                              const float* __restrict__ f2,
+                                                              uint4* __restrict__ sp1,
+                                                              uint4* __restrict__ sp2,
+                                                              int* __restrict__ e1,
+                                                              int* __restrict__ e2, int D, int N) {
+  static_assert(PX == 64 || (!NHWC && PX == 32), "NHWC: 64 pixels per workgroup");
+  __shared__ float red[16][PX + 1];
+  __shared__ __attribute__((aligned(16))) uint4 tr[PX / 4][64 * 5];   // per wave: 64 records, 80-B pitch
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int kb0 = NHWC ? (tid & 15) : (tid >> 6), pl = NHWC ? (tid >> 4) : (tid & 63);
-  const int p = blockIdx.x * 64 + pl;
+  // NCHW: thread = (16-channel block kb0, pixel pl), pixels fastest (PX = 32:
+  // a wave holds two channel blocks' 128-byte pixel runs)
+  const int kb0 = NHWC ? (tid & 15) : (tid / PX), pl = NHWC ? (tid >> 4) : (tid % PX);
+  const int p = blockIdx.x * PX + pl;
   const bool live = p < N;
   const int b = blockIdx.y;
   const float* src = (blockIdx.z == 0 ? f1 : f2) + (long long)b * D * N;
@@ -1430,8 +1433,8 @@ __global__ __launch_bounds__(1024) void split_pairs_kernel(const float* __restri
     for (int i = 0; i < 4; ++i) {
       // 1 KB of contiguous records per instruction: LDS record u2, slot c
       const int u2 = 16 * i + (lane >> 2), c = lane & 3;
-      const int kbs = NHWC ? 16 * it + (u2 >> 2) : kb;
-      const int px = NHWC ? blockIdx.x * 64 + wave * 4 + (u2 & 3) : blockIdx.x * 64 + u2;
+      const int kbs = NHWC ? 16 * it + (u2 >> 2) : 16 * it + (wave * 64 + u2) / PX;
+      const int px = NHWC ? blockIdx.x * 64 + wave * 4 + (u2 & 3) : blockIdx.x * PX + u2 % PX;
       if (px < N && kbs < nkb) {
         const uint4 v = tw[u2 * 5 + c];
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), rs,
@@ -1959,9 +1962,13 @@ int launch_dma(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, in
   uint8_t* sp2 = w + spb;
   int* e1 = reinterpret_cast<int*>(w + 2 * spb);
   int* e2 = reinterpret_cast<int*>(w + 2 * spb + eb);
-  hipLaunchKernelGGL((split_pairs_kernel<NHWC>), dim3((unsigned)((N + 63) / 64), (unsigned)B, 2),
-                     dim3(1024), 0, stream, f1, f2, reinterpret_cast<uint4*>(sp1),
-                     reinterpret_cast<uint4*>(sp2), e1, e2, g.D, g.N);
+  // NCHW: 32 pixels per workgroup, two workgroups per CU (round 4, same-process
+  // whole-build A/B: Sintel B=1 115.5 -> 114.4 us, split kernel 13.6 -> 12.4 us)
+  constexpr int PX = NHWC ? 64 : 32;
+  hipLaunchKernelGGL((split_pairs_kernel<NHWC, false, PX>),
+                     dim3((unsigned)((N + PX - 1) / PX), (unsigned)B, 2), dim3(PX * 16), 0, stream,
+                     f1, f2, reinterpret_cast<uint4*>(sp1), reinterpret_cast<uint4*>(sp2), e1, e2,
+                     g.D, g.N);
   int st = dxr::launch_status();
   if (st != DXR_OK) return st;
   const dim3 rg = remap_grid(g, B, 2);
