@@ -345,7 +345,7 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
   // first (3 / 2 / 1 / 0), so co-resident level-0 waves, which move the most
   // lines, issue ahead.  Same-process A/B in the step (r4af): Sintel B=1 203.1 ->
   // 201.2 us; on multi-round grids (Sintel B=8, KITTI B=8) it cost 0.7-1.5 %.
-  if constexpr (QB_ == 16) {
+  if constexpr (QB_ != 0 && QB_ <= 16) {
     if (l == 0) __builtin_amdgcn_s_setprio(3);
     else if (l == 1) __builtin_amdgcn_s_setprio(2);
     else if (l == 2) __builtin_amdgcn_s_setprio(1);
