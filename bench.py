@@ -92,6 +92,40 @@ def lookup_bytes(B, H, W, s_pyr=4):
     return B * H * W * (win * s_pyr + 8 + LEVELS * rd * rd * 4)
 
 
+def lookup_line_floor_bytes(coords, H, W, s_pyr=4, line=128):
+    """Line-granular floor of one lookup (scripts/lookup_lines.py
+    restated vectorised): for the step's own coordinate sets, the 128-byte lines
+    of the paged pyramid (§3.3) that hold each query's window cells (2r+2 per
+    axis from floor(c / 2^l) - r, clipped to the level) — a query's map is its own
+    page slice, so no line is shared between queries — plus the float32 output and
+    the coords, which every layout must move.  Mean over the coordinate sets."""
+    tx = (W + 15) // 16
+    offs = np.arange(2 * RADIUS + 2)
+    lines = []
+    for c in coords:
+        a = c.detach().float().cpu().numpy()
+        B = a.shape[0]
+        x = a[:, 0].reshape(-1).astype(np.float64)
+        y = a[:, 1].reshape(-1).astype(np.float64)
+        n = 0
+        for lvl, (h, w) in enumerate(level_sizes(H, W)):
+            th, tw = 8 >> lvl, 16 >> lvl
+            fx, fy = np.floor(x / 2 ** lvl), np.floor(y / 2 ** lvl)
+            ok = np.isfinite(fx) & np.isfinite(fy) & (np.abs(fx) < 1e8) & (np.abs(fy) < 1e8)
+            cx = np.where(ok, fx, -1e6).astype(np.int64)[:, None] - RADIUS + offs
+            cy = np.where(ok, fy, -1e6).astype(np.int64)[:, None] - RADIUS + offs
+            vx, vy = (cx >= 0) & (cx < w), (cy >= 0) & (cy < h)
+            tile = (cy // th)[:, :, None] * tx + (cx // tw)[:, None, :]
+            elem = tile * (th * tw) + ((cy % th) * tw)[:, :, None] + (cx % tw)[:, None, :]
+            key = np.where(vy[:, :, None] & vx[:, None, :], elem * s_pyr // line, -1)
+            key = np.sort(key.reshape(key.shape[0], -1), axis=1)
+            n += int(((key[:, 1:] != key[:, :-1]) & (key[:, 1:] >= 0)).sum() +
+                     (key[:, 0] >= 0).sum())
+        lines.append(n)
+    rd = 2 * RADIUS + 1
+    return float(np.mean(lines)) * line + B * H * W * (8 + LEVELS * rd * rd * 4)
+
+
 def build_kernel(dtype, H, W):
     """The build kernel the library runs for this workload (csrc/corr_build.hip:
     CorrBlock passes a workspace, so dxr_corr_pyramid_build_ws takes its LDS-DMA
@@ -135,6 +169,31 @@ def pmc_traffic(workload, kernel_prefix):
             if name.split("::")[-1].startswith(kernel_prefix):
                 return rec["traffic_bytes"], f"{f.relative_to(REPO)}: {rec['correction']}"
     return None, None
+
+
+def trace_timeline(workload):
+    """The step's kernel timeline for this workload from the newest committed
+    rocprofv3 kernel trace of this bench (profiles/<round>/<config>/trace_gaps.json,
+    scripts/trace_gaps.py): the build's in-step span, the idle time per step
+    split by kernel boundary, and the first lookup after the build — the measured
+    decomposition of `step_boundary_us`.  None when not profiled."""
+    files = sorted((REPO / "profiles").glob("*/*/trace_gaps.json"),
+                   key=lambda f: f.relative_to(REPO / "profiles").parts[0])
+    for f in reversed(files):
+        try:
+            data = json.loads(f.read_text())
+        except ValueError:
+            continue
+        if data.get("workload") == workload and data.get("steps", 0) > 0:
+            return {"build_in_step_us": data.get("build_in_step_us_median"),
+                    "idle_us_per_step": data.get("idle_us_per_step_median"),
+                    "idle_us_by_boundary": data.get("idle_us_median_by_boundary"),
+                    "first_lookup_us": data.get("first_lookup_us_median"),
+                    "lookup_us": data.get("lookup_us_median"),
+                    "step_span_us": data.get("step_span_us_median"),
+                    "source": f"{f.relative_to(REPO)} (rocprofv3 kernel trace of this bench, "
+                              f"medians over {data['steps']} steps)"}
+    return None
 
 
 def _free_port() -> int:
@@ -401,9 +460,11 @@ def main():
             with torch.cuda.graph(g_look, stream=stream, pool=g_step.pool()):
                 [cb(c) for c in coords]
             # the build alone, as a graph of back-to-back builds (each block freed
-            # before the next is built, as in the step)
+            # before the next is built, as in the step); in the step graph's pool,
+            # so its blocks reuse that pool's free memory (a private
+            # pool held another pyramid + workspace, ~5.7 GB at 1080p)
             g_build = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_build, stream=stream):
+            with torch.cuda.graph(g_build, stream=stream, pool=g_step.pool()):
                 for _ in range(BUILDS_PER_GRAPH):
                     block_cls(f1, f2, radius=RADIUS)
             # the captures left the GPU idle: bring the clocks back up first
@@ -511,13 +572,19 @@ def main():
                 "hbm_frac": round(bb / (build_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
                 "avg_launch_us": round(build_ms * 1e3, 2),
                 "step_boundary_us": round(boundary_ms * 1e3, 2),
+                "step_timeline": trace_timeline(wl_key),
             }
+            lf = lookup_line_floor_bytes(coords, H, W, s_pyr=s_in)
             res["lookup_roofline"] = {
                 "kernel": "corr_lookup_wide_kernel (stage c)",
                 "bound": "hbm", "achieved": round(lb / (look_ms * 1e-3) / 1e9, 1),
                 "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(lb / (look_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
                 "algorithmic_bytes_per_launch": lb,
+                # the achievable floor of this layout: whole 128-B lines holding the
+                # taps' cells + output + coords, and the time at 8 TB/s
+                "line_floor_bytes": round(lf),
+                "frac_of_line_floor": round(lf / (look_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
                 "traffic": l_traffic, "traffic_source": l_src,
                 "avg_launch_us": round(look_ms * 1e3, 2),
             }

@@ -321,9 +321,9 @@ int dxr_pyramid_backward(const void* grad_pyramid, int grad_dtype,
  *   grad_fmap1 = fmap2 . dV^T,  grad_fmap2 = fmap1 . dV   (dV as above),
  * on MFMA with a three-way bf16 split of both operands (six products, f32
  * accumulation: f32-class).  Deterministic (fixed summation order).
- * Range: a finite operand beyond bfloat16's largest finite value (|x| >
- * 3.3895e38) rounds its bf16 high part to +-inf, so products with it come out
- * +-inf where an f32 GEMM could stay finite; inf and NaN operands propagate as
+ * Range: every finite operand stays finite in the split (one beyond
+ * bfloat16's largest finite value, |x| > 3.3895e38, keeps its truncation as the
+ * high part instead of rounding it to +-inf); inf and NaN operands propagate as
  * in an f32 GEMM.
  *   grad_pyramid : float32, the paged layout of dxr_corr_pyramid_build
  *   fmap1, fmap2 : [B, D, H, W] float32, NCHW contiguous

@@ -154,6 +154,9 @@ class _GradState:
         self.pending = []
         self.grad_pyr = None
         self.zero_ev = None
+        # a pass that failed elsewhere never runs its queued _end: re-arm
+        # (a second queued _end is harmless, it is idempotent)
+        self.end_hook = False
 
     def arm_end_of_pass(self):
         """Queue (once per backward pass) a callback that runs when autograd's
@@ -206,6 +209,9 @@ class _BuildGrad(torch.autograd.Function):
         except BaseException:
             gs.reset()
             raise
+        # the state is consumed here: a later pass (retain_graph) arms its own
+        # end-of-pass cleanup
+        gs.end_hook = False
         if gs.grad_pyr is None:
             return None, None, None
         slots = gs.slots_ptr()

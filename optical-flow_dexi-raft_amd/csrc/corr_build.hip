@@ -54,6 +54,8 @@ struct BuildGeom {
   float recip;          // 1/divisor when that is exact (power of two), else 0
   int lh[4], lw[4];     // level sizes
   long long loff[4];    // element offset of each level
+  int nmain;            // DMA build: workgroups [0, nmain) take whole units, the
+                        // rest quarter units of the tail (dma_tail_split)
 };
 
 // Page coordinates of this workgroup.  3-D grid (tiles, query blocks, pairs), or
@@ -106,7 +108,7 @@ __device__ __forceinline__ PageCoord unit_coord(const BuildGeom& g, long long wl
 template <bool REMAP, int QB = 1>
 __device__ __forceinline__ PageCoord page_coord(const BuildGeom& g) {
   if constexpr (REMAP) {
-    const long long nwg = (long long)gridDim.x;
+    const long long nwg = (long long)min((unsigned)g.nmain, gridDim.x);
     const long long w = blockIdx.x;
     const long long q8 = nwg / 8, r8 = nwg % 8, xcd = w % 8;
     const long long wl = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + w / 8;
@@ -1449,202 +1451,54 @@ __global__ __launch_bounds__(PX * 16) void split_pairs_kernel(const float* __res
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-// A workgroup whose sums are not finite (an inf/NaN operand pixel) recomputes
-// its pages from the f32 operands (`f1`, `f2`: element (pixel p, channel k) at
-// p * ps + k * ks of a pair's fmap) on the exact-f32 MFMA, in place: IEEE
-// semantics as the reference's f32 matmul (inf x finite = inf, inf x 0 = NaN,
-// NaN propagates).  Grid: remap_grid(g, B, 2) (page_coord<true, 2>).
-//
-// BF (bf16 mode, C3): the same K loop on bf16 operand records — a 64-B record
-// is 32 consecutive channels of one pixel (k 0-7 | 8-15 | 16-23 | 24-31 in the
-// four 16-B slots), so a stage is two 16-deep bf16 MFMA steps (slots kh, then
-// 2 + kh), accumulated in the order of corr_build_bf16_q2_kernel: the same
-// pages bit for bit.  Records come straight from channels-last bf16 fmaps
-// (pixel stride D * 2 B, stage stride 64 B) or from the pack pass's blocked copy
-// of NCHW fmaps (pixel stride 64 B, stage stride N * 64 B): `pstr` / `kstr`.
-// No scales, no non-finite fallback (bf16 MFMA propagates inf/NaN itself), and
-// the bf16 build's non-temporal pyramid stores.
-template <typename OT, bool DIV, bool BF = false>
-__global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
-    const uint8_t* __restrict__ sp1, const uint8_t* __restrict__ sp2, const int* __restrict__ ex1,
-    const int* __restrict__ ex2, OT* __restrict__ pyr, const float* __restrict__ f1,
-    const float* __restrict__ f2, int ps, int ks, int pstr, int kstr, BuildGeom g) {
-  constexpr int LDS_RING = DMA_RING * DMA_STAGE;
-  constexpr int LDS_E = 2 * WAVES * 16 * P0 * 4;          // epilogue staging (8 waves)
-  static_assert(LDS_E <= LDS_RING, "the epilogue staging aliases the ring");
-  // one LDS array (cdna_hip_programming.md §5 item 4(a)): ring | target
-  // exponents (128 int) | redo flag
-  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_RING + NTGT * 4 + 16];
-  int* const sexp = reinterpret_cast<int*>(smem + LDS_RING);
-  int* const redo = reinterpret_cast<int*>(smem + LDS_RING + NTGT * 4);
+// LDS of corr_build_dma_kernel: ring | target scale exponents s (128 int) |
+// flag (a non-finite sum: recompute).
+constexpr int DMA_LDS_RING = DMA_RING * DMA_STAGE;
+constexpr int DMA_LDS_BYTES = DMA_LDS_RING + NTGT * 4 + 16;
+// Tail quarter units (dma_tail_split): the exchange region (two 32-query groups
+// x four 32-target tiles of accumulators) and the epilogue staging after it.
+constexpr int DMA_XS_BYTES = 2 * 4 * 16 * 64 * 4;
+static_assert(DMA_XS_BYTES + WAVES * 16 * P0 * 4 <= DMA_LDS_RING, "tail exchange + staging fit");
 
-  const int tid = threadIdx.x, lane = tid & 63;
-  // wave-uniform (SGPR): the DMA's LDS base must be, or the compiler emits a
-  // waterfall loop around every buffer_load ... lds
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int half = wave >> 2, w4 = wave & 3;
-  const PageCoord pc = page_coord<true, 2>(g);
-  const int th0 = pc.tyi * TH, tw0 = pc.txi * TW;
-  const int q0 = pc.qblk * BM;                        // first of the two blocks
-  const int b = pc.b;
-  const int j = lane & 31, kh = lane >> 5;
-  const long long spstride = (long long)g.D * g.N * (BF ? 2 : 4);   // operand bytes per pair
-
-  // exponents: the lane's query, the tile's 128 targets (LDS, by tile pixel)
-  const int qj = q0 + wave * 32 + j;
-  int sq = 0;
-  if constexpr (!BF) {
-    sq = qj < g.N ? ex1[(long long)b * g.N + qj] : 0;
-    if (tid < NTGT) {
-      // the target pixel's unscale factor 2^-s (exact: s in [-125, 125])
-      const int r = tid >> 4, c = tid & 15;
-      const bool in = th0 + r < g.H && tw0 + c < g.W;
-      const int e = in ? ex2[(long long)b * g.N + (th0 + r) * g.W + tw0 + c] : 0;
-      sexp[tid] = __float_as_int(__builtin_ldexpf(1.f, -e));
-    }
-    if (tid == 0) *redo = 0;
+// Unscale, divide by sqrt(D) and write one wave's 32 queries x 8x16 targets
+// (f32 build), then — if the workgroup saw a non-finite sum — recompute them on
+// the exact-f32 MFMA and write them again.  acc[t][r] is query qj x tile pixel
+// (row 2t + kh, col r).  Shared by the whole-unit and the quarter-unit forms.
+template <typename OT, bool DIV>
+__device__ __forceinline__ void dma_finish_f32(f32x16 (&acc)[4], const BuildGeom& g,
+                                               OT* __restrict__ pyr, float* stage, long long page,
+                                               int w4, int lane, int flags, int sq, int qj,
+                                               int trow0, int th0, int tw0, int b,
+                                               const float* __restrict__ f1,
+                                               const float* __restrict__ f2, int ps, int ks,
+                                               const int* sexp) {
+  const int kh = lane >> 5;
+  // ldexp by the exponent sum -(s_q + s_t) + log2(1/sqrt(D)) (when that is
+  // exact): one rounding of the exact value whatever the pixel magnitudes.
+  // (Round 4 multiplied by 2^-s_q / sqrt(D), then by 2^-s_t: the same two VALU
+  // ops per value, but the product overflowed or went subnormal between them for
+  // pixel pairs of very different magnitudes)
+  int eq = -sq;
+  if constexpr (!DIV) {
+    int e2;
+    (void)__builtin_frexpf(g.recip, &e2);
+    eq += e2 - 1;   // recip = 2^(e2 - 1)
   }
-
-  const __amdgpu_buffer_rsrc_t rq =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sp1 + b * spstride), (short)0,
-                                        (int)spstride, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rt =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sp2 + b * spstride), (short)0,
-                                        (int)spstride, 0x00020000);
-  // DMA source offsets (fixed over K; the step's offset ks * kstr in soffset).
-  // Query instruction i of this wave: LDS rows 16 i + (lane >> 2) of the wave's
-  // 2 KB region; target instruction: tile row r = wave.
-  uint32_t vq[2], vt;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = 16 * i + (lane >> 2), ps = lane & 3;
-    const int q = q0 + wave * 32 + row;
-    const int cq = ps ^ ((row >> 2) & 3);
-    vq[i] = q < g.N ? (uint32_t)q * (uint32_t)pstr + 16u * cq : 0x80000000u;
-  }
-  {
-    const int ps = lane & 3, r = wave, col = lane >> 2, trow = r * 16 + col;
-    const int ct = ps ^ (((trow >> 2) & 1) | ((trow >> 3) & 2));
-    const int hh = th0 + r, ww = tw0 + col;
-    vt = (hh < g.H && ww < g.W) ? (uint32_t)(hh * g.W + ww) * (uint32_t)pstr + 16u * ct
-                                : 0x80000000u;
-  }
-  auto dma = [&](int ks) {
-    unsigned char* st = smem + (ks % DMA_RING) * DMA_STAGE;
-    const int so = ks * kstr;
+  for (int t = 0; t < 4; ++t) {
+    const int4* se = reinterpret_cast<const int4*>(sexp + (2 * t + kh) * 16);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rq, (lds_void_t*)(st + wave * 2048 + i * 1024), 16, vq[i], so, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (lds_void_t*)(st + DMA_TILE + wave * 1024), 16,
-                                             vt, so, 0, 0);
-  };
-  // fragment byte offsets within a stage (hi; lo = the other two slots)
-  const int kq = (j >> 2) & 3;
-  const int qh_off = wave * 2048 + j * 64 + 16 * (kh ^ kq);
-  const int ql_off = wave * 2048 + j * 64 + 16 * ((2 + kh) ^ kq);
-  const int trow0 = ((j >> 2) & 1) * 16 + (j & 3) + 4 * (j >> 3);     // tile t adds 32 rows
-  const int kt = ((trow0 >> 2) & 1) | ((trow0 >> 3) & 2);
-  const int th_off = DMA_TILE + trow0 * 64 + 16 * (kh ^ kt);
-  const int tl_off = DMA_TILE + trow0 * 64 + 16 * ((2 + kh) ^ kt);
-
-  f32x16 acc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-
-  // exponent loads and LDS writes above must not count against the ring's vmcnt
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int nk = g.D / (BF ? 2 * BKS : BKS);
-  dma(0);
-  if (nk > 1) dma(1);
-  for (int ks = 0; ks < nk; ++ks) {
-    // this wave's 3 DMAs of step ks have landed (those of ks + 1 stay in flight);
-    // the barrier publishes every wave's, and orders the ring slot's previous
-    // readers (step ks - 1) before the refill below
-    if (ks + 1 < nk) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (ks + 2 < nk) dma(ks + 2);
-    const unsigned char* st = smem + (ks % DMA_RING) * DMA_STAGE;
-    if constexpr (BF) {
-      // k 0-15 of the stage for every tile, then k 16-31 (the q2 kernel's order)
-      const bf8v q0v = *reinterpret_cast<const bf8v*>(st + qh_off);
-      const bf8v q1v = *reinterpret_cast<const bf8v*>(st + ql_off);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const bf8v t0v = *reinterpret_cast<const bf8v*>(st + th_off + t * 2048);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(t0v, q0v, acc[t], 0, 0, 0);
-      }
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const bf8v t1v = *reinterpret_cast<const bf8v*>(st + tl_off + t * 2048);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(t1v, q1v, acc[t], 0, 0, 0);
-      }
-    } else {
-      const h8v qh = *reinterpret_cast<const h8v*>(st + qh_off);
-      const h8v ql = *reinterpret_cast<const h8v*>(st + ql_off);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const h8v th = *reinterpret_cast<const h8v*>(st + th_off + t * 2048);
-        const h8v tl = *reinterpret_cast<const h8v*>(st + tl_off + t * 2048);
-        // small terms first
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qh, acc[t], 0, 0, 0);
-      }
+    for (int u = 0; u < 4; ++u) {
+      const int4 s4 = se[u];
+      acc[t][4 * u + 0] = __builtin_ldexpf(acc[t][4 * u + 0], eq - s4.x);
+      acc[t][4 * u + 1] = __builtin_ldexpf(acc[t][4 * u + 1], eq - s4.y);
+      acc[t][4 * u + 2] = __builtin_ldexpf(acc[t][4 * u + 2], eq - s4.z);
+      acc[t][4 * u + 3] = __builtin_ldexpf(acc[t][4 * u + 3], eq - s4.w);
     }
   }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();   // ring reads done: the LDS is free for reuse
-  const bool live = pc.qblk + half < g.qt;            // this half's query block exists
-  const long long page = pc.page + (live ? (long long)half * g.tiles_h * g.tiles_w : 0);
-  if constexpr (BF) {
-    if (live) {
-      scale_acc<DIV>(acc, g);
-      paged_epilogue<OT, 3>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0, pyr, g,
-                            page, w4, lane);
-    }
-    return;
-  }
-
-  // vote: a non-finite sum means an operand pixel was not finite; the
-  // workgroup's pages are then recomputed from the f32 operands
-  bool bad = false;
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) bad |= !(__builtin_fabsf(acc[t][r]) <= 3.40282347e38f);
-  if (bad) *redo = 1;
-  __syncthreads();
-  // undo the pixel scales and divide by sqrt(D): acc[t][r] is query qj x tile
-  // pixel (row 2t + kh, col r).  Two multiplies by powers of two (the query's
-  // 2^-sq, with an exact 1/sqrt(D) folded in, and the target's 2^-st from LDS):
-  // exact while the values stay normal, so the same pages as ldexp(acc,
-  // -(sq + st)) * (1/sqrt(D)) — two packed multiplies per pair instead of an
-  // exponent add, an ldexp and a multiply per value (round 4)
-  if (live) {   // a half past the last query block has no page (epilogue syncs per wave)
-    const float qs = DIV ? __builtin_ldexpf(1.f, -sq) : __builtin_ldexpf(g.recip, -sq);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const float4* se = reinterpret_cast<const float4*>(sexp + (2 * t + kh) * 16);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float4 s4 = se[u];
-        acc[t][4 * u + 0] = (acc[t][4 * u + 0] * qs) * s4.x;
-        acc[t][4 * u + 1] = (acc[t][4 * u + 1] * qs) * s4.y;
-        acc[t][4 * u + 2] = (acc[t][4 * u + 2] * qs) * s4.z;
-        acc[t][4 * u + 3] = (acc[t][4 * u + 3] * qs) * s4.w;
-      }
-    }
-    if constexpr (DIV) scale_acc<DIV>(acc, g);
-    paged_epilogue<OT, 1 | 4>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0, pyr,
-                              g, page, w4, lane);
-  }
-  if (*redo && live) {
+  if constexpr (DIV) scale_acc<DIV>(acc, g);
+  paged_epilogue<OT, 1 | 4>(acc, stage, pyr, g, page, w4, lane);
+  if (flags & 1) {
     // The workgroup saw a non-finite sum: its pages are recomputed on the
     // exact-f32 MFMA (v_mfma_f32_32x32x2_f32: each lane supplies channel k0 + kh
     // of its A row = target trow0 + 32 t and of its B column = query qj; same
@@ -1682,9 +1536,339 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
       }
     }
     scale_acc<DIV>(acc, g);
-    paged_epilogue<OT, 1 | 4>(acc, reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0, pyr,
-                              g, page, w4, lane);
+    paged_epilogue<OT, 1 | 4>(acc, stage, pyr, g, page, w4, lane);
   }
+}
+
+// Per-workgroup prologue of both forms: the lane's query exponent, the tile's
+// 128 target exponents (LDS), the flag word.
+__device__ __forceinline__ void dma_scales(const BuildGeom& g, const int* __restrict__ ex1,
+                                           const int* __restrict__ ex2, int b, int qj, int th0,
+                                           int tw0, int tid, int& sq, int* sexp,
+                                           int* flags) {
+  sq = qj < g.N ? ex1[(long long)b * g.N + qj] : 0;
+  if (tid < NTGT) {
+    // the target pixel's scale exponent s (in [-125, 125])
+    const int r = tid >> 4, c = tid & 15;
+    const bool in = th0 + r < g.H && tw0 + c < g.W;
+    const int e = in ? ex2[(long long)b * g.N + (th0 + r) * g.W + tw0 + c] : 0;
+    sexp[tid] = e;
+  }
+  if (tid == 0) *flags = 0;
+}
+
+// Quarter units of the tail (dma_tail_split): workgroup blockIdx.x >= nmain
+// takes query groups 2 sub, 2 sub + 1 (64 queries) of unit nmain + (x - nmain)/4
+// against the unit's whole 8x16 tile; wave = (group gl, 32-target MFMA tile t).
+// Every accumulator runs the whole-unit form's MFMA sequence on the same
+// operands, so the pages are the same bits; the four tiles of a group meet in
+// LDS and one wave per group runs the shared epilogue.  A quarter unit's K
+// loop is a quarter of the MFMA work at the same per-step latency, so the
+// last, partial dispatch round of whole units (1,568 units on 512 slots at
+// Sintel B=1: 32 units alone for a whole unit time) becomes 128 short ones.
+template <typename OT, bool DIV, bool BF>
+__device__ __forceinline__ void dma_quarter(unsigned char* smem, const uint8_t* __restrict__ sp1,
+                                            const uint8_t* __restrict__ sp2,
+                                            const int* __restrict__ ex1,
+                                            const int* __restrict__ ex2, OT* __restrict__ pyr,
+                                            const float* __restrict__ f1,
+                                            const float* __restrict__ f2, int ps, int ks, int pstr,
+                                            int kstr, const BuildGeom& g) {
+  int* const sexp = reinterpret_cast<int*>(smem + DMA_LDS_RING);
+  int* const flags = reinterpret_cast<int*>(smem + DMA_LDS_RING + NTGT * 4);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int gl = wave >> 2, t = wave & 3;
+  const long long xq = (long long)blockIdx.x - g.nmain;
+  const int sub = (int)(xq & 3), half = sub >> 1;
+  const PageCoord pc = unit_coord<2>(g, (long long)g.nmain + (xq >> 2));
+  if (pc.qblk + half >= g.qt) return;                  // padding query block (uniform)
+  const int qgrp = 2 * sub + gl, w4 = qgrp & 3;
+  const int th0 = pc.tyi * TH, tw0 = pc.txi * TW;
+  const int q0 = pc.qblk * BM + 64 * sub;              // first of the workgroup's 64 queries
+  const int b = pc.b;
+  const int j = lane & 31, kh = lane >> 5;
+  const long long spstride = (long long)g.D * g.N * (BF ? 2 : 4);
+  const int qj = q0 + gl * 32 + j;
+  int sq = 0;
+  if constexpr (!BF) dma_scales(g, ex1, ex2, b, qj, th0, tw0, tid, sq, sexp, flags);
+
+  const __amdgpu_buffer_rsrc_t rq =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sp1 + b * spstride), (short)0,
+                                        (int)spstride, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rt =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sp2 + b * spstride), (short)0,
+                                        (int)spstride, 0x00020000);
+  // waves 0-3 stage the 64 query rows (16 each, the whole-unit form's LDS
+  // image: group gl at gl * 2 KB), every wave its target tile row
+  uint32_t vq = 0x80000000u, vt;
+  {
+    const int row = 16 * wave + (lane >> 2), sl = lane & 3;
+    const int q = q0 + row;
+    const int cq = sl ^ ((row >> 2) & 3);
+    if (wave < 4 && q < g.N) vq = (uint32_t)q * (uint32_t)pstr + 16u * cq;
+  }
+  {
+    const int sl = lane & 3, r = wave, col = lane >> 2, trow = r * 16 + col;
+    const int ct = sl ^ (((trow >> 2) & 1) | ((trow >> 3) & 2));
+    const int hh = th0 + r, ww = tw0 + col;
+    vt = (hh < g.H && ww < g.W) ? (uint32_t)(hh * g.W + ww) * (uint32_t)pstr + 16u * ct
+                                : 0x80000000u;
+  }
+  auto dma = [&](int kk) {
+    unsigned char* st = smem + (kk % DMA_RING) * DMA_STAGE;
+    const int so = kk * kstr;
+    if (wave < 4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rq, (lds_void_t*)(st + wave * 1024), 16, vq, so, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (lds_void_t*)(st + DMA_TILE + wave * 1024), 16,
+                                             vt, so, 0, 0);
+  };
+  const int kq = (j >> 2) & 3;
+  const int qh_off = gl * 2048 + j * 64 + 16 * (kh ^ kq);
+  const int ql_off = gl * 2048 + j * 64 + 16 * ((2 + kh) ^ kq);
+  const int trow0 = ((j >> 2) & 1) * 16 + (j & 3) + 4 * (j >> 3);
+  const int kt = ((trow0 >> 2) & 1) | ((trow0 >> 3) & 2);
+  const int th_off = DMA_TILE + t * 2048 + trow0 * 64 + 16 * (kh ^ kt);
+  const int tl_off = DMA_TILE + t * 2048 + trow0 * 64 + 16 * ((2 + kh) ^ kt);
+
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int nk = g.D / (BF ? 2 * BKS : BKS);
+  dma(0);
+  if (nk > 1) dma(1);
+  for (int kk = 0; kk < nk; ++kk) {
+    if (kk + 1 < nk) {
+      if (wave < 4) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kk + 2 < nk) dma(kk + 2);
+    const unsigned char* st = smem + (kk % DMA_RING) * DMA_STAGE;
+    if constexpr (BF) {
+      const bf8v q0v = *reinterpret_cast<const bf8v*>(st + qh_off);
+      const bf8v q1v = *reinterpret_cast<const bf8v*>(st + ql_off);
+      const bf8v t0v = *reinterpret_cast<const bf8v*>(st + th_off);
+      const bf8v t1v = *reinterpret_cast<const bf8v*>(st + tl_off);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(t0v, q0v, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(t1v, q1v, acc, 0, 0, 0);
+    } else {
+      const h8v qh = *reinterpret_cast<const h8v*>(st + qh_off);
+      const h8v ql = *reinterpret_cast<const h8v*>(st + ql_off);
+      const h8v th = *reinterpret_cast<const h8v*>(st + th_off);
+      const h8v tl = *reinterpret_cast<const h8v*>(st + tl_off);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qh, acc, 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();   // ring reads done: the LDS is free for reuse
+  if constexpr (!BF) {
+    bool bad = false;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) bad |= !(__builtin_fabsf(acc[r]) <= 3.40282347e38f);
+    if (bad) *flags = 1;
+  }
+  // the group's four tiles meet in LDS: [group][tile][r / 4][lane][4] f32
+  float* const xs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    *reinterpret_cast<float4*>(xs + (((gl * 4 + t) * 4 + u) * 64 + lane) * 4) =
+        make_float4(acc[4 * u], acc[4 * u + 1], acc[4 * u + 2], acc[4 * u + 3]);
+  __syncthreads();
+  if (t != 0) return;             // one wave per group writes (wave-local syncs below)
+  f32x16 a4[4];
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float4 v = *reinterpret_cast<const float4*>(xs + (((gl * 4 + tt) * 4 + u) * 64 + lane) * 4);
+      a4[tt][4 * u] = v.x; a4[tt][4 * u + 1] = v.y; a4[tt][4 * u + 2] = v.z; a4[tt][4 * u + 3] = v.w;
+    }
+  const long long page = pc.page + (long long)half * g.tiles_h * g.tiles_w;
+  float* const stage = reinterpret_cast<float*>(smem + DMA_XS_BYTES);
+  if constexpr (BF) {
+    scale_acc<DIV>(a4, g);
+    paged_epilogue<OT, 3>(a4, stage, pyr, g, page, w4, lane);
+  } else {
+    dma_finish_f32<OT, DIV>(a4, g, pyr, stage, page, w4, lane, *flags, sq, qj, trow0, th0, tw0, b,
+                            f1, f2, ps, ks, sexp);
+  }
+}
+
+// A workgroup whose sums are not finite (an inf/NaN operand pixel) recomputes
+// its pages from the f32 operands (`f1`, `f2`: element (pixel p, channel k) at
+// p * ps + k * ks of a pair's fmap) on the exact-f32 MFMA, in place: IEEE
+// semantics as the reference's f32 matmul (inf x finite = inf, inf x 0 = NaN,
+// NaN propagates).  Grid: dma_grid(g, B) — [0, g.nmain) whole units in the
+// XCD-banded order (page_coord<true, 2>), then the tail's quarter units.
+//
+// BF (bf16 mode, C3): the same K loop on bf16 operand records — a 64-B record
+// is 32 consecutive channels of one pixel (k 0-7 | 8-15 | 16-23 | 24-31 in the
+// four 16-B slots), so a stage is two 16-deep bf16 MFMA steps (slots kh, then
+// 2 + kh), accumulated in the order of corr_build_bf16_q2_kernel: the same
+// pages bit for bit.  Records come straight from channels-last bf16 fmaps
+// (pixel stride D * 2 B, stage stride 64 B) or from the pack pass's blocked copy
+// of NCHW fmaps (pixel stride 64 B, stage stride N * 64 B): `pstr` / `kstr`.
+// No scales, no non-finite fallback (bf16 MFMA propagates inf/NaN itself), and
+// the bf16 build's non-temporal pyramid stores.
+template <typename OT, bool DIV, bool BF = false>
+__global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
+    const uint8_t* __restrict__ sp1, const uint8_t* __restrict__ sp2, const int* __restrict__ ex1,
+    const int* __restrict__ ex2, OT* __restrict__ pyr, const float* __restrict__ f1,
+    const float* __restrict__ f2, int ps, int ks, int pstr, int kstr, BuildGeom g) {
+  static_assert(WAVES * 16 * P0 * 4 * 2 <= DMA_LDS_RING, "the epilogue staging aliases the ring");
+  // one LDS array (cdna_hip_programming.md §5 item 4(a))
+  __shared__ __attribute__((aligned(16))) unsigned char smem[DMA_LDS_BYTES];
+  if (blockIdx.x >= (unsigned)g.nmain) {
+    dma_quarter<OT, DIV, BF>(smem, sp1, sp2, ex1, ex2, pyr, f1, f2, ps, ks, pstr, kstr, g);
+    return;
+  }
+  int* const sexp = reinterpret_cast<int*>(smem + DMA_LDS_RING);
+  int* const flags = reinterpret_cast<int*>(smem + DMA_LDS_RING + NTGT * 4);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  // wave-uniform (SGPR): the DMA's LDS base must be, or the compiler emits a
+  // waterfall loop around every buffer_load ... lds
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int half = wave >> 2, w4 = wave & 3;
+  const PageCoord pc = page_coord<true, 2>(g);
+  const int th0 = pc.tyi * TH, tw0 = pc.txi * TW;
+  const int q0 = pc.qblk * BM;                        // first of the two blocks
+  const int b = pc.b;
+  const int j = lane & 31, kh = lane >> 5;
+  const long long spstride = (long long)g.D * g.N * (BF ? 2 : 4);   // operand bytes per pair
+
+  // exponents: the lane's query, the tile's 128 targets (LDS, by tile pixel)
+  const int qj = q0 + wave * 32 + j;
+  int sq = 0;
+  if constexpr (!BF) dma_scales(g, ex1, ex2, b, qj, th0, tw0, tid, sq, sexp, flags);
+
+  const __amdgpu_buffer_rsrc_t rq =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sp1 + b * spstride), (short)0,
+                                        (int)spstride, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rt =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sp2 + b * spstride), (short)0,
+                                        (int)spstride, 0x00020000);
+  // DMA source offsets (fixed over K; the step's offset ks * kstr in soffset).
+  // Query instruction i of this wave: LDS rows 16 i + (lane >> 2) of the wave's
+  // 2 KB region; target instruction: tile row r = wave.
+  uint32_t vq[2], vt;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 16 * i + (lane >> 2), sl = lane & 3;
+    const int q = q0 + wave * 32 + row;
+    const int cq = sl ^ ((row >> 2) & 3);
+    vq[i] = q < g.N ? (uint32_t)q * (uint32_t)pstr + 16u * cq : 0x80000000u;
+  }
+  {
+    const int sl = lane & 3, r = wave, col = lane >> 2, trow = r * 16 + col;
+    const int ct = sl ^ (((trow >> 2) & 1) | ((trow >> 3) & 2));
+    const int hh = th0 + r, ww = tw0 + col;
+    vt = (hh < g.H && ww < g.W) ? (uint32_t)(hh * g.W + ww) * (uint32_t)pstr + 16u * ct
+                                : 0x80000000u;
+  }
+  auto dma = [&](int kk) {
+    unsigned char* st = smem + (kk % DMA_RING) * DMA_STAGE;
+    const int so = kk * kstr;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rq, (lds_void_t*)(st + wave * 2048 + i * 1024), 16, vq[i], so, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (lds_void_t*)(st + DMA_TILE + wave * 1024), 16,
+                                             vt, so, 0, 0);
+  };
+  // fragment byte offsets within a stage (hi; lo = the other two slots)
+  const int kq = (j >> 2) & 3;
+  const int qh_off = wave * 2048 + j * 64 + 16 * (kh ^ kq);
+  const int ql_off = wave * 2048 + j * 64 + 16 * ((2 + kh) ^ kq);
+  const int trow0 = ((j >> 2) & 1) * 16 + (j & 3) + 4 * (j >> 3);     // tile t adds 32 rows
+  const int kt = ((trow0 >> 2) & 1) | ((trow0 >> 3) & 2);
+  const int th_off = DMA_TILE + trow0 * 64 + 16 * (kh ^ kt);
+  const int tl_off = DMA_TILE + trow0 * 64 + 16 * ((2 + kh) ^ kt);
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  // exponent loads and LDS writes above must not count against the ring's vmcnt
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int nk = g.D / (BF ? 2 * BKS : BKS);
+  dma(0);
+  if (nk > 1) dma(1);
+  for (int kk = 0; kk < nk; ++kk) {
+    // this wave's 3 DMAs of step kk have landed (those of kk + 1 stay in flight);
+    // the barrier publishes every wave's, and orders the ring slot's previous
+    // readers (step kk - 1) before the refill below
+    if (kk + 1 < nk) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kk + 2 < nk) dma(kk + 2);
+    const unsigned char* st = smem + (kk % DMA_RING) * DMA_STAGE;
+    if constexpr (BF) {
+      // k 0-15 of the stage for every tile, then k 16-31 (the q2 kernel's order)
+      const bf8v q0v = *reinterpret_cast<const bf8v*>(st + qh_off);
+      const bf8v q1v = *reinterpret_cast<const bf8v*>(st + ql_off);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf8v t0v = *reinterpret_cast<const bf8v*>(st + th_off + t * 2048);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(t0v, q0v, acc[t], 0, 0, 0);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf8v t1v = *reinterpret_cast<const bf8v*>(st + tl_off + t * 2048);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(t1v, q1v, acc[t], 0, 0, 0);
+      }
+    } else {
+      const h8v qh = *reinterpret_cast<const h8v*>(st + qh_off);
+      const h8v ql = *reinterpret_cast<const h8v*>(st + ql_off);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const h8v th = *reinterpret_cast<const h8v*>(st + th_off + t * 2048);
+        const h8v tl = *reinterpret_cast<const h8v*>(st + tl_off + t * 2048);
+        // small terms first
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qh, acc[t], 0, 0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();   // ring reads done: the LDS is free for reuse
+  const bool live = pc.qblk + half < g.qt;            // this half's query block exists
+  const long long page = pc.page + (live ? (long long)half * g.tiles_h * g.tiles_w : 0);
+  float* const stage = reinterpret_cast<float*>(smem) + half * WAVES * 16 * P0;
+  if constexpr (BF) {
+    if (live) {
+      scale_acc<DIV>(acc, g);
+      paged_epilogue<OT, 3>(acc, stage, pyr, g, page, w4, lane);
+    }
+    return;
+  }
+
+  // vote: a non-finite sum means an operand pixel was not finite; the
+  // workgroup's pages are then recomputed from the f32 operands
+  bool bad = false;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) bad |= !(__builtin_fabsf(acc[t][r]) <= 3.40282347e38f);
+  if (bad) *flags = 1;
+  __syncthreads();
+  // a half past the last query block has no page (the epilogue syncs per wave)
+  if (live)
+    dma_finish_f32<OT, DIV>(acc, g, pyr, stage, page, w4, lane, *flags, sq, qj, trow0, th0, tw0, b,
+                            f1, f2, ps, ks, sexp);
 }
 
 // Floor-mode 2x2 average pool of one pyramid level into the next, for levels
@@ -1944,6 +2128,41 @@ int launch_split(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, 
   return dxr::launch_status();
 }
 
+// Dispatch slots of the DMA build: two workgroups per CU (74.8 KB of LDS and 4
+// waves per SIMD each), per device (cached).
+int dma_slots() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 512;
+  if (cache[dev] == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus < 1)
+      cus = 256;
+    cache[dev] = 2 * cus;
+  }
+  return cache[dev];
+}
+
+// Grid of a DMA build (corr_build_dma_kernel) and its tail split.  U units (two
+// query blocks x one target tile each) on S dispatch slots leave T = U mod S
+// units for a last, partial round in which most CUs idle while T units take a
+// whole unit time (Sintel B=1: 1,568 = 3 x 512 + 32).  Those T units run as 4T
+// quarter units instead (dma_quarter: the same bits).  `tail`: split when
+// 8 T <= tail * S (0: never; 8: always).  Same-process A/B (round 5, µs per
+// build incl. the split pass, scripts/ab_build.py): Sintel B=1 (T = S/16) 107.5
+// never -> 103.4 split; Sintel B=8 (T = S/2) 870.5 -> 883.2; KITTI B=8 bf16
+// (T = S/5.3) 394.0 -> 395.9; Chairs (U < S) 35.2 -> 38.6: split only a short tail.
+constexpr int DMA_TAIL_DEFAULT = 1;
+dim3 dma_grid(BuildGeom& g, int B, int tail = DMA_TAIL_DEFAULT) {
+  const long long U = (long long)B * ((g.qt + 1) / 2) * g.tiles_h * g.tiles_w;
+  const long long S = dma_slots();
+  long long T = U % S;
+  if (8 * T > (long long)tail * S) T = 0;
+  g.nmain = (int)(U - T);
+  return dim3((unsigned)(U + 3 * T));
+}
+
 // Pre-split + LDS-DMA f32 build (round 3): workspace = SP1 | SP2 | E1 | E2.
 long long align256(long long x) { return (x + 255) & ~255LL; }
 long long dma_workspace_bytes(long long B, long long D, long long H, long long W) {
@@ -1952,8 +2171,8 @@ long long dma_workspace_bytes(long long B, long long D, long long H, long long W
 }
 
 template <typename OT, bool NHWC>
-int launch_dma(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, int B, void* ws,
-               hipStream_t stream) {
+int launch_dma(const float* f1, const float* f2, OT* pyr, BuildGeom g, int B, void* ws,
+               hipStream_t stream, int tail = DMA_TAIL_DEFAULT) {
   const dim3 grid = build_grid(g, B);
   if (grid.y > 65535) return DXR_EINVAL;
   const long long N = g.N, spb = align256((long long)B * g.D * N * 4), eb = align256((long long)B * N * 4);
@@ -1971,7 +2190,7 @@ int launch_dma(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, in
                      g.D, g.N);
   int st = dxr::launch_status();
   if (st != DXR_OK) return st;
-  const dim3 rg = remap_grid(g, B, 2);
+  const dim3 rg = dma_grid(g, B, tail);
   const int ps = NHWC ? g.D : 1, ks = NHWC ? 1 : g.N;   // fallback operand strides
   if (g.recip == 0.f)
     hipLaunchKernelGGL((corr_build_dma_kernel<OT, true>), rg, dim3(2 * NT), 0, stream, sp1, sp2,
@@ -1985,9 +2204,9 @@ int launch_dma(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, in
 // bf16 operand records by LDS-DMA (corr_build_dma_kernel<.., BF>): channels-last
 // bf16 fmaps are read in place (pixel stride D * 2 B, stage stride 64 B).
 template <typename OT>
-int launch_dma_bf16_nhwc(const uint16_t* f1, const uint16_t* f2, OT* pyr, const BuildGeom& g,
-                         int B, hipStream_t stream) {
-  const dim3 rg = remap_grid(g, B, 2);
+int launch_dma_bf16_nhwc(const uint16_t* f1, const uint16_t* f2, OT* pyr, BuildGeom g, int B,
+                         hipStream_t stream, int tail = DMA_TAIL_DEFAULT) {
+  const dim3 rg = dma_grid(g, B, tail);
   const uint8_t* a = reinterpret_cast<const uint8_t*>(f1);
   const uint8_t* c = reinterpret_cast<const uint8_t*>(f2);
   if (g.recip == 0.f)
@@ -2060,8 +2279,8 @@ long long bf16_pack_bytes(long long B, long long D, long long H, long long W) {
 // NCHW bf16 fmaps with a workspace: pack pass + the bf16 DMA build
 // (blocked records: pixel stride 64 B, stage stride N * 64 B).
 template <typename OT>
-int launch_dma_bf16_nchw(const uint16_t* f1, const uint16_t* f2, OT* pyr, const BuildGeom& g,
-                         int B, void* ws, hipStream_t stream) {
+int launch_dma_bf16_nchw(const uint16_t* f1, const uint16_t* f2, OT* pyr, BuildGeom g, int B,
+                         void* ws, hipStream_t stream, int tail = DMA_TAIL_DEFAULT) {
   const long long half = align256((long long)B * g.D * g.N * 2);
   uint8_t* o1 = static_cast<uint8_t*>(ws);
   uint8_t* o2 = o1 + half;
@@ -2073,7 +2292,7 @@ int launch_dma_bf16_nchw(const uint16_t* f1, const uint16_t* f2, OT* pyr, const 
     hipLaunchKernelGGL(pack_bf16_kernel<false>, pg, dim3(256), 0, stream, f1, f2, o1, o2, g.D, g.N);
   int st = dxr::launch_status();
   if (st != DXR_OK) return st;
-  const dim3 rg = remap_grid(g, B, 2);
+  const dim3 rg = dma_grid(g, B, tail);
   if (g.recip == 0.f)
     hipLaunchKernelGGL((corr_build_dma_kernel<OT, true, true>), rg, dim3(2 * NT), 0, stream, o1, o2,
                        nullptr, nullptr, pyr, nullptr, nullptr, 0, 0, 64, g.N * 64, g);
@@ -2106,6 +2325,7 @@ BuildGeom make_geom(int64_t D, int64_t H, int64_t W, float divisor, const dxr::L
   g.tiles_h = (int)((H + TH - 1) / TH);
   g.qt = (int)((H * W + BM - 1) / BM);
   g.strip = STRIP;
+  g.nmain = 0x7fffffff;
   g.divisor = divisor;
   int e2 = 0;
   g.recip = (std::frexp(divisor, &e2) == 0.5f) ? 1.f / divisor : 0.f;  // exact iff 2^k

@@ -1139,3 +1139,24 @@ extern "C" int dxr_xp_build_pipe(const void* f1, const void* f2, int in_dtype, i
   return launch_pipe_bf16_nhwc(static_cast<const uint16_t*>(f1), static_cast<const uint16_t*>(f2),
                                static_cast<uint16_t*>(pyr), g, (int)B, stream);
 }
+
+// The product's DMA builds under another tail policy (dma_grid `tail`: split
+// the last partial dispatch round into quarter units when 8 T <= tail x S; 0
+// never, 8 always): f32 NCHW (ws as dxr_corr_pyramid_build_ws), bf16
+// channels-last (no workspace) or bf16 NCHW (ws: the pack pass's records).
+// Same pages bit for bit.
+extern "C" int dxr_xp_build_tail(const void* f1, const void* f2, int in_dtype, int fmap_layout,
+                                 int64_t B, int64_t D, int64_t H, int64_t W, void* pyr, void* ws,
+                                 int tail, hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, 4, &L) || tail < 0) return DXR_EINVAL;
+  const BuildGeom g = make_geom(D, H, W, std::sqrt((float)D), L);
+  if (in_dtype == DXR_F32)
+    return launch_dma<float, false>(static_cast<const float*>(f1), static_cast<const float*>(f2),
+                                    static_cast<float*>(pyr), g, (int)B, ws, stream, tail);
+  if (fmap_layout == DXR_NHWC)
+    return launch_dma_bf16_nhwc(static_cast<const uint16_t*>(f1), static_cast<const uint16_t*>(f2),
+                                static_cast<uint16_t*>(pyr), g, (int)B, stream, tail);
+  return launch_dma_bf16_nchw(static_cast<const uint16_t*>(f1), static_cast<const uint16_t*>(f2),
+                              static_cast<uint16_t*>(pyr), g, (int)B, ws, stream, tail);
+}

@@ -5,6 +5,9 @@
   nows : dxr_corr_pyramid_build    (register-split build, round 2)
   exact: DXR_BUILD_EXACT_F32       (exact-f32 MFMA build)
   prev : dxr_corr_pyramid_build_ws of an earlier product library (--prev-lib)
+  tailN: the product's DMA build under tail policy N (dxr_xp_build_tail of the
+         experiments library: split the last partial dispatch round into
+         quarter units when 8 T <= N x slots; tail0 never, tail8 always)
 
 Each variant is captured as a HIP graph of --reps back-to-back builds and the
 graphs are replayed in interleaved rounds after a clock warm-up (HIP events;
@@ -35,7 +38,7 @@ def main():
                     help="bf16: bf16 fmaps -> bf16 pyramid (variants ws / prev)")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=7)
-    ap.add_argument("--prev-lib", default=str(REPO / "scripts" / "libdexiraft_corr_prev.so"))
+    ap.add_argument("--prev-lib", default=str(REPO / "scripts" / "libdexiraft_corr_r04.so"))
     a = ap.parse_args()
     import dexiraft_amd
     from dexiraft_amd import _native as nat
@@ -48,6 +51,13 @@ def main():
             if hasattr(prev, name):
                 getattr(prev, name).restype = res
                 getattr(prev, name).argtypes = args
+    xlib = None
+    if any(v.startswith("tail") for v in a.variants):
+        import ctypes
+        xlib = ctypes.CDLL(str(nat.LIB_PATH.with_name("libdexiraft_corr_exp.so")))
+        vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+        xlib.dxr_xp_build_tail.restype = i32
+        xlib.dxr_xp_build_tail.argtypes = [vp, vp, i32, i32, i64, i64, i64, i64, vp, vp, i32, vp]
     dev = torch.device("cuda", 0)
     D = 256
     stream = torch.cuda.Stream(device=dev)
@@ -73,7 +83,10 @@ def main():
 
         def build(v):
             s = stream.cuda_stream
-            if v in ("ws", "prev"):
+            if v.startswith("tail"):
+                st = xlib.dxr_xp_build_tail(f1.data_ptr(), f2.data_ptr(), dt, layout, B, D, H, W,
+                                            pyr.data_ptr(), ws.data_ptr(), int(v[4:]), s)
+            elif v in ("ws", "prev"):
                 fn = lib if v == "ws" else prev
                 st = fn.dxr_corr_pyramid_build_ws(f1.data_ptr(), f2.data_ptr(), dt,
                                                    layout, B, D, H, W, 4, div, pyr.data_ptr(),
@@ -92,7 +105,7 @@ def main():
             for v in a.variants:
                 build(v)
                 torch.cuda.synchronize()
-                if v in ("ws", "prev"):
+                if v in ("ws", "prev") or v.startswith("tail"):
                     if ref is None:
                         ref = pyr.clone()
                     same = torch.equal(torch.nan_to_num(pyr.float(), nan=3.0),

@@ -7,7 +7,8 @@ then 12 lookups with 12 different coordinate sets.  This script captures that
 step as one HIP graph per variant, with the same synthetic inputs as bench.py,
 and times interleaved rounds of replays (HIP events, after a clock warm-up):
 
-  --block corr  build (product CorrBlock) + 12 lookups by dxr_xp_lookup variant
+  --block corr  build (product CorrBlock; variant -4: the --prev-lib library's
+                dxr_corr_pyramid_build_ws, product lookups) + 12 lookups by dxr_xp_lookup variant
                 (libdexiraft_corr_exp.so: 0 spatial level-2/3 gathers, 32 query-major,
                 64 the 256 x 16 shape, 128 1024 x 64) or the product's (-1);
   --block alt   12 on-the-fly lookups: dxr_alt_corr_lookup (-1, tile order),
@@ -46,8 +47,9 @@ def main():
     ap.add_argument("--no-check", type=int, nargs="*", default=[],
                     help="variants whose outputs are not checked (timing ablations)")
     ap.add_argument("--rounds", type=int, default=7)
-    ap.add_argument("--prev-lib", default=str(REPO / "scripts" / "libdexiraft_corr_prev.so"),
-                    help="variant -3: dxr_corr_lookup of this earlier product library")
+    ap.add_argument("--prev-lib", default=str(REPO / "scripts" / "libdexiraft_corr_r04.so"),
+                    help="variant -3: dxr_corr_lookup of this earlier product library; "
+                         "-4: its build")
     a = ap.parse_args()
     import dexiraft_amd
     from dexiraft_amd import _native as nat
@@ -60,10 +62,12 @@ def main():
     xp.dxr_xp_alt_lookup.argtypes = [vp, ctypes.POINTER(vp), vp, vp, i64, i64, i64, i64, i32,
                                      ctypes.c_float, vp, i32, vp]
     prev = None
-    if -3 in a.variants:
+    if -3 in a.variants or -4 in a.variants:
         prev = ctypes.CDLL(a.prev_lib)
-        prev.dxr_corr_lookup.restype = i32
-        prev.dxr_corr_lookup.argtypes = [vp, i32, i64, i64, i64, i32, i32, vp, vp, vp]
+        for name, (res, args) in nat.SIGNATURES.items():
+            if hasattr(prev, name):
+                getattr(prev, name).restype = res
+                getattr(prev, name).argtypes = args
     dev = torch.device("cuda", 0)
     B, (H, W), D = a.batch, SHAPES[a.workload], 256
     g = torch.Generator(device=dev)
@@ -90,13 +94,24 @@ def main():
         ws = torch.empty(max(nws, 0), dtype=torch.uint8, device=dev)
         s = stream.cuda_stream
 
+        bws = None
+        if a.block == "corr":
+            nb = lib.dxr_build_workspace_bytes(cb._in_dt, B, D, H, W)
+            bws = torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
+
         def step(v):
             if a.block == "corr":
-                f_1, f_2, st = cb._launch_build(f1, f2)
+                if v == -4:   # the previous library's build into the same buffer
+                    st = prev.dxr_corr_pyramid_build_ws(
+                        f1.data_ptr(), f2.data_ptr(), cb._in_dt, nat.DXR_NCHW, B, D, H, W, 4,
+                        float(D) ** 0.5, cb._buf.data_ptr(), cb._pyr_dt, nat.DXR_BUILD_AUTO,
+                        bws.data_ptr(), nb, s)
+                else:
+                    f_1, f_2, st = cb._launch_build(f1, f2)
                 assert st == 0
                 for c, o in zip(coords, outs):
-                    if v in (-1, -3):
-                        fn = lib.dxr_corr_lookup if v == -1 else prev.dxr_corr_lookup
+                    if v in (-1, -3, -4):
+                        fn = prev.dxr_corr_lookup if v == -3 else lib.dxr_corr_lookup
                         st = fn(cb._buf.data_ptr(), cb._pyr_dt, B, H, W, 4, 4, c.data_ptr(),
                                 o.data_ptr(), s)
                     else:

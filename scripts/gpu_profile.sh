@@ -17,7 +17,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/
 rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 find "$O/prof" -name '*kernel_stats.csv' -exec cp {} "$O/kernel_stats.csv" \;
 grep '^{' "$O/prof.log" | tail -n 1 > "$O/bench_under_rocprof.json"
-find "$O/prof" -name '*kernel_trace.csv' -exec python scripts/trace_gaps.py {} \; > "$O/trace_gaps.json" 2>&1
+find "$O/prof" -name '*kernel_trace.csv' -exec python scripts/trace_gaps.py {} "$WKEY" \; > "$O/trace_gaps.json" 2>&1
 rm -rf "$O/prof"
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $C --kernel-include-regex "corr_" --output-format csv \

@@ -7,9 +7,12 @@ followed by exactly 12 lookup kernels and then the next step's build (the back-t
 replays of the clock warm-up, the warmup steps and the timed steps), this
 reports medians of: the build kernels' duration, the lookup kernels' durations,
 the step span (build start to next build start), and the idle time of the span
-(span minus the kernels' durations: kernel boundaries and graph launches).
+(span minus the kernels' durations: kernel boundaries and graph launches), split
+by boundary: inside the build (split pass -> DMA build), build -> first lookup,
+between the lookups, and last lookup -> the next step's build (the graph
+replay boundary); the build's in-step span and the first lookup's duration.
 
-Usage: python scripts/trace_gaps.py <run_kernel_trace.csv>
+Usage: python scripts/trace_gaps.py <run_kernel_trace.csv> [workload key, e.g. sintel_b1_f32]
 """
 from __future__ import annotations
 
@@ -20,7 +23,7 @@ import sys
 import numpy as np
 
 
-def main(path: str) -> None:
+def main(path: str, workload: str | None = None) -> None:
     rows = []
     with open(path, newline="") as f:
         for r in csv.DictReader(f):
@@ -36,6 +39,8 @@ def main(path: str) -> None:
     # step starts: a build-side kernel right after a lookup (or first in the trace)
     starts = [i for i in range(len(rows)) if is_prep[i] and (i == 0 or is_look[i - 1])]
     b_us, l_us, x_us, span_us, idle_us = [], [], [], [], []
+    bspan_us, l1_us, gaps = [], [], {"in_build": [], "build_to_lookup": [], "between_lookups": [],
+                                     "step_to_step": []}
     for a, b in zip(starts, starts[1:]):
         looks = [i for i in range(a, b) if is_look[i]]
         aux = [i for i in range(a, b) if is_aux[i]]
@@ -44,20 +49,31 @@ def main(path: str) -> None:
             continue
         b_us.append(sum(rows[i][1] - rows[i][0] for i in prep) / 1e3)
         l_us.extend((rows[i][1] - rows[i][0]) / 1e3 for i in looks)
+        l1_us.append((rows[looks[0]][1] - rows[looks[0]][0]) / 1e3)
         x_us.append(sum(rows[i][1] - rows[i][0] for i in aux) / 1e3 / 12)
         span = (rows[b][0] - rows[a][0]) / 1e3
         busy = sum((rows[i][1] - rows[i][0]) for i in range(a, b)) / 1e3
         span_us.append(span)
         idle_us.append(span - busy)
+        # the build as the step sees it: first build kernel start to last build kernel end
+        bspan_us.append((rows[prep[-1]][1] - rows[prep[0]][0]) / 1e3)
+        gap = lambda i: max(rows[i + 1][0] - rows[i][1], 0) / 1e3  # noqa: E731
+        gaps["in_build"].append(sum(gap(i) for i in prep[:-1]))
+        gaps["build_to_lookup"].append(gap(prep[-1]))
+        gaps["between_lookups"].append(sum(gap(i) for i in range(prep[-1] + 1, b - 1)))
+        gaps["step_to_step"].append(gap(b - 1))
     if not b_us:
         print(json.dumps({"steps": 0, "note": "no build + 12 lookup steps found"}))
         return
     med = lambda v: round(float(np.median(v)), 2)  # noqa: E731
     print(json.dumps({
+        **({"workload": workload} if workload else {}),
         "steps": len(b_us),
         "build_us_median": med(b_us), "lookup_us_median": med(l_us),
         "lookup_order_us_median": med(x_us),
         "step_span_us_median": med(span_us), "idle_us_per_step_median": med(idle_us),
+        "build_in_step_us_median": med(bspan_us), "first_lookup_us_median": med(l1_us),
+        "idle_us_median_by_boundary": {k: med(v) for k, v in gaps.items()},
         "what": "back-to-back steps of the bench's step graph: build + 12 lookups, from the "
                 "rocprofv3 kernel trace of the same command (durations are kernel begin-end; "
                 "lookup_order_us: the on-the-fly lookup's ordering launches per lookup)",
@@ -65,4 +81,4 @@ def main(path: str) -> None:
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)

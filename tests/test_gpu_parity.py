@@ -487,6 +487,69 @@ def test_split_build_overflow_fallback(dx):
     assert (lv0[rest] - base[0][rest]).abs().max().item() <= 1e-5 * base[0].abs().max().item()
 
 
+@pytest.mark.parametrize("big_side", ["query", "target"])
+def test_prescaled_build_extreme_pixel_magnitudes(dx, big_side):
+    """pixels of very different magnitudes (1e36 queries against
+    1e-36 targets, and the reverse) give finite products of order one.  The
+    pre-split build undoes both pixels' scales with one ldexp by the exponent
+    sum, so these cells are f32-class like every other (the round-4 unscale
+    multiplied by the two factors in turn and overflowed / went subnormal in
+    between)."""
+    H, W = 24, 32
+    f1, f2 = _pair(H=H, W=W, seed=191)
+    f1, f2 = f1.clone(), f2.clone()
+    big, tiny = (f1, f2) if big_side == "query" else (f2, f1)
+    big[0, :, 5, 9] *= 1.0e36                       # one pixel of one map ~1e36
+    tiny[0, :, 11, 20] *= 1.0e-36                   # pixels of the other ~1e-36, ~1e-30
+    tiny[0, :, 2, 3] *= 1.0e-30
+    cb = dx.CorrBlock(f1, f2)
+    r1 = f1[0].reshape(256, -1).double().cpu().numpy()
+    r2 = f2[0].reshape(256, -1).double().cpu().numpy()
+    ref = (r1.T @ r2) / 16.0                        # float64 level 0 [query, target]
+    absref = (np.abs(r1).T @ np.abs(r2)) / 16.0     # scale of each dot product
+    got = cb.corr_pyramid[0][:, 0].reshape(H * W, H * W).double().cpu().numpy()
+    assert np.isfinite(got).all()
+    err = np.abs(got - ref) / absref
+    big_px, tiny_px = 5 * W + 9, [11 * W + 20, 2 * W + 3]
+    cells = [(big_px, t) for t in tiny_px] if big_side == "query" else \
+        [(q, big_px) for q in tiny_px]
+    for q, t in cells:
+        assert 0.1 < abs(ref[q, t]) < 1e8, (q, t, ref[q, t])    # a finite, normal product
+        assert err[q, t] <= 4e-6, (q, t, got[q, t], ref[q, t])
+    assert err.max() <= 4e-5
+
+
+def _dma_units(B, H, W):
+    """Units of the DMA build (two 128-query blocks x one 8x16 tile)."""
+    qt = (H * W + 127) // 128
+    return B * ((qt + 1) // 2) * ((H + 7) // 8) * ((W + 15) // 16)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_tail_quarter_units_bit_identical(dx, dtype):
+    """The DMA build runs the last partial dispatch round as quarter units
+    (corr_build.hip dma_grid / dma_quarter) when it is at most an eighth of a round.  A
+    pair whose units fall in that tail (Sintel B=1: 1,568 units on 512 slots)
+    gets the same pages bit for bit as in a batch whose grid has no tail split."""
+    H, W = 55, 128
+    slots = 2 * torch.cuda.get_device_properties(0).multi_processor_count
+    t1 = _dma_units(1, H, W) % slots
+    if t1 == 0 or 8 * t1 > slots:
+        pytest.skip("no tail split at B=1 on this device")
+    b2 = next((b for b in range(2, 33) if _dma_units(b, H, W) % slots == 0 or
+               8 * (_dma_units(b, H, W) % slots) > slots), None)
+    if b2 is None:
+        pytest.skip("no batch without a tail split")
+    f1, f2 = _pair(B=b2, H=H, W=W, seed=201, dist="fnet")
+    if dtype == "bf16":
+        f1, f2 = f1.bfloat16(), f2.bfloat16()
+    one = dx.CorrBlock(f1[:1].contiguous(), f2[:1].contiguous())
+    many = dx.CorrBlock(f1, f2)
+    for lvl in range(4):
+        a, b = one.corr_pyramid[lvl][:, 0], many.corr_pyramid[lvl][: H * W, 0]
+        assert torch.equal(torch.nan_to_num(a, nan=2.0), torch.nan_to_num(b, nan=2.0)), lvl
+
+
 @pytest.mark.parametrize("W,layout", [(62, "nchw"), (32, "nhwc"), (44, "nchw")])
 def test_prescaled_build_nonfinite_fallback_forms(dx, W, layout):
     """Pages that see an inf/NaN operand are recomputed from the f32 operands on

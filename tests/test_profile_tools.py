@@ -39,6 +39,23 @@ def test_trace_gaps_step_timeline(tmp_path):
     assert r["lookup_us_median"] == 8.0
     assert r["step_span_us_median"] == round((100_000 + 12 * 8_000 + 13 * 700) / 1e3, 2)
     assert r["idle_us_per_step_median"] == round(13 * 700 / 1e3, 2)
+    assert r["build_in_step_us_median"] == 100.0
+    assert r["first_lookup_us_median"] == 8.0
+    assert r["idle_us_median_by_boundary"] == {"in_build": 0.0, "build_to_lookup": 0.7,
+                                               "between_lookups": round(11 * 0.7, 2),
+                                               "step_to_step": 0.7}
+
+
+def test_trace_gaps_split_build_boundaries(tmp_path):
+    """Two build kernels (split pass + DMA build): the gap between them is the
+    build's own, and the build's in-step span covers both."""
+    p = tmp_path / "run_kernel_trace.csv"
+    _trace(p, steps=4, prep=("split_pairs_kernel<false>", "corr_build_dma_kernel<float>"),
+           build_ns=50_000)
+    r = _run(p)
+    assert r["build_us_median"] == 100.0
+    assert r["build_in_step_us_median"] == 100.7
+    assert r["idle_us_median_by_boundary"]["in_build"] == 0.7
 
 
 def test_trace_gaps_on_the_fly_block_prep_kernels(tmp_path):
