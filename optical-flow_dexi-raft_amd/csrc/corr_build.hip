@@ -345,38 +345,37 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
   }
   if (g.levels < 2) return;
 
-  // Levels 1 and 2, streamed one tile pair at a time to keep register pressure
-  // low: level-1 row t (2x2 pool of level-0 rows 2t, 2t+1, which live in lane
-  // halves 0 / 1; both halves compute identical values) goes to LDS at once, and
-  // the level-2 row u is pooled from level-1 rows 2u, 2u+1 while they are live.
-  float l2[2][4];
+  // Levels 1 and 2 (round 5): lane half h pools the level-1 cells 4h .. 4h+3 of
+  // every level-1 row t.  acc[t][c] holds level-0 row 2t + h, col c; one
+  // v_permlane32_swap of the pair (col k, col 8 + k) leaves every lane with
+  // rows 2t AND 2t + 1 of col 8h + k (x: row 2t, y: row 2t + 1), so each cell is
+  // pooled in-lane in the reference's window order ((v00 + v01) + v10) + v11.
+  // Per row t: 8 swaps + 16 VALU (round 4: both halves pooled all 8 cells from
+  // self-swapped copies, 64 VALU + 4 selects).  acc is consumed (level 0 is out).
+  // Level 2 follows in-lane for cols 2h, 2h + 1 (l2[u][i]: level-2 row u, col 2h + i).
+  float l2[2][2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    float l1[2][8];
+    float l1[2][4];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int t = 2 * u + s;
+      float x[8], y[8];
 #pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        // v_permlane32_swap of a value with itself gives every lane both halves'
-        // values: the lower (row 2t, kh = 0) and the upper (row 2t + 1) — no LDS
-        // shuffle, no selects (round 4; was __shfl_xor + four selects per pair)
-        const auto x0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[t][2 * m]),
-                                                         __float_as_uint(acc[t][2 * m]), false, false);
-        const auto x1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[t][2 * m + 1]),
-                                                         __float_as_uint(acc[t][2 * m + 1]), false, false);
-        const float t0 = __uint_as_float(x0[0]), t1 = __uint_as_float(x1[0]);
-        const float b0 = __uint_as_float(x0[1]), b1 = __uint_as_float(x1[1]);
-        l1[s][m] = (((t0 + t1) + b0) + b1) * 0.25f;
+      for (int k = 0; k < 8; ++k) {
+        const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[t][k]),
+                                                        __float_as_uint(acc[t][8 + k]), false, false);
+        x[k] = __uint_as_float(p[0]);
+        y[k] = __uint_as_float(p[1]);
       }
-      // the lane half's four values by selects (indexing l1 by the runtime h
-      // compiled to an 8-way compare/select chain per value)
-      st4(wl + j * P1 + t * 8 + 4 * h, h ? l1[s][4] : l1[s][0], h ? l1[s][5] : l1[s][1],
-          h ? l1[s][6] : l1[s][2], h ? l1[s][7] : l1[s][3]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        l1[s][i] = (((x[2 * i] + x[2 * i + 1]) + y[2 * i]) + y[2 * i + 1]) * 0.25f;
+      st4(wl + j * P1 + t * 8 + 4 * h, l1[s][0], l1[s][1], l1[s][2], l1[s][3]);
     }
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
-      l2[u][n] = (((l1[0][2 * n] + l1[0][2 * n + 1]) + l1[1][2 * n]) + l1[1][2 * n + 1]) * 0.25f;
+    for (int i = 0; i < 2; ++i)
+      l2[u][i] = (((l1[0][2 * i] + l1[0][2 * i + 1]) + l1[1][2 * i]) + l1[1][2 * i + 1]) * 0.25f;
   }
   epi_sync<EX>();
   {
@@ -401,32 +400,38 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
   }
   if (g.levels < 3) return;   // no barriers below this point
 
+  // Level 3 (8x8 of level 0) is in-lane too: lane half h pools cell h.
+  const float l3 = (((l2[0][0] + l2[0][1]) + l2[1][0]) + l2[1][1]) * 0.25f;
+
   // Level 2: [q][2][4] per page; lane (j, h) writes row h (a 1 KiB wave run).
+  // Swapping (row 0, row 1) of each of the half's two cols gives lane half h
+  // row h whole: x = cols 0-1, y = cols 2-3.
   {
     OT* const pb2 = pyr + g.loff[2] + page * (BM * NTGT / 16);
     OT* pg2 = pb2 + (long long)wave * 32 * 8 + j * 8 + 4 * h;
-    // row h of the lane half (selects, not a runtime index into a private array)
-    const float r0 = h ? l2[1][0] : l2[0][0], r1 = h ? l2[1][1] : l2[0][1];
-    const float r2 = h ? l2[1][2] : l2[0][2], r3 = h ? l2[1][3] : l2[0][3];
+    float r[4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(l2[0][i]),
+                                                      __float_as_uint(l2[1][i]), false, false);
+      r[i] = __uint_as_float(p[0]);
+      r[2 + i] = __uint_as_float(p[1]);
+    }
     if constexpr (sizeof(OT) == 4) {
-      epi_put<EX>(pb2, pg2, f32x4v{r0, r1, r2, r3});
+      epi_put<EX>(pb2, pg2, f32x4v{r[0], r[1], r[2], r[3]});
     } else {
       u32x2v w;
-      w.x = to_out2<OT>(r0, r1);
-      w.y = to_out2<OT>(r2, r3);
+      w.x = to_out2<OT>(r[0], r[1]);
+      w.y = to_out2<OT>(r[2], r[3]);
       epi_put<EX>(pb2, pg2, w);
     }
   }
   if (g.levels < 4) return;
 
-  // Level 3 (8x8 of level 0): lane (j, h) writes cell h.
-  float l3[2];
-#pragma unroll
-  for (int v = 0; v < 2; ++v)
-    l3[v] = (((l2[0][2 * v] + l2[0][2 * v + 1]) + l2[1][2 * v]) + l2[1][2 * v + 1]) * 0.25f;
+  // Level 3: lane (j, h) writes cell h.
   OT* const pb3 = pyr + g.loff[3] + page * (BM * 2);
   OT* pg3 = pb3 + (long long)wave * 32 * 2;
-  epi_put<EX>(pb3, pg3 + j * 2 + h, to_out<OT>(h ? l3[1] : l3[0]));
+  epi_put<EX>(pb3, pg3 + j * 2 + h, to_out<OT>(l3));
 }
 
 // PAGED: write the paged pyramid (levels 1..4 fused).  !PAGED: write level 0

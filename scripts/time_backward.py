@@ -28,6 +28,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="sintel", choices=["sintel", "chairs"])
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--loss", default="vdot", choices=["vdot", "mulsum"])
+    ap.add_argument("--clone-inputs", action="store_true")
     a = ap.parse_args()
     import dexiraft_amd
     dev = torch.device("cuda", 0)
@@ -49,11 +51,26 @@ def main():
         cb = dexiraft_amd.CorrBlock(a1, a2)
         loss = 0.0
         for c, w in zip(coords, wts):
-            loss = loss + (cb(c) * w).sum()
+            out = cb(c)
+            # the stand-in for the update block: <w_k, lookup_k>.  --loss mulsum
+            # (rounds 1-4) as a multiply, a sum and their backwards; vdot one
+            # fused reduction whose backward is w_k * grad (the same gradients)
+            loss = loss + ((out * w).sum() if a.loss == "mulsum" else
+                           torch.vdot(out.reshape(-1), w.reshape(-1)))
         return loss
 
+    # the fmaps are the encoders' outputs (core/raft.py:139-142), allocated before
+    # the correlation path runs: leaves that persist across steps, so the peak
+    # below is the path's own extra memory (--clone-inputs: rounds 1-4, a fresh
+    # clone of both per step inside the measured window, 13.8 MB at Sintel)
+    a1p, a2p = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
+
     def step(backward=True):
-        a1, a2 = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
+        if a.clone_inputs:
+            a1, a2 = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
+        else:
+            a1, a2 = a1p, a2p
+            a1.grad = a2.grad = None      # the gradients are this step's outputs
         loss = forward_loss(a1, a2)
         if backward:
             loss.backward()
@@ -61,6 +78,7 @@ def main():
 
     for _ in range(2):
         step()
+    a1p.grad = a2p.grad = None          # the fmap gradients count as the step's memory
     torch.cuda.synchronize()
     torch.cuda.reset_peak_memory_stats()
     base = torch.cuda.memory_allocated()
@@ -96,7 +114,9 @@ def main():
                 if t is None:
                     t = getattr(ev, "cuda_time_total", 0.0)
                 kern[key] = round(kern.get(key, 0.0) + t / 1e3, 3)
-    print(json.dumps({"workload": a.workload, "fmap": [H, W], "forward_ms": round(t_fwd, 3),
+    print(json.dumps({"workload": a.workload, "fmap": [H, W], "loss": a.loss,
+                      "inputs": "cloned per step" if a.clone_inputs else "persistent leaves",
+                      "forward_ms": round(t_fwd, 3),
                       "train_step_ms": round(t_step, 3), "backward_ms": round(t_step - t_fwd, 3),
                       "peak_extra_MB": round(peak / 2 ** 20, 1),
                       "dV_MB": round(B * (H * W) ** 2 * 4 / 2 ** 20, 1),
