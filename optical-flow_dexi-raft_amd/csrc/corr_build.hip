@@ -303,9 +303,9 @@ __device__ __forceinline__ void store8(OT* ub, OT* dst, const float* src) {
 }
 
 template <typename OT, int EX = 0>
-__device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT* __restrict__ pyr,
-                                               const BuildGeom& g, long long page, int wave,
-                                               int lane) {
+__device__ __forceinline__ float paged_epilogue(f32x16 (&acc)[4], float* lds, OT* __restrict__ pyr,
+                                                const BuildGeom& g, long long page, int wave,
+                                                int lane) {
   const int j = lane & 31, h = lane >> 5;
   float* wl = lds + wave * 16 * P0;   // this wave's private LDS region
 
@@ -343,7 +343,7 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
     }
     epi_sync<EX>();
   }
-  if (g.levels < 2) return;
+  if (g.levels < 2) return 0.f;
 
   // Levels 1 and 2 (round 5): lane half h pools the level-1 cells 4h .. 4h+3 of
   // every level-1 row t.  acc[t][c] holds level-0 row 2t + h, col c; one
@@ -398,7 +398,7 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
       }
     }
   }
-  if (g.levels < 3) return;   // no barriers below this point
+  if (g.levels < 3) return 0.f;   // no barriers below this point
 
   // Level 3 (8x8 of level 0) is in-lane too: lane half h pools cell h.
   const float l3 = (((l2[0][0] + l2[0][1]) + l2[1][0]) + l2[1][1]) * 0.25f;
@@ -426,12 +426,15 @@ __device__ __forceinline__ void paged_epilogue(f32x16 (&acc)[4], float* lds, OT*
       epi_put<EX>(pb2, pg2, w);
     }
   }
-  if (g.levels < 4) return;
+  if (g.levels < 4) return 0.f;
 
   // Level 3: lane (j, h) writes cell h.
   OT* const pb3 = pyr + g.loff[3] + page * (BM * 2);
   OT* pg3 = pb3 + (long long)wave * 32 * 2;
   epi_put<EX>(pb3, pg3 + j * 2 + h, to_out<OT>(l3));
+  // the lane pair (j, 0), (j, 1) pools every f32 value of query j into its two
+  // level-3 cells: a non-finite value anywhere in the wave's acc shows here
+  return l3;
 }
 
 // PAGED: write the paged pyramid (levels 1..4 fused).  !PAGED: write level 0
@@ -1456,28 +1459,41 @@ __global__ __launch_bounds__(PX * 16) void split_pairs_kernel(const float* __res
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-// LDS of corr_build_dma_kernel: ring | target scale exponents s (128 int) |
-// flag (a non-finite sum: recompute).
+// LDS of corr_build_dma_kernel: ring | target scale exponents s (128 int).
 constexpr int DMA_LDS_RING = DMA_RING * DMA_STAGE;
-constexpr int DMA_LDS_BYTES = DMA_LDS_RING + NTGT * 4 + 16;
+constexpr int DMA_LDS_BYTES = DMA_LDS_RING + NTGT * 4;
 // Tail quarter units (dma_tail_split): the exchange region (two 32-query groups
 // x four 32-target tiles of accumulators) and the epilogue staging after it.
 constexpr int DMA_XS_BYTES = 2 * 4 * 16 * 64 * 4;
 static_assert(DMA_XS_BYTES + WAVES * 16 * P0 * 4 <= DMA_LDS_RING, "tail exchange + staging fit");
 
 // Unscale, divide by sqrt(D) and write one wave's 32 queries x 8x16 targets
-// (f32 build), then — if the workgroup saw a non-finite sum — recompute them on
+// (f32 build), then — if the wave saw a non-finite sum — recompute them on
 // the exact-f32 MFMA and write them again.  acc[t][r] is query qj x tile pixel
 // (row 2t + kh, col r).  Shared by the whole-unit and the quarter-unit forms.
 template <typename OT, bool DIV>
 __device__ __forceinline__ void dma_finish_f32(f32x16 (&acc)[4], const BuildGeom& g,
                                                OT* __restrict__ pyr, float* stage, long long page,
-                                               int w4, int lane, int flags, int sq, int qj,
+                                               int w4, int lane, int sq, int qj,
                                                int trow0, int th0, int tw0, int b,
                                                const float* __restrict__ f1,
                                                const float* __restrict__ f2, int ps, int ks,
                                                const int* sexp) {
   const int kh = lane >> 5;
+  // Non-finite sums (an inf/NaN operand pixel) are found per wave after the
+  // epilogue from the level-3 cells, which pool every value of the lane's query
+  // (round 5: one compare instead of 64 compares + 64 scalar ORs per wave and a
+  // workgroup flag; the recompute only rewrites the wave's own pages anyway).
+  // An exponent sum that overflows a finite value also reads as non-finite and
+  // takes the exact path, whose f32 result overflows the same way.  Fewer than 4
+  // levels: the values themselves are checked before the epilogue consumes them.
+  bool bad = false;
+  if (g.levels < 4) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) bad |= !(__builtin_fabsf(acc[t][r]) <= 3.40282347e38f);
+  }
   // ldexp by the exponent sum -(s_q + s_t) + log2(1/sqrt(D)) (when that is
   // exact): one rounding of the exact value whatever the pixel magnitudes.
   // (Round 4 multiplied by 2^-s_q / sqrt(D), then by 2^-s_t: the same two VALU
@@ -1502,9 +1518,10 @@ __device__ __forceinline__ void dma_finish_f32(f32x16 (&acc)[4], const BuildGeom
     }
   }
   if constexpr (DIV) scale_acc<DIV>(acc, g);
-  paged_epilogue<OT, 1 | 4>(acc, stage, pyr, g, page, w4, lane);
-  if (flags & 1) {
-    // The workgroup saw a non-finite sum: its pages are recomputed on the
+  const float l3 = paged_epilogue<OT, 1 | 4>(acc, stage, pyr, g, page, w4, lane);
+  if (g.levels >= 4) bad = !(__builtin_fabsf(l3) <= 3.40282347e38f);
+  if (__ballot(bad) != 0) {   // wave-uniform
+    // The wave saw a non-finite sum: its pages are recomputed on the
     // exact-f32 MFMA (v_mfma_f32_32x32x2_f32: each lane supplies channel k0 + kh
     // of its A row = target trow0 + 32 t and of its B column = query qj; same
     // output layout as the f16 products, nothing to undo) and written again over
@@ -1546,11 +1563,10 @@ __device__ __forceinline__ void dma_finish_f32(f32x16 (&acc)[4], const BuildGeom
 }
 
 // Per-workgroup prologue of both forms: the lane's query exponent, the tile's
-// 128 target exponents (LDS), the flag word.
+// 128 target exponents (LDS).
 __device__ __forceinline__ void dma_scales(const BuildGeom& g, const int* __restrict__ ex1,
                                            const int* __restrict__ ex2, int b, int qj, int th0,
-                                           int tw0, int tid, int& sq, int* sexp,
-                                           int* flags) {
+                                           int tw0, int tid, int& sq, int* sexp) {
   sq = qj < g.N ? ex1[(long long)b * g.N + qj] : 0;
   if (tid < NTGT) {
     // the target pixel's scale exponent s (in [-125, 125])
@@ -1559,7 +1575,6 @@ __device__ __forceinline__ void dma_scales(const BuildGeom& g, const int* __rest
     const int e = in ? ex2[(long long)b * g.N + (th0 + r) * g.W + tw0 + c] : 0;
     sexp[tid] = e;
   }
-  if (tid == 0) *flags = 0;
 }
 
 // Quarter units of the tail (dma_tail_split): workgroup blockIdx.x >= nmain
@@ -1580,7 +1595,6 @@ __device__ __forceinline__ void dma_quarter(unsigned char* smem, const uint8_t* 
                                             const float* __restrict__ f2, int ps, int ks, int pstr,
                                             int kstr, const BuildGeom& g) {
   int* const sexp = reinterpret_cast<int*>(smem + DMA_LDS_RING);
-  int* const flags = reinterpret_cast<int*>(smem + DMA_LDS_RING + NTGT * 4);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int gl = wave >> 2, t = wave & 3;
@@ -1596,7 +1610,7 @@ __device__ __forceinline__ void dma_quarter(unsigned char* smem, const uint8_t* 
   const long long spstride = (long long)g.D * g.N * (BF ? 2 : 4);
   const int qj = q0 + gl * 32 + j;
   int sq = 0;
-  if constexpr (!BF) dma_scales(g, ex1, ex2, b, qj, th0, tw0, tid, sq, sexp, flags);
+  if constexpr (!BF) dma_scales(g, ex1, ex2, b, qj, th0, tw0, tid, sq, sexp);
 
   const __amdgpu_buffer_rsrc_t rq =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sp1 + b * spstride), (short)0,
@@ -1674,12 +1688,6 @@ __device__ __forceinline__ void dma_quarter(unsigned char* smem, const uint8_t* 
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();   // ring reads done: the LDS is free for reuse
-  if constexpr (!BF) {
-    bool bad = false;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) bad |= !(__builtin_fabsf(acc[r]) <= 3.40282347e38f);
-    if (bad) *flags = 1;
-  }
   // the group's four tiles meet in LDS: [group][tile][r / 4][lane][4] f32
   float* const xs = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -1702,12 +1710,12 @@ __device__ __forceinline__ void dma_quarter(unsigned char* smem, const uint8_t* 
     scale_acc<DIV>(a4, g);
     paged_epilogue<OT, 3>(a4, stage, pyr, g, page, w4, lane);
   } else {
-    dma_finish_f32<OT, DIV>(a4, g, pyr, stage, page, w4, lane, *flags, sq, qj, trow0, th0, tw0, b,
-                            f1, f2, ps, ks, sexp);
+    dma_finish_f32<OT, DIV>(a4, g, pyr, stage, page, w4, lane, sq, qj, trow0, th0, tw0, b, f1,
+                            f2, ps, ks, sexp);
   }
 }
 
-// A workgroup whose sums are not finite (an inf/NaN operand pixel) recomputes
+// A wave whose sums are not finite (an inf/NaN operand pixel) recomputes
 // its pages from the f32 operands (`f1`, `f2`: element (pixel p, channel k) at
 // p * ps + k * ks of a pair's fmap) on the exact-f32 MFMA, in place: IEEE
 // semantics as the reference's f32 matmul (inf x finite = inf, inf x 0 = NaN,
@@ -1736,7 +1744,6 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
     return;
   }
   int* const sexp = reinterpret_cast<int*>(smem + DMA_LDS_RING);
-  int* const flags = reinterpret_cast<int*>(smem + DMA_LDS_RING + NTGT * 4);
 
   const int tid = threadIdx.x, lane = tid & 63;
   // wave-uniform (SGPR): the DMA's LDS base must be, or the compiler emits a
@@ -1753,7 +1760,7 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
   // exponents: the lane's query, the tile's 128 targets (LDS, by tile pixel)
   const int qj = q0 + wave * 32 + j;
   int sq = 0;
-  if constexpr (!BF) dma_scales(g, ex1, ex2, b, qj, th0, tw0, tid, sq, sexp, flags);
+  if constexpr (!BF) dma_scales(g, ex1, ex2, b, qj, th0, tw0, tid, sq, sexp);
 
   const __amdgpu_buffer_rsrc_t rq =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sp1 + b * spstride), (short)0,
@@ -1799,17 +1806,15 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
   const int tl_off = DMA_TILE + trow0 * 64 + 16 * ((2 + kh) ^ kt);
 
   f32x16 acc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-
   // exponent loads and LDS writes above must not count against the ring's vmcnt
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int nk = g.D / (BF ? 2 * BKS : BKS);
   dma(0);
   if (nk > 1) dma(1);
-  for (int kk = 0; kk < nk; ++kk) {
+  // one k step; the first starts every accumulator from the MFMA's inline zero
+  // (no 64 v_mov per wave to clear them)
+  auto kstep = [&](int kk, auto first_tag) {
+    constexpr bool FIRST = decltype(first_tag)::value;
     // this wave's 3 DMAs of step kk have landed (those of kk + 1 stay in flight);
     // the barrier publishes every wave's, and orders the ring slot's previous
     // readers (step kk - 1) before the refill below
@@ -1827,7 +1832,8 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const bf8v t0v = *reinterpret_cast<const bf8v*>(st + th_off + t * 2048);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(t0v, q0v, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(t0v, q0v, FIRST ? f32x16{} : acc[t], 0, 0,
+                                                         0);
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -1842,12 +1848,14 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
         const h8v th = *reinterpret_cast<const h8v*>(st + th_off + t * 2048);
         const h8v tl = *reinterpret_cast<const h8v*>(st + tl_off + t * 2048);
         // small terms first
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, FIRST ? f32x16{} : acc[t], 0, 0, 0);
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc[t], 0, 0, 0);
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qh, acc[t], 0, 0, 0);
       }
     }
-  }
+  };
+  kstep(0, std::true_type{});
+  for (int kk = 1; kk < nk; ++kk) kstep(kk, std::false_type{});
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();   // ring reads done: the LDS is free for reuse
   const bool live = pc.qblk + half < g.qt;            // this half's query block exists
@@ -1861,19 +1869,11 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
     return;
   }
 
-  // vote: a non-finite sum means an operand pixel was not finite; the
-  // workgroup's pages are then recomputed from the f32 operands
-  bool bad = false;
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) bad |= !(__builtin_fabsf(acc[t][r]) <= 3.40282347e38f);
-  if (bad) *flags = 1;
-  __syncthreads();
-  // a half past the last query block has no page (the epilogue syncs per wave)
+  // a half past the last query block has no page (the epilogue syncs per wave;
+  // a wave whose sums are not finite recomputes its pages from the f32 operands)
   if (live)
-    dma_finish_f32<OT, DIV>(acc, g, pyr, stage, page, w4, lane, *flags, sq, qj, trow0, th0, tw0, b,
-                            f1, f2, ps, ks, sexp);
+    dma_finish_f32<OT, DIV>(acc, g, pyr, stage, page, w4, lane, sq, qj, trow0, th0, tw0, b, f1,
+                            f2, ps, ks, sexp);
 }
 
 // Floor-mode 2x2 average pool of one pyramid level into the next, for levels
