@@ -17,9 +17,15 @@ the max elapsed time over ranks is used.  After timing, a float64 checksum of
 every pair's 12th lookup output is all-gathered over RCCL (shard.gather_pairs)
 and reported.  Rank 0 prints ONE JSON line.
 
-Execution (``--mode graph``, default): ``value`` is timed on ONE HIP graph per
-step (build + 12 lookups), replayed K times — the launch-bound lookups would
-otherwise be host-bound in Python.  Before the W warmup steps the step is
+Execution (``--mode graph``, default): ``value`` is timed on ONE HIP graph of
+G = ``--steps-per-graph`` (4) consecutive whole steps (build + 12 lookups each),
+replayed K / G times — the launch-bound lookups would otherwise be host-bound in
+Python, and every replay of a graph pays the HIP runtime's graph-launch boundary
+(~10 us on a Sintel step, round 5), which G steps per graph pay once.
+Every step runs on the rank's synthetic pair set (fmaps + 12 coordinate sets), as
+in rounds 1-4; ``--pair-sets S`` cycles S distinct sets over a graph's steps
+instead (the fmaps then come from HBM, not from the caches a just-run encoder
+leaves them in).  Before the W warmup steps the step is
 replayed untimed for ``--clock-warmup-s`` (0.5 s): MI355X raises its clocks only
 after some milliseconds of load, and 30 timed steps behind 3 warmups read 11 %
 below the steady rate (round 2: 3,936 vs 4,414-4,454 pairs/s at 300-2,000 steps).
@@ -35,6 +41,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import socket
 import subprocess
@@ -185,14 +192,19 @@ def trace_timeline(workload):
         except ValueError:
             continue
         if data.get("workload") == workload and data.get("steps", 0) > 0:
+            mean = "idle_us_per_step_mean" in data    # round 5+: means over the steps
             return {"build_in_step_us": data.get("build_in_step_us_median"),
-                    "idle_us_per_step": data.get("idle_us_per_step_median"),
-                    "idle_us_by_boundary": data.get("idle_us_median_by_boundary"),
+                    "idle_us_per_step": data.get("idle_us_per_step_mean" if mean
+                                                 else "idle_us_per_step_median"),
+                    "idle_us_by_boundary": data.get("idle_us_mean_by_boundary" if mean
+                                                    else "idle_us_median_by_boundary"),
                     "first_lookup_us": data.get("first_lookup_us_median"),
                     "lookup_us": data.get("lookup_us_median"),
-                    "step_span_us": data.get("step_span_us_median"),
+                    "step_span_us": data.get("step_span_us_mean" if mean
+                                             else "step_span_us_median"),
                     "source": f"{f.relative_to(REPO)} (rocprofv3 kernel trace of this bench, "
-                              f"medians over {data['steps']} steps)"}
+                              f"{data['steps']} steps: idle and span "
+                              f"{'means' if mean else 'medians'}, kernel durations medians)"}
     return None
 
 
@@ -346,6 +358,12 @@ def main():
                     help="strong scaling: this many pairs per step split over the ranks (C4: 64)")
     ap.add_argument("--dtype", default=None, choices=["f32", "bf16"])
     ap.add_argument("--mode", default="graph", choices=["graph", "eager"])
+    ap.add_argument("--steps-per-graph", type=int, default=4,
+                    help="graph mode: consecutive steps (each its own pair set) captured in one "
+                         "HIP graph; reduced to gcd(--steps, this) so exactly K steps are timed")
+    ap.add_argument("--pair-sets", type=int, default=1,
+                    help="distinct synthetic pair sets cycled over a graph's steps (default 1: "
+                         "every step on the rank's one pair set, as rounds 1-4; DESIGN §6)")
     ap.add_argument("--block", default="corr", choices=["corr", "alt"],
                     help="corr: CorrBlock (full pyramid); alt: AlternateCorrBlock (on the fly, C5)")
     ap.add_argument("--layout", default="nchw", choices=["nchw", "nhwc"],
@@ -380,24 +398,34 @@ def main():
         B = args.batch or b_default
         total = world * B
     dtype = args.dtype or dt_default
-    f1, f2, coords = make_inputs(B, H, W, dtype, seed=1234 + rank, dev=dev)
-    if args.layout == "nhwc":
-        f1 = f1.contiguous(memory_format=torch.channels_last)
-        f2 = f2.contiguous(memory_format=torch.channels_last)
+    # steps per graph replay; each step of a replay runs on its own pair set
+    G = math.gcd(args.steps, max(args.steps_per_graph, 1)) if args.mode == "graph" else 1
+    sets = []
+    for i in range(min(G, max(args.pair_sets, 1))):
+        f1, f2, coords = make_inputs(B, H, W, dtype, seed=1234 + rank + 7919 * i, dev=dev)
+        if args.layout == "nhwc":
+            f1 = f1.contiguous(memory_format=torch.channels_last)
+            f2 = f2.contiguous(memory_format=torch.channels_last)
+        sets.append((f1, f2, coords))
+    sets = [sets[i % len(sets)] for i in range(G)]
+    f1, f2, coords = sets[0]
     stream = torch.cuda.Stream(device=dev)
 
     state = {}
     block_cls = dexiraft_amd.CorrBlock if args.block == "corr" else dexiraft_amd.AlternateCorrBlock
 
-    def build():
-        state["cb"] = block_cls(f1, f2, radius=RADIUS)
+    def build(i=0):
+        # the previous step's block and outputs go first (one pyramid alive at a time)
+        state.pop("outs", None)
+        state.pop("cb", None)
+        state["cb"] = block_cls(sets[i][0], sets[i][1], radius=RADIUS)
 
-    def lookups():
-        state["outs"] = [state["cb"](c) for c in coords]
+    def lookups(i=0):
+        state["outs"] = [state["cb"](c) for c in sets[i][2]]
 
-    def step():
-        build()
-        lookups()
+    def step(i=0):
+        build(i)
+        lookups(i)
 
     timing = ("lookup = hip events around back-to-back replays of a graph of the step's 12 "
               "lookups / 12; build = hip events around back-to-back replays of a graph of "
@@ -408,11 +436,12 @@ def main():
             step()
         torch.cuda.synchronize()
         if args.mode == "graph":
-            # The whole step (build + 12 lookups) as ONE graph: what a serving loop
-            # replays; `value` is timed on it.
+            # G whole steps (build + 12 lookups each, G pair sets) as ONE graph: what
+            # a serving loop over a stream of pairs replays; `value` is timed on it.
             g_step = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_step, stream=stream):
-                step()
+                for i in range(G):
+                    step(i)
             run_step = g_step.replay
         else:
             run_step = step
@@ -427,13 +456,13 @@ def main():
                 run_step()
             n_clock += 20
             torch.cuda.synchronize()
-        for _ in range(args.warmup):
+        for _ in range(-(-args.warmup // G)):
             run_step()
         torch.cuda.synchronize()
 
         barrier(world)
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(args.steps // G):     # exactly K steps
             run_step()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
@@ -455,10 +484,10 @@ def main():
         # the same command's kernel trace (scripts/trace_gaps.py, profiles/).
         if args.mode == "graph":
             keep = dict(state)            # the step graph's own tensors stay allocated
-            cb = state["cb"]
+            cb = state["cb"]              # the last step's block, with its pair set's coords
             g_look = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_look, stream=stream, pool=g_step.pool()):
-                [cb(c) for c in coords]
+                [cb(c) for c in sets[G - 1][2]]
             # the build alone, as a graph of back-to-back builds (each block freed
             # before the next is built, as in the step); in the step graph's pool,
             # so its blocks reuse that pool's free memory (a private
@@ -533,8 +562,10 @@ def main():
                             f"{img_h}x{img_w} (fmap {H}x{W}), D={D}, r={RADIUS}, L={LEVELS}",
                 "pairs_per_gpu": B, "fmap_layout": args.layout, "mode": args.mode,
                 "parallelism": f"pairs sharded x{world}",
-                "step_timing": "one HIP graph per step (build + 12 lookups)"
-                               if args.mode == "graph" else "eager launches",
+                "step_timing": (f"one HIP graph per {G} consecutive whole steps (build + 12 "
+                                f"lookups each); {args.steps // G} replays"
+                                if args.mode == "graph" else "eager launches"),
+                "steps_per_graph": G, "pair_sets": len({id(t[0]) for t in sets}),
                 "kernel_timing": timing,
                 "clock_warmup": f"{n_clock} untimed step replays ({args.clock_warmup_s} s) before "
                                 f"the {args.warmup} warmup steps",

@@ -9,7 +9,10 @@ around back-to-back replays:
   one_step   the bench's step graph (build + 12 lookups), per replay;
   two_steps  a graph holding the same step twice, per step;
   tiny       a graph of one tiny kernel (torch fill of 1 element), per replay;
-  tiny_x14   a graph of 14 such kernels (the step's kernel count), per replay.
+  tiny_x14   a graph of 14 such kernels (the step's kernel count), per replay;
+  four_steps a graph holding the step four times, per step;
+  alt_execs  two separately captured one-step graphs replayed alternately, per
+             step (does the boundary come from relaunching the same graph exec?).
 one_step - two_steps is the per-replay boundary cost; tiny bounds the runtime's
 graph-launch floor.
 Usage: python scripts/probe_graph_boundary.py [--workload sintel] [--reps 200]
@@ -57,6 +60,8 @@ def main():
         return [cb(c) for c in coords]
 
     bodies = {"one_step": (lambda: step(), 1), "two_steps": (lambda: (step(), step()), 2),
+              "four_steps": (lambda: [step() for _ in range(4)], 4),
+              "alt_a": (lambda: step(), 1), "alt_b": (lambda: step(), 1),
               "tiny": (lambda: small.fill_(1.0), 1),
               "tiny_x14": (lambda: [small.fill_(float(i)) for i in range(14)], 1)}
     graphs = {}
@@ -72,10 +77,22 @@ def main():
         while time.perf_counter() - t0 < 0.5:
             graphs["one_step"].replay()
             torch.cuda.synchronize()
-        res = {n: [] for n in graphs}
+        res = {n: [] for n in graphs if n != "alt_b"}
         for _ in range(a.rounds):
             for n, gr in graphs.items():
+                if n == "alt_b":
+                    continue
                 reps = a.reps if n.startswith("tiny") else max(20, a.reps // 4)
+                if n == "alt_a":   # alternate the two execs: 2 * reps replays
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    for _ in range(reps):
+                        gr.replay()
+                        graphs["alt_b"].replay()
+                    e1.record(stream)
+                    torch.cuda.synchronize()
+                    res[n].append(e0.elapsed_time(e1) * 1e3 / (2 * reps))
+                    continue
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
                 for _ in range(reps):
@@ -83,7 +100,8 @@ def main():
                 e1.record(stream)
                 torch.cuda.synchronize()
                 res[n].append(e0.elapsed_time(e1) * 1e3 / reps / bodies[n][1])
-    med = {n: round(float(np.median(v)), 2) for n, v in res.items()}
+    med = {("alt_execs" if n == "alt_a" else n): round(float(np.median(v)), 2)
+           for n, v in res.items()}
     print(json.dumps({"workload": a.workload, "us_per_step_or_replay_median": med,
                       "boundary_us_estimate": round(med["one_step"] - med["two_steps"], 2) * 2,
                       "what": "one_step - two_steps = half a replay boundary per step; x2 = "

@@ -11,6 +11,9 @@ the step span (build start to next build start), and the idle time of the span
 by boundary: inside the build (split pass -> DMA build), build -> first lookup,
 between the lookups, and last lookup -> the next step's build (the graph
 replay boundary); the build's in-step span and the first lookup's duration.
+With several steps per graph (bench.py --steps-per-graph) only every G-th
+step_to_step boundary is a graph replay boundary, so the idle times are also
+reported as means over the steps (the per-step cost the bench's value sees).
 
 Usage: python scripts/trace_gaps.py <run_kernel_trace.csv> [workload key, e.g. sintel_b1_f32]
 """
@@ -66,6 +69,7 @@ def main(path: str, workload: str | None = None) -> None:
         print(json.dumps({"steps": 0, "note": "no build + 12 lookup steps found"}))
         return
     med = lambda v: round(float(np.median(v)), 2)  # noqa: E731
+    mean = lambda v: round(float(np.mean(v)), 2)  # noqa: E731
     print(json.dumps({
         **({"workload": workload} if workload else {}),
         "steps": len(b_us),
@@ -74,6 +78,8 @@ def main(path: str, workload: str | None = None) -> None:
         "step_span_us_median": med(span_us), "idle_us_per_step_median": med(idle_us),
         "build_in_step_us_median": med(bspan_us), "first_lookup_us_median": med(l1_us),
         "idle_us_median_by_boundary": {k: med(v) for k, v in gaps.items()},
+        "step_span_us_mean": mean(span_us), "idle_us_per_step_mean": mean(idle_us),
+        "idle_us_mean_by_boundary": {k: mean(v) for k, v in gaps.items()},
         "what": "back-to-back steps of the bench's step graph: build + 12 lookups, from the "
                 "rocprofv3 kernel trace of the same command (durations are kernel begin-end; "
                 "lookup_order_us: the on-the-fly lookup's ordering launches per lookup)",

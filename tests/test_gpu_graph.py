@@ -48,3 +48,45 @@ def test_step_graph_matches_eager(dx, block):
             stream.synchronize()
             for a, b in zip(state["outs"], ref):
                 assert torch.equal(a, b)
+
+
+def test_multi_step_graph_matches_eager(dx):
+    """bench.py's graph of G whole steps (--steps-per-graph): each step's block is
+    released before the next is built, so later steps reuse the graph pool's
+    memory; every step still produces its eager outputs, here over two pair sets."""
+    B, D, H, W, iters, G = 1, 256, 24, 40, 12, 4
+    sets = []
+    for s in range(2):
+        f1 = torch.from_numpy(dg.fmap(301 + 10 * s, B, D, H, W, "fnet")).to(DEV)
+        f2 = torch.from_numpy(dg.fmap(302 + 10 * s, B, D, H, W, "fnet")).to(DEV)
+        cs = [torch.from_numpy(dg.coords(310 + 10 * s + k, B, H, W, "normal", 4.0)).to(DEV)
+              for k in range(iters)]
+        sets.append((f1, f2, cs))
+    state, kept = {}, {}
+
+    def step(i):
+        state.pop("cb", None)
+        f1, f2, cs = sets[i % 2]
+        state["cb"] = dx.CorrBlock(f1, f2, radius=4)
+        kept[i] = [state["cb"](c) for c in cs]
+
+    stream = torch.cuda.Stream(device=DEV)
+    with torch.no_grad(), torch.cuda.stream(stream):
+        ref = {}
+        for i in range(2):
+            step(i)
+            ref[i] = [o.clone() for o in kept[i]]
+        kept.clear()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=stream):
+            for i in range(G):
+                step(i)
+        for _ in range(2):
+            for outs in kept.values():
+                for o in outs:
+                    o.fill_(float("nan"))
+            g.replay()
+            stream.synchronize()
+            for i in range(G):
+                for a, b in zip(kept[i], ref[i % 2]):
+                    assert torch.equal(a, b)

@@ -8,9 +8,12 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parents[1]
 
 
-def _trace(path, steps, build_ns=100_000, look_ns=8_000, gap_ns=700, prep=("corr_build_split_kernel<f>",)):
+def _trace(path, steps, build_ns=100_000, look_ns=8_000, gap_ns=700, prep=("corr_build_split_kernel<f>",),
+           graph_every=0, graph_gap_ns=0):
     t, rows = 0, []
-    for _ in range(steps):
+    for s in range(steps):
+        if graph_every and s and s % graph_every == 0:
+            t += graph_gap_ns            # a graph replay boundary before this step
         for name in prep:
             rows.append((name, t, t + build_ns))
             t += build_ns + gap_ns
@@ -73,3 +76,15 @@ def test_trace_gaps_without_steps(tmp_path):
         w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
         w.writerow(["corr_lookup_wide_kernel<4>", 0, 10])
     assert _run(p)["steps"] == 0
+
+
+def test_trace_gaps_means_with_steps_per_graph(tmp_path):
+    """Four steps per graph replay: 3 of 4 step boundaries are in-graph, so the
+    median hides the replay boundary and the mean carries it per step."""
+    p = tmp_path / "run_kernel_trace.csv"
+    _trace(p, steps=9, graph_every=4, graph_gap_ns=10_000)
+    r = _run(p)
+    assert r["steps"] == 8
+    assert r["idle_us_median_by_boundary"]["step_to_step"] == 0.7
+    assert r["idle_us_mean_by_boundary"]["step_to_step"] == round(0.7 + 2 * 10.0 / 8, 2)
+    assert r["idle_us_per_step_mean"] == round(13 * 0.7 + 2 * 10.0 / 8, 2)
