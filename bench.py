@@ -160,15 +160,38 @@ def alt_lookup_flops(B, H, W):
     return 2.0 * B * n * LEVELS * (2 * RADIUS + 2) ** 2 * D
 
 
-def pmc_traffic(workload, kernel_prefix):
+def profile_config(workload, B, b_default, layout, block):
+    """Directory name of this bench configuration under profiles/<round>/
+    (scripts/gpu_final.sh): sintel, sintel_b8, chairs, kitti, kitti_nhwc, hd_alt,
+    hd_full — workload key + non-default batch + layout + block."""
+    name = {"1080p": "hd"}.get(workload, workload)
+    if B != b_default:
+        name += f"_b{B}"
+    if layout == "nhwc":
+        name += "_nhwc"
+    if workload == "1080p":
+        name += "_alt" if block == "alt" else "_full"
+    return name
+
+
+def _profile_files(pattern, cfg):
+    """profiles/<round>/<cfg>/<pattern> newest round first, then every other
+    match of profiles/*/<pattern> and profiles/*/*/<pattern>, newest round first."""
+    root = REPO / "profiles"
+    rnd = lambda f: f.relative_to(root).parts[0]  # noqa: E731
+    own = sorted(root.glob(f"*/{cfg}/{pattern}"), key=rnd, reverse=True) if cfg else []
+    rest = sorted((set(root.glob(f"*/{pattern}")) | set(root.glob(f"*/*/{pattern}"))) - set(own),
+                  key=lambda f: (rnd(f), str(f)), reverse=True)
+    return own + rest
+
+
+def pmc_traffic(workload, kernel_prefix, cfg=None):
     """Per-launch HBM bytes of a kernel from the newest committed PMC summary of
-    this workload (profiles/<round>/traffic*.json, written by
-    scripts/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes
-    of this bench), or None when that workload was not profiled."""
-    files = sorted((REPO / "profiles").glob("*/traffic*.json")) + \
-        sorted((REPO / "profiles").glob("*/*/traffic*.json"))
-    files.sort(key=lambda f: f.relative_to(REPO / "profiles").parts[0])
-    for f in reversed(files):
+    this configuration (profiles/<round>/<cfg>/traffic.json), else of this
+    workload key (profiles/<round>/traffic*.json; written by scripts/pmc_traffic.py
+    from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench), or None
+    when that workload was not profiled."""
+    for f in _profile_files("traffic*.json", cfg):
         data = json.loads(f.read_text())
         if data.get("workload") != workload:
             continue
@@ -178,15 +201,14 @@ def pmc_traffic(workload, kernel_prefix):
     return None, None
 
 
-def trace_timeline(workload):
-    """The step's kernel timeline for this workload from the newest committed
-    rocprofv3 kernel trace of this bench (profiles/<round>/<config>/trace_gaps.json,
-    scripts/trace_gaps.py): the build's in-step span, the idle time per step
-    split by kernel boundary, and the first lookup after the build — the measured
-    decomposition of `step_boundary_us`.  None when not profiled."""
-    files = sorted((REPO / "profiles").glob("*/*/trace_gaps.json"),
-                   key=lambda f: f.relative_to(REPO / "profiles").parts[0])
-    for f in reversed(files):
+def trace_timeline(workload, cfg=None):
+    """The step's kernel timeline for this configuration (else workload key) from
+    the newest committed rocprofv3 kernel trace of this bench
+    (profiles/<round>/<config>/trace_gaps.json, scripts/trace_gaps.py): the build's
+    in-step span, the idle time per step split by kernel boundary, and the first
+    lookup after the build — the measured decomposition of `step_boundary_us`
+    (DESIGN §6).  None when not profiled."""
+    for f in _profile_files("trace_gaps.json", cfg):
         try:
             data = json.loads(f.read_text())
         except ValueError:
@@ -542,6 +564,7 @@ def main():
         s_in = 2 if dtype == "bf16" else 4
         flops = build_flops(B, H, W)
         wl_key = f"{args.workload}_b{B}_{dtype}"
+        cfg = profile_config(args.workload, B, b_default, args.layout, args.block)
         lb = lookup_bytes(B, H, W, s_pyr=s_in)
         res = {
             "metric": METRIC,
@@ -586,8 +609,8 @@ def main():
             # SURVEY §8(d)'s f32 pricing beside it.
             achieved = flops / (build_ms * 1e-3) / 1e12
             ceiling = pipe_peak / mfma_per_flop
-            b_traffic, b_src = pmc_traffic(wl_key, kname.split(" ")[0] + "<")
-            l_traffic, l_src = pmc_traffic(wl_key, "corr_lookup_wide_kernel<")
+            b_traffic, b_src = pmc_traffic(wl_key, kname.split(" ")[0] + "<", cfg)
+            l_traffic, l_src = pmc_traffic(wl_key, "corr_lookup_wide_kernel<", cfg)
             bb = build_bytes(B, H, W, s_in, s_in)
             res["roofline"] = {
                 "kernel": kname + " (stage a+b)",
@@ -603,7 +626,7 @@ def main():
                 "hbm_frac": round(bb / (build_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
                 "avg_launch_us": round(build_ms * 1e3, 2),
                 "step_boundary_us": round(boundary_ms * 1e3, 2),
-                "step_timeline": trace_timeline(wl_key),
+                "step_timeline": trace_timeline(wl_key, cfg),
             }
             lf = lookup_line_floor_bytes(coords, H, W, s_pyr=s_in)
             res["lookup_roofline"] = {
@@ -626,7 +649,7 @@ def main():
             aflops = alt_lookup_flops(B, H, W)
             achieved = aflops / (look_ms * 1e-3) / 1e12
             akern = "alt_corr_mfma_kernel"
-            a_traffic, a_src = pmc_traffic(wl_key, akern + "<")
+            a_traffic, a_src = pmc_traffic(wl_key, akern + "<", cfg)
             pipe = PEAK_BF16_TFLOPS / SPLIT_PRODUCTS   # the f16-pair split's own ceiling (833 TF)
             res["roofline"] = {
                 "kernel": akern + " (f16-pair split MFMA over the window boxes of 32 queries "

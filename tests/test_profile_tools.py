@@ -88,3 +88,21 @@ def test_trace_gaps_means_with_steps_per_graph(tmp_path):
     assert r["idle_us_median_by_boundary"]["step_to_step"] == 0.7
     assert r["idle_us_mean_by_boundary"]["step_to_step"] == round(0.7 + 2 * 10.0 / 8, 2)
     assert r["idle_us_per_step_mean"] == round(13 * 0.7 + 2 * 10.0 / 8, 2)
+
+
+def test_bench_profile_config_names_match_gpu_final():
+    """bench.py reads its traffic / timeline from profiles/<round>/<config>/, the
+    directories scripts/gpu_final.sh writes — one name per configuration, so two
+    configurations sharing a workload key (kitti NCHW / NHWC, 1080p alt / full)
+    never borrow each other's counters."""
+    sys.path.insert(0, str(REPO))
+    import bench
+    cases = {("sintel", 1, 1, "nchw", "corr"): "sintel", ("sintel", 8, 1, "nchw", "corr"): "sintel_b8",
+             ("chairs", 1, 1, "nchw", "corr"): "chairs", ("kitti", 8, 8, "nchw", "corr"): "kitti",
+             ("kitti", 8, 8, "nhwc", "corr"): "kitti_nhwc", ("1080p", 1, 1, "nchw", "alt"): "hd_alt",
+             ("1080p", 1, 1, "nchw", "corr"): "hd_full"}
+    for args, name in cases.items():
+        assert bench.profile_config(*args) == name
+    script = (REPO / "scripts" / "gpu_final.sh").read_text()
+    for name in cases.values():
+        assert f"$R/{name} " in script
