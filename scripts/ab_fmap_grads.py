@@ -4,7 +4,10 @@
 random gradient pyramid and fmaps, graphs of --reps calls replayed in
 interleaved rounds, timed with HIP events.  Also prints both results' max error
 against a float64 reference of dfmap1 (volume gradient + GEMM).
-Usage: python scripts/ab_fmap_grads.py [--shape B D H W L] [--reps 10] [--rounds 7]
+With --prev-lib, the same two entry points of an earlier product library run
+beside them ("six_prev", "f16_prev") and their outputs must equal this
+library's bit for bit.
+Usage: python scripts/ab_fmap_grads.py [--shape B D H W L] [--reps 10] [--rounds 7] [--prev-lib X.so]
 """
 from __future__ import annotations
 
@@ -24,11 +27,20 @@ def main():
     ap.add_argument("--shape", type=int, nargs=5, default=[1, 256, 55, 128, 4])
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--prev-lib", default=None)
     a = ap.parse_args()
     import dexiraft_amd
     from dexiraft_amd import _native as nat
     dexiraft_amd.load_native()
     lib = nat.load()
+    import ctypes
+    prev = None
+    if a.prev_lib:
+        prev = ctypes.CDLL(a.prev_lib)
+        for name, (res, args) in nat.SIGNATURES.items():
+            if hasattr(prev, name):
+                getattr(prev, name).restype = res
+                getattr(prev, name).argtypes = args
     B, D, H, W, L = a.shape
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev)
@@ -48,17 +60,19 @@ def main():
     div = float(np.sqrt(np.float32(D)))
     wsb = lib.dxr_fmap_grads_workspace_bytes(B, D, H, W, L)
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
-    outs = {v: (torch.empty_like(f1), torch.empty_like(f2)) for v in ("six", "f16")}
+    names = ("six", "f16") + (("six_prev", "f16_prev") if prev else ())
+    outs = {v: (torch.empty_like(f1), torch.empty_like(f2)) for v in names}
     stream = torch.cuda.Stream(device=dev)
 
     def call(v):
         d1, d2 = outs[v]
         s = stream.cuda_stream
-        if v == "six":
-            st = lib.dxr_fmap_grads(gp.data_ptr(), nat.DXR_F32, f1.data_ptr(), f2.data_ptr(), B, D, H,
+        L_ = prev if v.endswith("_prev") else lib
+        if v.startswith("six"):
+            st = L_.dxr_fmap_grads(gp.data_ptr(), nat.DXR_F32, f1.data_ptr(), f2.data_ptr(), B, D, H,
                                     W, L, div, d1.data_ptr(), d2.data_ptr(), ws.data_ptr(), wsb, s)
         else:
-            st = lib.dxr_fmap_grads_bounded(gp.data_ptr(), nat.DXR_F32, f1.data_ptr(), f2.data_ptr(),
+            st = L_.dxr_fmap_grads_bounded(gp.data_ptr(), nat.DXR_F32, f1.data_ptr(), f2.data_ptr(),
                                             B, D, H, W, L, div, slots.data_ptr(), 1, d1.data_ptr(),
                                             d2.data_ptr(), ws.data_ptr(), wsb, s)
         assert st == 0, (v, st)
@@ -86,6 +100,10 @@ def main():
                 e1.record(stream)
                 torch.cuda.synchronize()
                 res[v].append(e0.elapsed_time(e1) * 1e3 / a.reps)
+    if prev:
+        for v in ("six", "f16"):
+            for x, y in zip(outs[v], outs[v + "_prev"]):
+                assert torch.equal(x, y), f"{v}: not bit-identical to --prev-lib"
     # accuracy of dfmap1 against float64 (pair 0)
     dv = torch.empty((B, H * W, H * W), device=dev)
     nat.check(lib.dxr_pyramid_backward(gp.data_ptr(), nat.DXR_F32, B, H, W, L, div, dv.data_ptr(),
