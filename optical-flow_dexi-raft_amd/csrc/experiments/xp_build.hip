@@ -1160,3 +1160,240 @@ extern "C" int dxr_xp_build_tail(const void* f1, const void* f2, int in_dtype, i
   return launch_dma_bf16_nchw(static_cast<const uint16_t*>(f1), static_cast<const uint16_t*>(f2),
                               static_cast<uint16_t*>(pyr), g, (int)B, ws, stream, tail);
 }
+
+// ---------------------------------------------------------------------------
+// Round 5 experiment ("cut the per-step LDS re-reads of the
+// 8x16 target tile"): the product's unit, ring and DMA, but each wave computes
+// 2 x 2 MFMA tiles — 64 queries (sub-blocks 2 qg, 2 qg + 1) x 64 targets (tile
+// rows 4 tg .. 4 tg + 3) — instead of 32 queries x the whole tile: per k-step
+// 8 ds_read_b128 per wave instead of 10 for the same 12 MFMAs.  The epilogue
+// writes half of each query's level-0 and level-1 rows per wave, level 2 per
+// wave row, and level 3 from the two target halves through LDS (the reference
+// order ((v00 + v01) + v10) + v11).  Whole units only (no quarter tail), no
+// non-finite recompute: a timing experiment on finite data, its pages checked
+// bit-identical to the product's by scripts/ab_build.py.  Measured (r5u/r5v,
+// against the product without its tail split): Sintel B=1 -1.6 %, B=8 +9.8 %,
+// Chairs +2.3 %, 1080p +7.4 % with plain stores on levels 1-3 (each line
+// completed by the two target halves in L2); written through, the half lines
+// cost far more (B=8 +30 %).  Not adopted.
+namespace {
+template <bool DIV>
+__global__ __launch_bounds__(2 * NT, 4) void xp_dma22_kernel(const uint8_t* __restrict__ sp1,
+                                                              const uint8_t* __restrict__ sp2,
+                                                              const int* __restrict__ ex1,
+                                                              const int* __restrict__ ex2,
+                                                              float* __restrict__ pyr, BuildGeom g) {
+  constexpr int PQ22 = 4 * 16 + 4;   // staged level-0 half row per query (floats)
+  __shared__ __attribute__((aligned(16))) unsigned char smem[DMA_LDS_BYTES + 8 * 32 * 2 * 4];
+  static_assert(8 * 32 * PQ22 * 4 <= DMA_LDS_RING, "staging aliases the ring");
+  int* const sexp = reinterpret_cast<int*>(smem + DMA_LDS_RING);
+  float* const x3 = reinterpret_cast<float*>(smem + DMA_LDS_BYTES);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int qg = wave & 3, tg = wave >> 2;
+  const PageCoord pc = page_coord<true, 2>(g);
+  const int th0 = pc.tyi * TH, tw0 = pc.txi * TW;
+  const int q0 = pc.qblk * BM;
+  const int b = pc.b;
+  const int j = lane & 31, kh = lane >> 5;
+  const long long spstride = (long long)g.D * g.N * 4;
+  int sq[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int qj = q0 + (2 * qg + s) * 32 + j;
+    sq[s] = qj < g.N ? ex1[(long long)b * g.N + qj] : 0;
+  }
+  if (tid < NTGT) {
+    const int r = tid >> 4, c = tid & 15;
+    const bool in = th0 + r < g.H && tw0 + c < g.W;
+    sexp[tid] = in ? ex2[(long long)b * g.N + (th0 + r) * g.W + tw0 + c] : 0;
+  }
+  const __amdgpu_buffer_rsrc_t rq =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sp1 + b * spstride), (short)0,
+                                        (int)spstride, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rt =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sp2 + b * spstride), (short)0,
+                                        (int)spstride, 0x00020000);
+  const int pstr = 64, kstr = g.N * 64;
+  uint32_t vq[2], vt;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 16 * i + (lane >> 2), sl = lane & 3;
+    const int q = q0 + wave * 32 + row;
+    const int cq = sl ^ ((row >> 2) & 3);
+    vq[i] = q < g.N ? (uint32_t)q * (uint32_t)pstr + 16u * cq : 0x80000000u;
+  }
+  {
+    const int sl = lane & 3, r = wave, col = lane >> 2, trow = r * 16 + col;
+    const int ct = sl ^ (((trow >> 2) & 1) | ((trow >> 3) & 2));
+    const int hh = th0 + r, ww = tw0 + col;
+    vt = (hh < g.H && ww < g.W) ? (uint32_t)(hh * g.W + ww) * (uint32_t)pstr + 16u * ct
+                                : 0x80000000u;
+  }
+  auto dma = [&](int kk) {
+    unsigned char* st = smem + (kk % DMA_RING) * DMA_STAGE;
+    const int so = kk * kstr;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rq, (lds_void_t*)(st + wave * 2048 + i * 1024), 16, vq[i], so, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (lds_void_t*)(st + DMA_TILE + wave * 1024), 16,
+                                             vt, so, 0, 0);
+  };
+  const int kq = (j >> 2) & 3;
+  const int trow0 = ((j >> 2) & 1) * 16 + (j & 3) + 4 * (j >> 3);
+  const int kt = ((trow0 >> 2) & 1) | ((trow0 >> 3) & 2);
+  const int qh_off = 2 * qg * 2048 + j * 64 + 16 * (kh ^ kq);
+  const int ql_off = 2 * qg * 2048 + j * 64 + 16 * ((2 + kh) ^ kq);
+  const int th_off = DMA_TILE + 2 * tg * 2048 + trow0 * 64 + 16 * (kh ^ kt);
+  const int tl_off = DMA_TILE + 2 * tg * 2048 + trow0 * 64 + 16 * ((2 + kh) ^ kt);
+
+  f32x16 acc[2][2];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int nk = g.D / BKS;
+  dma(0);
+  if (nk > 1) dma(1);
+  auto kstep = [&](int kk, auto first_tag) {
+    constexpr bool FIRST = decltype(first_tag)::value;
+    if (kk + 1 < nk) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kk + 2 < nk) dma(kk + 2);
+    const unsigned char* st = smem + (kk % DMA_RING) * DMA_STAGE;
+    h8v qh[2], ql[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      qh[s] = *reinterpret_cast<const h8v*>(st + qh_off + s * 2048);
+      ql[s] = *reinterpret_cast<const h8v*>(st + ql_off + s * 2048);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const h8v th = *reinterpret_cast<const h8v*>(st + th_off + u * 2048);
+      const h8v tl = *reinterpret_cast<const h8v*>(st + tl_off + u * 2048);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        acc[s][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh[s], FIRST ? f32x16{} : acc[s][u], 0, 0, 0);
+        acc[s][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql[s], acc[s][u], 0, 0, 0);
+        acc[s][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qh[s], acc[s][u], 0, 0, 0);
+      }
+    }
+  };
+  kstep(0, std::true_type{});
+  for (int kk = 1; kk < nk; ++kk) kstep(kk, std::false_type{});
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();   // ring reads done
+
+  const int blk = qg >> 1;                          // both sub-blocks of the wave: one block
+  const bool live = pc.qblk + blk < g.qt;
+  const long long page = pc.page + (live ? (long long)blk * g.tiles_h * g.tiles_w : 0);
+  int e2 = 0;
+  if constexpr (!DIV) (void)__builtin_frexpf(g.recip, &e2);
+  // unscale: ldexp by -(s_q + s_t) (+ log2 1/sqrt(D)), as the product
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int eq = -sq[s] + (DIV ? 0 : e2 - 1);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int* se = sexp + (2 * (2 * tg + u) + kh) * 16;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = __builtin_ldexpf(acc[s][u][r], eq - se[r]);
+        if constexpr (DIV) v = v / g.divisor;
+        acc[s][u][r] = v;
+      }
+    }
+  }
+  float* const wl = reinterpret_cast<float*>(smem) + wave * 32 * PQ22;
+  float* const pb0 = pyr + g.loff[0] + page * (BM * NTGT);
+  float* const pb1 = pyr + g.loff[1] + page * (BM * NTGT / 4);
+  float* const pb2 = pyr + g.loff[2] + page * (BM * NTGT / 16);
+  float* const pb3 = pyr + g.loff[3] + page * (BM * 2);
+  float l2[2][2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int qbase = ((2 * qg + s) & 3) * 32;
+    // level 0: this wave's half rows (tile rows 4 tg .. 4 tg + 3) of 32 queries
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float* row = wl + j * PQ22 + (2 * u + kh) * 16;
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4)
+        st4(row + 4 * c4, acc[s][u][4 * c4], acc[s][u][4 * c4 + 1], acc[s][u][4 * c4 + 2],
+            acc[s][u][4 * c4 + 3]);
+    }
+    epi_sync<1>();
+    if (live) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int q = 4 * k + (lane >> 4), pc16 = lane & 15;
+        const float4 x = f4(wl + q * PQ22 + pc16 * 4);
+        epi_put<4>(pb0, pb0 + (long long)(qbase + q) * NTGT + tg * 64 + pc16 * 4,
+                   f32x4v{x.x, x.y, x.z, x.w});
+      }
+    }
+    epi_sync<1>();
+    // level 1: rows t = 2 tg + u, cols 4 kh .. 4 kh + 3 (pair-swap pooling)
+    float l1[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float x[8], y[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[s][u][k]),
+                                                        __float_as_uint(acc[s][u][8 + k]), false, false);
+        x[k] = __uint_as_float(p[0]);
+        y[k] = __uint_as_float(p[1]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        l1[u][i] = (((x[2 * i] + x[2 * i + 1]) + y[2 * i]) + y[2 * i + 1]) * 0.25f;
+      if (live)   // plain stores: the two target halves complete each line in L2
+        *reinterpret_cast<float4*>(pb1 + (long long)(qbase + j) * 32 + (2 * tg + u) * 8 + 4 * kh) =
+            make_float4(l1[u][0], l1[u][1], l1[u][2], l1[u][3]);
+    }
+    // level 2: row tg, cols 2 kh, 2 kh + 1
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      l2[s][i] = (((l1[0][2 * i] + l1[0][2 * i + 1]) + l1[1][2 * i]) + l1[1][2 * i + 1]) * 0.25f;
+    if (live)
+      *reinterpret_cast<float2*>(pb2 + (long long)(qbase + j) * 8 + tg * 4 + 2 * kh) =
+          make_float2(l2[s][0], l2[s][1]);
+    if (tg == 0) x3[((qg * 2 + s) * 32 + j) * 2 + kh] = l2[s][0] + l2[s][1];
+  }
+  __syncthreads();   // level 3: row 0's pair sums from the tg = 0 waves
+  if (tg == 1 && live) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int qbase = ((2 * qg + s) & 3) * 32;
+      const float a = x3[((qg * 2 + s) * 32 + j) * 2 + kh];
+      pb3[(long long)(qbase + j) * 2 + kh] = ((a + l2[s][0]) + l2[s][1]) * 0.25f;
+    }
+  }
+}
+}  // namespace
+
+extern "C" int dxr_xp_build22(const float* f1, const float* f2, int64_t B, int64_t D, int64_t H,
+                              int64_t W, float* pyr, void* ws, hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, 4, &L) || D % 16 != 0) return DXR_EINVAL;
+  BuildGeom g = make_geom(D, H, W, std::sqrt((float)D), L);
+  const long long N = g.N, spb = align256(B * D * N * 4), eb = align256(B * N * 4);
+  uint8_t* w = static_cast<uint8_t*>(ws);
+  uint8_t* sp1 = w;
+  uint8_t* sp2 = w + spb;
+  int* e1 = reinterpret_cast<int*>(w + 2 * spb);
+  int* e2 = reinterpret_cast<int*>(w + 2 * spb + eb);
+  hipLaunchKernelGGL((split_pairs_kernel<false, false, 32>), dim3((unsigned)((N + 31) / 32), (unsigned)B, 2),
+                     dim3(512), 0, stream, f1, f2, reinterpret_cast<uint4*>(sp1),
+                     reinterpret_cast<uint4*>(sp2), e1, e2, g.D, g.N);
+  int st = dxr::launch_status();
+  if (st != DXR_OK) return st;
+  const dim3 rg = dma_grid(g, (int)B, 0);   // whole units only
+  if (g.recip == 0.f)
+    hipLaunchKernelGGL((xp_dma22_kernel<true>), rg, dim3(2 * NT), 0, stream, sp1, sp2, e1, e2, pyr, g);
+  else
+    hipLaunchKernelGGL((xp_dma22_kernel<false>), rg, dim3(2 * NT), 0, stream, sp1, sp2, e1, e2, pyr, g);
+  return dxr::launch_status();
+}

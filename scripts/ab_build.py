@@ -8,6 +8,8 @@
   tailN: the product's DMA build under tail policy N (dxr_xp_build_tail of the
          experiments library: split the last partial dispatch round into
          quarter units when 8 T <= N x slots; tail0 never, tail8 always)
+  x22  : dxr_xp_build22 (experiments): each wave 2 x 2 MFMA tiles (64 queries x
+         64 targets), whole units only — compare with tail0
 
 Each variant is captured as a HIP graph of --reps back-to-back builds and the
 graphs are replayed in interleaved rounds after a clock warm-up (HIP events;
@@ -52,12 +54,14 @@ def main():
                 getattr(prev, name).restype = res
                 getattr(prev, name).argtypes = args
     xlib = None
-    if any(v.startswith("tail") for v in a.variants):
+    if any(v.startswith("tail") or v == "x22" for v in a.variants):
         import ctypes
         xlib = ctypes.CDLL(str(nat.LIB_PATH.with_name("libdexiraft_corr_exp.so")))
         vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
         xlib.dxr_xp_build_tail.restype = i32
         xlib.dxr_xp_build_tail.argtypes = [vp, vp, i32, i32, i64, i64, i64, i64, vp, vp, i32, vp]
+        xlib.dxr_xp_build22.restype = i32
+        xlib.dxr_xp_build22.argtypes = [vp, vp, i64, i64, i64, i64, vp, vp, vp]
     dev = torch.device("cuda", 0)
     D = 256
     stream = torch.cuda.Stream(device=dev)
@@ -83,7 +87,10 @@ def main():
 
         def build(v):
             s = stream.cuda_stream
-            if v.startswith("tail"):
+            if v == "x22":
+                st = xlib.dxr_xp_build22(f1.data_ptr(), f2.data_ptr(), B, D, H, W, pyr.data_ptr(),
+                                         ws.data_ptr(), s)
+            elif v.startswith("tail"):
                 st = xlib.dxr_xp_build_tail(f1.data_ptr(), f2.data_ptr(), dt, layout, B, D, H, W,
                                             pyr.data_ptr(), ws.data_ptr(), int(v[4:]), s)
             elif v in ("ws", "prev"):
@@ -105,7 +112,7 @@ def main():
             for v in a.variants:
                 build(v)
                 torch.cuda.synchronize()
-                if v in ("ws", "prev") or v.startswith("tail"):
+                if v in ("ws", "prev", "x22") or v.startswith("tail"):
                     if ref is None:
                         ref = pyr.clone()
                     same = torch.equal(torch.nan_to_num(pyr.float(), nan=3.0),
