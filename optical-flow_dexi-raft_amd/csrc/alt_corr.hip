@@ -264,7 +264,9 @@ __device__ __forceinline__ void alt_split8h(const float (&x)[8], uint4& h, uint4
 // PF: k steps of cell-vector loads kept in flight (a ring of PF register stages).
 // XP (experiments only; 0 in the product): bit 0 feeds the cell vectors' raw
 // bits to the f16 MFMAs instead of splitting them (and skips the non-finite
-// fallback) — a timing ablation of the split's VALU work, results meaningless.
+// fallback) — a timing ablation of the split's VALU work, results meaningless;
+// bit 1 stores only outputs that are exactly 12345.0 (none: an ablation of the
+// output stores).
 template <int R, int NRB, int CMAX, bool H2 = false, int MINW = 2, bool BIN = false, int PF = 1,
           bool DMA = false, int XP = 0>
 __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* __restrict__ f1,
@@ -661,7 +663,8 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
       v = __fadd_rn(v, __fmul_rn(__fmul_rn(s10, dy), 1.f - dx));
       v = __fadd_rn(v, __fmul_rn(__fmul_rn(s11, dy), dx));
       // v / divisor; a power-of-two divisor (sqrt(256) = 16) scales exactly by its reciprocal
-      o[(long long)(oy + RD * ox) * g.N] = g.div_recip != 0.f ? v * g.div_recip : v / g.divisor;
+      const float res = g.div_recip != 0.f ? v * g.div_recip : v / g.divisor;
+      if ((XP & 2) == 0 || res == 12345.0f) o[(long long)(oy + RD * ox) * g.N] = res;
     }
   }
 }

@@ -47,6 +47,9 @@ extern "C" int dxr_xp_alt_lookup(const float* fmap1, const float* const* fmap2_l
   if (variant == 5)
     return launch_alt_mfma_r<4, 1, false, 8>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
                                              stream, ws);
+  if (variant == 11)  // variant 3 without the output stores (timing ablation)
+    return launch_alt_mfma_r<4, 1, false, 4, 2>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+                                                stream, ws);
   if (variant == 8)   // variant 3 without the cell split (timing ablation)
     return launch_alt_mfma_r<4, 1, false, 4, 1>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
                                                 stream, ws);
