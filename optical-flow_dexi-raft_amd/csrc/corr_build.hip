@@ -1459,6 +1459,13 @@ __global__ __launch_bounds__(PX * 16) void split_pairs_kernel(const float* __res
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
+// Pyramid store policy of the bf16 DMA build's epilogue (paged_epilogue EX):
+// wave-private staging + non-temporal stores.  (The experiments target
+// redefines it for store-policy A/Bs.)
+#ifndef DXR_BF16_EPI_EX
+#define DXR_BF16_EPI_EX 3
+#endif
+
 // LDS of corr_build_dma_kernel: ring | target scale exponents s (128 int).
 constexpr int DMA_LDS_RING = DMA_RING * DMA_STAGE;
 constexpr int DMA_LDS_BYTES = DMA_LDS_RING + NTGT * 4;
@@ -1708,7 +1715,7 @@ __device__ __forceinline__ void dma_quarter(unsigned char* smem, const uint8_t* 
   float* const stage = reinterpret_cast<float*>(smem + DMA_XS_BYTES);
   if constexpr (BF) {
     scale_acc<DIV>(a4, g);
-    paged_epilogue<OT, 3>(a4, stage, pyr, g, page, w4, lane);
+    paged_epilogue<OT, DXR_BF16_EPI_EX>(a4, stage, pyr, g, page, w4, lane);
   } else {
     dma_finish_f32<OT, DIV>(a4, g, pyr, stage, page, w4, lane, sq, qj, trow0, th0, tw0, b, f1,
                             f2, ps, ks, sexp);
@@ -1864,7 +1871,7 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
   if constexpr (BF) {
     if (live) {
       scale_acc<DIV>(acc, g);
-      paged_epilogue<OT, 3>(acc, stage, pyr, g, page, w4, lane);
+      paged_epilogue<OT, DXR_BF16_EPI_EX>(acc, stage, pyr, g, page, w4, lane);
     }
     return;
   }
