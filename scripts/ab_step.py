@@ -8,7 +8,8 @@ step as one HIP graph per variant, with the same synthetic inputs as bench.py,
 and times interleaved rounds of replays (HIP events, after a clock warm-up):
 
   --block corr  build (product CorrBlock; variant -4: the --prev-lib library's
-                dxr_corr_pyramid_build_ws, product lookups) + 12 lookups by dxr_xp_lookup variant
+                dxr_corr_pyramid_build_ws, product lookups; -5: the --prev-lib library's
+                build and lookups, for A/Bs across a pyramid-layout change) + 12 lookups by dxr_xp_lookup variant
                 (libdexiraft_corr_exp.so: 0 spatial level-2/3 gathers, 32 query-major,
                 64 the 256 x 16 shape, 128 1024 x 64) or the product's (-1);
   --block alt   12 on-the-fly lookups: dxr_alt_corr_lookup (-1, tile order),
@@ -62,7 +63,7 @@ def main():
     xp.dxr_xp_alt_lookup.argtypes = [vp, ctypes.POINTER(vp), vp, vp, i64, i64, i64, i64, i32,
                                      ctypes.c_float, vp, i32, vp]
     prev = None
-    if -3 in a.variants or -4 in a.variants:
+    if -3 in a.variants or -4 in a.variants or -5 in a.variants:
         prev = ctypes.CDLL(a.prev_lib)
         for name, (res, args) in nat.SIGNATURES.items():
             if hasattr(prev, name):
@@ -98,9 +99,20 @@ def main():
         if a.block == "corr":
             nb = lib.dxr_build_workspace_bytes(cb._in_dt, B, D, H, W)
             bws = torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
+            ppyr = torch.empty_like(cb._buf) if -5 in a.variants else None
 
         def step(v):
-            if a.block == "corr":
+            if a.block == "corr" and v == -5:   # the previous library end to end, own buffer
+                st = prev.dxr_corr_pyramid_build_ws(
+                    f1.data_ptr(), f2.data_ptr(), cb._in_dt, nat.DXR_NCHW, B, D, H, W, 4,
+                    float(D) ** 0.5, ppyr.data_ptr(), cb._pyr_dt, nat.DXR_BUILD_AUTO,
+                    bws.data_ptr(), nb, s)
+                assert st == 0
+                for c, o in zip(coords, outs):
+                    st = prev.dxr_corr_lookup(ppyr.data_ptr(), cb._pyr_dt, B, H, W, 4, 4, c.data_ptr(),
+                                              o.data_ptr(), s)
+                    assert st == 0
+            elif a.block == "corr":
                 if v == -4:   # the previous library's build into the same buffer
                     st = prev.dxr_corr_pyramid_build_ws(
                         f1.data_ptr(), f2.data_ptr(), cb._in_dt, nat.DXR_NCHW, B, D, H, W, 4,
