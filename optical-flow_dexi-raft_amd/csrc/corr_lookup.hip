@@ -53,6 +53,7 @@ struct LookupGeom {
   int N;          // H * W query pixels per pair
   int levels;
   int cout;       // levels * (2r+1)^2
+  int out_nt = 0; // wide lookup: non-temporal output stores (launch_lookup_r decides)
   LevelAddr lv[8];
 };
 
@@ -400,10 +401,14 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
     // write-through (sc1) output stores (round 2): the outputs leave the XCD's
     // L2 while the kernel runs instead of as dirty lines the next kernel
     // boundary writes back (Sintel B=1 9.5 -> 8.5 us, B=8 58.0 -> 54.6 us).
+    // Round 5: non-temporal stores where a wave's output segments are whole or
+    // aligned half lines (g.out_nt, launch_lookup_r) — they leave the caches
+    // entirely, so the pyramid lines the next lookups gather stay resident.
     // Round 4: routing them through LDS as 16-byte stores of 4 queries was
     // slower in the step (Sintel B=1 237.9 vs 222.8 us, B=8 1,623 vs 1,583 us,
     // KITTI B=8 bf16 1,268 vs 1,193 us).
-    __hip_atomic_store(op, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (g.out_nt) __builtin_nontemporal_store(r, op);
+    else __hip_atomic_store(op, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     op += ostep;
   }
 }
@@ -687,18 +692,29 @@ int launch_lookup_backward_r(const BwSets& sets, float* gpyr, const LookupGeom& 
 // Sintel B=1: one CU in four no longer runs a fourth workgroup after the rest).
 // Round 3, same-process A/B (bit-identical): Sintel B=1 8.0 -> 7.4 us, Chairs
 // 5.6 -> 5.2 us; multi-round grids keep 512 x 32 (Sintel B=8 50.4 vs 53.3 us).
+// Output store policy (round 5, same-process A/Bs in the step, scripts/ab_step.py,
+// profiles/r05/experiments/r6e_lookup_output_nt.jsonl): non-temporal stores
+// gained 2-9 % per step wherever a wave stores whole lines (the 512 x 32 shape: 32
+// consecutive queries of a channel = 128 B; Sintel B=8 -2.3 %, KITTI B=8 bf16
+// -5.6 %, Chairs B=4 -8.9 %, Sintel B=2 -2.3 %) and with the 256 x 16 shape
+// (64-B segments) when those are half-line aligned (N % 32 == 0: Sintel B=1 f32
+// -4.0 %, bf16 -4.4 %); with misaligned 64-B segments (KITTI, Chairs at B=1)
+// write-through stores, which L2 merges, were 2-12 % faster.
 template <int R, typename PT>
-int launch_lookup_r(const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
+int launch_lookup_r(const PT* pyr, const float* coords, float* out, const LookupGeom& g0, int B,
                     hipStream_t stream) {
   using W = WideCfg<R>;
+  LookupGeom g = g0;
   const long long wg32 = (long long)((g.N + W::QB - 1) / W::QB) * g.levels * B;
   if (R <= 4 && wg32 <= 1024) {
     using S = WideCfg<R, 256, 16>;
+    g.out_nt = g.N % 32 == 0 ? 1 : 0;
     const dim3 grid((unsigned)((g.N + S::QB - 1) / S::QB), (unsigned)g.levels, (unsigned)B);
     hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT, 256, 16>), grid, dim3(256), 0, stream, pyr,
                        coords, out, g);
     return dxr::launch_status();
   }
+  g.out_nt = 1;
   const dim3 grid((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
   hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT>), grid, dim3(W::NT), 0, stream, pyr, coords,
                      out, g);

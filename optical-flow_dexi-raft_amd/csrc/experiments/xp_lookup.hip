@@ -213,6 +213,7 @@ int xp_dispatch(int xp, const PT* pyr, const float* coords, float* out, const Lo
   switch (xp) {
     case 64: return xp_shape<256, 16>(pyr, coords, out, g, B, stream);
     case 65: return xp_shape<128, 8>(pyr, coords, out, g, B, stream);
+    case 66: return xp_shape<512, 32>(pyr, coords, out, g, B, stream);   // the product's multi-round shape
     case 128: return xp_shape<1024, 64>(pyr, coords, out, g, B, stream);
     case 0: return xp_launch<0>(pyr, coords, out, g, B, trace, stream);
     case 1: return xp_launch<1>(pyr, coords, out, g, B, trace, stream);
