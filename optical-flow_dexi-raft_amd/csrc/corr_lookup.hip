@@ -699,14 +699,20 @@ int launch_lookup_backward_r(const BwSets& sets, float* gpyr, const LookupGeom& 
 // -5.6 %, Chairs B=4 -8.9 %, Sintel B=2 -2.3 %) and with the 256 x 16 shape
 // (64-B segments) when those are half-line aligned (N % 32 == 0: Sintel B=1 f32
 // -4.0 %, bf16 -4.4 %); with misaligned 64-B segments (KITTI, Chairs at B=1)
-// write-through stores, which L2 merges, were 2-12 % faster.
+// write-through stores, which L2 merges, were 2-12 % faster — except with a large
+// pyramid (>= 128 MB: KITTI B=1, 286 MB f32 / 143 MB bf16), where the 512 x 32 shape
+// with non-temporal stores beat both (-6.3 % / -3.9 %, r6k); a small one (Chairs
+// B=1, 43 MB, resident anyway) keeps 256 x 16 with write-through (+13 % otherwise).
 template <int R, typename PT>
 int launch_lookup_r(const PT* pyr, const float* coords, float* out, const LookupGeom& g0, int B,
                     hipStream_t stream) {
   using W = WideCfg<R>;
   LookupGeom g = g0;
   const long long wg32 = (long long)((g.N + W::QB - 1) / W::QB) * g.levels * B;
-  if (R <= 4 && wg32 <= 1024) {
+  // pyramid bytes: B x N queries x N level-0 cells, x 4/3 for levels 1-3
+  const double pyr_bytes = (double)B * g.N * (double)g.N * sizeof(PT) * (4.0 / 3.0);
+  const bool big_misaligned = g.N % 32 != 0 && pyr_bytes >= 128.0 * (1 << 20);
+  if (R <= 4 && wg32 <= 1024 && !big_misaligned) {
     using S = WideCfg<R, 256, 16>;
     g.out_nt = g.N % 32 == 0 ? 1 : 0;
     const dim3 grid((unsigned)((g.N + S::QB - 1) / S::QB), (unsigned)g.levels, (unsigned)B);

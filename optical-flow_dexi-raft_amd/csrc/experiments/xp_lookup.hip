@@ -199,8 +199,10 @@ int xp_launch(const PT* pyr, const float* coords, float* out, const LookupGeom& 
 // The product kernel with another workgroup shape: NT threads x QB queries
 // (the same 16 threads per query as the product's 512 x 32).
 template <int NT, int QB, typename PT>
-int xp_shape(const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
-             hipStream_t stream) {
+int xp_shape(const PT* pyr, const float* coords, float* out, const LookupGeom& g0, int B,
+             hipStream_t stream, int out_nt = 0) {
+  LookupGeom g = g0;
+  g.out_nt = out_nt;
   const dim3 grid((unsigned)((g.N + QB - 1) / QB), (unsigned)g.levels, (unsigned)B);
   hipLaunchKernelGGL((corr_lookup_wide_kernel<4, PT, NT, QB>), grid, dim3(NT), 0, stream, pyr,
                      coords, out, g);
@@ -214,6 +216,8 @@ int xp_dispatch(int xp, const PT* pyr, const float* coords, float* out, const Lo
     case 64: return xp_shape<256, 16>(pyr, coords, out, g, B, stream);
     case 65: return xp_shape<128, 8>(pyr, coords, out, g, B, stream);
     case 66: return xp_shape<512, 32>(pyr, coords, out, g, B, stream);   // the product's multi-round shape
+    case 67: return xp_shape<512, 32>(pyr, coords, out, g, B, stream, 1);   // + non-temporal outputs
+    case 68: return xp_shape<256, 16>(pyr, coords, out, g, B, stream, 1);
     case 128: return xp_shape<1024, 64>(pyr, coords, out, g, B, stream);
     case 0: return xp_launch<0>(pyr, coords, out, g, B, trace, stream);
     case 1: return xp_launch<1>(pyr, coords, out, g, B, trace, stream);
