@@ -1465,6 +1465,9 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 #ifndef DXR_BF16_EPI_EX
 #define DXR_BF16_EPI_EX 3
 #endif
+// The f32 DMA build picks its store policy per launch (EXF, launch_dma): staging +
+// write-through buffer stores (5), or non-temporal stores (3) for pyramids far
+// beyond the Infinity Cache.
 
 // LDS of corr_build_dma_kernel: ring | target scale exponents s (128 int).
 constexpr int DMA_LDS_RING = DMA_RING * DMA_STAGE;
@@ -1478,7 +1481,7 @@ static_assert(DMA_XS_BYTES + WAVES * 16 * P0 * 4 <= DMA_LDS_RING, "tail exchange
 // (f32 build), then — if the wave saw a non-finite sum — recompute them on
 // the exact-f32 MFMA and write them again.  acc[t][r] is query qj x tile pixel
 // (row 2t + kh, col r).  Shared by the whole-unit and the quarter-unit forms.
-template <typename OT, bool DIV>
+template <typename OT, bool DIV, int EXF = 5>
 __device__ __forceinline__ void dma_finish_f32(f32x16 (&acc)[4], const BuildGeom& g,
                                                OT* __restrict__ pyr, float* stage, long long page,
                                                int w4, int lane, int sq, int qj,
@@ -1525,7 +1528,7 @@ __device__ __forceinline__ void dma_finish_f32(f32x16 (&acc)[4], const BuildGeom
     }
   }
   if constexpr (DIV) scale_acc<DIV>(acc, g);
-  const float l3 = paged_epilogue<OT, 1 | 4>(acc, stage, pyr, g, page, w4, lane);
+  const float l3 = paged_epilogue<OT, EXF>(acc, stage, pyr, g, page, w4, lane);
   if (g.levels >= 4) bad = !(__builtin_fabsf(l3) <= 3.40282347e38f);
   if (__ballot(bad) != 0) {   // wave-uniform
     // The wave saw a non-finite sum: its pages are recomputed on the
@@ -1565,7 +1568,7 @@ __device__ __forceinline__ void dma_finish_f32(f32x16 (&acc)[4], const BuildGeom
       }
     }
     scale_acc<DIV>(acc, g);
-    paged_epilogue<OT, 1 | 4>(acc, stage, pyr, g, page, w4, lane);
+    paged_epilogue<OT, EXF>(acc, stage, pyr, g, page, w4, lane);
   }
 }
 
@@ -1593,7 +1596,7 @@ __device__ __forceinline__ void dma_scales(const BuildGeom& g, const int* __rest
 // loop is a quarter of the MFMA work at the same per-step latency, so the
 // last, partial dispatch round of whole units (1,568 units on 512 slots at
 // Sintel B=1: 32 units alone for a whole unit time) becomes 128 short ones.
-template <typename OT, bool DIV, bool BF>
+template <typename OT, bool DIV, bool BF, int EXF = 5>
 __device__ __forceinline__ void dma_quarter(unsigned char* smem, const uint8_t* __restrict__ sp1,
                                             const uint8_t* __restrict__ sp2,
                                             const int* __restrict__ ex1,
@@ -1717,7 +1720,7 @@ __device__ __forceinline__ void dma_quarter(unsigned char* smem, const uint8_t* 
     scale_acc<DIV>(a4, g);
     paged_epilogue<OT, DXR_BF16_EPI_EX>(a4, stage, pyr, g, page, w4, lane);
   } else {
-    dma_finish_f32<OT, DIV>(a4, g, pyr, stage, page, w4, lane, sq, qj, trow0, th0, tw0, b, f1,
+    dma_finish_f32<OT, DIV, EXF>(a4, g, pyr, stage, page, w4, lane, sq, qj, trow0, th0, tw0, b, f1,
                             f2, ps, ks, sexp);
   }
 }
@@ -1738,7 +1741,7 @@ __device__ __forceinline__ void dma_quarter(unsigned char* smem, const uint8_t* 
 // of NCHW fmaps (pixel stride 64 B, stage stride N * 64 B): `pstr` / `kstr`.
 // No scales, no non-finite fallback (bf16 MFMA propagates inf/NaN itself), and
 // the bf16 build's non-temporal pyramid stores.
-template <typename OT, bool DIV, bool BF = false>
+template <typename OT, bool DIV, bool BF = false, int EXF = 5>
 __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
     const uint8_t* __restrict__ sp1, const uint8_t* __restrict__ sp2, const int* __restrict__ ex1,
     const int* __restrict__ ex2, OT* __restrict__ pyr, const float* __restrict__ f1,
@@ -1747,7 +1750,7 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
   // one LDS array (cdna_hip_programming.md §5 item 4(a))
   __shared__ __attribute__((aligned(16))) unsigned char smem[DMA_LDS_BYTES];
   if (blockIdx.x >= (unsigned)g.nmain) {
-    dma_quarter<OT, DIV, BF>(smem, sp1, sp2, ex1, ex2, pyr, f1, f2, ps, ks, pstr, kstr, g);
+    dma_quarter<OT, DIV, BF, EXF>(smem, sp1, sp2, ex1, ex2, pyr, f1, f2, ps, ks, pstr, kstr, g);
     return;
   }
   int* const sexp = reinterpret_cast<int*>(smem + DMA_LDS_RING);
@@ -1879,7 +1882,7 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
   // a half past the last query block has no page (the epilogue syncs per wave;
   // a wave whose sums are not finite recomputes its pages from the f32 operands)
   if (live)
-    dma_finish_f32<OT, DIV>(acc, g, pyr, stage, page, w4, lane, sq, qj, trow0, th0, tw0, b, f1,
+    dma_finish_f32<OT, DIV, EXF>(acc, g, pyr, stage, page, w4, lane, sq, qj, trow0, th0, tw0, b, f1,
                             f2, ps, ks, sexp);
 }
 
@@ -2204,12 +2207,30 @@ int launch_dma(const float* f1, const float* f2, OT* pyr, BuildGeom g, int B, vo
   if (st != DXR_OK) return st;
   const dim3 rg = dma_grid(g, B, tail);
   const int ps = NHWC ? g.D : 1, ks = NHWC ? 1 : g.N;   // fallback operand strides
-  if (g.recip == 0.f)
-    hipLaunchKernelGGL((corr_build_dma_kernel<OT, true>), rg, dim3(2 * NT), 0, stream, sp1, sp2,
-                       e1, e2, pyr, f1, f2, ps, ks, 64, g.N * 64, g);
-  else
-    hipLaunchKernelGGL((corr_build_dma_kernel<OT, false>), rg, dim3(2 * NT), 0, stream, sp1, sp2,
-                       e1, e2, pyr, f1, f2, ps, ks, 64, g.N * 64, g);
+  // Pyramid store policy (round 5, in the step with 12 lookups, scripts/ab_step.py
+  // -6, profiles/r05/experiments/r6n_build_store_policy.jsonl): write-through keeps
+  // part of a pyramid near the Infinity Cache's size resident for the lookups
+  // (Sintel B=1, 261 MB: non-temporal +2.2 %, plain +1.6 % per step); beyond
+  // twice that size nothing stays, and non-temporal stores stream it out faster
+  // (Sintel B=8, 2.1 GB: -9.3 % per step; plain +3.1 %).
+  const double pyr_bytes = (double)B * g.qt * BM * g.tiles_h * g.tiles_w * NTGT * (4.0 / 3.0) *
+                           sizeof(OT);   // paged level 0 (queries x cells) + levels 1-3
+  const bool stream_out = pyr_bytes > 512.0 * (1 << 20);
+  auto go = [&](auto div_tag, auto ex_tag) {
+    constexpr bool DV = decltype(div_tag)::value;
+    constexpr int EXF = decltype(ex_tag)::value;
+    hipLaunchKernelGGL((corr_build_dma_kernel<OT, DV, false, EXF>), rg, dim3(2 * NT), 0, stream,
+                       sp1, sp2, e1, e2, pyr, f1, f2, ps, ks, 64, g.N * 64, g);
+  };
+  using T5 = std::integral_constant<int, 5>;
+  using T3 = std::integral_constant<int, 3>;
+  if (g.recip == 0.f) {
+    if (stream_out) go(std::true_type{}, T3{});
+    else go(std::true_type{}, T5{});
+  } else {
+    if (stream_out) go(std::false_type{}, T3{});
+    else go(std::false_type{}, T5{});
+  }
   return dxr::launch_status();
 }
 

@@ -9,7 +9,8 @@ and times interleaved rounds of replays (HIP events, after a clock warm-up):
 
   --block corr  build (product CorrBlock; variant -4: the --prev-lib library's
                 dxr_corr_pyramid_build_ws, product lookups; -5: the --prev-lib library's
-                build and lookups, for A/Bs across a pyramid-layout change) + 12 lookups by dxr_xp_lookup variant
+                build and lookups, for A/Bs across a pyramid-layout change; -6: the experiments
+                target's DMA build, product lookups) + 12 lookups by dxr_xp_lookup variant
                 (libdexiraft_corr_exp.so: 0 spatial level-2/3 gathers, 32 query-major,
                 64 the 256 x 16 shape, 128 1024 x 64) or the product's (-1);
   --block alt   12 on-the-fly lookups: dxr_alt_corr_lookup (-1, tile order),
@@ -57,6 +58,8 @@ def main():
     lib = dexiraft_amd.load_native()
     xp = ctypes.CDLL(str(nat.LIB_PATH.with_name("libdexiraft_corr_exp.so")))
     vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+    xp.dxr_xp_build_tail.restype = i32
+    xp.dxr_xp_build_tail.argtypes = [vp, vp, i32, i32, i64, i64, i64, i64, vp, vp, i32, vp]
     xp.dxr_xp_lookup.restype = i32
     xp.dxr_xp_lookup.argtypes = [vp, i32, i64, i64, i64, i32, vp, vp, i32, vp, vp]
     xp.dxr_xp_alt_lookup.restype = i32
@@ -111,6 +114,15 @@ def main():
                 for c, o in zip(coords, outs):
                     st = prev.dxr_corr_lookup(ppyr.data_ptr(), cb._pyr_dt, B, H, W, 4, 4, c.data_ptr(),
                                               o.data_ptr(), s)
+                    assert st == 0
+            elif a.block == "corr" and v == -6:   # the experiments target's DMA build (tail
+                # policy 1, the product's), product lookups
+                st = xp.dxr_xp_build_tail(f1.data_ptr(), f2.data_ptr(), cb._in_dt, nat.DXR_NCHW, B, D,
+                                          H, W, cb._buf.data_ptr(), bws.data_ptr(), 1, s)
+                assert st == 0
+                for c, o in zip(coords, outs):
+                    st = lib.dxr_corr_lookup(cb._buf.data_ptr(), cb._pyr_dt, B, H, W, 4, 4, c.data_ptr(),
+                                             o.data_ptr(), s)
                     assert st == 0
             elif a.block == "corr":
                 if v == -4:   # the previous library's build into the same buffer
