@@ -1459,15 +1459,10 @@ __global__ __launch_bounds__(PX * 16) void split_pairs_kernel(const float* __res
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-// Pyramid store policy of the bf16 DMA build's epilogue (paged_epilogue EX):
-// wave-private staging + non-temporal stores.  (The experiments target
-// redefines it for store-policy A/Bs.)
-#ifndef DXR_BF16_EPI_EX
-#define DXR_BF16_EPI_EX 3
-#endif
-// The f32 DMA build picks its store policy per launch (EXF, launch_dma): staging +
-// write-through buffer stores (5), or non-temporal stores (3) for pyramids far
-// beyond the Infinity Cache.
+// Pyramid store policy of the DMA builds' epilogue (paged_epilogue EX), picked per
+// launch (EXF; dma_exf): wave-private staging + write-through buffer stores (5),
+// or non-temporal stores (3) for pyramids far beyond the Infinity Cache.  (The
+// experiments target can force the bf16 build's with DXR_BF16_EPI_EX.)
 
 // LDS of corr_build_dma_kernel: ring | target scale exponents s (128 int).
 constexpr int DMA_LDS_RING = DMA_RING * DMA_STAGE;
@@ -1718,7 +1713,11 @@ __device__ __forceinline__ void dma_quarter(unsigned char* smem, const uint8_t* 
   float* const stage = reinterpret_cast<float*>(smem + DMA_XS_BYTES);
   if constexpr (BF) {
     scale_acc<DIV>(a4, g);
+#ifdef DXR_BF16_EPI_EX
     paged_epilogue<OT, DXR_BF16_EPI_EX>(a4, stage, pyr, g, page, w4, lane);
+#else
+    paged_epilogue<OT, EXF>(a4, stage, pyr, g, page, w4, lane);
+#endif
   } else {
     dma_finish_f32<OT, DIV, EXF>(a4, g, pyr, stage, page, w4, lane, sq, qj, trow0, th0, tw0, b, f1,
                             f2, ps, ks, sexp);
@@ -1874,7 +1873,11 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
   if constexpr (BF) {
     if (live) {
       scale_acc<DIV>(acc, g);
+#ifdef DXR_BF16_EPI_EX
       paged_epilogue<OT, DXR_BF16_EPI_EX>(acc, stage, pyr, g, page, w4, lane);
+#else
+      paged_epilogue<OT, EXF>(acc, stage, pyr, g, page, w4, lane);
+#endif
     }
     return;
   }
@@ -2178,6 +2181,44 @@ dim3 dma_grid(BuildGeom& g, int B, int tail = DMA_TAIL_DEFAULT) {
   return dim3((unsigned)(U + 3 * T));
 }
 
+// Pyramid store policy of a DMA build (round 5, in the step with 12 lookups,
+// scripts/ab_step.py -6; profiles/r05/experiments/r6n_build_store_policy.jsonl,
+// r6q_bf16_build_store_policy.jsonl): write-through keeps part of a pyramid up to
+// about twice the Infinity Cache resident for the lookups (f32 Sintel B=1, 261 MB:
+// non-temporal +2.2 % per step; bf16 Sintel / KITTI / Chairs B=1: write-through
+// -8.9 / -4.0 / -20.5 % against the bf16 build's earlier non-temporal stores,
+// KITTI B=2 -2.0 %); beyond that nothing stays, and non-temporal stores stream it
+// out faster (f32 Sintel B=8, 2.1 GB: -9.3 % per step; bf16 KITTI B=8, 1.1 GB,
+// build alone: 393.7 vs 421.4 us).
+template <typename OT>
+bool dma_stream_out(const BuildGeom& g, int B) {
+  const double pyr_bytes = (double)B * g.qt * BM * g.tiles_h * g.tiles_w * NTGT * (4.0 / 3.0) *
+                           sizeof(OT);   // paged level 0 (queries x cells) + levels 1-3
+  return pyr_bytes > 512.0 * (1 << 20);
+}
+
+// Launch corr_build_dma_kernel<OT, DIV, BF, EXF> with DIV from g.recip and EXF
+// from dma_stream_out.
+template <typename OT, bool BF, typename... A>
+void launch_dma_kernel(const dim3& rg, const BuildGeom& g, int B, hipStream_t stream, A... args) {
+  const bool so = dma_stream_out<OT>(g, B);
+  auto go = [&](auto div_tag, auto ex_tag) {
+    constexpr bool DV = decltype(div_tag)::value;
+    constexpr int EXF = decltype(ex_tag)::value;
+    hipLaunchKernelGGL((corr_build_dma_kernel<OT, DV, BF, EXF>), rg, dim3(2 * NT), 0, stream,
+                       args..., g);
+  };
+  using T5 = std::integral_constant<int, 5>;
+  using T3 = std::integral_constant<int, 3>;
+  if (g.recip == 0.f) {
+    if (so) go(std::true_type{}, T3{});
+    else go(std::true_type{}, T5{});
+  } else {
+    if (so) go(std::false_type{}, T3{});
+    else go(std::false_type{}, T5{});
+  }
+}
+
 // Pre-split + LDS-DMA f32 build (round 3): workspace = SP1 | SP2 | E1 | E2.
 long long align256(long long x) { return (x + 255) & ~255LL; }
 long long dma_workspace_bytes(long long B, long long D, long long H, long long W) {
@@ -2207,30 +2248,8 @@ int launch_dma(const float* f1, const float* f2, OT* pyr, BuildGeom g, int B, vo
   if (st != DXR_OK) return st;
   const dim3 rg = dma_grid(g, B, tail);
   const int ps = NHWC ? g.D : 1, ks = NHWC ? 1 : g.N;   // fallback operand strides
-  // Pyramid store policy (round 5, in the step with 12 lookups, scripts/ab_step.py
-  // -6, profiles/r05/experiments/r6n_build_store_policy.jsonl): write-through keeps
-  // part of a pyramid near the Infinity Cache's size resident for the lookups
-  // (Sintel B=1, 261 MB: non-temporal +2.2 %, plain +1.6 % per step); beyond
-  // twice that size nothing stays, and non-temporal stores stream it out faster
-  // (Sintel B=8, 2.1 GB: -9.3 % per step; plain +3.1 %).
-  const double pyr_bytes = (double)B * g.qt * BM * g.tiles_h * g.tiles_w * NTGT * (4.0 / 3.0) *
-                           sizeof(OT);   // paged level 0 (queries x cells) + levels 1-3
-  const bool stream_out = pyr_bytes > 512.0 * (1 << 20);
-  auto go = [&](auto div_tag, auto ex_tag) {
-    constexpr bool DV = decltype(div_tag)::value;
-    constexpr int EXF = decltype(ex_tag)::value;
-    hipLaunchKernelGGL((corr_build_dma_kernel<OT, DV, false, EXF>), rg, dim3(2 * NT), 0, stream,
-                       sp1, sp2, e1, e2, pyr, f1, f2, ps, ks, 64, g.N * 64, g);
-  };
-  using T5 = std::integral_constant<int, 5>;
-  using T3 = std::integral_constant<int, 3>;
-  if (g.recip == 0.f) {
-    if (stream_out) go(std::true_type{}, T3{});
-    else go(std::true_type{}, T5{});
-  } else {
-    if (stream_out) go(std::false_type{}, T3{});
-    else go(std::false_type{}, T5{});
-  }
+  launch_dma_kernel<OT, false>(rg, g, B, stream, (const uint8_t*)sp1, (const uint8_t*)sp2,
+                               (const int*)e1, (const int*)e2, pyr, f1, f2, ps, ks, 64, g.N * 64);
   return dxr::launch_status();
 }
 
@@ -2242,12 +2261,8 @@ int launch_dma_bf16_nhwc(const uint16_t* f1, const uint16_t* f2, OT* pyr, BuildG
   const dim3 rg = dma_grid(g, B, tail);
   const uint8_t* a = reinterpret_cast<const uint8_t*>(f1);
   const uint8_t* c = reinterpret_cast<const uint8_t*>(f2);
-  if (g.recip == 0.f)
-    hipLaunchKernelGGL((corr_build_dma_kernel<OT, true, true>), rg, dim3(2 * NT), 0, stream, a, c,
-                       nullptr, nullptr, pyr, nullptr, nullptr, 0, 0, g.D * 2, 64, g);
-  else
-    hipLaunchKernelGGL((corr_build_dma_kernel<OT, false, true>), rg, dim3(2 * NT), 0, stream, a, c,
-                       nullptr, nullptr, pyr, nullptr, nullptr, 0, 0, g.D * 2, 64, g);
+  launch_dma_kernel<OT, true>(rg, g, B, stream, a, c, (const int*)nullptr, (const int*)nullptr, pyr,
+                              (const float*)nullptr, (const float*)nullptr, 0, 0, g.D * 2, 64);
   return dxr::launch_status();
 }
 
@@ -2326,12 +2341,9 @@ int launch_dma_bf16_nchw(const uint16_t* f1, const uint16_t* f2, OT* pyr, BuildG
   int st = dxr::launch_status();
   if (st != DXR_OK) return st;
   const dim3 rg = dma_grid(g, B, tail);
-  if (g.recip == 0.f)
-    hipLaunchKernelGGL((corr_build_dma_kernel<OT, true, true>), rg, dim3(2 * NT), 0, stream, o1, o2,
-                       nullptr, nullptr, pyr, nullptr, nullptr, 0, 0, 64, g.N * 64, g);
-  else
-    hipLaunchKernelGGL((corr_build_dma_kernel<OT, false, true>), rg, dim3(2 * NT), 0, stream, o1,
-                       o2, nullptr, nullptr, pyr, nullptr, nullptr, 0, 0, 64, g.N * 64, g);
+  launch_dma_kernel<OT, true>(rg, g, B, stream, (const uint8_t*)o1, (const uint8_t*)o2,
+                              (const int*)nullptr, (const int*)nullptr, pyr, (const float*)nullptr,
+                              (const float*)nullptr, 0, 0, 64, g.N * 64);
   return dxr::launch_status();
 }
 
