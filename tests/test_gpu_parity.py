@@ -175,6 +175,29 @@ def test_batch_independence_and_determinism(dx):
         assert torch.equal(cb1(c[b:b + 1]), ob[b:b + 1])
 
 
+@pytest.mark.parametrize("dtype,B", [(torch.float32, 2), (torch.bfloat16, 4)])
+def test_pyramid_store_policy_bit_identical(dx, dtype, B):
+    """The DMA builds pick their pyramid stores per launch (csrc/corr_build.hip
+    dma_stream_out): write-through up to 512 MB of pyramid, non-temporal above.
+    At Sintel size a one-pair pyramid is below the threshold (f32 269 MB, bf16
+    135 MB) and this batch above it (538 MB): every slot's pages and lookups must
+    be the one-pair build's bit for bit."""
+    H, W = 55, 128
+    f1, f2 = _pair(B=B, H=H, W=W, seed=21, dist="fnet")
+    f1, f2 = f1.to(dtype), f2.to(dtype)
+    c = _t(dg.coords(22, B, H, W, "normal", 4.0))
+    cbb = dx.CorrBlock(f1, f2)
+    ob = cbb(c)
+    pyr = cbb.corr_pyramid
+    n = H * W
+    for b in range(B):
+        cb1 = dx.CorrBlock(f1[b:b + 1], f2[b:b + 1])
+        for lvl in range(4):
+            assert torch.equal(cb1.corr_pyramid[lvl], pyr[lvl][b * n:(b + 1) * n]), (b, lvl)
+        assert torch.equal(cb1(c[b:b + 1]), ob[b:b + 1]), b
+        del cb1
+
+
 def test_linearity(dx):
     """Scaling fmap1 by 2 scales the pyramid by 2 (the reference's f32 matmul does
     so bit for bit).  Bit for bit on the default (pre-split) build, whose
