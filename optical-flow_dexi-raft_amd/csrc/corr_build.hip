@@ -1460,9 +1460,8 @@ __global__ __launch_bounds__(PX * 16) void split_pairs_kernel(const float* __res
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 // Pyramid store policy of the DMA builds' epilogue (paged_epilogue EX), picked per
-// launch (EXF; dma_exf): wave-private staging + write-through buffer stores (5),
-// or non-temporal stores (3) for pyramids far beyond the Infinity Cache.  (The
-// experiments target can force the bf16 build's with DXR_BF16_EPI_EX.)
+// launch (EXF; dma_stream_out): wave-private staging + write-through buffer stores (5),
+// or non-temporal stores (3) for pyramids far beyond the Infinity Cache.
 
 // LDS of corr_build_dma_kernel: ring | target scale exponents s (128 int).
 constexpr int DMA_LDS_RING = DMA_RING * DMA_STAGE;
@@ -1713,11 +1712,7 @@ __device__ __forceinline__ void dma_quarter(unsigned char* smem, const uint8_t* 
   float* const stage = reinterpret_cast<float*>(smem + DMA_XS_BYTES);
   if constexpr (BF) {
     scale_acc<DIV>(a4, g);
-#ifdef DXR_BF16_EPI_EX
-    paged_epilogue<OT, DXR_BF16_EPI_EX>(a4, stage, pyr, g, page, w4, lane);
-#else
     paged_epilogue<OT, EXF>(a4, stage, pyr, g, page, w4, lane);
-#endif
   } else {
     dma_finish_f32<OT, DIV, EXF>(a4, g, pyr, stage, page, w4, lane, sq, qj, trow0, th0, tw0, b, f1,
                             f2, ps, ks, sexp);
@@ -1873,11 +1868,7 @@ __global__ __launch_bounds__(2 * NT, 4) void corr_build_dma_kernel(
   if constexpr (BF) {
     if (live) {
       scale_acc<DIV>(acc, g);
-#ifdef DXR_BF16_EPI_EX
-      paged_epilogue<OT, DXR_BF16_EPI_EX>(acc, stage, pyr, g, page, w4, lane);
-#else
       paged_epilogue<OT, EXF>(acc, stage, pyr, g, page, w4, lane);
-#endif
     }
     return;
   }

@@ -1,9 +1,8 @@
 // Experiments target only (libdexiraft_corr_exp.so, build.py --experiments):
 // timing ablations and a per-workgroup timeline of the pre-split LDS-DMA f32
 // build (csrc/corr_build.hip corr_build_dma_kernel).  Never loaded by the package.
-// (DXR_BF16_EPI_EX: define it here to A/B the bf16 DMA build's store policy —
-// round 5, KITTI B=8 channels-last: non-temporal 393.7 / 388.7 us, write-through
-// 421.4, plain 412.3; profiles/r05/experiments/r5x_bf16_store_policy.jsonl)
+// (The builds' pyramid store policy is chosen per launch, dma_stream_out; its
+// A/Bs are profiles/r05/experiments/r5x_*, r6n_* and r6q_*.)
 #include "../corr_build.hip"
 
 namespace {
