@@ -382,7 +382,9 @@ class _Launch:
         self._ctx = None
 
     def __enter__(self):
-        if self.device.index is not None and self.device.index != torch.cuda.current_device():
+        # torch._C._cuda_getDevice: torch.cuda.current_device() without its
+        # lazy-init check (a block exists only on an initialised device)
+        if self.device.index is not None and self.device.index != torch._C._cuda_getDevice():
             self._ctx = torch.cuda.device(self.device)
             self._ctx.__enter__()
         return self

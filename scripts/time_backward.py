@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--loss", default="vdot", choices=["vdot", "mulsum"])
     ap.add_argument("--clone-inputs", action="store_true")
+    ap.add_argument("--no-breakdown", action="store_true",
+                    help="skip the torch-profiler kernel breakdown (under rocprofv3)")
     a = ap.parse_args()
     import dexiraft_amd
     dev = torch.device("cuda", 0)
@@ -99,12 +101,15 @@ def main():
     t_step = timed(step)
     peak = torch.cuda.max_memory_allocated() - base
     # kernel breakdown of one step from the profiler
-    from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CUDA]) as prof:
-        step()
-        torch.cuda.synchronize()
     kern = {}
-    for ev in prof.key_averages():
+    events = []
+    if not a.no_breakdown:
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            step()
+            torch.cuda.synchronize()
+        events = prof.key_averages()
+    for ev in events:
         name = ev.key
         for key in ("corr_lookup_backward", "pyramid_backward", "fmap_grad", "fmap_split",
                     "chunk_sum", "corr_build", "split_pairs", "corr_lookup_wide", "Cijk", "gemm",
