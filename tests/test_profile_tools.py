@@ -1,4 +1,5 @@
-"""CPU tests of the profile tooling: scripts/trace_gaps.py's step timeline."""
+"""CPU tests of the profile tooling: scripts/trace_gaps.py's step timeline and
+scripts/train_step_timeline.py's training-step timeline."""
 import csv
 import json
 import subprocess
@@ -106,3 +107,32 @@ def test_bench_profile_config_names_match_gpu_final():
     script = (REPO / "scripts" / "gpu_final.sh").read_text()
     for name in cases.values():
         assert f"$R/{name} " in script
+
+
+def test_train_step_timeline(tmp_path):
+    """scripts/train_step_timeline.py: steps split at the split pass, the
+    second-to-last complete step printed with per-kernel idle and totals."""
+    p = tmp_path / "run_kernel_trace.csv"
+    rows, t = [], 0
+    for _ in range(4):
+        for name, dur, gap in (("void (anonymous namespace)::split_pairs_kernel<false, false, 32>(float const*)", 9_000, 0),
+                               ("void (anonymous namespace)::corr_build_dma_kernel<float, false, false, 5>(x)", 100_000, 0),
+                               ("void at::native::vectorized_elementwise_kernel<4, at::native::FillFunctor<float>>(int)", 5_000, 20_000),
+                               ("void (anonymous namespace)::corr_lookup_wide_kernel<4, float, 256, 16>(x)", 8_000, 3_000)):
+            t += gap
+            rows.append((name, t, t + dur))
+            t += dur
+        t += 50_000
+    with open(p, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        w.writerows(rows)
+    out = subprocess.run([sys.executable, str(REPO / "scripts" / "train_step_timeline.py"), str(p)],
+                         capture_output=True, text=True, check=True).stdout.splitlines()
+    ks = [json.loads(line) for line in out]
+    assert [k["kernel"] for k in ks[:-1]] == [
+        "split_pairs_kernel", "corr_build_dma_kernel",
+        "at::native::vectorized_elementwise_kernel<4, at::native::FillFunctor<float>>",
+        "corr_lookup_wide_kernel"]
+    assert [k["idle_before_us"] for k in ks[:-1]] == [0.0, 0.0, 20.0, 3.0]
+    assert ks[-1] == {"kernels": 4, "kernel_us": 122.0, "idle_us": 23.0, "span_us": 145.0}
