@@ -218,6 +218,8 @@ int xp_dispatch(int xp, const PT* pyr, const float* coords, float* out, const Lo
     case 66: return xp_shape<512, 32>(pyr, coords, out, g, B, stream);   // the product's multi-round shape
     case 67: return xp_shape<512, 32>(pyr, coords, out, g, B, stream, 1);   // + non-temporal outputs
     case 68: return xp_shape<256, 16>(pyr, coords, out, g, B, stream, 1);
+    case 69: return xp_shape<128, 8>(pyr, coords, out, g, B, stream, 1);
+    case 70: return xp_shape<1024, 64>(pyr, coords, out, g, B, stream, 1);
     case 128: return xp_shape<1024, 64>(pyr, coords, out, g, B, stream);
     case 0: return xp_launch<0>(pyr, coords, out, g, B, trace, stream);
     case 1: return xp_launch<1>(pyr, coords, out, g, B, trace, stream);
