@@ -36,6 +36,11 @@ of 10 back-to-back builds, / 10 (the split pass, the build and their
 boundaries); what the timed step spends beyond 12 lookups + one build (the
 graph launch, the build -> lookup boundary) is reported as step_boundary_us.
 ``--mode eager`` times plain Python calls instead.
+The line also carries ``box`` (host, GPU UUID) and ``calibration`` (a bf16 GEMM
+and an HBM copy timed in this process before the timed region: boxes differ by
+up to ~18 % in the build kernel, round 5), and ``value_one_step_per_graph`` (the
+same K steps replayed one graph per step, rounds 1-4's protocol).  Kernel-trace
+step timelines are not in the line: they come from another run.
 """
 from __future__ import annotations
 
@@ -201,33 +206,49 @@ def pmc_traffic(workload, kernel_prefix, cfg=None):
     return None, None
 
 
-def trace_timeline(workload, cfg=None):
-    """The step's kernel timeline for this configuration (else workload key) from
-    the newest committed rocprofv3 kernel trace of this bench
-    (profiles/<round>/<config>/trace_gaps.json, scripts/trace_gaps.py): the build's
-    in-step span, the idle time per step split by kernel boundary, and the first
-    lookup after the build — the measured decomposition of `step_boundary_us`
-    (DESIGN §6).  None when not profiled."""
-    for f in _profile_files("trace_gaps.json", cfg):
-        try:
-            data = json.loads(f.read_text())
-        except ValueError:
-            continue
-        if data.get("workload") == workload and data.get("steps", 0) > 0:
-            mean = "idle_us_per_step_mean" in data    # round 5+: means over the steps
-            return {"build_in_step_us": data.get("build_in_step_us_median"),
-                    "idle_us_per_step": data.get("idle_us_per_step_mean" if mean
-                                                 else "idle_us_per_step_median"),
-                    "idle_us_by_boundary": data.get("idle_us_mean_by_boundary" if mean
-                                                    else "idle_us_median_by_boundary"),
-                    "first_lookup_us": data.get("first_lookup_us_median"),
-                    "lookup_us": data.get("lookup_us_median"),
-                    "step_span_us": data.get("step_span_us_mean" if mean
-                                             else "step_span_us_median"),
-                    "source": f"{f.relative_to(REPO)} (rocprofv3 kernel trace of this bench, "
-                              f"{data['steps']} steps: idle and span "
-                              f"{'means' if mean else 'medians'}, kernel durations medians)"}
-    return None
+def calibrate(dev, stream, reps=10):
+    """In-process speed of this box, timed before the timed region (VERDICT r05
+    item 4: boxes differ by up to ~18 % in the build kernel, so each result is
+    recorded beside the box's own speed): a bf16 GEMM 8192^3 (torch -> hipBLASLt,
+    MFMA-bound; its clock is the DVFS clock under MFMA load) and a 1 GiB
+    device-to-device copy (HBM-bound), each as HIP events around `reps`
+    back-to-back launches on the bench's stream after two untimed ones."""
+    n = 8192
+    out = {}
+    with torch.cuda.stream(stream):
+        a = torch.randn((n, n), device=dev, dtype=torch.bfloat16)
+        b = torch.randn((n, n), device=dev, dtype=torch.bfloat16)
+        c = torch.empty((n, n), device=dev, dtype=torch.bfloat16)
+        src = torch.empty(1 << 28, device=dev, dtype=torch.float32)   # 1 GiB
+        dst = torch.empty_like(src)
+        src.fill_(1.0)
+
+        def timed(fn):
+            for _ in range(2):
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                fn()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) * 1e-3 / reps
+
+        t_mm = timed(lambda: torch.matmul(a, b, out=c))
+        t_cp = timed(lambda: dst.copy_(src))
+        out["bf16_gemm_tflops"] = round(2.0 * n ** 3 / t_mm / 1e12, 1)
+        out["hbm_copy_gbs"] = round(2.0 * src.numel() * 4 / t_cp / 1e9, 1)
+        out["what"] = (f"bf16 GEMM {n}^3 (torch.matmul) and a 1 GiB device copy (read + write "
+                       f"counted), HIP events around {reps} launches each, before the timed region")
+        del a, b, c, src, dst
+    torch.cuda.synchronize()
+    return out
+
+
+def box_identity(dev):
+    """Which box produced the line (hostname, GPU name and UUID)."""
+    p = torch.cuda.get_device_properties(dev)
+    return {"host": socket.gethostname(), "gpu": p.name, "gpu_uuid": str(getattr(p, "uuid", ""))}
 
 
 def _free_port() -> int:
@@ -395,6 +416,8 @@ def main():
                     help="untimed replays of the step for this long before the W warmup steps: "
                          "the GPU raises its clocks only after ~ms of load (30 timed steps after "
                          "3 warmups read 11 %% low on MI355X)")
+    ap.add_argument("--no-calibration", action="store_true",
+                    help="skip the in-process box calibration (bf16 GEMM + HBM copy)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-impl", default="torch", choices=["torch", "numpy"],
@@ -478,6 +501,7 @@ def main():
                 run_step()
             n_clock += 20
             torch.cuda.synchronize()
+        calib = calibrate(dev, stream) if not args.no_calibration else None
         for _ in range(-(-args.warmup // G)):
             run_step()
         torch.cuda.synchronize()
@@ -541,9 +565,21 @@ def main():
 
             look_ms = events(g_look, reps) / ITERS
             build_ms = events(g_build, max(5, reps // 4)) / BUILDS_PER_GRAPH
+            one_ms = None
+            if G > 1:
+                # the same K steps as one graph per step (rounds 1-4's protocol;
+                # each replay pays the runtime's replay boundary), for comparison
+                g_one = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g_one, stream=stream, pool=g_step.pool()):
+                    step(G - 1)
+                for _ in range(5):
+                    g_one.replay()
+                one_ms = events(g_one, args.steps)
+                del g_one
             boundary_ms = elapsed / args.steps * 1e3 - ITERS * look_ms - build_ms
             del keep, g_build
         else:
+            one_ms = None
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             ev[0].record(stream)
             build()
@@ -577,6 +613,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong" if args.total_pairs is not None else "weak",
             "vs_baseline": None,
+            "value_one_step_per_graph": (round(total / (one_ms * 1e-3), 3) if one_ms else None),
             "dtype": dtype,
             "data": "synthetic (torch.randn fmaps, coords = grid + N(0,4^2) px)",
             "config": {
@@ -593,6 +630,8 @@ def main():
                 "clock_warmup": f"{n_clock} untimed step replays ({args.clock_warmup_s} s) before "
                                 f"the {args.warmup} warmup steps",
             },
+            "box": box_identity(dev),
+            "calibration": calib,
             "pair_checksums": {
                 "what": "float64 sum of each pair's 12th lookup output, all-gathered over "
                         f"{'RCCL' if world > 1 else 'no collective (1 rank)'}",
@@ -626,9 +665,8 @@ def main():
                 "hbm_frac": round(bb / (build_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
                 "avg_launch_us": round(build_ms * 1e3, 2),
                 "step_boundary_us": round(boundary_ms * 1e3, 2),
-                "step_timeline": trace_timeline(wl_key, cfg),
             }
-            lf = lookup_line_floor_bytes(coords, H, W, s_pyr=s_in)
+            lf = lookup_line_floor_bytes(sets[G - 1][2], H, W, s_pyr=s_in)
             res["lookup_roofline"] = {
                 "kernel": "corr_lookup_wide_kernel (stage c)",
                 "bound": "hbm", "achieved": round(lb / (look_ms * 1e-3) / 1e9, 1),

@@ -1490,14 +1490,9 @@ __device__ __forceinline__ void dma_finish_f32(f32x16 (&acc)[4], const BuildGeom
   // workgroup flag; the recompute only rewrites the wave's own pages anyway).
   // An exponent sum that overflows a finite value also reads as non-finite and
   // takes the exact path, whose f32 result overflows the same way.  Fewer than 4
-  // levels: the values themselves are checked before the epilogue consumes them.
+  // levels: the unscaled values themselves are checked before the epilogue
+  // consumes them (so an exponent-sum overflow takes the exact path either way).
   bool bad = false;
-  if (g.levels < 4) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) bad |= !(__builtin_fabsf(acc[t][r]) <= 3.40282347e38f);
-  }
   // ldexp by the exponent sum -(s_q + s_t) + log2(1/sqrt(D)) (when that is
   // exact): one rounding of the exact value whatever the pixel magnitudes.
   // (Round 4 multiplied by 2^-s_q / sqrt(D), then by 2^-s_t: the same two VALU
@@ -1522,6 +1517,12 @@ __device__ __forceinline__ void dma_finish_f32(f32x16 (&acc)[4], const BuildGeom
     }
   }
   if constexpr (DIV) scale_acc<DIV>(acc, g);
+  if (g.levels < 4) {   // after the unscale, as the level-3 check
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) bad |= !(__builtin_fabsf(acc[t][r]) <= 3.40282347e38f);
+  }
   const float l3 = paged_epilogue<OT, EXF>(acc, stage, pyr, g, page, w4, lane);
   if (g.levels >= 4) bad = !(__builtin_fabsf(l3) <= 3.40282347e38f);
   if (__ballot(bad) != 0) {   // wave-uniform
@@ -1723,7 +1724,7 @@ __device__ __forceinline__ void dma_quarter(unsigned char* smem, const uint8_t* 
 // its pages from the f32 operands (`f1`, `f2`: element (pixel p, channel k) at
 // p * ps + k * ks of a pair's fmap) on the exact-f32 MFMA, in place: IEEE
 // semantics as the reference's f32 matmul (inf x finite = inf, inf x 0 = NaN,
-// NaN propagates).  Grid: dma_grid(g, B) — [0, g.nmain) whole units in the
+// NaN propagates).  Grid: dma_grid(g, B, stream) — [0, g.nmain) whole units in the
 // XCD-banded order (page_coord<true, 2>), then the tail's quarter units.
 //
 // BF (bf16 mode, C3): the same K loop on bf16 operand records — a 64-B record
@@ -2138,11 +2139,13 @@ int launch_split(const float* f1, const float* f2, OT* pyr, const BuildGeom& g, 
 }
 
 // Dispatch slots of the DMA build: two workgroups per CU (74.8 KB of LDS and 4
-// waves per SIMD each), per device (cached).
-int dma_slots() {
+// waves per SIMD each), per device (cached) — the launch stream's device, which
+// a C-API caller's current device need not be.
+int dma_slots(hipStream_t stream) {
   static int cache[64] = {0};
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 512;
+  if (hipStreamGetDevice(stream, &dev) != hipSuccess && hipGetDevice(&dev) != hipSuccess) return 512;
+  if (dev < 0 || dev >= 64) return 512;
   if (cache[dev] == 0) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -2163,9 +2166,9 @@ int dma_slots() {
 // never -> 103.4 split; Sintel B=8 (T = S/2) 870.5 -> 883.2; KITTI B=8 bf16
 // (T = S/5.3) 394.0 -> 395.9; Chairs (U < S) 35.2 -> 38.6: split only a short tail.
 constexpr int DMA_TAIL_DEFAULT = 1;
-dim3 dma_grid(BuildGeom& g, int B, int tail = DMA_TAIL_DEFAULT) {
+dim3 dma_grid(BuildGeom& g, int B, hipStream_t stream, int tail = DMA_TAIL_DEFAULT) {
   const long long U = (long long)B * ((g.qt + 1) / 2) * g.tiles_h * g.tiles_w;
-  const long long S = dma_slots();
+  const long long S = dma_slots(stream);
   long long T = U % S;
   if (8 * T > (long long)tail * S) T = 0;
   g.nmain = (int)(U - T);
@@ -2237,7 +2240,7 @@ int launch_dma(const float* f1, const float* f2, OT* pyr, BuildGeom g, int B, vo
                      g.D, g.N);
   int st = dxr::launch_status();
   if (st != DXR_OK) return st;
-  const dim3 rg = dma_grid(g, B, tail);
+  const dim3 rg = dma_grid(g, B, stream, tail);
   const int ps = NHWC ? g.D : 1, ks = NHWC ? 1 : g.N;   // fallback operand strides
   launch_dma_kernel<OT, false>(rg, g, B, stream, (const uint8_t*)sp1, (const uint8_t*)sp2,
                                (const int*)e1, (const int*)e2, pyr, f1, f2, ps, ks, 64, g.N * 64);
@@ -2249,7 +2252,7 @@ int launch_dma(const float* f1, const float* f2, OT* pyr, BuildGeom g, int B, vo
 template <typename OT>
 int launch_dma_bf16_nhwc(const uint16_t* f1, const uint16_t* f2, OT* pyr, BuildGeom g, int B,
                          hipStream_t stream, int tail = DMA_TAIL_DEFAULT) {
-  const dim3 rg = dma_grid(g, B, tail);
+  const dim3 rg = dma_grid(g, B, stream, tail);
   const uint8_t* a = reinterpret_cast<const uint8_t*>(f1);
   const uint8_t* c = reinterpret_cast<const uint8_t*>(f2);
   launch_dma_kernel<OT, true>(rg, g, B, stream, a, c, (const int*)nullptr, (const int*)nullptr, pyr,
@@ -2331,7 +2334,7 @@ int launch_dma_bf16_nchw(const uint16_t* f1, const uint16_t* f2, OT* pyr, BuildG
     hipLaunchKernelGGL(pack_bf16_kernel<false>, pg, dim3(256), 0, stream, f1, f2, o1, o2, g.D, g.N);
   int st = dxr::launch_status();
   if (st != DXR_OK) return st;
-  const dim3 rg = dma_grid(g, B, tail);
+  const dim3 rg = dma_grid(g, B, stream, tail);
   launch_dma_kernel<OT, true>(rg, g, B, stream, (const uint8_t*)o1, (const uint8_t*)o2,
                               (const int*)nullptr, (const int*)nullptr, pyr, (const float*)nullptr,
                               (const float*)nullptr, 0, 0, 64, g.N * 64);

@@ -414,6 +414,193 @@ __global__ __launch_bounds__(NT_) void corr_lookup_wide_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Query-minor lookup (round 6).  The wide kernel stages each query's window as
+// its own block of rows (qq * 180 + row * 16 + col floats), so the phase-2 tap
+// reads of a half-wave (32 lanes = 32 queries at one output) fall on banks set
+// by each query's own window origin: ~2.7 LDS cycles per read where 1 is the
+// floor (PMC r05: SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE = 0.42).  Here the
+// window cells are staged query-minor, cell (row, col) of query qq at
+//   ((row * RSC + col) * QB + qq)
+// so a lane's bank is qq + QB * (cell index) mod 32: with QB = 32 every tap read
+// of a half-wave is conflict-free whatever the windows; with QB = 16 (the
+// one-round 256 x 16 shape) a half-wave holds outputs k and k + 1 of 16 queries,
+// whose cells are one row apart, and the odd row pitch RSC = 17 puts them in
+// opposite bank halves.  Gathers walk the queries fastest on every level, so
+// each 4-cell vector goes out as four conflict-free ds_write_b32.  Tap data is
+// 8 bytes per sample ({LDS offset, f}, 1 - f recomputed with the same rounding).
+// Same arithmetic, same outputs bit for bit.
+// ---------------------------------------------------------------------------
+template <int R, int NT_ = 512, int QB_ = 32>
+struct QmCfg {
+  using C = WideCfg<R, NT_, QB_>;
+  static constexpr int RD = C::RD, WD = C::WD, K = C::K, QB = C::QB, NT = NT_;
+  static constexpr int NQ = C::NQ;                    // 4-cell vectors per staged row
+  static constexpr int RSC = 4 * NQ + 1;              // odd row pitch (cells)
+  static constexpr int NCELL = WD * RSC;
+  static constexpr int VSLOTS = QB * WD * NQ;
+  static constexpr int VIT = (VSLOTS + NT - 1) / NT;
+  static constexpr int NCLS = NT / QB;
+  static_assert(QB == 16 || QB == 32, "bank arithmetic assumes 16 or 32 queries");
+};
+
+// Phase 0 taps in the query-minor form: per sample {LDS offset in floats, f}.
+template <int R, int NT_, int QB_>
+__device__ __forceinline__ void qm_phase0_taps(const Phase0Coords<R, NT_, QB_>& c, const LevelAddr& A,
+                                               int l, int tid, float2* xs, float2* ys, int2* org) {
+  using C = WideCfg<R, NT_, QB_>;
+  using Q = QmCfg<R, NT_, QB_>;
+  constexpr int RD = C::RD, WD = C::WD, QB = C::QB, G = C::G;
+  const int Hl = A.h, Wl = A.w;
+#pragma unroll
+  for (int it = 0; it < C::SIT; ++it) {
+    const int slot = tid + it * C::NT;
+    if (slot >= QB * G) break;   // whole waves
+    const int j = slot & (G - 1), qq = slot >> C::LG;
+    const float cx = c.x[it], cy = c.y[it];
+    const float inv = __builtin_ldexpf(1.f, -l);
+    const float wm1 = (float)(Wl - 1), hm1 = (float)(Hl - 1);
+    const float ux = sample_coord(__fadd_rn(cx * inv, (float)(j - R)), wm1, wm1 / 2.f);
+    const float uy = sample_coord(__fadd_rn(cy * inv, (float)(j - R)), hm1, hm1 / 2.f);
+    const float flx = floorf(ux), fly = floorf(uy);
+    const bool act = j < RD;
+    int mx = 0x7fffffff, my = 0x7fffffff;
+    if (act) {
+      const bool bad = !(fabsf(flx) < 1.0e7f) || !(fabsf(fly) < 1.0e7f);
+      mx = bad ? FAR_ORIGIN : (int)flx - j;
+      my = bad ? FAR_ORIGIN : (int)fly - j;
+    }
+    mx = group_min<G>(mx);
+    my = group_min<G>(my);
+    const bool far = mx + WD <= 0 || mx >= Wl || my + WD <= 0 || my >= Hl;
+    if (j == 0) org[qq] = far ? make_int2(FAR_ORIGIN, FAR_ORIGIN) : make_int2(mx, my);
+    if (act) {
+      const int col = far ? 0 : (int)flx - (mx & ~3);
+      const int row = far ? 0 : (int)fly - my;
+      xs[j * QB + qq] = make_float2(__int_as_float(col * QB), __fsub_rn(ux, flx));
+      ys[j * QB + qq] = make_float2(__int_as_float(row * Q::RSC * QB), __fsub_rn(uy, fly));
+    }
+  }
+}
+
+// One 4-cell window vector (row r, vector k of the staged row) of query qq:
+// the wide kernel's gather_load arithmetic for one slot.
+template <int V, typename PT>
+__device__ __forceinline__ void qm_load_vec(const PT* __restrict__ base, int qb0, const LevelAddr& A,
+                                            int2 o, int qq, int r, int k, float (&c)[4]) {
+  c[0] = c[1] = c[2] = c[3] = 0.f;
+  const int yy = o.y + r, x0 = (o.x & ~3) + 4 * k;
+  if (o.x != FAR_ORIGIN && (unsigned)yy < (unsigned)A.h && x0 >= 0 && x0 < A.w) {
+    const unsigned qoff = V > 1 ? (unsigned)(qb0 + qq) << A.lS : (unsigned)(qb0 + qq) * (unsigned)A.S;
+    const unsigned yoff = V > 1 ? __umul24((unsigned)(yy >> A.lth), (unsigned)A.tx)
+                                : (unsigned)(yy >> A.lth) * (unsigned)A.tx;
+    const unsigned yin = V > 1 ? (unsigned)(yy & A.mh) << A.ltw : (unsigned)((yy & A.mh) * A.tw);
+#pragma unroll
+    for (int h = 0; h < 4; h += V) {
+      const int x = x0 + h;
+      const unsigned tl = yoff + (unsigned)(x >> A.ltw);
+      const unsigned e = qoff + (V > 1 ? tl << A.lpS : tl * (unsigned)A.pageS) + yin +
+                         (unsigned)(x & A.mw);
+      if (V == 4 || x < A.w) load_vec<V, PT>(base + e, c + h);
+    }
+#pragma unroll
+    for (int h = 1; h < 4; ++h)
+      if (x0 + h >= A.w) c[h] = 0.f;
+  }
+}
+
+// Phase 1, query-minor: slot s -> query s % QB, (row, vector) s / QB; all loads
+// in flight before the LDS writes.
+template <int R, int NT_, int QB_, int V, typename PT>
+__device__ __forceinline__ void qm_gather(const PT* __restrict__ base, int qb0, const LevelAddr& A,
+                                          const int2* org, float* cells, int q0, int N, int tid) {
+  using Q = QmCfg<R, NT_, QB_>;
+  constexpr int QB = Q::QB, NQ = Q::NQ, RSC = Q::RSC;
+  float c[Q::VIT][4];
+#pragma unroll
+  for (int i = 0; i < Q::VIT; ++i) {
+    const int s = tid + i * Q::NT;
+    const int qq = s % QB, rem = s / QB, r = rem / NQ, k = rem - r * NQ;
+    if (s < Q::VSLOTS && q0 + qq < N) {
+      qm_load_vec<V, PT>(base, qb0, A, org[qq], qq, r, k, c[i]);
+    } else {
+      c[i][0] = c[i][1] = c[i][2] = c[i][3] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < Q::VIT; ++i) {
+    const int s = tid + i * Q::NT;
+    if (s < Q::VSLOTS) {
+      const int qq = s % QB, rem = s / QB, r = rem / NQ, k = rem - r * NQ;
+      float* d = cells + (r * RSC + 4 * k) * QB + qq;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d[e * QB] = c[i][e];
+    }
+  }
+}
+
+template <int R, typename PT, int NT_ = 512, int QB_ = 32>
+__global__ __launch_bounds__(NT_) void corr_lookup_qm_kernel(
+    const PT* __restrict__ pyr, const float* __restrict__ coords, float* __restrict__ out,
+    LookupGeom g) {
+  using Q = QmCfg<R, NT_, QB_>;
+  constexpr int RD = Q::RD, K = Q::K, QB = Q::QB, RSC = Q::RSC;
+  __shared__ __attribute__((aligned(16))) float cells[Q::NCELL * QB];
+  __shared__ float2 xs[RD * QB];   // {LDS column offset (int bits), fx}
+  __shared__ float2 ys[RD * QB];   // {LDS row offset (int bits), fy}
+  __shared__ int2 org[QB];
+
+  const int tid = threadIdx.x;
+  const int l = blockIdx.y, b = blockIdx.z;
+  const int q0 = blockIdx.x * QB;
+  const LevelAddr A = g.lv[l];
+  if constexpr (QB_ == 16) {   // one-round grids: finest level first (as the wide kernel)
+    if (l == 0) __builtin_amdgcn_s_setprio(3);
+    else if (l == 1) __builtin_amdgcn_s_setprio(2);
+    else if (l == 2) __builtin_amdgcn_s_setprio(1);
+  }
+
+  {
+    Phase0Coords<R, NT_, QB_> c;
+    wide_phase0_load<R, NT_, QB_>(coords, g, b, q0, tid, c);
+    qm_phase0_taps<R, NT_, QB_>(c, A, l, tid, xs, ys, org);
+  }
+  __syncthreads();
+  {
+    const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
+    const int qb0 = q0 & ((1 << A.lqb) - 1);
+    if (A.lth == 30 || A.tw == 1)
+      qm_gather<R, NT_, QB_, 1, PT>(base, qb0, A, org, cells, q0, g.N, tid);
+    else if (A.tw >= 4)
+      qm_gather<R, NT_, QB_, 4, PT>(base, qb0, A, org, cells, q0, g.N, tid);
+    else
+      qm_gather<R, NT_, QB_, 2, PT>(base, qb0, A, org, cells, q0, g.N, tid);
+  }
+  __syncthreads();
+
+  const int qq = tid % QB, cls = tid / QB;
+  if (q0 + qq >= g.N) return;
+  const float* cq = cells + qq;
+  float* op = out + ((long long)b * g.cout + (long long)l * K + cls) * g.N + q0 + qq;
+  const long long ostep = (long long)Q::NCLS * g.N;
+  for (int k = cls; k < K; k += Q::NCLS) {
+    const int ox = k / RD, oy = k - ox * RD;
+    const float2 xd = xs[ox * QB + qq], yd = ys[oy * QB + qq];
+    const float* p = cq + __float_as_int(yd.x) + __float_as_int(xd.x);
+    const float v00 = p[0], v01 = p[QB], v10 = p[RSC * QB], v11 = p[RSC * QB + QB];
+    const float gx = __fsub_rn(1.f, xd.y), gy = __fsub_rn(1.f, yd.y);
+    const float nw = __fmul_rn(gy, gx), ne = __fmul_rn(gy, xd.y);
+    const float sw = __fmul_rn(yd.y, gx), se = __fmul_rn(yd.y, xd.y);
+    float r = __fmul_rn(nw, v00);
+    r = __builtin_fmaf(ne, v01, r);
+    r = __builtin_fmaf(sw, v10, r);
+    r = __builtin_fmaf(se, v11, r);
+    if (g.out_nt) __builtin_nontemporal_store(r, op);
+    else __hip_atomic_store(op, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    op += ostep;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Lookup backward (training: train.py:175-178 backpropagates through the
 // grid_sample calls of core/utils/utils.py:65).  The gradient of one query's
 // level-l image comes only from that query's (2r+1)^2 samples at level l, so a
@@ -709,8 +896,9 @@ int launch_lookup_r(const PT* pyr, const float* coords, float* out, const Lookup
   using W = WideCfg<R>;
   LookupGeom g = g0;
   const long long wg32 = (long long)((g.N + W::QB - 1) / W::QB) * g.levels * B;
-  // pyramid bytes: B x N queries x N level-0 cells, x 4/3 for levels 1-3
-  const double pyr_bytes = (double)B * g.N * (double)g.N * sizeof(PT) * (4.0 / 3.0);
+  // pyramid bytes as the build's store rule counts them (dma_stream_out): padded
+  // level-0 pages (qt x 128 queries x whole tiles), x 4/3 for levels 1-3
+  const double pyr_bytes = (double)B * g.lv[0].qt * (double)g.lv[0].qstride * sizeof(PT) * (4.0 / 3.0);
   const bool big_misaligned = g.N % 32 != 0 && pyr_bytes >= 128.0 * (1 << 20);
   if (R <= 4 && wg32 <= 1024 && !big_misaligned) {
     using S = WideCfg<R, 256, 16>;
@@ -723,6 +911,31 @@ int launch_lookup_r(const PT* pyr, const float* coords, float* out, const Lookup
   g.out_nt = 1;
   const dim3 grid((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
   hipLaunchKernelGGL((corr_lookup_wide_kernel<R, PT>), grid, dim3(W::NT), 0, stream, pyr, coords,
+                     out, g);
+  return dxr::launch_status();
+}
+
+// The query-minor kernel with launch_lookup_r's shape and output policy
+// (`one_round_qb`: queries per workgroup on one-round grids, 16 or 32 at 256
+// threads).
+template <int R, typename PT, int ONE_QB = 16>
+int launch_lookup_qm_r(const PT* pyr, const float* coords, float* out, const LookupGeom& g0, int B,
+                       hipStream_t stream) {
+  using W = WideCfg<R>;
+  LookupGeom g = g0;
+  const long long wg32 = (long long)((g.N + W::QB - 1) / W::QB) * g.levels * B;
+  const double pyr_bytes = (double)B * g.lv[0].qt * (double)g.lv[0].qstride * sizeof(PT) * (4.0 / 3.0);
+  const bool big_misaligned = g.N % 32 != 0 && pyr_bytes >= 128.0 * (1 << 20);
+  if (R <= 4 && wg32 <= 1024 && !big_misaligned) {
+    g.out_nt = g.N % 32 == 0 ? 1 : 0;
+    const dim3 grid((unsigned)((g.N + ONE_QB - 1) / ONE_QB), (unsigned)g.levels, (unsigned)B);
+    hipLaunchKernelGGL((corr_lookup_qm_kernel<R, PT, 256, ONE_QB>), grid, dim3(256), 0, stream, pyr,
+                       coords, out, g);
+    return dxr::launch_status();
+  }
+  g.out_nt = 1;
+  const dim3 grid((unsigned)((g.N + 31) / 32), (unsigned)g.levels, (unsigned)B);
+  hipLaunchKernelGGL((corr_lookup_qm_kernel<R, PT, 512, 32>), grid, dim3(512), 0, stream, pyr, coords,
                      out, g);
   return dxr::launch_status();
 }

@@ -1392,7 +1392,7 @@ extern "C" int dxr_xp_build22(const float* f1, const float* f2, int64_t B, int64
                      reinterpret_cast<uint4*>(sp2), e1, e2, g.D, g.N);
   int st = dxr::launch_status();
   if (st != DXR_OK) return st;
-  const dim3 rg = dma_grid(g, (int)B, 0);   // whole units only
+  const dim3 rg = dma_grid(g, (int)B, stream, 0);   // whole units only
   if (g.recip == 0.f)
     hipLaunchKernelGGL((xp_dma22_kernel<true>), rg, dim3(2 * NT), 0, stream, sp1, sp2, e1, e2, pyr, g);
   else

@@ -209,6 +209,125 @@ int xp_shape(const PT* pyr, const float* coords, float* out, const LookupGeom& g
   return dxr::launch_status();
 }
 
+typedef __attribute__((address_space(3))) void xl_lds_void_t;
+
+// Round 6: the wide kernel with its window gathers by
+// LDS-DMA (buffer_load ... lds, 16 B per lane) on the f32 paged levels whose
+// tile rows hold >= 4 cells and whose width is a multiple of 4 (no partial
+// vectors): the per-query LDS block of QS = 180 floats is 45 16-B granules (44
+// window vectors + the bank-skew granule), so granule g of the workgroup's
+// staging area is (query g / 45, vector g % 45) and a wave instruction covers
+// 64 consecutive granules, lane-linear as the DMA writes them; the skew granules
+// get an out-of-range offset (zeros).  Off-level rows / vectors and far queries
+// read as zero by the range check.  Other levels keep the register gather.
+template <int R, typename PT, int NT_, int QB_>
+__global__ __launch_bounds__(NT_) void xp_lookup_dma_kernel(const PT* __restrict__ pyr,
+                                                           const float* __restrict__ coords,
+                                                           float* __restrict__ out, LookupGeom g) {
+  using C = WideCfg<R, NT_, QB_>;
+  constexpr int RD = C::RD, RS = C::RS, K = C::K, QB = C::QB, NT = NT_;
+  static_assert(C::QS == 4 * (C::WD * C::NQ + 1), "one skew granule per query");
+  constexpr int GQ = C::QS / 4, NG = QB * GQ, GIT = (NG + NT - 1) / NT;
+  __shared__ __attribute__((aligned(16))) float cells[QB * C::QS];
+  __shared__ float4 xs[RD * QB];
+  __shared__ float4 ys[RD * QB];
+  __shared__ int2 org[QB];
+  const int tid = threadIdx.x;
+  const int l = blockIdx.y, b = blockIdx.z;
+  const int q0 = blockIdx.x * QB;
+  const LevelAddr A = g.lv[l];
+  if constexpr (QB_ <= 16) {
+    if (l == 0) __builtin_amdgcn_s_setprio(3);
+    else if (l == 1) __builtin_amdgcn_s_setprio(2);
+    else if (l == 2) __builtin_amdgcn_s_setprio(1);
+  }
+  wide_phase0<R, NT_, QB_>(coords, g, A, b, l, q0, tid, xs, ys, org);
+  __syncthreads();
+  {
+    const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
+    const int qb0 = q0 & ((1 << A.lqb) - 1);
+    if (sizeof(PT) == 4 && A.lth != 30 && A.tw >= 4 && (A.w & 3) == 0) {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<PT*>(base), (short)0, 0x7fffffff, 0x00020000);
+      const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+#pragma unroll
+      for (int i = 0; i < GIT; ++i) {
+        const int gw = i * NT + wave * 64;            // the wave's first granule (uniform)
+        if (gw >= NG) break;
+        const int gi = gw + lane, qq = gi / GQ, rem = gi - qq * GQ;
+        uint32_t voff = 0x80000000u;
+        if (gi < NG && rem < GQ - 1 && q0 + qq < g.N) {
+          const int2 o = org[qq];
+          const int r = rem / C::NQ, k = rem - r * C::NQ;
+          const int yy = o.y + r, x0 = (o.x & ~3) + 4 * k;
+          if (o.x != FAR_ORIGIN && (unsigned)yy < (unsigned)A.h && x0 >= 0 && x0 < A.w) {
+            const unsigned tl = __umul24((unsigned)(yy >> A.lth), (unsigned)A.tx) + (unsigned)(x0 >> A.ltw);
+            const unsigned e = ((unsigned)(qb0 + qq) << A.lS) + (tl << A.lpS) +
+                               ((unsigned)(yy & A.mh) << A.ltw) + (unsigned)(x0 & A.mw);
+            voff = e * 4u;
+          }
+        }
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (xl_lds_void_t*)(cells + gw * 4), 16, voff, 0, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (A.lth == 30) {
+      gather_windows<R, NT_, 1, PT, false, QB_>(base, qb0, A, org, cells, q0, g.N, tid);
+    } else if (A.tw >= 8) {
+      gather_windows<R, NT_, 4, PT, false, QB_>(base, qb0, A, org, cells, q0, g.N, tid);
+    } else if (A.tw == 4) {
+      gather_windows<R, NT_, 4, PT, true, QB_>(base, qb0, A, org, cells, q0, g.N, tid);
+    } else if (A.tw == 2) {
+      gather_windows<R, NT_, 2, PT, true, QB_>(base, qb0, A, org, cells, q0, g.N, tid);
+    } else {
+      gather_windows<R, NT_, 1, PT, false, QB_>(base, qb0, A, org, cells, q0, g.N, tid);
+    }
+  }
+  __syncthreads();
+  const int qq = tid % QB, cls = tid / QB;
+  if (q0 + qq >= g.N) return;
+  const float* cq = cells + qq * C::QS;
+  float* op = out + ((long long)b * g.cout + (long long)l * K + cls) * g.N + q0 + qq;
+  const long long ostep = (long long)C::NCLS * g.N;
+  for (int k = cls; k < K; k += C::NCLS) {
+    const int ox = k / RD, oy = k - ox * RD;
+    const float4 xd = xs[ox * QB + qq], yd = ys[oy * QB + qq];
+    const float* p = cq + __float_as_int(yd.x) + __float_as_int(xd.x);
+    const float v00 = p[0], v01 = p[1], v10 = p[RS], v11 = p[RS + 1];
+    const float nw = __fmul_rn(yd.z, xd.z), ne = __fmul_rn(yd.z, xd.y);
+    const float sw = __fmul_rn(yd.y, xd.z), se = __fmul_rn(yd.y, xd.y);
+    float r = __fmul_rn(nw, v00);
+    r = __builtin_fmaf(ne, v01, r);
+    r = __builtin_fmaf(sw, v10, r);
+    r = __builtin_fmaf(se, v11, r);
+    if (g.out_nt) __builtin_nontemporal_store(r, op);
+    else __hip_atomic_store(op, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    op += ostep;
+  }
+}
+
+template <typename PT>
+int xp_dma_launch(const PT* pyr, const float* coords, float* out, const LookupGeom& g0, int B,
+                  hipStream_t stream) {
+  // launch_lookup_r's shape and output policy
+  using W = WideCfg<4>;
+  LookupGeom g = g0;
+  const long long wg32 = (long long)((g.N + W::QB - 1) / W::QB) * g.levels * B;
+  const double pyr_bytes = (double)B * g.lv[0].qt * (double)g.lv[0].qstride * sizeof(PT) * (4.0 / 3.0);
+  const bool big_misaligned = g.N % 32 != 0 && pyr_bytes >= 128.0 * (1 << 20);
+  if (wg32 <= 1024 && !big_misaligned) {
+    g.out_nt = g.N % 32 == 0 ? 1 : 0;
+    const dim3 grid((unsigned)((g.N + 15) / 16), (unsigned)g.levels, (unsigned)B);
+    hipLaunchKernelGGL((xp_lookup_dma_kernel<4, PT, 256, 16>), grid, dim3(256), 0, stream, pyr,
+                       coords, out, g);
+    return dxr::launch_status();
+  }
+  g.out_nt = 1;
+  const dim3 grid((unsigned)((g.N + 31) / 32), (unsigned)g.levels, (unsigned)B);
+  hipLaunchKernelGGL((xp_lookup_dma_kernel<4, PT, 512, 32>), grid, dim3(512), 0, stream, pyr,
+                     coords, out, g);
+  return dxr::launch_status();
+}
+
 template <typename PT>
 int xp_dispatch(int xp, const PT* pyr, const float* coords, float* out, const LookupGeom& g, int B,
                 unsigned long long* trace, hipStream_t stream) {
@@ -221,6 +340,11 @@ int xp_dispatch(int xp, const PT* pyr, const float* coords, float* out, const Lo
     case 69: return xp_shape<128, 8>(pyr, coords, out, g, B, stream, 1);
     case 70: return xp_shape<1024, 64>(pyr, coords, out, g, B, stream, 1);
     case 128: return xp_shape<1024, 64>(pyr, coords, out, g, B, stream);
+    // round 6: query-minor staging (corr_lookup_qm_kernel) with the product's
+    // shape / output policy; 91: 256 x 32 on one-round grids
+    case 90: return launch_lookup_qm_r<4, PT, 16>(pyr, coords, out, g, B, stream);
+    case 91: return launch_lookup_qm_r<4, PT, 32>(pyr, coords, out, g, B, stream);
+    case 92: return xp_dma_launch(pyr, coords, out, g, B, stream);   // LDS-DMA gathers
     case 0: return xp_launch<0>(pyr, coords, out, g, B, trace, stream);
     case 1: return xp_launch<1>(pyr, coords, out, g, B, trace, stream);
     case 2: return xp_launch<2>(pyr, coords, out, g, B, trace, stream);

@@ -601,6 +601,37 @@ def test_prescaled_build_nonfinite_fallback_forms(dx, W, layout):
         assert (g[fin] - r[fin]).abs().max().item() <= 1e-5 * r[fin].abs().max().item(), lvl
 
 
+@pytest.mark.parametrize("B,L", [(3, 4), (2, 4), (1, 2), (1, 3)])
+def test_prescaled_build_nonfinite_on_whole_units(dx, B, L):
+    """inf/NaN operands on the grids real inputs take.
+    Sintel-size maps run whole units (B=3: 4,704 units, no tail split, so every
+    page goes through the whole-unit kernel's per-wave vote and recompute); B=2
+    has a 522 MB pyramid, so its pages are streamed out non-temporally (EXF 3)
+    and the recompute rewrites pages that first pass wrote (its 64-unit tail
+    also runs as quarter units); num_levels 2 and 3 take the vote on the
+    unscaled values instead of the level-3 cells.  Each against the exact-f32
+    build: NaN / inf patterns equal, f32 class elsewhere."""
+    H, W = 55, 128
+    f1, f2 = _pair(B=B, H=H, W=W, seed=301 + B + L, dist="fnet")
+    f1, f2 = f1.clone(), f2.clone()
+    for b in range(B):
+        f2[b, 3 + b, 40 - b, 100 + b] = float("nan")      # a target: NaN for every query
+        f1[b, 9 + b, 50 - b, 3 + 2 * b] = float("inf")    # a query: +-inf / NaN row
+        f1[b, 200, 20 + b, 64] = -float("inf")
+    base = _build_exact_f32(f1, f2, num_levels=L)
+    cb = dx.CorrBlock(f1, f2, num_levels=L)
+    for lvl in range(L):
+        got, ref = cb.corr_pyramid[lvl][:, 0], base[lvl]
+        assert torch.equal(torch.isnan(got), torch.isnan(ref)), lvl
+        assert torch.equal(torch.isinf(got), torch.isinf(ref)), lvl
+        assert torch.equal(got[torch.isinf(ref)], ref[torch.isinf(ref)]), lvl   # signs too
+        fin = torch.isfinite(ref)
+        assert fin.float().mean().item() > 0.95, lvl           # the pages around stay finite
+        assert (got[fin] - ref[fin]).abs().max().item() <= 1e-5 * ref[fin].abs().max().item(), lvl
+    del cb, base
+    torch.cuda.empty_cache()
+
+
 def _build_exact_f32(f1: torch.Tensor, f2: torch.Tensor, num_levels: int = 4,
                      algo: int | None = None):
     """The exact-f32 MFMA build (DXR_BUILD_EXACT_F32) through the C-ABI, as
