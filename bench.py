@@ -649,7 +649,7 @@ def main():
             achieved = flops / (build_ms * 1e-3) / 1e12
             ceiling = pipe_peak / mfma_per_flop
             b_traffic, b_src = pmc_traffic(wl_key, kname.split(" ")[0] + "<", cfg)
-            l_traffic, l_src = pmc_traffic(wl_key, "corr_lookup_wide_kernel<", cfg)
+            l_traffic, l_src = pmc_traffic(wl_key, "corr_lookup_qm_kernel<", cfg)
             bb = build_bytes(B, H, W, s_in, s_in)
             res["roofline"] = {
                 "kernel": kname + " (stage a+b)",
@@ -668,7 +668,7 @@ def main():
             }
             lf = lookup_line_floor_bytes(sets[G - 1][2], H, W, s_pyr=s_in)
             res["lookup_roofline"] = {
-                "kernel": "corr_lookup_wide_kernel (stage c)",
+                "kernel": "corr_lookup_qm_kernel (stage c; window cells staged query-minor in LDS)",
                 "bound": "hbm", "achieved": round(lb / (look_ms * 1e-3) / 1e9, 1),
                 "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(lb / (look_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),

@@ -268,7 +268,7 @@ __device__ __forceinline__ void alt_split8h(const float (&x)[8], uint4& h, uint4
 // bit 1 stores only outputs that are exactly 12345.0 (none: an ablation of the
 // output stores).
 template <int R, int NRB, int CMAX, bool H2 = false, int MINW = 2, bool BIN = false, int PF = 1,
-          bool DMA = false, int XP = 0>
+          int DMA = 0, int XP = 0>
 __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* __restrict__ f1,
                                                                const float* __restrict__ coords,
                                                                float* __restrict__ out,
@@ -285,7 +285,8 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
   __shared__ int box[4];                                    // bx0, by0, bw, bh
   __shared__ int qlist[TQ];                                 // BIN: query index or -1
   __shared__ float2 qxy[TQ];                                // BIN: its coordinates
-  // DMA: per wave two 4 KB buffers of 32 cells x 128 B (two k steps), swizzled 16-B slots
+  // DMA 1: per wave two 4 KB buffers of 32 cells x 128 B (two k steps), swizzled 16-B slots;
+  // DMA 2: per wave a ring of 4 one-k-step stages of 32 cells x 64 B (round 6)
   __shared__ __attribute__((aligned(16))) unsigned char cbuf[DMA ? 4 * 2 * 4096 : 16];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -497,6 +498,68 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[0][r] = __builtin_fmaf(acc2[r], 0x1p-11f, acc[0][r]);
     };
+    // DMA 2 (round 6, experiments): one k step (32 cells x 64 B) per stage, a ring of
+    // NS = 4 stages per wave, so three k steps of cell data are in flight (DMA 1 keeps
+    // one two-step batch ahead).  An instruction covers 16 cells x 64 B (4 lanes per
+    // cell); physical slot p of cell row r holds logical 16-B piece p ^ ((r >> 2) & 3),
+    // so the fragment reads (row j, pieces 2 kh, 2 kh + 1) are conflict-free
+    // ds_read_b128.  Same operands, split and products: bit-identical.
+    auto kloop_dma2 = [&]() {
+      static_assert(NRB == 1, "the DMA form stages one 32-cell block per wave");
+      constexpr int NS = 4;
+      af16 acc2 = {};
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[0][r] = 0.f;
+      const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(f2b), (short)0, lv.H2 * lv.W2 * g.C * 4, 0x00020000);
+      uint32_t voff[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = 16 * i + (lane >> 2), slot = lane & 3;
+        const int c = min(c0 + wave * 32 + row, ncells - 1);
+        const int cy = divbw(c), cx = c - cy * bw;
+        const int piece = slot ^ ((row >> 2) & 3);
+        voff[i] = (uint32_t)(((by0 + cy) * lv.W2 + bx0 + cx) * g.C) * 4u + 16u * piece;
+      }
+      unsigned char* wreg = cbuf + __builtin_amdgcn_readfirstlane(wave) * (NS * 2048);
+      auto issue = [&](int ks) {
+        unsigned char* dst = wreg + (ks % NS) * 2048;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rf, (lds_void_t*)(dst + i * 1024), 16, voff[i],
+                                                   ks * 64, 0, 0);
+      };
+      const int nst = nkb / 2;
+      const int sw = (j >> 2) & 3;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < NS - 1; ++u)
+        if (u < nst) issue(u);
+      for (int ks = 0; ks < nst; ++ks) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads of the slot refilled next
+        if (ks + NS - 1 < nst) {
+          issue(ks + NS - 1);
+          asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // stage ks landed (3 stages behind it)
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const unsigned char* rb0 = wreg + (ks % NS) * 2048 + j * 64;
+        const float4 a = *reinterpret_cast<const float4*>(rb0 + 16 * ((2 * kh) ^ sw));
+        const float4 b = *reinterpret_cast<const float4*>(rb0 + 16 * ((2 * kh + 1) ^ sw));
+        const ah8 qh = __builtin_bit_cast(ah8, qplanes[(0 * KB + 2 * ks + kh) * TQ + j]);
+        const ah8 ql = __builtin_bit_cast(ah8, qplanes[(1 * KB + 2 * ks + kh) * TQ + j]);
+        const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint4 h, l;
+        alt_split8h(x, h, l);
+        const ah8 th = __builtin_bit_cast(ah8, h), tl = __builtin_bit_cast(ah8, l);
+        acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc2, 0, 0, 0);
+        acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc2, 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qh, acc[0], 0, 0, 0);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[0][r] = __builtin_fmaf(acc2[r], 0x1p-11f, acc[0][r]);
+    };
     // cell vectors one k step ahead in registers
     auto kloop = [&](auto h2tag) {
       constexpr bool M2 = decltype(h2tag)::value;
@@ -604,7 +667,10 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
       }
     };
     if constexpr (H2) {
-      if constexpr (DMA && NRB == 1) {
+      if constexpr (DMA == 2 && NRB == 1) {
+        if (nkb % 2 == 0) kloop_dma2();
+        else kloop(std::integral_constant<bool, true>{});
+      } else if constexpr (DMA == 1 && NRB == 1) {
         if (nkb % 4 == 0) kloop_dma();
         else kloop(std::integral_constant<bool, true>{});
       } else {
@@ -927,7 +993,7 @@ long long alt_order_bytes(long long H, long long W) {
 // PF: cell loads of the ordered form kept 4 k steps ahead (round 3: with compact boxes the
 // waves wait on L2 latency, 62 % of wave cycles at PF = 1; 1080p 12 lookups 2,033 -> 1,972 us,
 // Sintel 626 -> 612 us in the step).  The tile-order form stays at 1 (its boxes are L1/TA-bound).
-template <int R, int NRB, bool DMA = false, int PF = 4, int XP = 0>
+template <int R, int NRB, int DMA = 0, int PF = 4, int XP = 0>
 int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const AltGeom& g,
                       int levels, int Z, int W1, hipStream_t stream, void* ws = nullptr,
                       int xl = -1) {
@@ -969,12 +1035,12 @@ int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const Al
     // entries of list (z, l) start at list (z * levels + l) * list_bytes: the kernel
     // indexes int4 entries by ((z * levels + l) * np + i), so lists are laid out
     // with a stride of list_bytes / 16 entries
-    if constexpr (DMA)
-      hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 2, true, 1, true>), grid,
+    if constexpr (DMA != 0)
+      hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 2, true, 1, DMA>), grid,
                          dim3(256), 0, stream, f1, coords, out, g, W1, tiles_x,
                          reinterpret_cast<const int4*>(ws), o.list_bytes / 16, XL);
     else
-      hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 3, true, PF, false, XP>), grid, dim3(256),
+      hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 3, true, PF, 0, XP>), grid, dim3(256),
                          0, stream, f1, coords, out, g, W1, tiles_x,
                          reinterpret_cast<const int4*>(ws), o.list_bytes / 16, XL);
     return dxr::launch_status();

@@ -437,9 +437,16 @@ struct QmCfg {
   static constexpr int NQ = C::NQ;                    // 4-cell vectors per staged row
   static constexpr int RSC = 4 * NQ + 1;              // odd row pitch (cells)
   static constexpr int NCELL = WD * RSC;
-  static constexpr int VSLOTS = QB * WD * NQ;
+  // gather slots: query fastest, then the window row over an even count WDE >= WD
+  // (row WD is a dummy when WD is odd), then the vector: the two slots of a
+  // 16-query half-wave are always rows r, r + 1 of one vector column
+  static constexpr int WDE = (WD + 1) & ~1;
+  static constexpr int VSLOTS = QB * WDE * NQ;
   static constexpr int VIT = (VSLOTS + NT - 1) / NT;
   static constexpr int NCLS = NT / QB;
+  // tap data pitch: phase 0 writes a query's samples from 16 consecutive lanes
+  // (xs[j * XP + qq]); with XP = QB every one of them hit one bank (16-way)
+  static constexpr int XP = QB + 1;
   static_assert(QB == 16 || QB == 32, "bank arithmetic assumes 16 or 32 queries");
 };
 
@@ -476,8 +483,8 @@ __device__ __forceinline__ void qm_phase0_taps(const Phase0Coords<R, NT_, QB_>& 
     if (act) {
       const int col = far ? 0 : (int)flx - (mx & ~3);
       const int row = far ? 0 : (int)fly - my;
-      xs[j * QB + qq] = make_float2(__int_as_float(col * QB), __fsub_rn(ux, flx));
-      ys[j * QB + qq] = make_float2(__int_as_float(row * Q::RSC * QB), __fsub_rn(uy, fly));
+      xs[j * Q::XP + qq] = make_float2(__int_as_float(col * QB), __fsub_rn(ux, flx));
+      ys[j * Q::XP + qq] = make_float2(__int_as_float(row * Q::RSC * QB), __fsub_rn(uy, fly));
     }
   }
 }
@@ -508,29 +515,74 @@ __device__ __forceinline__ void qm_load_vec(const PT* __restrict__ base, int qb0
   }
 }
 
-// Phase 1, query-minor: slot s -> query s % QB, (row, vector) s / QB; all loads
-// in flight before the LDS writes.
-template <int R, int NT_, int QB_, int V, typename PT>
+// The same vector by a range-checked buffer load (paged levels, V = 4): an
+// invalid slot (off the level, far query, padding) gets an out-of-range offset
+// and reads as zeros, so the load needs no branch.
+template <typename PT>
+__device__ __forceinline__ void qm_load_vec_buf(__amdgpu_buffer_rsrc_t rs, int qb0, const LevelAddr& A,
+                                                int2 o, int qq, int r, int k, bool live,
+                                                float (&c)[4]) {
+  const int yy = o.y + r, x0 = (o.x & ~3) + 4 * k;
+  unsigned voff = 0x80000000u;
+  if (live && o.x != FAR_ORIGIN && (unsigned)yy < (unsigned)A.h && x0 >= 0 && x0 < A.w) {
+    const unsigned tl = __umul24((unsigned)(yy >> A.lth), (unsigned)A.tx) + (unsigned)(x0 >> A.ltw);
+    const unsigned e = ((unsigned)(qb0 + qq) << A.lS) + (tl << A.lpS) +
+                       ((unsigned)(yy & A.mh) << A.ltw) + (unsigned)(x0 & A.mw);
+    voff = e * (unsigned)sizeof(PT);
+  }
+  if constexpr (sizeof(PT) == 4) {
+    const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0);
+    c[0] = __uint_as_float(v[0]); c[1] = __uint_as_float(v[1]);
+    c[2] = __uint_as_float(v[2]); c[3] = __uint_as_float(v[3]);
+  } else {
+    typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+    const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, 0, 0);
+    c[0] = __uint_as_float(v[0] << 16); c[1] = __uint_as_float(v[0] & 0xffff0000u);
+    c[2] = __uint_as_float(v[1] << 16); c[3] = __uint_as_float(v[1] & 0xffff0000u);
+  }
+#pragma unroll
+  for (int h = 1; h < 4; ++h)
+    if (x0 + h >= A.w) c[h] = 0.f;   // tile padding past the level's right edge
+}
+
+// Phase 1, query-minor: slot s -> query s % QB, (vector, row) s / QB with the
+// row fastest over WDE rows (so the two slots of a 16-query half-wave are one
+// row = RSC cells apart: opposite bank halves); all loads in flight before the
+// LDS writes.
+template <int R, int NT_, int QB_, int V, typename PT, bool BUF = false>
 __device__ __forceinline__ void qm_gather(const PT* __restrict__ base, int qb0, const LevelAddr& A,
                                           const int2* org, float* cells, int q0, int N, int tid) {
   using Q = QmCfg<R, NT_, QB_>;
-  constexpr int QB = Q::QB, NQ = Q::NQ, RSC = Q::RSC;
+  constexpr int QB = Q::QB, RSC = Q::RSC;
   float c[Q::VIT][4];
+  if constexpr (BUF && V == 4) {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<PT*>(base), (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < Q::VIT; ++i) {
+      const int s = tid + i * Q::NT;
+      const int qq = s % QB, rem = s / QB, k = rem / Q::WDE, r = rem - k * Q::WDE;
+      const bool live = s < Q::VSLOTS && r < Q::WD && q0 + qq < N;
+      qm_load_vec_buf<PT>(rs, qb0, A, org[live ? qq : 0], qq, r, k, live, c[i]);
+    }
+  } else {
 #pragma unroll
   for (int i = 0; i < Q::VIT; ++i) {
     const int s = tid + i * Q::NT;
-    const int qq = s % QB, rem = s / QB, r = rem / NQ, k = rem - r * NQ;
-    if (s < Q::VSLOTS && q0 + qq < N) {
+    const int qq = s % QB, rem = s / QB, k = rem / Q::WDE, r = rem - k * Q::WDE;
+    if (s < Q::VSLOTS && r < Q::WD && q0 + qq < N) {
       qm_load_vec<V, PT>(base, qb0, A, org[qq], qq, r, k, c[i]);
     } else {
       c[i][0] = c[i][1] = c[i][2] = c[i][3] = 0.f;
     }
   }
+  }
 #pragma unroll
   for (int i = 0; i < Q::VIT; ++i) {
     const int s = tid + i * Q::NT;
     if (s < Q::VSLOTS) {
-      const int qq = s % QB, rem = s / QB, r = rem / NQ, k = rem - r * NQ;
+      const int qq = s % QB, rem = s / QB, k = rem / Q::WDE, r = rem - k * Q::WDE;
+      if (r >= Q::WD) continue;
       float* d = cells + (r * RSC + 4 * k) * QB + qq;
 #pragma unroll
       for (int e = 0; e < 4; ++e) d[e * QB] = c[i][e];
@@ -538,15 +590,15 @@ __device__ __forceinline__ void qm_gather(const PT* __restrict__ base, int qb0, 
   }
 }
 
-template <int R, typename PT, int NT_ = 512, int QB_ = 32>
+template <int R, typename PT, int NT_ = 512, int QB_ = 32, int UNR = 1, bool BUF = false>
 __global__ __launch_bounds__(NT_) void corr_lookup_qm_kernel(
     const PT* __restrict__ pyr, const float* __restrict__ coords, float* __restrict__ out,
     LookupGeom g) {
   using Q = QmCfg<R, NT_, QB_>;
   constexpr int RD = Q::RD, K = Q::K, QB = Q::QB, RSC = Q::RSC;
   __shared__ __attribute__((aligned(16))) float cells[Q::NCELL * QB];
-  __shared__ float2 xs[RD * QB];   // {LDS column offset (int bits), fx}
-  __shared__ float2 ys[RD * QB];   // {LDS row offset (int bits), fy}
+  __shared__ float2 xs[RD * Q::XP];   // {LDS column offset (int bits), fx}
+  __shared__ float2 ys[RD * Q::XP];   // {LDS row offset (int bits), fy}
   __shared__ int2 org[QB];
 
   const int tid = threadIdx.x;
@@ -571,7 +623,7 @@ __global__ __launch_bounds__(NT_) void corr_lookup_qm_kernel(
     if (A.lth == 30 || A.tw == 1)
       qm_gather<R, NT_, QB_, 1, PT>(base, qb0, A, org, cells, q0, g.N, tid);
     else if (A.tw >= 4)
-      qm_gather<R, NT_, QB_, 4, PT>(base, qb0, A, org, cells, q0, g.N, tid);
+      qm_gather<R, NT_, QB_, 4, PT, BUF>(base, qb0, A, org, cells, q0, g.N, tid);
     else
       qm_gather<R, NT_, QB_, 2, PT>(base, qb0, A, org, cells, q0, g.N, tid);
   }
@@ -582,9 +634,10 @@ __global__ __launch_bounds__(NT_) void corr_lookup_qm_kernel(
   const float* cq = cells + qq;
   float* op = out + ((long long)b * g.cout + (long long)l * K + cls) * g.N + q0 + qq;
   const long long ostep = (long long)Q::NCLS * g.N;
+#pragma unroll UNR
   for (int k = cls; k < K; k += Q::NCLS) {
     const int ox = k / RD, oy = k - ox * RD;
-    const float2 xd = xs[ox * QB + qq], yd = ys[oy * QB + qq];
+    const float2 xd = xs[ox * Q::XP + qq], yd = ys[oy * Q::XP + qq];
     const float* p = cq + __float_as_int(yd.x) + __float_as_int(xd.x);
     const float v00 = p[0], v01 = p[QB], v10 = p[RSC * QB], v11 = p[RSC * QB + QB];
     const float gx = __fsub_rn(1.f, xd.y), gy = __fsub_rn(1.f, yd.y);
@@ -872,6 +925,7 @@ int launch_lookup_backward_r(const BwSets& sets, float* gpyr, const LookupGeom& 
   return dxr::launch_status();
 }
 
+// Round-5 product launcher of the wide kernel (kept for the experiments target).
 // Workgroup shape: 512 threads x 32 queries (4 resident per CU), or — when that
 // grid fits in one dispatch round (<= 1024 workgroups: Sintel / Chairs B=1) —
 // 256 threads x 16 queries, the same 16 threads per query in twice the
@@ -891,7 +945,7 @@ int launch_lookup_backward_r(const BwSets& sets, float* gpyr, const LookupGeom& 
 // with non-temporal stores beat both (-6.3 % / -3.9 %, r6k); a small one (Chairs
 // B=1, 43 MB, resident anyway) keeps 256 x 16 with write-through (+13 % otherwise).
 template <int R, typename PT>
-int launch_lookup_r(const PT* pyr, const float* coords, float* out, const LookupGeom& g0, int B,
+int launch_lookup_wide_r(const PT* pyr, const float* coords, float* out, const LookupGeom& g0, int B,
                     hipStream_t stream) {
   using W = WideCfg<R>;
   LookupGeom g = g0;
@@ -915,11 +969,19 @@ int launch_lookup_r(const PT* pyr, const float* coords, float* out, const Lookup
   return dxr::launch_status();
 }
 
-// The query-minor kernel with launch_lookup_r's shape and output policy
-// (`one_round_qb`: queries per workgroup on one-round grids, 16 or 32 at 256
-// threads).
-template <int R, typename PT, int ONE_QB = 16>
-int launch_lookup_qm_r(const PT* pyr, const float* coords, float* out, const LookupGeom& g0, int B,
+// The product lookup (round 6): the query-minor kernel with the round-5 shape
+// and output policy below (launch_lookup_wide_r).  One-round grids (256 x 16)
+// load their window vectors with plain global loads, multi-round grids (512 x
+// 32) with range-checked buffer loads (BUF; the loads need no branch).  Same
+// process, in the step (build + 12 lookups, scripts/ab_step.py, outputs checked
+// bit-identical; profiles/r06/experiments/r6d_*): Sintel B=1 184.9 -> 177.0 us
+// (plain) / 178.8 (buffer), B=8 1,288.4 -> 1,280.1 / 1,258.0, KITTI B=8 bf16
+// 913.1 -> 884.6 / 854.0, 1080p full 2,176 -> 2,170 / 2,149, Chairs 98.2 -> 96.4
+// / 97.4, Sintel B=2 348.2 -> 355.6 / 349.7.  `ONE_QB` / `UNR` / `MULTI_BUF`:
+// experiment knobs (queries per one-round workgroup, phase-2 unroll, buffer loads
+// on multi-round grids); `ONE_BUF`: buffer loads on one-round grids too.
+template <int R, typename PT, int ONE_QB = 16, int UNR = 1, bool ONE_BUF = false, bool MULTI_BUF = true>
+int launch_lookup_r(const PT* pyr, const float* coords, float* out, const LookupGeom& g0, int B,
                        hipStream_t stream) {
   using W = WideCfg<R>;
   LookupGeom g = g0;
@@ -929,14 +991,14 @@ int launch_lookup_qm_r(const PT* pyr, const float* coords, float* out, const Loo
   if (R <= 4 && wg32 <= 1024 && !big_misaligned) {
     g.out_nt = g.N % 32 == 0 ? 1 : 0;
     const dim3 grid((unsigned)((g.N + ONE_QB - 1) / ONE_QB), (unsigned)g.levels, (unsigned)B);
-    hipLaunchKernelGGL((corr_lookup_qm_kernel<R, PT, 256, ONE_QB>), grid, dim3(256), 0, stream, pyr,
+    hipLaunchKernelGGL((corr_lookup_qm_kernel<R, PT, 256, ONE_QB, UNR, ONE_BUF>), grid, dim3(256), 0, stream, pyr,
                        coords, out, g);
     return dxr::launch_status();
   }
   g.out_nt = 1;
-  const dim3 grid((unsigned)((g.N + 31) / 32), (unsigned)g.levels, (unsigned)B);
-  hipLaunchKernelGGL((corr_lookup_qm_kernel<R, PT, 512, 32>), grid, dim3(512), 0, stream, pyr, coords,
-                     out, g);
+  const dim3 grid((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
+  hipLaunchKernelGGL((corr_lookup_qm_kernel<R, PT, 512, W::QB, UNR, MULTI_BUF>), grid, dim3(512), 0, stream, pyr,
+                     coords, out, g);
   return dxr::launch_status();
 }
 

@@ -7,7 +7,7 @@
 // CU; the product keeps 4 ahead = variant 3); 1: cell vectors by LDS-DMA into per-wave swizzled buffers (2 per CU);
 // 2 / 3 / 4 / 5: cell loads 2 / 4 / 6 / 8 k steps ahead (register ring); 6 / 7: variant 3
 // with the level-by-XCD workgroup mapping off / on (3 = the product's choice); 8: variant 3
-// without the cell vectors' f16 split (a timing ablation).
+// without the cell vectors' f16 split (a timing ablation); 9: DMA with one-k-step stages, 4 deep.
 // Radius 4, C % 32 == 0, 16-byte aligned NHWC fmaps; ws as dxr_alt_corr_lookup_ws.
 extern "C" int dxr_xp_alt_lookup(const float* fmap1, const float* const* fmap2_levels,
                                  const float* coords, float* out, int64_t B, int64_t H,
@@ -30,31 +30,33 @@ extern "C" int dxr_xp_alt_lookup(const float* fmap1, const float* const* fmap2_l
   for (int l = 0; l < num_levels; ++l)
     g.lv[l] = AltLevel{fmap2_levels[l], L.h[l], L.w[l], 1.f / (float)(1 << l), l * 81};
   if (variant == 0)
-    return launch_alt_mfma_r<4, 1, false, 1>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+    return launch_alt_mfma_r<4, 1, 0, 1>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
                                           stream, ws);
   if (variant == 1)
-    return launch_alt_mfma_r<4, 1, true>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+    return launch_alt_mfma_r<4, 1, 1>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
                                          stream, ws);
+  if (variant == 9)   // round 6: one-k-step DMA stages, 4-deep ring per wave
+    return launch_alt_mfma_r<4, 1, 2>(fmap1, coords, out, g, num_levels, (int)B, (int)W, stream, ws);
   if (variant == 2)
-    return launch_alt_mfma_r<4, 1, false, 2>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+    return launch_alt_mfma_r<4, 1, 0, 2>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
                                              stream, ws);
   if (variant == 3)
-    return launch_alt_mfma_r<4, 1, false, 4>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+    return launch_alt_mfma_r<4, 1, 0, 4>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
                                              stream, ws);
   if (variant == 4)
-    return launch_alt_mfma_r<4, 1, false, 6>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+    return launch_alt_mfma_r<4, 1, 0, 6>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
                                              stream, ws);
   if (variant == 5)
-    return launch_alt_mfma_r<4, 1, false, 8>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+    return launch_alt_mfma_r<4, 1, 0, 8>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
                                              stream, ws);
   if (variant == 11)  // variant 3 without the output stores (timing ablation)
-    return launch_alt_mfma_r<4, 1, false, 4, 2>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+    return launch_alt_mfma_r<4, 1, 0, 4, 2>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
                                                 stream, ws);
   if (variant == 8)   // variant 3 without the cell split (timing ablation)
-    return launch_alt_mfma_r<4, 1, false, 4, 1>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+    return launch_alt_mfma_r<4, 1, 0, 4, 1>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
                                                 stream, ws);
   if (variant == 6 || variant == 7)
-    return launch_alt_mfma_r<4, 1, false, 4>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+    return launch_alt_mfma_r<4, 1, 0, 4>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
                                              stream, ws, variant - 6);
   return DXR_EINVAL;
 }

@@ -228,7 +228,9 @@ __global__ __launch_bounds__(NT_) void xp_lookup_dma_kernel(const PT* __restrict
   constexpr int RD = C::RD, RS = C::RS, K = C::K, QB = C::QB, NT = NT_;
   static_assert(C::QS == 4 * (C::WD * C::NQ + 1), "one skew granule per query");
   constexpr int GQ = C::QS / 4, NG = QB * GQ, GIT = (NG + NT - 1) / NT;
-  __shared__ __attribute__((aligned(16))) float cells[QB * C::QS];
+  // every lane of a DMA instruction writes its 16 B (zeros when out of range):
+  // the staging area is padded to whole 64-granule wave instructions
+  __shared__ __attribute__((aligned(16))) float cells[((NG + 63) / 64) * 64 * 4];
   __shared__ float4 xs[RD * QB];
   __shared__ float4 ys[RD * QB];
   __shared__ int2 org[QB];
@@ -342,9 +344,12 @@ int xp_dispatch(int xp, const PT* pyr, const float* coords, float* out, const Lo
     case 128: return xp_shape<1024, 64>(pyr, coords, out, g, B, stream);
     // round 6: query-minor staging (corr_lookup_qm_kernel) with the product's
     // shape / output policy; 91: 256 x 32 on one-round grids
-    case 90: return launch_lookup_qm_r<4, PT, 16>(pyr, coords, out, g, B, stream);
-    case 91: return launch_lookup_qm_r<4, PT, 32>(pyr, coords, out, g, B, stream);
+    case 89: return launch_lookup_wide_r<4, PT>(pyr, coords, out, g, B, stream);   // the round-5 product
+    case 90: return launch_lookup_r<4, PT, 16, 1, false, false>(pyr, coords, out, g, B, stream);
+    case 91: return launch_lookup_r<4, PT, 32, 1, false, false>(pyr, coords, out, g, B, stream);
     case 92: return xp_dma_launch(pyr, coords, out, g, B, stream);   // LDS-DMA gathers
+    case 93: return launch_lookup_r<4, PT, 16, 2, false, false>(pyr, coords, out, g, B, stream);  // phase 2 x2
+    case 94: return launch_lookup_r<4, PT, 16, 1, true, true>(pyr, coords, out, g, B, stream);  // buffer loads
     case 0: return xp_launch<0>(pyr, coords, out, g, B, trace, stream);
     case 1: return xp_launch<1>(pyr, coords, out, g, B, trace, stream);
     case 2: return xp_launch<2>(pyr, coords, out, g, B, trace, stream);

@@ -112,7 +112,7 @@ def main():
     for ev in events:
         name = ev.key
         for key in ("corr_lookup_backward", "pyramid_backward", "fmap_grad", "fmap_split",
-                    "chunk_sum", "corr_build", "split_pairs", "corr_lookup_wide", "Cijk", "gemm",
+                    "chunk_sum", "corr_build", "split_pairs", "corr_lookup_wide", "corr_lookup_qm", "Cijk", "gemm",
                     "elementwise", "reduce", "fill"):
             if key in name:
                 t = getattr(ev, "device_time_total", None)

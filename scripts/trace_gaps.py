@@ -34,7 +34,9 @@ def main(path: str, workload: str | None = None) -> None:
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
     rows.sort()
     prod = ("corr_build", "split_pairs", "pack_bf16", "pool", "transpose")
-    is_look = [("corr_lookup_wide_kernel" in n or "alt_corr_mfma_kernel" in n) for _, _, n in rows]
+    # forward lookups: the query-minor kernel (round 6) or the wide one (rounds 1-5)
+    is_look = [("corr_lookup_qm_kernel" in n or "corr_lookup_wide_kernel" in n or
+                "alt_corr_mfma_kernel" in n) for _, _, n in rows]
     # the ordered on-the-fly lookup's three ordering launches belong to its lookup
     is_aux = [("alt_bin_" in n) for _, _, n in rows]
     is_prep = [any(p in n for p in prod) and not is_look[i] and not is_aux[i]

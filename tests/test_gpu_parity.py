@@ -95,6 +95,65 @@ def test_lookup_bitexact_on_reference_pyramid(dx, name):
             f"max diff {np.abs(got[fin] - ref[fin]).max():.3e}"
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_lookup_grid_shapes_agree_on_padded_pyramid(dx, dtype):
+    """Round 6: the query-minor lookup runs one-round grids (256 x 16, plain
+    loads) and multi-round grids (512 x 32, range-checked buffer loads).  A B=6
+    batch at Chairs size (level widths 62, 31, 15, 7: partial 4-cell vectors on
+    every level; N % 32 = 4: a partial query block) runs the multi-round form;
+    each pair alone runs the one-round form.  On a NaN-prefilled paged buffer
+    (any read of page padding would surface as NaN) both give the same bits,
+    with normal, integer, uniform (many taps off the map), far and non-finite
+    coordinates; pair 0 also against the oracle's lookup (bit-exact, f32)."""
+    from dexiraft_amd import _native as nat
+    lib = nat.load()
+    B, D, H, W, L, r = 6, 256, 46, 62, 4, 4
+    f1, f2 = _pair(B=B, D=D, H=H, W=W, seed=411, dist="fnet")
+    cb = dx.CorrBlock(f1, f2)
+    levels = [cb.corr_pyramid[lvl] for lvl in range(L)]        # reference layout, f32
+    pdt = nat.DXR_F32 if dtype == "f32" else nat.DXR_BF16
+    n = lib.dxr_pyramid_numel(B, H, W, L)
+    buf = torch.full((n,), float("nan"), device=DEV,
+                     dtype=torch.float32 if dtype == "f32" else torch.bfloat16)
+    for lvl in range(L):
+        lev = levels[lvl].contiguous()
+        assert lib.dxr_pyramid_pack(lev.data_ptr(), B, H, W, L, lvl, buf.data_ptr(), pdt,
+                                    nat.stream_of(lev)) == 0
+    cs = [dg.coords(500 + i, B, H, W, m, s) for i, (m, s) in
+          enumerate([("normal", 4.0), ("integer", 4.0), ("uniform", 30.0), ("far", 4.0)])]
+    bad = dg.coords(510, B, H, W, "normal", 4.0)
+    bad[0, 0, 3, 5], bad[1, 1, 7, 7], bad[2, 0, 0, 0] = np.nan, np.inf, -np.inf
+    cs.append(bad)
+    K = L * (2 * r + 1) ** 2
+    N = H * W
+    singles = []   # each pair packed alone (B=1 buffers: the one-round grid)
+    for b in range(B):
+        b1 = torch.full((lib.dxr_pyramid_numel(1, H, W, L),), float("nan"), device=DEV,
+                        dtype=buf.dtype)
+        for lvl in range(L):
+            lev = levels[lvl][b * N:(b + 1) * N].contiguous()
+            assert lib.dxr_pyramid_pack(lev.data_ptr(), 1, H, W, L, lvl, b1.data_ptr(), pdt,
+                                        nat.stream_of(lev)) == 0
+        singles.append(b1)
+    for c in cs:
+        ct = _t(c)
+        many = torch.empty((B, K, H, W), device=DEV)
+        assert lib.dxr_corr_lookup(buf.data_ptr(), pdt, B, H, W, L, r, ct.data_ptr(),
+                                   many.data_ptr(), nat.stream_of(ct)) == 0
+        for b in range(B):
+            cb1 = ct[b:b + 1].contiguous()
+            one = torch.empty((1, K, H, W), device=DEV)
+            assert lib.dxr_corr_lookup(singles[b].data_ptr(), pdt, 1, H, W, L, r,
+                                       cb1.data_ptr(), one.data_ptr(), nat.stream_of(ct)) == 0
+            assert torch.equal(torch.nan_to_num(one[0], nan=7.0), torch.nan_to_num(many[b], nan=7.0)), b
+        if dtype == "f32":
+            pyr0 = [levels[lvl][: H * W, 0].cpu().numpy() for lvl in range(L)]
+            ref = oracle.corr_lookup(pyr0, c[:1], r)
+            got = many[:1].cpu().numpy()
+            assert np.array_equal(np.isnan(got), np.isnan(ref))
+            assert np.array_equal(got[~np.isnan(ref)], ref[~np.isnan(ref)])
+
+
 @pytest.mark.parametrize("name", ["fnet", "ragged", "levels2_r1"])
 def test_corr_static_method(dx, name):
     d = load_tiny(name)
