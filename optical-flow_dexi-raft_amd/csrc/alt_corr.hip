@@ -280,7 +280,11 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
   constexpr int KB = CMAX / 8;                              // 8-channel blocks
   constexpr int NPL = H2 ? 2 : 3;                           // query operand planes
   __shared__ __attribute__((aligned(16))) uint4 qplanes[NPL * KB * TQ]; // [plane][kb][q]
-  __shared__ float S[TQ * NCELL];                           // window dot products
+  // window dot products, row pitch SP: odd (round 6), so the 32 lanes of a
+  // half-wave reading S[q * SP + cell] for 32 queries hit 32 banks (pitch 100:
+  // 4 q mod 32, a 4-way conflict on every phase-2 read).  XP bit 4: the old pitch.
+  constexpr int SP = (XP & 16) ? NCELL : NCELL + 1;
+  __shared__ float S[TQ * SP];
   __shared__ int4 qinfo[TQ];                                // {x0, y0, live, -}
   __shared__ int box[4];                                    // bx0, by0, bw, bh
   __shared__ int qlist[TQ];                                 // BIN: query index or -1
@@ -381,7 +385,7 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
       box[3] = any ? ly1 - ly0 : 0;
     }
   }
-  for (int i = tid; i < TQ * NCELL; i += 256) S[i] = 0.f;
+  for (int i = tid; i < TQ * SP; i += 256) S[i] = 0.f;
   // query operand planes: unit (kb, q) -> f1[q][8 kb .. 8 kb + 8), split once
   for (int u = tid; u < nkb * TQ; u += 256) {
     const int kb = u / TQ, qq = u - kb * TQ;
@@ -432,6 +436,7 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
       const int c = min(c0 + (wave * NRB + rb) * 32 + j, ncells - 1);
       const int cy = divbw(c), cx = c - cy * bw;
       src[rb] = f2b + ((long long)(by0 + cy) * lv.W2 + bx0 + cx) * g.C + 8 * kh;
+      if constexpr ((XP & 4) != 0) src[rb] = f2b + (long long)(j & 7) * g.C + 8 * kh;   // ablation: 8 hot cells
     }
     // DMA (f16 pair form): the wave's 32 cell vectors move by LDS-DMA, two k steps (128 B per cell)
     // per batch into a double-buffered wave region: an instruction covers 8 cells x 128 B (8 lanes
@@ -621,9 +626,13 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
               alt_split8h(x, h, l);
             }
             const ah8 th = __builtin_bit_cast(ah8, h), tl = __builtin_bit_cast(ah8, l);
+            if constexpr ((XP & 8) != 0) {   // ablation: no MFMAs (results meaningless)
+              acc[rb][0] += __uint_as_float(h.x ^ l.y) + (float)qh[0] + (float)ql[1];
+            } else {
             acc2[rb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, qh, acc2[rb], 0, 0, 0);
             acc2[rb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ql, acc2[rb], 0, 0, 0);
             acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, qh, acc[rb], 0, 0, 0);
+            }
           }
         } else {
           abf8 qh, qm, ql;
@@ -681,7 +690,7 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
       for (int rb = 0; rb < NRB; ++rb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) bad |= !(__builtin_fabsf(acc[rb][r]) <= 3.40282347e38f);
-      if ((XP & 1) == 0 && __ballot(bad) != 0)
+      if ((XP & 13) == 0 && __ballot(bad) != 0)
         kloop(std::integral_constant<bool, false>{});   // wave-uniform
     } else {
       kloop(std::integral_constant<bool, false>{});
@@ -697,7 +706,7 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
             const int cy = divbw(c), cx = c - cy * bw;
             const int iy = by0 + cy - qi.y, ix = bx0 + cx - qi.x;
             if ((unsigned)iy < (unsigned)RD1 && (unsigned)ix < (unsigned)RD1)
-              S[j * NCELL + iy * RD1 + ix] = acc[rb][r];
+              S[j * SP + iy * RD1 + ix] = acc[rb][r];
           }
         }
     }
@@ -717,7 +726,7 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
     y = cz[(long long)q * g.coord_qstride + g.coord_cstride] * lv.inv;
   }
   const float dx = x - floorf(x), dy = y - floorf(y);
-  const float* s = S + qq * NCELL;
+  const float* s = S + qq * SP;
   float* o = out + (long long)z * g.cout * g.N + (long long)lv.ch_off * g.N + q;
   for (int ox = cls; ox < RD; ox += 256 / TQ) {
 #pragma unroll
@@ -993,6 +1002,11 @@ long long alt_order_bytes(long long H, long long W) {
 // PF: cell loads of the ordered form kept 4 k steps ahead (round 3: with compact boxes the
 // waves wait on L2 latency, 62 % of wave cycles at PF = 1; 1080p 12 lookups 2,033 -> 1,972 us,
 // Sintel 626 -> 612 us in the step).  The tile-order form stays at 1 (its boxes are L1/TA-bound).
+// Occupancy bound of the f16-pair form: 3 workgroups per CU (the 1080p r02
+// A/B); from r = 6 the window buffers and index registers do not fit that bound
+// (hipcc: "desired occupancy 3, final 2"), so those radii ask for 2.
+constexpr int alt_minw(int r) { return r >= 6 ? 2 : 3; }
+
 template <int R, int NRB, int DMA = 0, int PF = 4, int XP = 0>
 int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const AltGeom& g,
                       int levels, int Z, int W1, hipStream_t stream, void* ws = nullptr,
@@ -1040,12 +1054,12 @@ int launch_alt_mfma_r(const float* f1, const float* coords, float* out, const Al
                          dim3(256), 0, stream, f1, coords, out, g, W1, tiles_x,
                          reinterpret_cast<const int4*>(ws), o.list_bytes / 16, XL);
     else
-      hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 3, true, PF, 0, XP>), grid, dim3(256),
+      hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, alt_minw(R), true, PF, 0, XP>), grid, dim3(256),
                          0, stream, f1, coords, out, g, W1, tiles_x,
                          reinterpret_cast<const int4*>(ws), o.list_bytes / 16, XL);
     return dxr::launch_status();
   }
-  hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, 3>), grid, dim3(256), 0, stream, f1,
+  hipLaunchKernelGGL((alt_corr_mfma_kernel<R, NRB, 256, true, alt_minw(R)>), grid, dim3(256), 0, stream, f1,
                      coords, out, g, W1, tiles_x, nullptr, 0, 0);
   return dxr::launch_status();
 }

@@ -276,11 +276,16 @@ __device__ __forceinline__ int group_min(int v) {
   return v;
 }
 
-template <int R, int NT_, int QB_ = 0>
+// XPITCH: pitch of the tap arrays (xs[j * XPITCH + qq]; 0 = QB).  A query's
+// samples are written by consecutive lanes, so at pitch QB every lane of an
+// 8-lane ds_write_b128 group hits one bank group (8-way); QB + 1 spreads them
+// (round 6: the lookup backward and the fused motion kernel).
+template <int R, int NT_, int QB_ = 0, int XPITCH = 0>
 __device__ __forceinline__ void wide_phase0_taps(const Phase0Coords<R, NT_, QB_>& c, const LevelAddr& A,
                                                  int l, int tid, float4* xs, float4* ys, int2* org) {
   using C = WideCfg<R, NT_, QB_>;
   constexpr int RD = C::RD, WD = C::WD, RS = C::RS, QB = C::QB, G = C::G;
+  constexpr int XPB = XPITCH ? XPITCH : QB;
   const int Hl = A.h, Wl = A.w;
 #pragma unroll
   for (int it = 0; it < C::SIT; ++it) {
@@ -310,19 +315,19 @@ __device__ __forceinline__ void wide_phase0_taps(const Phase0Coords<R, NT_, QB_>
       const float fx = __fsub_rn(ux, flx), fy = __fsub_rn(uy, fly);
       const int col = far ? 0 : (int)flx - (mx & ~3);
       const int row = far ? 0 : ((int)fly - my) * RS;
-      xs[j * QB + qq] = make_float4(__int_as_float(col), fx, __fsub_rn(1.f, fx), 0.f);
-      ys[j * QB + qq] = make_float4(__int_as_float(row), fy, __fsub_rn(1.f, fy), 0.f);
+      xs[j * XPB + qq] = make_float4(__int_as_float(col), fx, __fsub_rn(1.f, fx), 0.f);
+      ys[j * XPB + qq] = make_float4(__int_as_float(row), fy, __fsub_rn(1.f, fy), 0.f);
     }
   }
 }
 
-template <int R, int NT_, int QB_ = 0>
+template <int R, int NT_, int QB_ = 0, int XPITCH = 0>
 __device__ __forceinline__ void wide_phase0(const float* __restrict__ coords, const LookupGeom& g,
                                             const LevelAddr& A, int b, int l, int q0, int tid,
                                             float4* xs, float4* ys, int2* org) {
   Phase0Coords<R, NT_, QB_> c;
   wide_phase0_load<R, NT_, QB_>(coords, g, b, q0, tid, c);
-  wide_phase0_taps<R, NT_, QB_>(c, A, l, tid, xs, ys, org);
+  wide_phase0_taps<R, NT_, QB_, XPITCH>(c, A, l, tid, xs, ys, org);
 }
 
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
@@ -709,8 +714,9 @@ __global__ __launch_bounds__(512, bw_min_waves(R)) void corr_lookup_backward_ker
                                                                    float* __restrict__ bound_slots) {
   using C = WideCfg<R, 512>;
   constexpr int RD = C::RD, WD = C::WD, RS = C::RS, K = C::K, QB = C::QB, NT = C::NT;
-  __shared__ float4 xs[RD * QB];
-  __shared__ float4 ys[RD * QB];
+  constexpr int XPB = QB + 1;              // tap-array pitch (wide_phase0_taps)
+  __shared__ float4 xs[RD * XPB];
+  __shared__ float4 ys[RD * XPB];
   __shared__ int2 org[QB];
   __shared__ float G[K * QB];              // [k][qq]
   __shared__ float T[QB * WD * RD];        // [qq][cy][ox]
@@ -750,7 +756,7 @@ __global__ __launch_bounds__(512, bw_min_waves(R)) void corr_lookup_backward_ker
   // it would hold ~100 VGPRs across passes and halve the resident workgroups)
   int tid = threadIdx.x;
   asm volatile("" : "+v"(tid));
-  wide_phase0_taps<R, 512>(cc, A, l, tid, xs, ys, org);
+  wide_phase0_taps<R, 512, 0, XPB>(cc, A, l, tid, xs, ys, org);
 #pragma unroll
   for (int it = 0; it < GIT; ++it) {
     const int i = tid + it * NT;
@@ -787,7 +793,7 @@ __global__ __launch_bounds__(512, bw_min_waves(R)) void corr_lookup_backward_ker
     for (int d = 2; d >= 0; --d) {
       const int oy = cy - d;
       if (oy < 0 || oy >= RD) continue;
-      const float4 yd = ys[oy * QB + qq];
+      const float4 yd = ys[oy * XPB + qq];
       const int row = __float_as_int(yd.x) / RS;
       if (row == cy || row + 1 == cy)
         acc = __builtin_fmaf(G[(ox * RD + oy) * QB + qq], row == cy ? yd.z : yd.y, acc);
@@ -797,7 +803,7 @@ __global__ __launch_bounds__(512, bw_min_waves(R)) void corr_lookup_backward_ker
   // the x factors query-major for the column pass (lanes there walk a window row)
   for (int i = tid; i < RD * QB; i += NT) {
     const int ox = i / QB, qq = i - ox * QB;
-    xq[qq * RD + ox] = xs[i];
+    xq[qq * RD + ox] = xs[ox * XPB + qq];
   }
   __syncthreads();
 
@@ -1132,7 +1138,8 @@ __global__ __launch_bounds__(NT, 4) void corr_lookup_conv1x1_h2_kernel(
   constexpr int RD = C::RD, RS = C::RS, K = C::K, QB = C::QB, KB = M::KB;
   constexpr int NW = NT / 64, KSPLIT = NW >= 16 ? 2 : 1;
   static_assert(NW == 8 || NW == 16, "8 output blocks of 32 per pass");
-  constexpr int CELLS_B = QB * C::QS * 4, XS_B = RD * QB * 16, ORG_B = QB * 8;
+  constexpr int XPB = QB + 1;   // tap-array pitch (wide_phase0_taps)
+  constexpr int CELLS_B = QB * C::QS * 4, XS_B = RD * XPB * 16, ORG_B = QB * 8;
   constexpr int STAGE_B = CELLS_B + 2 * XS_B + ORG_B, RED_B = KSPLIT > 1 ? 8 * 16 * 64 * 4 : 0;
   __shared__ __attribute__((aligned(16))) char stage[STAGE_B > RED_B ? STAGE_B : RED_B];
   __shared__ __attribute__((aligned(16))) float spl[KB * QB * 8];   // samples [k/8][q][8], f32
@@ -1164,7 +1171,7 @@ __global__ __launch_bounds__(NT, 4) void corr_lookup_conv1x1_h2_kernel(
   // ---- per level: phase 0, gather, samples -> spl
   for (int l = 0; l < g.levels; ++l) {
     const LevelAddr& A = g.lv[l];
-    wide_phase0<R, NT>(coords, g, A, b, l, q0, tid, xs, ys, org);
+    wide_phase0<R, NT, 0, XPB>(coords, g, A, b, l, q0, tid, xs, ys, org);
     __syncthreads();
     {
       float4 win[C::VIT];
@@ -1188,7 +1195,7 @@ __global__ __launch_bounds__(NT, 4) void corr_lookup_conv1x1_h2_kernel(
       const float* cq = cells + qq * C::QS;
       for (int k = cls; k < K; k += C::NCLS) {
         const int ox = k / RD, oy = k - ox * RD;
-        const float4 xd = xs[ox * QB + qq], yd = ys[oy * QB + qq];
+        const float4 xd = xs[ox * XPB + qq], yd = ys[oy * XPB + qq];
         const float* p = cq + __float_as_int(yd.x) + __float_as_int(xd.x);
         const float v00 = p[0], v01 = p[1], v10 = p[RS], v11 = p[RS + 1];
         const float nw = __fmul_rn(yd.z, xd.z), ne = __fmul_rn(yd.z, xd.y);

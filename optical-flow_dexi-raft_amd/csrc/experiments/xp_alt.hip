@@ -55,6 +55,18 @@ extern "C" int dxr_xp_alt_lookup(const float* fmap1, const float* const* fmap2_l
   if (variant == 8)   // variant 3 without the cell split (timing ablation)
     return launch_alt_mfma_r<4, 1, 0, 4, 1>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
                                                 stream, ws);
+  if (variant == 12)  // variant 3 with every lane loading one of 8 hot cells (ablation: the gather's cost)
+    return launch_alt_mfma_r<4, 1, 0, 4, 4>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+                                                stream, ws);
+  if (variant == 13)  // variant 3 without MFMAs (ablation)
+    return launch_alt_mfma_r<4, 1, 0, 4, 8>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+                                                stream, ws);
+  if (variant == 14)  // neither cell gathers nor MFMAs nor stores (ablation: the skeleton)
+    return launch_alt_mfma_r<4, 1, 0, 4, 14>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+                                                 stream, ws);
+  if (variant == 15)  // variant 3 with the round-5 S pitch (100: 4-way phase-2 conflicts)
+    return launch_alt_mfma_r<4, 1, 0, 4, 16>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
+                                                 stream, ws);
   if (variant == 6 || variant == 7)
     return launch_alt_mfma_r<4, 1, 0, 4>(fmap1, coords, out, g, num_levels, (int)B, (int)W,
                                              stream, ws, variant - 6);
