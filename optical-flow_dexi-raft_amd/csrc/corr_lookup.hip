@@ -595,7 +595,10 @@ __device__ __forceinline__ void qm_gather(const PT* __restrict__ base, int qb0, 
   }
 }
 
-template <int R, typename PT, int NT_ = 512, int QB_ = 32, int UNR = 1, bool BUF = false>
+// XA: timing ablations for the experiments target (0 in the product): bit 0 skips
+// the window gathers, bit 1 the output stores (only values equal to 12345 are
+// stored), bit 2 returns after phase 0.
+template <int R, typename PT, int NT_ = 512, int QB_ = 32, int UNR = 1, bool BUF = false, int XA = 0>
 __global__ __launch_bounds__(NT_) void corr_lookup_qm_kernel(
     const PT* __restrict__ pyr, const float* __restrict__ coords, float* __restrict__ out,
     LookupGeom g) {
@@ -622,7 +625,11 @@ __global__ __launch_bounds__(NT_) void corr_lookup_qm_kernel(
     qm_phase0_taps<R, NT_, QB_>(c, A, l, tid, xs, ys, org);
   }
   __syncthreads();
-  {
+  if constexpr ((XA & 4) != 0) {
+    if (xs[tid % (RD * Q::XP)].y == 1234.5f) out[tid] = 0.f;
+    return;
+  }
+  if constexpr ((XA & 1) == 0) {
     const PT* base = pyr + A.off + ((long long)b * A.qt + (q0 >> A.lqb)) * A.qstride;
     const int qb0 = q0 & ((1 << A.lqb) - 1);
     if (A.lth == 30 || A.tw == 1)
@@ -652,8 +659,10 @@ __global__ __launch_bounds__(NT_) void corr_lookup_qm_kernel(
     r = __builtin_fmaf(ne, v01, r);
     r = __builtin_fmaf(sw, v10, r);
     r = __builtin_fmaf(se, v11, r);
-    if (g.out_nt) __builtin_nontemporal_store(r, op);
-    else __hip_atomic_store(op, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((XA & 2) == 0 || r == 12345.f) {
+      if (g.out_nt) __builtin_nontemporal_store(r, op);
+      else __hip_atomic_store(op, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     op += ostep;
   }
 }
@@ -986,7 +995,8 @@ int launch_lookup_wide_r(const PT* pyr, const float* coords, float* out, const L
 // / 97.4, Sintel B=2 348.2 -> 355.6 / 349.7.  `ONE_QB` / `UNR` / `MULTI_BUF`:
 // experiment knobs (queries per one-round workgroup, phase-2 unroll, buffer loads
 // on multi-round grids); `ONE_BUF`: buffer loads on one-round grids too.
-template <int R, typename PT, int ONE_QB = 16, int UNR = 1, bool ONE_BUF = false, bool MULTI_BUF = true>
+template <int R, typename PT, int ONE_QB = 16, int UNR = 1, bool ONE_BUF = false, bool MULTI_BUF = true,
+          int XA = 0, int MULTI_NT = 512, int MULTI_QB = 0>
 int launch_lookup_r(const PT* pyr, const float* coords, float* out, const LookupGeom& g0, int B,
                        hipStream_t stream) {
   using W = WideCfg<R>;
@@ -997,14 +1007,15 @@ int launch_lookup_r(const PT* pyr, const float* coords, float* out, const Lookup
   if (R <= 4 && wg32 <= 1024 && !big_misaligned) {
     g.out_nt = g.N % 32 == 0 ? 1 : 0;
     const dim3 grid((unsigned)((g.N + ONE_QB - 1) / ONE_QB), (unsigned)g.levels, (unsigned)B);
-    hipLaunchKernelGGL((corr_lookup_qm_kernel<R, PT, 256, ONE_QB, UNR, ONE_BUF>), grid, dim3(256), 0, stream, pyr,
+    hipLaunchKernelGGL((corr_lookup_qm_kernel<R, PT, 256, ONE_QB, UNR, ONE_BUF, XA>), grid, dim3(256), 0, stream, pyr,
                        coords, out, g);
     return dxr::launch_status();
   }
   g.out_nt = 1;
-  const dim3 grid((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)g.levels, (unsigned)B);
-  hipLaunchKernelGGL((corr_lookup_qm_kernel<R, PT, 512, W::QB, UNR, MULTI_BUF>), grid, dim3(512), 0, stream, pyr,
-                     coords, out, g);
+  constexpr int MQB = MULTI_QB ? MULTI_QB : W::QB;
+  const dim3 grid((unsigned)((g.N + MQB - 1) / MQB), (unsigned)g.levels, (unsigned)B);
+  hipLaunchKernelGGL((corr_lookup_qm_kernel<R, PT, MULTI_NT, MQB, UNR, MULTI_BUF, XA>), grid,
+                     dim3(MULTI_NT), 0, stream, pyr, coords, out, g);
   return dxr::launch_status();
 }
 

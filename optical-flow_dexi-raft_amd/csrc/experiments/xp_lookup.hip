@@ -350,6 +350,13 @@ int xp_dispatch(int xp, const PT* pyr, const float* coords, float* out, const Lo
     case 92: return xp_dma_launch(pyr, coords, out, g, B, stream);   // LDS-DMA gathers
     case 93: return launch_lookup_r<4, PT, 16, 2, false, false>(pyr, coords, out, g, B, stream);  // phase 2 x2
     case 94: return launch_lookup_r<4, PT, 16, 1, true, true>(pyr, coords, out, g, B, stream);  // buffer loads
+    // multi-round grids at 256 x 32 / 256 x 16 (the product: 512 x 32)
+    case 95: return launch_lookup_r<4, PT, 16, 1, false, true, 0, 256, 32>(pyr, coords, out, g, B, stream);
+    case 96: return launch_lookup_r<4, PT, 16, 1, false, true, 0, 256, 16>(pyr, coords, out, g, B, stream);
+    // product shapes, timing ablations: no gathers / no output stores / phase 0 only
+    case 97: return launch_lookup_r<4, PT, 16, 1, false, true, 1>(pyr, coords, out, g, B, stream);
+    case 98: return launch_lookup_r<4, PT, 16, 1, false, true, 2>(pyr, coords, out, g, B, stream);
+    case 99: return launch_lookup_r<4, PT, 16, 1, false, true, 4>(pyr, coords, out, g, B, stream);
     case 0: return xp_launch<0>(pyr, coords, out, g, B, trace, stream);
     case 1: return xp_launch<1>(pyr, coords, out, g, B, trace, stream);
     case 2: return xp_launch<2>(pyr, coords, out, g, B, trace, stream);
