@@ -37,7 +37,7 @@ boundaries); what the timed step spends beyond 12 lookups + one build (the
 graph launch, the build -> lookup boundary) is reported as step_boundary_us.
 ``--mode eager`` times plain Python calls instead.
 The line also carries ``box`` (host, GPU UUID) and ``calibration`` (a bf16 GEMM
-and an HBM copy timed in this process before the timed region: boxes differ by
+and an HBM copy timed in this process before the clock warm-up: boxes differ by
 up to ~18 % in the build kernel, round 5), and ``value_one_step_per_graph`` (the
 same K steps replayed one graph per step, rounds 1-4's protocol).  Kernel-trace
 step timelines are not in the line: they come from another run.
@@ -492,6 +492,11 @@ def main():
             run_step = step
             timing = "hip events around eager launches"
         torch.cuda.synchronize()
+        # box calibration first, so that its GEMM burst is followed by the whole
+        # clock warm-up on the step itself (placed after the warm-up it left the
+        # driver's 5-replay timed region ~5 % below the same steps re-timed later,
+        # round 6: 5,300 vs 5,585 pairs/s on one box)
+        calib = calibrate(dev, stream) if not args.no_calibration else None
         # clock warm-up: replay the full step (same work, same outputs) until the
         # chip has been under load for --clock-warmup-s, then the W warmup steps
         t_w = time.perf_counter()
@@ -501,7 +506,6 @@ def main():
                 run_step()
             n_clock += 20
             torch.cuda.synchronize()
-        calib = calibrate(dev, stream) if not args.no_calibration else None
         for _ in range(-(-args.warmup // G)):
             run_step()
         torch.cuda.synchronize()
