@@ -409,6 +409,9 @@ def main():
                          "every step on the rank's one pair set, as rounds 1-4; DESIGN §6)")
     ap.add_argument("--block", default="corr", choices=["corr", "alt"],
                     help="corr: CorrBlock (full pyramid); alt: AlternateCorrBlock (on the fly, C5)")
+    ap.add_argument("--alt-coarse-cells", type=int, default=None,
+                    help="--block alt: AlternateCorrBlock.COARSE_LEVEL_MAX_CELLS (levels of at most "
+                         "this many cells computed once per block as whole volumes; 0: none)")
     ap.add_argument("--layout", default="nchw", choices=["nchw", "nhwc"],
                     help="fmap memory format: nchw (the reference's) or nhwc (channels-last "
                          "encoders, SURVEY §8(f) row 4)")
@@ -458,6 +461,8 @@ def main():
 
     state = {}
     block_cls = dexiraft_amd.CorrBlock if args.block == "corr" else dexiraft_amd.AlternateCorrBlock
+    if args.block == "alt" and args.alt_coarse_cells is not None:
+        block_cls.COARSE_LEVEL_MAX_CELLS = args.alt_coarse_cells
 
     def build(i=0):
         # the previous step's block and outputs go first (one pyramid alive at a time)

@@ -77,7 +77,7 @@ extern "C" {
 /* HIP's own definition; repeating an identical typedef is legal in C11/C++. */
 typedef struct ihipStream_t* hipStream_t;
 
-#define DXR_ABI_VERSION 8
+#define DXR_ABI_VERSION 9
 
 enum dxr_status {
   DXR_OK = 0,
@@ -456,6 +456,53 @@ int dxr_alt_corr_lookup_ws(const float* fmap1, const float* const* fmap2_levels,
                            int num_levels, int radius, float divisor,
                            void* workspace, int64_t workspace_bytes,
                            hipStream_t stream);
+
+/*
+ * dxr_alt_corr_lookup_ws for levels [0, n_levels) only of a num_levels-level
+ * output (channels of the other levels untouched): the alternate block's
+ * on-the-fly part when its coarse levels come from dxr_alt_volume_lookup.
+ * Workspace: dxr_alt_workspace_bytes(B, H, W, n_levels).  Replaces
+ * core/corr.py:74-91 for those levels.  ABI 9.
+ */
+int dxr_alt_corr_lookup_levels_ws(const float* fmap1, const float* const* fmap2_levels,
+                                  const float* coords, float* out,
+                                  int64_t B, int64_t H, int64_t W, int64_t C,
+                                  int num_levels, int n_levels, int radius, float divisor,
+                                  void* workspace, int64_t workspace_bytes,
+                                  hipStream_t stream);
+
+/*
+ * Coarse-level volumes of the alternate block (round 6).  An on-the-fly
+ * lookup recomputes each level's window dot products on every call; for a
+ * coarse level the whole volume (every fmap1 pixel against every cell of the
+ * pooled fmap2 level) costs less than one lookup, once per block.
+ *   dxr_alt_volume_numel    floats of the volumes of levels
+ *                           [first_level, num_levels) (-1: bad geometry);
+ *   dxr_alt_coarse_volumes  computes them: raw dot products <fmap1[q],
+ *                           fmap2_levels[l][cell]> (not divided), the same
+ *                           f16-pair MFMA products as dxr_alt_corr_lookup's,
+ *                           stored in the paged layout of those pyramid levels
+ *                           (the tail of a num_levels-level pyramid buffer);
+ *                           fmap1 / fmap2_levels as dxr_alt_corr_lookup
+ *                           (NHWC, 16-byte aligned), C % 16 == 0, C <= 256;
+ *   dxr_alt_volume_lookup   reads the windows of levels [first_level,
+ *                           num_levels) from them with correlation_kernel.cu's
+ *                           arithmetic (origin floor(c / 2^l) - r, bilinear
+ *                           weights of the fraction, :92-114's order, divided
+ *                           by divisor) into those levels' channels of `out`
+ *                           ([B, num_levels*(2r+1)^2, H, W]); r <= 8.
+ * With finite operands inside the f16 pair's range the outputs are
+ * dxr_alt_corr_lookup's bit for bit.  Replaces core/corr.py:74-91 (levels
+ * >= first_level) with the reference's alt_cuda_corr semantics.  ABI 9.
+ */
+int64_t dxr_alt_volume_numel(int64_t B, int64_t H, int64_t W, int num_levels, int first_level);
+int dxr_alt_coarse_volumes(const float* fmap1, const float* const* fmap2_levels,
+                           int64_t B, int64_t H, int64_t W, int64_t C,
+                           int num_levels, int first_level, float* volumes,
+                           hipStream_t stream);
+int dxr_alt_volume_lookup(const float* volumes, const float* coords, float* out,
+                          int64_t B, int64_t H, int64_t W, int num_levels, int first_level,
+                          int radius, float divisor, hipStream_t stream);
 
 #ifdef __cplusplus
 }

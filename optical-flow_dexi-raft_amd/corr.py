@@ -643,12 +643,30 @@ class CorrBlock:
 class AlternateCorrBlock:
     """On-the-fly correlation lookup (reference core/corr.py:63-91 + alt_cuda_corr).
 
-    Memory is O(H*W*D) instead of O((H*W)^2): only pooled fmaps are kept and each
-    ``__call__`` computes the (2r+2)^2 window dot products of every level in one
-    launch (``dxr_alt_corr_lookup``), already divided by sqrt(D).  As in the
+    Memory is O(H*W*D) at the fine levels instead of O((H*W)^2): only pooled fmaps
+    are kept and each ``__call__`` computes the (2r+2)^2 window dot products of
+    those levels in one launch (``dxr_alt_corr_lookup_levels_ws``), divided by
+    sqrt(D).  Round 6: on large maps (``COARSE_MIN_QUERIES``) the coarse levels —
+    from the first level of at most ``COARSE_LEVEL_MAX_CELLS`` cells on, within
+    ``COARSE_VOLUME_MAX_BYTES`` — are computed once per block as whole volumes of the
+    same dot products (``dxr_alt_coarse_volumes``) and read by
+    ``dxr_alt_volume_lookup``: an on-the-fly lookup pays each level's box GEMMs
+    again on every call (~15-26 us per coarse level at 1080p), while the coarsest
+    level's whole volume costs less than one call (1080p: level 3).
+    With finite operands in the f16 pair's range the outputs are the all-on-the-
+    fly form's bit for bit (``coarse_first_level`` None: no volumes).  As in the
     reference, the constructor pools ``num_levels`` times, so fmaps smaller than
     2^num_levels in either dimension raise (core/corr.py:69-71).
     """
+
+    # Which levels are precomputed (round 6, bench.py --block alt, profiles/r06/experiments/
+    # r6l_*): at 1080p (32,640 queries) level 3 (510 cells) as a volume takes the lookup from
+    # 163.8 to 148.8 us for 89 us per block (+5.1 % pairs/s); level 2 as well (2,040 cells)
+    # gets it to 126.9 us but costs 426 us per block (+0.9 %); at Sintel (7,040 queries) the
+    # on-the-fly coarse levels cost ~2-3 us per lookup and volumes lose 7 %.
+    COARSE_LEVEL_MAX_CELLS = 512           # a level of at most this many cells is precomputed
+    COARSE_MIN_QUERIES = 16384             # on maps of at least this many query pixels
+    COARSE_VOLUME_MAX_BYTES = 1 << 30      # and all precomputed volumes fit in this
 
     def __init__(self, fmap1, fmap2, num_levels=4, radius=4):
         self.num_levels = num_levels
@@ -682,6 +700,31 @@ class AlternateCorrBlock:
         for _ in range(1, num_levels):
             self._f2_nhwc.append(_pool_nhwc(self._f2_nhwc[-1]))
         self._f2_ptrs = (ctypes.c_void_p * num_levels)(*[t.data_ptr() for t in self._f2_nhwc])
+        self.coarse_first_level = None
+        self._volumes = None
+        if D % 16 == 0 and D <= 256 and radius <= 6 and B > 0 and H * W >= self.COARSE_MIN_QUERIES:
+            self._make_volumes(B, D, H, W)
+
+    def _make_volumes(self, B, D, H, W):
+        lib = nat.load()
+        sizes = _level_sizes(H, W, self.num_levels)
+        first = next((lvl for lvl in range(1, self.num_levels)
+                      if sizes[lvl][0] * sizes[lvl][1] <= self.COARSE_LEVEL_MAX_CELLS), None)
+        while first is not None and first < self.num_levels:
+            n = lib.dxr_alt_volume_numel(B, H, W, self.num_levels, first)
+            if 0 < n * 4 <= self.COARSE_VOLUME_MAX_BYTES:
+                break
+            first += 1
+        if first is None or first >= self.num_levels:
+            return
+        vol = torch.empty((n,), dtype=torch.float32, device=self._device)
+        with _Launch(self._device):
+            st = lib.dxr_alt_coarse_volumes(self._f1_nhwc.data_ptr(), self._f2_ptrs, B, H, W, D,
+                                            self.num_levels, first, vol.data_ptr(),
+                                            nat.stream_of(vol))
+        nat.check(st, "AlternateCorrBlock coarse volumes (dxr_alt_coarse_volumes)")
+        self.coarse_first_level = first
+        self._volumes = vol
 
     @property
     def pyramid(self):
@@ -716,14 +759,31 @@ class AlternateCorrBlock:
         out = torch.empty((B, self.num_levels * rd * rd, H, W), dtype=torch.float32,
                           device=self._device)
         lib = nat.load()
-        # query-order workspace (dxr_alt_corr_lookup_ws), from torch's caching
-        # allocator: freed once the launches that use it have run
-        nbytes = lib.dxr_alt_workspace_bytes(B, H, W, self.num_levels)
-        ws = torch.empty(max(nbytes, 0), dtype=torch.uint8, device=self._device)
+        first = self.coarse_first_level
+        if first is None:
+            # query-order workspace (dxr_alt_corr_lookup_ws), from torch's caching
+            # allocator: freed once the launches that use it have run
+            nbytes = lib.dxr_alt_workspace_bytes(B, H, W, self.num_levels)
+            ws = torch.empty(max(nbytes, 0), dtype=torch.uint8, device=self._device)
+            with _Launch(self._device):
+                st = lib.dxr_alt_corr_lookup_ws(self._f1_nhwc.data_ptr(), self._f2_ptrs,
+                                                c.data_ptr(), out.data_ptr(), B, H, W, D,
+                                                self.num_levels, self.radius, _sqrt_dim(D),
+                                                nat.ptr(ws), max(nbytes, 0), nat.stream_of(c))
+            nat.check(st, "AlternateCorrBlock lookup (dxr_alt_corr_lookup_ws)")
+            return out
         with _Launch(self._device):
-            st = lib.dxr_alt_corr_lookup_ws(self._f1_nhwc.data_ptr(), self._f2_ptrs, c.data_ptr(),
-                                            out.data_ptr(), B, H, W, D, self.num_levels,
-                                            self.radius, _sqrt_dim(D), nat.ptr(ws),
-                                            max(nbytes, 0), nat.stream_of(c))
-        nat.check(st, "AlternateCorrBlock lookup (dxr_alt_corr_lookup_ws)")
+            if first > 0:   # the fine levels on the fly
+                nbytes = lib.dxr_alt_workspace_bytes(B, H, W, first)
+                ws = torch.empty(max(nbytes, 0), dtype=torch.uint8, device=self._device)
+                st = lib.dxr_alt_corr_lookup_levels_ws(self._f1_nhwc.data_ptr(), self._f2_ptrs,
+                                                       c.data_ptr(), out.data_ptr(), B, H, W, D,
+                                                       self.num_levels, first, self.radius,
+                                                       _sqrt_dim(D), nat.ptr(ws), max(nbytes, 0),
+                                                       nat.stream_of(c))
+                nat.check(st, "AlternateCorrBlock lookup (dxr_alt_corr_lookup_levels_ws)")
+            st = lib.dxr_alt_volume_lookup(self._volumes.data_ptr(), c.data_ptr(), out.data_ptr(),
+                                           B, H, W, self.num_levels, first, self.radius,
+                                           _sqrt_dim(D), nat.stream_of(c))
+        nat.check(st, "AlternateCorrBlock lookup (dxr_alt_volume_lookup)")
         return out

@@ -49,6 +49,7 @@ struct AltGeom {
   long long f1_bstride;   // H1 * W1 * C
   long long coord_zstride, coord_cstride, coord_qstride;
   AltLevel lv[8];
+  dxr::LevelLayout vlay{};  // FULL: the volume's paged level layout (offset from the volume buffer)
 };
 
 template <int R>
@@ -267,8 +268,17 @@ __device__ __forceinline__ void alt_split8h(const float (&x)[8], uint4& h, uint4
 // fallback) — a timing ablation of the split's VALU work, results meaningless;
 // bit 1 stores only outputs that are exactly 12345.0 (none: an ablation of the
 // output stores).
+// FULL (round 6, the coarse-level volumes of dxr_alt_coarse_volumes): the box is
+// the whole level and every (cell, query) sum is stored, raw (not divided), into
+// `out` in the pyramid's paged layout of that level (g.vlay, dxr_common.h
+// cell_index): the same products in the same order as the windowed form, so a
+// lookup that reads its windows from the volume reproduces the on-the-fly
+// outputs bit for bit (finite operands inside the f16 pair's range; a chunk with
+// a non-finite sum is recomputed on the bf16 split in either form, and chunks
+// group different cells in the two forms).  Tile order only (BIN = false);
+// coordinates are not read.
 template <int R, int NRB, int CMAX, bool H2 = false, int MINW = 2, bool BIN = false, int PF = 1,
-          int DMA = 0, int XP = 0>
+          int DMA = 0, int XP = 0, bool FULL = false>
 __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* __restrict__ f1,
                                                                const float* __restrict__ coords,
                                                                float* __restrict__ out,
@@ -346,7 +356,16 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
   }
 
   // ---- query coordinates, window origins, the windows' union box
-  if (tid < TQ) {
+  if constexpr (FULL) {
+    static_assert(!BIN, "the full-level box runs in tile order");
+    if (tid < TQ) qinfo[tid] = make_int4(0, 0, 0, 0);
+    if (tid == 0) {
+      box[0] = 0;
+      box[1] = 0;
+      box[2] = lv.W2;
+      box[3] = lv.H2;
+    }
+  } else if (tid < TQ) {
     const int qsel = query_of(tid);
     int x0 = 0, y0 = 0, live = 0;
     if (qsel >= 0) {
@@ -385,7 +404,8 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
       box[3] = any ? ly1 - ly0 : 0;
     }
   }
-  for (int i = tid; i < TQ * SP; i += 256) S[i] = 0.f;
+  if constexpr (!FULL)
+    for (int i = tid; i < TQ * SP; i += 256) S[i] = 0.f;
   // query operand planes: unit (kb, q) -> f1[q][8 kb .. 8 kb + 8), split once
   for (int u = tid; u < nkb * TQ; u += 256) {
     const int kb = u / TQ, qq = u - kb * TQ;
@@ -695,6 +715,24 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
     } else {
       kloop(std::integral_constant<bool, false>{});
     }
+    if constexpr (FULL) {
+      // every sum of query j to its row of the volume: D rows (r & 3) + 8 (r >> 2)
+      // + 4 kh, i.e. four runs of four consecutive cells per lane
+      const int qv = query_of(j);
+      if (qv >= 0) {
+#pragma unroll
+        for (int rb = 0; rb < NRB; ++rb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int c = c0 + (wave * NRB + rb) * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+            if (c < ncells) {
+              const int cy = divbw(c), cx = c - cy * bw;
+              out[dxr::cell_index(g.vlay, bf, qv, cy, cx)] = acc[rb][r];
+            }
+          }
+      }
+      continue;
+    }
     // keep the entries inside query j's window: D row = (r & 3) + 8 (r >> 2) + 4 kh
     if (qi.z) {
 #pragma unroll
@@ -711,6 +749,7 @@ __global__ __launch_bounds__(256, MINW) void alt_corr_mfma_kernel(const float* _
         }
     }
   }
+  if constexpr (FULL) return;
   __syncthreads();
 
   // ---- bilinear combination, as the per-query form (reference order)
@@ -1432,11 +1471,16 @@ extern "C" int dxr_avg_pool2x2_nhwc(const float* in, float* out, int64_t B, int6
 }
 
 namespace {
+// n_levels < 0: every level; else only levels [0, n_levels) of a num_levels-level
+// output (the rest come from dxr_alt_volume_lookup).
 int alt_lookup(const float* fmap1, const float* const* fmap2_levels, const float* coords, float* out,
                int64_t B, int64_t H, int64_t W, int64_t C, int num_levels, int radius,
-               float divisor, void* workspace, int64_t workspace_bytes, hipStream_t stream) {
+               float divisor, void* workspace, int64_t workspace_bytes, hipStream_t stream,
+               int n_levels = -1) {
   dxr::Levels L;
   if (!dxr::make_levels(B, H, W, num_levels, &L)) return DXR_EINVAL;
+  if (n_levels > num_levels || n_levels == 0) return DXR_EINVAL;
+  const int nl = n_levels < 0 ? num_levels : n_levels;
   if (C < 1 || radius < 0 || !(divisor == divisor) || divisor == 0.f) return DXR_EINVAL;
   if (radius > 6) return DXR_EUNSUPPORTED;
   if (H * W > (1LL << 30) || B > 65535 || C > (1 << 20)) return DXR_EINVAL;
@@ -1455,18 +1499,72 @@ int alt_lookup(const float* fmap1, const float* const* fmap2_levels, const float
   g.coord_cstride = H * W;
   g.coord_qstride = 1;
   bool vec = (C % 4 == 0) && aligned16(fmap1);
-  for (int l = 0; l < num_levels; ++l) {
+  for (int l = 0; l < nl; ++l) {
     if (!fmap2_levels[l]) return DXR_EINVAL;
     vec = vec && aligned16(fmap2_levels[l]);
     g.lv[l] = AltLevel{fmap2_levels[l], L.h[l], L.w[l], 1.f / (float)(1 << l), l * rd * rd};
   }
   void* ord = nullptr;
   if (workspace != nullptr && aligned16(workspace) &&
-      workspace_bytes >= (long long)B * num_levels * alt_order_bytes(H, W))
+      workspace_bytes >= (long long)B * nl * alt_order_bytes(H, W))
     ord = workspace;
-  return launch_alt(fmap1, coords, out, g, num_levels, (int)B, radius, vec, stream, (int)W, ord);
+  return launch_alt(fmap1, coords, out, g, nl, (int)B, radius, vec, stream, (int)W, ord);
 }
 }  // namespace
+
+// ---------------------------------------------------------------------------
+// Coarse-level volumes (round 6).  An on-the-fly lookup pays each level's box
+// GEMMs again on every call, ~26 us per level and 1080p lookup whatever the
+// level's size; a coarse level's whole correlation volume costs less than one
+// such lookup to compute once per block.  dxr_alt_coarse_volumes computes levels
+// [first_level, num_levels) of fmap1 against the pooled fmap2 levels (the
+// alternate block's own operands) with the FULL form of the box kernel and
+// stores them, raw, in the paged layout of those pyramid levels, one buffer of
+// dxr_alt_volume_numel floats; dxr_alt_volume_lookup (csrc/corr_lookup.hip)
+// reads its windows from there with the alternate block's arithmetic.
+extern "C" int64_t dxr_alt_volume_numel(int64_t B, int64_t H, int64_t W, int num_levels,
+                                        int first_level) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, num_levels, &L) || first_level < 0 || first_level >= num_levels)
+    return -1;
+  return L.numel - L.off[first_level];
+}
+
+extern "C" int dxr_alt_coarse_volumes(const float* fmap1, const float* const* fmap2_levels,
+                                      int64_t B, int64_t H, int64_t W, int64_t C, int num_levels,
+                                      int first_level, float* volumes, hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, num_levels, &L) || first_level < 0 || first_level >= num_levels)
+    return DXR_EINVAL;
+  if (C < 1 || B > 65535 || H * W > (1LL << 30)) return DXR_EINVAL;
+  if (C % 16 != 0 || C > 256) return DXR_EUNSUPPORTED;
+  if (B == 0) return DXR_OK;
+  if (!fmap1 || !fmap2_levels || !volumes || !aligned16(fmap1)) return DXR_EINVAL;
+  AltGeom g;
+  g.N = (int)(H * W);
+  g.C = (int)C;
+  g.Nc = 1;
+  g.cout = 0;
+  g.divisor = 1.f;
+  g.f1_bstride = H * W * C;
+  g.coord_zstride = g.coord_cstride = 0;
+  g.coord_qstride = 0;
+  const int tiles_x = (int)((W + TQX - 1) / TQX);
+  const int ntiles = tiles_x * (int)((H + TQY - 1) / TQY);
+  for (int l = first_level; l < num_levels; ++l) {
+    if (!fmap2_levels[l] || !aligned16(fmap2_levels[l])) return DXR_EINVAL;
+    g.lv[0] = AltLevel{fmap2_levels[l], L.h[l], L.w[l], 1.f, 0};
+    g.vlay = L.lay[l];
+    g.vlay.off -= L.off[first_level];
+    hipLaunchKernelGGL((alt_corr_mfma_kernel<0, 1, 256, true, 3, false, 4, 0, 0, true>),
+                       dim3((unsigned)ntiles, 1u, (unsigned)B), dim3(256), 0, stream, fmap1,
+                       (const float*)nullptr, volumes, g, (int)W, tiles_x, (const int4*)nullptr,
+                       0LL, 0);
+    const int st = dxr::launch_status();
+    if (st != DXR_OK) return st;
+  }
+  return DXR_OK;
+}
 
 extern "C" int dxr_alt_corr_lookup(const float* fmap1, const float* const* fmap2_levels,
                                    const float* coords, float* out, int64_t B, int64_t H,
@@ -1489,5 +1587,15 @@ extern "C" int dxr_alt_corr_lookup_ws(const float* fmap1, const float* const* fm
                                       hipStream_t stream) {
   return alt_lookup(fmap1, fmap2_levels, coords, out, B, H, W, C, num_levels, radius, divisor,
                     workspace, workspace_bytes, stream);
+}
+
+extern "C" int dxr_alt_corr_lookup_levels_ws(const float* fmap1, const float* const* fmap2_levels,
+                                             const float* coords, float* out, int64_t B, int64_t H,
+                                             int64_t W, int64_t C, int num_levels, int n_levels,
+                                             int radius, float divisor, void* workspace,
+                                             int64_t workspace_bytes, hipStream_t stream) {
+  if (n_levels < 1) return DXR_EINVAL;
+  return alt_lookup(fmap1, fmap2_levels, coords, out, B, H, W, C, num_levels, radius, divisor,
+                    workspace, workspace_bytes, stream, n_levels);
 }
 

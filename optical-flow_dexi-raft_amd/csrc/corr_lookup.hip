@@ -29,6 +29,7 @@
 //            gathers thrash the 32 KiB L1 and become L2-bandwidth bound);
 //   phase 2  thread = (query, x-offset class): taps from LDS, fused sum, and
 //            every output store is a coalesced 256-B wave store along queries.
+#include <cmath>
 #include <type_traits>
 
 #include "dxr_common.h"
@@ -54,6 +55,8 @@ struct LookupGeom {
   int levels;
   int cout;       // levels * (2r+1)^2
   int out_nt = 0; // wide lookup: non-temporal output stores (launch_lookup_r decides)
+  int l0 = 0;     // level of blockIdx.y == 0 (the alternate block's volume lookup: its first coarse level)
+  float divisor = 1.f, div_recip = 0.f;   // ALT: the alternate block's division of each output
   LevelAddr lv[8];
 };
 
@@ -494,6 +497,41 @@ __device__ __forceinline__ void qm_phase0_taps(const Phase0Coords<R, NT_, QB_>& 
   }
 }
 
+// Phase 0 of the ALT form: every sample of a query shares its window origin
+// floor(c / 2^l) - r and its fractions (no per-sample floors, no reduction);
+// outside +-1e8 or with the window wholly off the level the query is far (its
+// staged cells are zeros, its outputs 0 or NaN as the fractions make them, as
+// alt_corr_mfma_kernel's).
+template <int R, int NT_, int QB_>
+__device__ __forceinline__ void qm_phase0_alt(const Phase0Coords<R, NT_, QB_>& c, const LevelAddr& A,
+                                              int l, int tid, float2* xs, float2* ys, int2* org) {
+  using C = WideCfg<R, NT_, QB_>;
+  using Q = QmCfg<R, NT_, QB_>;
+  constexpr int RD = C::RD, QB = C::QB, G = C::G;
+#pragma unroll
+  for (int it = 0; it < C::SIT; ++it) {
+    const int slot = tid + it * C::NT;
+    if (slot >= QB * G) break;   // whole waves
+    const int j = slot & (G - 1), qq = slot >> C::LG;
+    const float inv = __builtin_ldexpf(1.f, -l);   // alt_corr: 1 / 2^l, exact
+    const float x = c.x[it] * inv, y = c.y[it] * inv;
+    const float xf = floorf(x), yf = floorf(y);
+    int x0 = 0, y0 = 0;
+    bool live = false;
+    if (fabsf(xf) < 1.0e8f && fabsf(yf) < 1.0e8f) {
+      x0 = (int)xf - R;
+      y0 = (int)yf - R;
+      live = x0 + RD + 1 > 0 && x0 < A.w && y0 + RD + 1 > 0 && y0 < A.h;
+    }
+    if (j == 0) org[qq] = live ? make_int2(x0, y0) : make_int2(FAR_ORIGIN, FAR_ORIGIN);
+    if (j < RD) {
+      const int col = live ? j + (x0 & 3) : 0, row = live ? j : 0;
+      xs[j * Q::XP + qq] = make_float2(__int_as_float(col * QB), __fsub_rn(x, xf));
+      ys[j * Q::XP + qq] = make_float2(__int_as_float(row * Q::RSC * QB), __fsub_rn(y, yf));
+    }
+  }
+}
+
 // One 4-cell window vector (row r, vector k of the staged row) of query qq:
 // the wide kernel's gather_load arithmetic for one slot.
 template <int V, typename PT>
@@ -598,7 +636,13 @@ __device__ __forceinline__ void qm_gather(const PT* __restrict__ base, int qb0, 
 // XA: timing ablations for the experiments target (0 in the product): bit 0 skips
 // the window gathers, bit 1 the output stores (only values equal to 12345 are
 // stored), bit 2 returns after phase 0.
-template <int R, typename PT, int NT_ = 512, int QB_ = 32, int UNR = 1, bool BUF = false, int XA = 0>
+// ALT (round 6, dxr_alt_volume_lookup): the alternate block's arithmetic on
+// coarse-level volumes of raw dot products (dxr_alt_coarse_volumes): window origin
+// floor(c / 2^l) - r with no coordinate round trip, the (2r+2)^2 window cells
+// weighted by the fractions of c / 2^l and combined in correlation_kernel.cu's
+// order (as alt_corr_mfma_kernel's last phase), then divided by sqrt(D).
+template <int R, typename PT, int NT_ = 512, int QB_ = 32, int UNR = 1, bool BUF = false, int XA = 0,
+          bool ALT = false>
 __global__ __launch_bounds__(NT_) void corr_lookup_qm_kernel(
     const PT* __restrict__ pyr, const float* __restrict__ coords, float* __restrict__ out,
     LookupGeom g) {
@@ -610,7 +654,7 @@ __global__ __launch_bounds__(NT_) void corr_lookup_qm_kernel(
   __shared__ int2 org[QB];
 
   const int tid = threadIdx.x;
-  const int l = blockIdx.y, b = blockIdx.z;
+  const int l = blockIdx.y + g.l0, b = blockIdx.z;
   const int q0 = blockIdx.x * QB;
   const LevelAddr A = g.lv[l];
   if constexpr (QB_ == 16) {   // one-round grids: finest level first (as the wide kernel)
@@ -622,7 +666,8 @@ __global__ __launch_bounds__(NT_) void corr_lookup_qm_kernel(
   {
     Phase0Coords<R, NT_, QB_> c;
     wide_phase0_load<R, NT_, QB_>(coords, g, b, q0, tid, c);
-    qm_phase0_taps<R, NT_, QB_>(c, A, l, tid, xs, ys, org);
+    if constexpr (ALT) qm_phase0_alt<R, NT_, QB_>(c, A, l, tid, xs, ys, org);
+    else qm_phase0_taps<R, NT_, QB_>(c, A, l, tid, xs, ys, org);
   }
   __syncthreads();
   if constexpr ((XA & 4) != 0) {
@@ -653,12 +698,22 @@ __global__ __launch_bounds__(NT_) void corr_lookup_qm_kernel(
     const float* p = cq + __float_as_int(yd.x) + __float_as_int(xd.x);
     const float v00 = p[0], v01 = p[QB], v10 = p[RSC * QB], v11 = p[RSC * QB + QB];
     const float gx = __fsub_rn(1.f, xd.y), gy = __fsub_rn(1.f, yd.y);
-    const float nw = __fmul_rn(gy, gx), ne = __fmul_rn(gy, xd.y);
-    const float sw = __fmul_rn(yd.y, gx), se = __fmul_rn(yd.y, xd.y);
-    float r = __fmul_rn(nw, v00);
-    r = __builtin_fmaf(ne, v01, r);
-    r = __builtin_fmaf(sw, v10, r);
-    r = __builtin_fmaf(se, v11, r);
+    float r;
+    if constexpr (ALT) {
+      // correlation_kernel.cu:92-114's order, as alt_corr_mfma_kernel
+      r = __fmul_rn(__fmul_rn(v00, gy), gx);
+      r = __fadd_rn(r, __fmul_rn(__fmul_rn(v01, gy), xd.y));
+      r = __fadd_rn(r, __fmul_rn(__fmul_rn(v10, yd.y), gx));
+      r = __fadd_rn(r, __fmul_rn(__fmul_rn(v11, yd.y), xd.y));
+      r = g.div_recip != 0.f ? r * g.div_recip : r / g.divisor;
+    } else {
+      const float nw = __fmul_rn(gy, gx), ne = __fmul_rn(gy, xd.y);
+      const float sw = __fmul_rn(yd.y, gx), se = __fmul_rn(yd.y, xd.y);
+      r = __fmul_rn(nw, v00);
+      r = __builtin_fmaf(ne, v01, r);
+      r = __builtin_fmaf(sw, v10, r);
+      r = __builtin_fmaf(se, v11, r);
+    }
     if ((XA & 2) == 0 || r == 12345.f) {
       if (g.out_nt) __builtin_nontemporal_store(r, op);
       else __hip_atomic_store(op, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1365,6 +1420,73 @@ int launch_lookup_conv1x1(const PT* pyr, const float* coords, const float4* wpl,
 }
 
 }  // namespace
+
+namespace {
+// The alternate block's coarse levels from their volumes (dxr_alt_coarse_volumes),
+// levels [first, num_levels): launch_lookup_r's shapes and output policy.
+template <int R>
+int launch_alt_volume_r(const float* vol, const float* coords, float* out, const LookupGeom& g0,
+                        int first, int B, hipStream_t stream) {
+  using W = WideCfg<R>;
+  LookupGeom g = g0;
+  const int nl = g.levels - first;
+  const long long wg32 = (long long)((g.N + W::QB - 1) / W::QB) * nl * B;
+  if (R <= 4 && wg32 <= 1024) {
+    g.out_nt = g.N % 32 == 0 ? 1 : 0;
+    const dim3 grid((unsigned)((g.N + 15) / 16), (unsigned)nl, (unsigned)B);
+    hipLaunchKernelGGL((corr_lookup_qm_kernel<R, float, 256, 16, 1, false, 0, true>), grid, dim3(256), 0,
+                       stream, vol, coords, out, g);
+    return dxr::launch_status();
+  }
+  g.out_nt = 1;
+  const dim3 grid((unsigned)((g.N + W::QB - 1) / W::QB), (unsigned)nl, (unsigned)B);
+  hipLaunchKernelGGL((corr_lookup_qm_kernel<R, float, 512, W::QB, 1, true, 0, true>), grid, dim3(512), 0,
+                     stream, vol, coords, out, g);
+  return dxr::launch_status();
+}
+}  // namespace
+
+extern "C" int dxr_alt_volume_lookup(const float* volumes, const float* coords, float* out,
+                                     int64_t B, int64_t H, int64_t W, int num_levels,
+                                     int first_level, int radius, float divisor,
+                                     hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, num_levels, &L) || first_level < 0 || first_level >= num_levels)
+    return DXR_EINVAL;
+  if (radius < 0 || !(divisor == divisor) || divisor == 0.f) return DXR_EINVAL;
+  if (radius > 8) return DXR_EUNSUPPORTED;
+  if (B > 65535) return DXR_EINVAL;
+  if (B == 0) return DXR_OK;
+  if (!volumes || !coords || !out) return DXR_EINVAL;
+  const int rd = 2 * radius + 1;
+  LookupGeom g;
+  g.N = (int)(H * W);
+  g.levels = num_levels;
+  g.cout = num_levels * rd * rd;
+  g.l0 = first_level;
+  g.divisor = divisor;
+  {
+    int e;
+    const float m = std::frexp(divisor, &e);
+    g.div_recip = (m == 0.5f && e > -125 && e < 126) ? 1.f / divisor : 0.f;   // exact: a power of two
+  }
+  for (int l = 0; l < L.n; ++l) {
+    g.lv[l] = level_addr(L.lay[l]);
+    g.lv[l].off -= L.off[first_level];
+  }
+  switch (radius) {
+    case 0: return launch_alt_volume_r<0>(volumes, coords, out, g, first_level, (int)B, stream);
+    case 1: return launch_alt_volume_r<1>(volumes, coords, out, g, first_level, (int)B, stream);
+    case 2: return launch_alt_volume_r<2>(volumes, coords, out, g, first_level, (int)B, stream);
+    case 3: return launch_alt_volume_r<3>(volumes, coords, out, g, first_level, (int)B, stream);
+    case 4: return launch_alt_volume_r<4>(volumes, coords, out, g, first_level, (int)B, stream);
+    case 5: return launch_alt_volume_r<5>(volumes, coords, out, g, first_level, (int)B, stream);
+    case 6: return launch_alt_volume_r<6>(volumes, coords, out, g, first_level, (int)B, stream);
+    case 7: return launch_alt_volume_r<7>(volumes, coords, out, g, first_level, (int)B, stream);
+    case 8: return launch_alt_volume_r<8>(volumes, coords, out, g, first_level, (int)B, stream);
+    default: return DXR_EUNSUPPORTED;
+  }
+}
 
 extern "C" int dxr_corr_lookup(const void* pyramid, int pyr_dtype, int64_t B, int64_t H,
                                int64_t W, int num_levels, int radius, const float* coords,

@@ -387,6 +387,77 @@ def test_alternate_block_overflow_fallback(dx):
     assert (np.abs(got[fin] - ref[fin]) <= 1e-4 * scale[fin] + 1e-30).all()
 
 
+def _alt_flow(B, H, W, flow, seed):
+    ys, xs = np.meshgrid(np.arange(H, dtype=np.float32), np.arange(W, dtype=np.float32),
+                         indexing="ij")
+    grid = np.stack([xs, ys])[None].repeat(B, 0)
+    rng = np.random.default_rng(seed)
+    c = (grid + rng.normal(0, 4, size=grid.shape)).astype(np.float32)
+    if flow == "far":
+        c[:, 0, 3, 5] = np.nan
+        c[:, 1, 7, 9] = np.inf
+        c[:, :, 10, 2:30:3] = -40.0
+        c[:, 0, 12, :20] = 3.0e9
+    return _t(np.ascontiguousarray(c))
+
+
+@pytest.mark.parametrize("flow", ["iid", "far"])
+@pytest.mark.parametrize("shape", [(1, 256, 55, 128, 4), (2, 64, 30, 44, 3), (1, 256, 136, 240, 4)])
+def test_alt_coarse_volumes_match_on_the_fly(dx, flow, shape, monkeypatch):
+    """Round 6: AlternateCorrBlock can compute its coarse levels once per block
+    as whole volumes of the same f16-pair MFMA dot products
+    (dxr_alt_coarse_volumes) and read their windows with the reference's alt
+    arithmetic (dxr_alt_volume_lookup); forced here from the first level of at
+    most 2048 cells (Sintel: levels 1-3, 1080p: levels 2-3), the outputs are the
+    all-on-the-fly block's bit for bit, NaN / inf / off-image coordinates
+    included.  The default policy (large maps, levels of <= 512 cells) picks
+    level 3 at 1080p and none at Sintel."""
+    B, D, H, W, r = shape
+    f1 = _t(dg.fmap(81, B, D, H, W, "fnet"))
+    f2 = _t(dg.fmap(82, B, D, H, W, "fnet"))
+    c = _alt_flow(B, H, W, flow, 83)
+    # the default policy: volumes only on large maps, for levels of <= 512 cells
+    assert dx.AlternateCorrBlock(f1, f2, radius=r).coarse_first_level == (3 if H > 100 else None)
+    monkeypatch.setattr(dx.AlternateCorrBlock, "COARSE_MIN_QUERIES", 0)
+    monkeypatch.setattr(dx.AlternateCorrBlock, "COARSE_LEVEL_MAX_CELLS", 2048)
+    hyb = dx.AlternateCorrBlock(f1, f2, radius=r)
+    assert hyb.coarse_first_level == (2 if H > 100 else 1)
+    monkeypatch.setattr(dx.AlternateCorrBlock, "COARSE_LEVEL_MAX_CELLS", 0)
+    fly = dx.AlternateCorrBlock(f1, f2, radius=r)
+    assert fly.coarse_first_level is None
+    a, b = hyb(c), fly(c)
+    assert torch.equal(torch.isnan(a), torch.isnan(b))
+    assert torch.equal(torch.nan_to_num(a, nan=3.0), torch.nan_to_num(b, nan=3.0))
+    assert torch.isfinite(a[0, :, 20, 40]).all()
+
+
+@pytest.mark.parametrize("levels", [4, 5])
+def test_alt_volume_lookup_every_level(dx, levels):
+    """dxr_alt_coarse_volumes + dxr_alt_volume_lookup from level 0 on (every
+    paged level layout: 8x16 .. 1x2 tiles, and a row-major level 4) against
+    dxr_alt_corr_lookup: bit for bit."""
+    from dexiraft_amd import _native as nat
+    lib = nat.load()
+    B, D, H, W, r = 2, 64, 48, 70, 3
+    f1 = _t(dg.fmap(91, B, D, H, W, "fnet"))
+    f2 = _t(dg.fmap(92, B, D, H, W, "fnet"))
+    ab = dx.AlternateCorrBlock(f1, f2, num_levels=levels, radius=r)
+    c = _alt_flow(B, H, W, "far", 93)
+    K = levels * (2 * r + 1) ** 2
+    n = lib.dxr_alt_volume_numel(B, H, W, levels, 0)
+    vol = torch.full((n,), float("nan"), device=DEV)
+    sq = float(np.sqrt(np.float32(D)))
+    assert lib.dxr_alt_coarse_volumes(ab._f1_nhwc.data_ptr(), ab._f2_ptrs, B, H, W, D, levels, 0,
+                                      vol.data_ptr(), nat.stream_of(vol)) == 0
+    got = torch.full((B, K, H, W), 7.0, device=DEV)
+    assert lib.dxr_alt_volume_lookup(vol.data_ptr(), c.data_ptr(), got.data_ptr(), B, H, W, levels,
+                                     0, r, sq, nat.stream_of(c)) == 0
+    ref = torch.full((B, K, H, W), 7.0, device=DEV)
+    assert lib.dxr_alt_corr_lookup(ab._f1_nhwc.data_ptr(), ab._f2_ptrs, c.data_ptr(), ref.data_ptr(),
+                                   B, H, W, D, levels, r, sq, nat.stream_of(c)) == 0
+    assert torch.equal(torch.nan_to_num(got, nan=3.0), torch.nan_to_num(ref, nan=3.0))
+
+
 @pytest.mark.parametrize("flow", ["iid", "smooth", "far"])
 @pytest.mark.parametrize("shape", [(1, 256, 55, 128, 4), (2, 64, 30, 44, 3)])
 def test_alt_lookup_query_order_is_bit_identical(dx, flow, shape):
