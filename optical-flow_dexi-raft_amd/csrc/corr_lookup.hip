@@ -21,14 +21,16 @@
 // is (2r+3)^2 cells: the per-sample floors span at most one extra row/column.
 //
 // MI355X mapping: one workgroup = QB consecutive query pixels x one level.
-//   phase 0  QB threads compute the 2(2r+1) sample positions of their query and
+//   phase 0  threads compute the 2(2r+1) sample positions of their query and
 //            the window origin (LDS);
-//   phase 1  each wave gathers whole windows of one query at a time into LDS —
-//            lanes walk consecutive cells of a window row, so one wave load
-//            touches a handful of 128-B lines instead of 64 (lane-per-query
-//            gathers thrash the 32 KiB L1 and become L2-bandwidth bound);
-//   phase 2  thread = (query, x-offset class): taps from LDS, fused sum, and
-//            every output store is a coalesced 256-B wave store along queries.
+//   phase 1  the windows are gathered into LDS as aligned 4-cell vectors;
+//   phase 2  thread = (query, output class): taps from LDS, fused sum, and
+//            every output store is a coalesced wave store along queries.
+// The product lookup (round 6) is corr_lookup_qm_kernel, which stages the
+// windows query-minor so the phase-2 tap reads are bank-conflict-free;
+// corr_lookup_wide_kernel (per-query LDS blocks, rounds 1-5) stays for the
+// experiments target, and its phase 0 / gathers serve the lookup backward and
+// the fused motion kernel.
 #include <cmath>
 #include <type_traits>
 
