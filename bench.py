@@ -696,7 +696,18 @@ def main():
             aflops = alt_lookup_flops(B, H, W)
             achieved = aflops / (look_ms * 1e-3) / 1e12
             akern = "alt_corr_mfma_kernel"
-            a_traffic, a_src = pmc_traffic(wl_key, akern + "<", cfg)
+            # the windowed instantiation (radius 4; the FULL one, radius 0, builds the
+            # coarse-level volumes once per block), plus the volume lookup when the
+            # block answers its coarse levels from volumes
+            a_traffic, a_src = pmc_traffic(wl_key, f"{akern}<{RADIUS},", cfg)
+            vol_first = getattr(state.get("cb"), "coarse_first_level", None)
+            if a_traffic is not None and vol_first is not None:
+                v_traffic, _ = pmc_traffic(wl_key, "corr_lookup_qm_kernel<", cfg)
+                if v_traffic is None:
+                    a_traffic = a_src = None
+                else:
+                    a_traffic += v_traffic
+                    a_src += f" (+ corr_lookup_qm_kernel ALT: levels >= {vol_first} from volumes)"
             pipe = PEAK_BF16_TFLOPS / SPLIT_PRODUCTS   # the f16-pair split's own ceiling (833 TF)
             res["roofline"] = {
                 "kernel": akern + " (f16-pair split MFMA over the window boxes of 32 queries "
