@@ -412,6 +412,9 @@ def main():
     ap.add_argument("--alt-coarse-cells", type=int, default=None,
                     help="--block alt: AlternateCorrBlock.COARSE_LEVEL_MAX_CELLS (levels of at most "
                          "this many cells computed once per block as whole volumes; 0: none)")
+    ap.add_argument("--alt-coarse-min-queries", type=int, default=None,
+                    help="--block alt: AlternateCorrBlock.COARSE_MIN_QUERIES (volumes only on maps "
+                         "of at least this many query pixels)")
     ap.add_argument("--layout", default="nchw", choices=["nchw", "nhwc"],
                     help="fmap memory format: nchw (the reference's) or nhwc (channels-last "
                          "encoders, SURVEY §8(f) row 4)")
@@ -463,6 +466,8 @@ def main():
     block_cls = dexiraft_amd.CorrBlock if args.block == "corr" else dexiraft_amd.AlternateCorrBlock
     if args.block == "alt" and args.alt_coarse_cells is not None:
         block_cls.COARSE_LEVEL_MAX_CELLS = args.alt_coarse_cells
+    if args.block == "alt" and args.alt_coarse_min_queries is not None:
+        block_cls.COARSE_MIN_QUERIES = args.alt_coarse_min_queries
 
     def build(i=0):
         # the previous step's block and outputs go first (one pyramid alive at a time)

@@ -649,10 +649,10 @@ class AlternateCorrBlock:
     sqrt(D).  Round 6: on large maps (``COARSE_MIN_QUERIES``) the coarse levels —
     from the first level of at most ``COARSE_LEVEL_MAX_CELLS`` cells on, within
     ``COARSE_VOLUME_MAX_BYTES`` — are computed once per block as whole volumes of the
-    same dot products (``dxr_alt_coarse_volumes``) and read by
-    ``dxr_alt_volume_lookup``: an on-the-fly lookup pays each level's box GEMMs
-    again on every call (~15-26 us per coarse level at 1080p), while the coarsest
-    level's whole volume costs less than one call (1080p: level 3).
+    same dot products (``dxr_alt_coarse_volumes``, one tiled GEMM per level) and read
+    by ``dxr_alt_volume_lookup``: an on-the-fly lookup pays each level's box GEMMs
+    again on every call (~15-26 us per coarse level at 1080p), while a coarse
+    level's whole volume costs about one or two calls (1080p: levels 2-3).
     With finite operands in the f16 pair's range the outputs are the all-on-the-
     fly form's bit for bit (``coarse_first_level`` None: no volumes).  As in the
     reference, the constructor pools ``num_levels`` times, so fmaps smaller than
@@ -660,11 +660,11 @@ class AlternateCorrBlock:
     """
 
     # Which levels are precomputed (round 6, bench.py --block alt, profiles/r06/experiments/
-    # r6l_*): at 1080p (32,640 queries) level 3 (510 cells) as a volume takes the lookup from
-    # 163.8 to 148.8 us for 89 us per block (+5.1 % pairs/s); level 2 as well (2,040 cells)
-    # gets it to 126.9 us but costs 426 us per block (+0.9 %); at Sintel (7,040 queries) the
-    # on-the-fly coarse levels cost ~2-3 us per lookup and volumes lose 7 %.
-    COARSE_LEVEL_MAX_CELLS = 512           # a level of at most this many cells is precomputed
+    # r6n_*): at 1080p (32,640 queries) levels 2-3 (2,040 + 510 cells) as volumes take the
+    # lookup from 164.1 to 127.2 us for ~200 us per block (tiled GEMM: level 2 149 us, level 3
+    # 42 us): 498.9 -> 568.0 pairs/s (+13.9 %; level 3 alone 536.8); at Sintel (7,040
+    # queries) the on-the-fly coarse levels cost ~2-4 us per lookup and volumes lose 3-4 %.
+    COARSE_LEVEL_MAX_CELLS = 2048          # a level of at most this many cells is precomputed
     COARSE_MIN_QUERIES = 16384             # on maps of at least this many query pixels
     COARSE_VOLUME_MAX_BYTES = 1 << 30      # and all precomputed volumes fit in this
 

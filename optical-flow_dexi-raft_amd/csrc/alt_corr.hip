@@ -1510,6 +1510,239 @@ int alt_lookup(const float* fmap1, const float* const* fmap2_levels, const float
     ord = workspace;
   return launch_alt(fmap1, coords, out, g, nl, (int)B, radius, vec, stream, (int)W, ord);
 }
+
+// ---------------------------------------------------------------------------
+// A coarse level's whole volume as one tiled GEMM (round 6): every (query, cell)
+// sum of the level, raw, into that level's pages of the volume buffer — the FULL
+// form's output (and so the on-the-fly lookup's dot products) bit for bit, since
+// each sum is the same three f16 products per k step (alt_split8h operands, cell
+// vectors as the A rows, queries as the B columns of v_mfma_f32_32x32x16_f16,
+// cross terms in a second accumulator folded by 2^-11 at the end) in the same k
+// order; only the tiling differs.  The FULL form streams every cell of the level
+// through each 32-query workgroup (1080p level 2: 337 us per block); here one
+// workgroup = one page's 128 queries x 128 cells (128 / T whole tiles of the
+// level, T = th * tw cells per tile, i.e. 128 / T consecutive pages), four waves
+// of 64 cells x 64 queries (2 x 2 MFMA tiles), so each loaded operand feeds 64
+// MFMA columns instead of 32 and the split is paid once per workgroup.
+// K runs in stages of 32 channels: every thread loads 8 float4 (4 of cells, 4 of
+// queries) one stage ahead, splits them and writes hi / lo to a double-buffered
+// LDS stage laid out [operand][plane][k step][row][kh] x 16 B, so every MFMA
+// fragment read is a conflict-free ds_read_b128 over 1 KB contiguous per wave
+// (blocks padded by 128 B so the split's 8-B writes of the two k steps of a row
+// land in different banks).  A 32 x 32 tile whose sums are not finite is redone
+// from fmap1 / fmap2 on the 3-way bf16 split (six products, the windowed form's
+// fallback arithmetic).  Rows past the level or the query count compute zeros;
+// pages past the level's last tile are not written.  C % 32 == 0.
+constexpr int VG_BLK = 4096 + 128;            // one [row][kh] block of 128 rows x 32 B
+constexpr int VG_STAGE = 8 * VG_BLK;          // [operand][plane][k step] blocks
+
+// XA (experiments only; 0 in the product): bit 0 stores only sums equal to
+// 12345.0 (none: an ablation of the stores), bit 1 writes the raw f32 bits as the
+// hi / lo planes (no split VALU; results meaningless), bit 2 skips the MFMAs.
+template <int T, int XA = 0>
+__global__ __launch_bounds__(256, 2) void alt_volume_gemm_kernel(
+    const float* __restrict__ f1, const float* __restrict__ f2, float* __restrict__ out,
+    dxr::LevelLayout vl, int N, int C, int ngroups) {
+  static_assert(T == 2 || T == 8 || T == 32 || T == 128, "tiled levels 0-3 only");
+  constexpr int TPG = 128 / T;                 // level tiles (pages) per workgroup
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * VG_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 31, kh = lane >> 5;
+  const int wc = wave & 1, wq = wave >> 1;     // the wave's 64-cell / 64-query half
+  // contiguous bands of (query block, cell group) per XCD (csrc/corr_build.hip's
+  // page_coord bijection): one XCD's workgroups share their query block's operand in L2
+  const int n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = (int)blockIdx.x % 8;
+  const int idx = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) +
+                  (int)blockIdx.x / 8;
+  const int qblk = idx / ngroups, grp = idx - qblk * ngroups;
+  const int b = blockIdx.z;
+  const int ntiles = vl.ty * vl.tx;
+  const float* f1b = f1 + (long long)b * N * C;
+  const float* f2b = f2 + (long long)b * vl.h * vl.w * C;
+  // element offset of cell row i (0..127) of this workgroup's group, -1 past the level
+  auto cell_off = [&](int i) -> int {
+    const int tile = grp * TPG + i / T, c = i % T;
+    if (tile >= ntiles) return -1;
+    const int ty = tile / vl.tx, tx = tile - ty * vl.tx;
+    const int cy = ty * vl.th + c / vl.tw, cx = tx * vl.tw + c % vl.tw;
+    return (cy < vl.h && cx < vl.w) ? (cy * vl.w + cx) * C : -1;
+  };
+  auto query_off = [&](int i) -> int {
+    const int q = qblk * 128 + i;
+    return q < N ? q * C : -1;
+  };
+  // this thread's 8 load slots: slot i < 4 cells, else queries; piece t + 256 (i % 4)
+  // -> row piece / 8, channels 4 (piece % 8) .. + 4 of the stage
+  int off[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int piece = tid + 256 * (i & 3), row = piece >> 3;
+    off[i] = i < 4 ? cell_off(row) : query_off(row);
+  }
+  const int f4 = tid & 7;
+  const int ch = 4 * f4;
+  // LDS byte offset of this thread's 8-B hi write for slot i (lo: + 2 VG_BLK)
+  auto wr_addr = [&](int i) -> int {
+    const int row = (tid + 256 * (i & 3)) >> 3, o = i >> 2;
+    return ((o * 2 + 0) * 2 + (f4 >> 2)) * VG_BLK + row * 32 + ((f4 >> 1) & 1) * 16 + (f4 & 1) * 8;
+  };
+  float4 pre[8];
+  auto load_stage = [&](int s) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float* base = i < 4 ? f2b : f1b;
+      pre[i] = off[i] >= 0 ? *reinterpret_cast<const float4*>(base + off[i] + 32 * s + ch)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto write_stage = [&](int buf) {
+    unsigned char* st = lds + buf * VG_STAGE;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float4 v = pre[i];
+      uint32_t h0, h1, l0, l1;
+      if constexpr ((XA & 2) != 0) {
+        h0 = __float_as_uint(v.x); h1 = __float_as_uint(v.y);
+        l0 = __float_as_uint(v.z); l1 = __float_as_uint(v.w);
+      } else {
+        h0 = alt_cvt_pk_h(v.x, v.y);
+        h1 = alt_cvt_pk_h(v.z, v.w);
+        const ah2 a0 = __builtin_bit_cast(ah2, h0), a1 = __builtin_bit_cast(ah2, h1);
+        l0 = alt_cvt_pk_h((v.x - (float)a0[0]) * 2048.f, (v.y - (float)a0[1]) * 2048.f);
+        l1 = alt_cvt_pk_h((v.z - (float)a1[0]) * 2048.f, (v.w - (float)a1[1]) * 2048.f);
+      }
+      const int a = wr_addr(i);
+      *reinterpret_cast<uint2*>(st + a) = make_uint2(h0, h1);
+      *reinterpret_cast<uint2*>(st + a + 2 * VG_BLK) = make_uint2(l0, l1);
+    }
+  };
+  af16 acc[2][2], acc2[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][q][r] = acc2[a][q][r] = 0.f;
+  const int nst = C / 32;
+  load_stage(0);
+  write_stage(0);
+  __syncthreads();
+  for (int s = 0; s < nst; ++s) {
+    if (s + 1 < nst) load_stage(s + 1);
+    const unsigned char* st = lds + (s & 1) * VG_STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      ah8 th[2], tl[2], qh[2], ql[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int rc = (wc * 64 + a * 32 + j) * 32 + kh * 16;
+        const int rq = (wq * 64 + a * 32 + j) * 32 + kh * 16;
+        th[a] = __builtin_bit_cast(ah8, *reinterpret_cast<const uint4*>(st + (0 + ks) * VG_BLK + rc));
+        tl[a] = __builtin_bit_cast(ah8, *reinterpret_cast<const uint4*>(st + (2 + ks) * VG_BLK + rc));
+        qh[a] = __builtin_bit_cast(ah8, *reinterpret_cast<const uint4*>(st + (4 + ks) * VG_BLK + rq));
+        ql[a] = __builtin_bit_cast(ah8, *reinterpret_cast<const uint4*>(st + (6 + ks) * VG_BLK + rq));
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          if constexpr ((XA & 4) != 0) {
+            acc[a][q][0] += (float)th[a][0] * (float)qh[q][1] + (float)tl[a][2] * (float)ql[q][3];
+            continue;
+          }
+          acc2[a][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl[a], qh[q], acc2[a][q], 0, 0, 0);
+          acc2[a][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th[a], ql[q], acc2[a][q], 0, 0, 0);
+          acc[a][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th[a], qh[q], acc[a][q], 0, 0, 0);
+        }
+    }
+    if (s + 1 < nst) write_stage((s + 1) & 1);
+    __syncthreads();
+  }
+  const long long page0 = ((long long)b * vl.qt + qblk) * ntiles + (long long)grp * TPG;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      bool bad = false;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        acc[a][q][r] = __builtin_fmaf(acc2[a][q][r], 0x1p-11f, acc[a][q][r]);
+        bad |= !(__builtin_fabsf(acc[a][q][r]) <= 3.40282347e38f);
+      }
+      if ((XA & 6) == 0 && __ballot(bad) != 0) {   // wave-uniform: the tile on the 3-way bf16 split
+        const int co = cell_off(wc * 64 + a * 32 + j), qo = query_off(wq * 64 + q * 32 + j);
+        af16 f = {};
+        for (int ks = 0; ks < C / 16; ++ks) {
+          float x[8], y[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            x[e] = co >= 0 ? f2b[co + 16 * ks + 8 * kh + e] : 0.f;
+            y[e] = qo >= 0 ? f1b[qo + 16 * ks + 8 * kh + e] : 0.f;
+          }
+          uint4 h, m, l, uh, um, ul;
+          alt_split8(x, h, m, l);
+          alt_split8(y, uh, um, ul);
+          const abf8 th = __builtin_bit_cast(abf8, h), tm = __builtin_bit_cast(abf8, m),
+                     tl = __builtin_bit_cast(abf8, l);
+          const abf8 qh = __builtin_bit_cast(abf8, uh), qm = __builtin_bit_cast(abf8, um),
+                     ql = __builtin_bit_cast(abf8, ul);
+          f = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm, f, 0, 0, 0);
+          f = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh, f, 0, 0, 0);
+          f = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, ql, f, 0, 0, 0);
+          f = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qh, f, 0, 0, 0);
+          f = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qm, f, 0, 0, 0);
+          f = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh, f, 0, 0, 0);
+        }
+        acc[a][q] = f;
+      }
+      // lane (j, kh) holds rows (r & 3) + 8 (r >> 2) + 4 kh of column j: runs of four
+      // consecutive cells, i.e. one 16-B store into one page (T >= 4) or two 8-B
+      // stores into two (T = 2)
+      const int ql_ = wq * 64 + q * 32 + j;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int row = wc * 64 + a * 32 + 8 * g4 + 4 * kh;
+        const float4 v = make_float4(acc[a][q][4 * g4], acc[a][q][4 * g4 + 1],
+                                     acc[a][q][4 * g4 + 2], acc[a][q][4 * g4 + 3]);
+        if constexpr ((XA & 1) != 0)
+          if (v.x != 12345.f) continue;
+        if constexpr (T >= 4) {
+          const int t = row / T;
+          if (grp * TPG + t < ntiles)
+            *reinterpret_cast<float4*>(out + vl.off + ((page0 + t) * 128 + ql_) * T + row % T) = v;
+        } else {
+          const int t = row / 2;
+          if (grp * TPG + t < ntiles)
+            *reinterpret_cast<float2*>(out + vl.off + ((page0 + t) * 128 + ql_) * 2) =
+                make_float2(v.x, v.y);
+          if (grp * TPG + t + 1 < ntiles)
+            *reinterpret_cast<float2*>(out + vl.off + ((page0 + t + 1) * 128 + ql_) * 2) =
+                make_float2(v.z, v.w);
+        }
+      }
+    }
+}
+
+// one level's volume by alt_volume_gemm_kernel (tiled levels 0-3, C % 32 == 0)
+template <int XA = 0>
+int launch_alt_volume_gemm(const float* f1, const float* f2, float* vol, const dxr::LevelLayout& vl,
+                           int B, int N, int C, hipStream_t stream) {
+  const int T = vl.th * vl.tw;
+  const int ngroups = (vl.ty * vl.tx + 128 / T - 1) / (128 / T);
+  const long long nwg = (long long)vl.qt * ngroups;
+  if (nwg > 0x7fffffffLL || (long long)N * C > 0x7fffffffLL ||
+      (long long)vl.h * vl.w * C > 0x7fffffffLL)
+    return DXR_EUNSUPPORTED;
+  const dim3 grid((unsigned)nwg, 1u, (unsigned)B);
+  switch (T) {
+    case 2: hipLaunchKernelGGL((alt_volume_gemm_kernel<2, XA>), grid, dim3(256), 0, stream, f1, f2, vol, vl, N, C, ngroups); break;
+    case 8: hipLaunchKernelGGL((alt_volume_gemm_kernel<8, XA>), grid, dim3(256), 0, stream, f1, f2, vol, vl, N, C, ngroups); break;
+    case 32: hipLaunchKernelGGL((alt_volume_gemm_kernel<32, XA>), grid, dim3(256), 0, stream, f1, f2, vol, vl, N, C, ngroups); break;
+    case 128: hipLaunchKernelGGL((alt_volume_gemm_kernel<128, XA>), grid, dim3(256), 0, stream, f1, f2, vol, vl, N, C, ngroups); break;
+    default: return DXR_EUNSUPPORTED;
+  }
+  return dxr::launch_status();
+}
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -1518,7 +1751,9 @@ int alt_lookup(const float* fmap1, const float* const* fmap2_levels, const float
 // level's size; a coarse level's whole correlation volume costs less than one
 // such lookup to compute once per block.  dxr_alt_coarse_volumes computes levels
 // [first_level, num_levels) of fmap1 against the pooled fmap2 levels (the
-// alternate block's own operands) with the FULL form of the box kernel and
+// alternate block's own operands) — the tiled levels (0-3) by
+// alt_volume_gemm_kernel when C % 32 == 0, others by the FULL form of the box
+// kernel, the same sums either way — and
 // stores them, raw, in the paged layout of those pyramid levels, one buffer of
 // dxr_alt_volume_numel floats; dxr_alt_volume_lookup (csrc/corr_lookup.hip)
 // reads its windows from there with the alternate block's arithmetic.
@@ -1530,9 +1765,11 @@ extern "C" int64_t dxr_alt_volume_numel(int64_t B, int64_t H, int64_t W, int num
   return L.numel - L.off[first_level];
 }
 
-extern "C" int dxr_alt_coarse_volumes(const float* fmap1, const float* const* fmap2_levels,
-                                      int64_t B, int64_t H, int64_t W, int64_t C, int num_levels,
-                                      int first_level, float* volumes, hipStream_t stream) {
+namespace {
+// full_form: every level by the FULL box kernel (experiments: the round-6 first form)
+int alt_coarse_volumes(const float* fmap1, const float* const* fmap2_levels, int64_t B, int64_t H,
+                       int64_t W, int64_t C, int num_levels, int first_level, float* volumes,
+                       hipStream_t stream, bool full_form) {
   dxr::Levels L;
   if (!dxr::make_levels(B, H, W, num_levels, &L) || first_level < 0 || first_level >= num_levels)
     return DXR_EINVAL;
@@ -1556,6 +1793,12 @@ extern "C" int dxr_alt_coarse_volumes(const float* fmap1, const float* const* fm
     g.lv[0] = AltLevel{fmap2_levels[l], L.h[l], L.w[l], 1.f, 0};
     g.vlay = L.lay[l];
     g.vlay.off -= L.off[first_level];
+    if (l < dxr::TILED_LEVELS && C % 32 == 0 && !full_form) {
+      const int st = launch_alt_volume_gemm(fmap1, fmap2_levels[l], volumes, g.vlay, (int)B, g.N,
+                                            (int)C, stream);
+      if (st != DXR_OK) return st;
+      continue;
+    }
     hipLaunchKernelGGL((alt_corr_mfma_kernel<0, 1, 256, true, 3, false, 4, 0, 0, true>),
                        dim3((unsigned)ntiles, 1u, (unsigned)B), dim3(256), 0, stream, fmap1,
                        (const float*)nullptr, volumes, g, (int)W, tiles_x, (const int4*)nullptr,
@@ -1564,6 +1807,14 @@ extern "C" int dxr_alt_coarse_volumes(const float* fmap1, const float* const* fm
     if (st != DXR_OK) return st;
   }
   return DXR_OK;
+}
+}  // namespace
+
+extern "C" int dxr_alt_coarse_volumes(const float* fmap1, const float* const* fmap2_levels,
+                                      int64_t B, int64_t H, int64_t W, int64_t C, int num_levels,
+                                      int first_level, float* volumes, hipStream_t stream) {
+  return alt_coarse_volumes(fmap1, fmap2_levels, B, H, W, C, num_levels, first_level, volumes,
+                            stream, false);
 }
 
 extern "C" int dxr_alt_corr_lookup(const float* fmap1, const float* const* fmap2_levels,

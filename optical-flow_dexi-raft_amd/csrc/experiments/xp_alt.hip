@@ -72,3 +72,35 @@ extern "C" int dxr_xp_alt_lookup(const float* fmap1, const float* const* fmap2_l
                                              stream, ws, variant - 6);
   return DXR_EINVAL;
 }
+
+// The coarse-level volumes with every level by the FULL box kernel (round 6's
+// first form; the product uses alt_volume_gemm_kernel for tiled levels).
+extern "C" int dxr_xp_alt_coarse_volumes_full(const float* fmap1, const float* const* fmap2_levels,
+                                              int64_t B, int64_t H, int64_t W, int64_t C,
+                                              int num_levels, int first_level, float* volumes,
+                                              hipStream_t stream) {
+  return alt_coarse_volumes(fmap1, fmap2_levels, B, H, W, C, num_levels, first_level, volumes,
+                            stream, true);
+}
+
+// One tiled level's volume by alt_volume_gemm_kernel with ablation bits xa (its XA):
+// the volume buffer from `level` on (dxr_alt_volume_numel(B, H, W, level + 1, level)).
+extern "C" int dxr_xp_alt_volume_gemm(const float* fmap1, const float* fmap2_level, float* vol,
+                                      int64_t B, int64_t H, int64_t W, int64_t C, int level,
+                                      int xa, hipStream_t stream) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, level + 1, &L) || level >= dxr::TILED_LEVELS || C % 32 != 0)
+    return DXR_EINVAL;
+  dxr::LevelLayout vl = L.lay[level];
+  vl.off = 0;
+  const int N = (int)(H * W);
+  switch (xa) {
+    case 0: return launch_alt_volume_gemm<0>(fmap1, fmap2_level, vol, vl, (int)B, N, (int)C, stream);
+    case 1: return launch_alt_volume_gemm<1>(fmap1, fmap2_level, vol, vl, (int)B, N, (int)C, stream);
+    case 2: return launch_alt_volume_gemm<2>(fmap1, fmap2_level, vol, vl, (int)B, N, (int)C, stream);
+    case 4: return launch_alt_volume_gemm<4>(fmap1, fmap2_level, vol, vl, (int)B, N, (int)C, stream);
+    case 6: return launch_alt_volume_gemm<6>(fmap1, fmap2_level, vol, vl, (int)B, N, (int)C, stream);
+    case 7: return launch_alt_volume_gemm<7>(fmap1, fmap2_level, vol, vl, (int)B, N, (int)C, stream);
+    default: return DXR_EINVAL;
+  }
+}

@@ -406,22 +406,23 @@ def _alt_flow(B, H, W, flow, seed):
 def test_alt_coarse_volumes_match_on_the_fly(dx, flow, shape, monkeypatch):
     """Round 6: AlternateCorrBlock can compute its coarse levels once per block
     as whole volumes of the same f16-pair MFMA dot products
-    (dxr_alt_coarse_volumes) and read their windows with the reference's alt
-    arithmetic (dxr_alt_volume_lookup); forced here from the first level of at
-    most 2048 cells (Sintel: levels 1-3, 1080p: levels 2-3), the outputs are the
+    (dxr_alt_coarse_volumes: the tiled GEMM alt_volume_gemm_kernel) and read
+    their windows with the reference's alt arithmetic (dxr_alt_volume_lookup);
+    forced here from level 1 on (8x16 >> 1 .. 1x2 tiles), the outputs are the
     all-on-the-fly block's bit for bit, NaN / inf / off-image coordinates
-    included.  The default policy (large maps, levels of <= 512 cells) picks
-    level 3 at 1080p and none at Sintel."""
+    included.  The default policy (large maps, levels of <= 2,048 cells) picks
+    levels 2-3 at 1080p and none at Sintel."""
     B, D, H, W, r = shape
     f1 = _t(dg.fmap(81, B, D, H, W, "fnet"))
     f2 = _t(dg.fmap(82, B, D, H, W, "fnet"))
     c = _alt_flow(B, H, W, flow, 83)
-    # the default policy: volumes only on large maps, for levels of <= 512 cells
-    assert dx.AlternateCorrBlock(f1, f2, radius=r).coarse_first_level == (3 if H > 100 else None)
+    # the default policy: volumes only on large maps, for levels of <= 2,048 cells
+    assert dx.AlternateCorrBlock(f1, f2, radius=r).coarse_first_level == (2 if H > 100 else None)
     monkeypatch.setattr(dx.AlternateCorrBlock, "COARSE_MIN_QUERIES", 0)
-    monkeypatch.setattr(dx.AlternateCorrBlock, "COARSE_LEVEL_MAX_CELLS", 2048)
+    monkeypatch.setattr(dx.AlternateCorrBlock, "COARSE_LEVEL_MAX_CELLS", 1 << 20)
+    monkeypatch.setattr(dx.AlternateCorrBlock, "COARSE_VOLUME_MAX_BYTES", 1 << 32)
     hyb = dx.AlternateCorrBlock(f1, f2, radius=r)
-    assert hyb.coarse_first_level == (2 if H > 100 else 1)
+    assert hyb.coarse_first_level == 1
     monkeypatch.setattr(dx.AlternateCorrBlock, "COARSE_LEVEL_MAX_CELLS", 0)
     fly = dx.AlternateCorrBlock(f1, f2, radius=r)
     assert fly.coarse_first_level is None
@@ -429,6 +430,49 @@ def test_alt_coarse_volumes_match_on_the_fly(dx, flow, shape, monkeypatch):
     assert torch.equal(torch.isnan(a), torch.isnan(b))
     assert torch.equal(torch.nan_to_num(a, nan=3.0), torch.nan_to_num(b, nan=3.0))
     assert torch.isfinite(a[0, :, 20, 40]).all()
+
+
+@pytest.mark.parametrize("case", ["finite", "nonfinite"])
+def test_alt_volume_gemm_against_float64(dx, case):
+    """Round 6: the coarse-level volumes' tiled GEMM (alt_volume_gemm_kernel,
+    levels 0-3: 8x16 .. 1x2 tiles, ragged level edges, a partial last query
+    page, two pairs, D = 96) against float64 dot products of fmap1 with the
+    pooled fmap2 levels: within 1e-5 of sum |a||b| per cell.  "nonfinite": a
+    channel of 1e5 (beyond the f16 pair's range: its tiles re-run on the bf16
+    split, and stay accurate), a NaN fmap2 pixel and an inf fmap1 pixel — the
+    volume is non-finite exactly where float64 is."""
+    from dexiraft_amd import _native as nat
+    lib = nat.load()
+    B, D, H, W, L = 2, 96, 45, 70, 4
+    a1 = dg.fmap(95, B, D, H, W, "fnet")
+    a2 = dg.fmap(96, B, D, H, W, "fnet")
+    if case == "nonfinite":
+        a1[1, 5, 10, 20] = 1.0e5
+        a1[0, 3, 2, 2] = np.inf
+        a2[0, 7, 30, 40] = np.nan
+    ab = dx.AlternateCorrBlock(_t(a1), _t(a2), num_levels=L, radius=4)
+    n = lib.dxr_alt_volume_numel(B, H, W, L, 0)
+    vol = torch.full((n,), float("nan"), device=DEV)
+    assert lib.dxr_alt_coarse_volumes(ab._f1_nhwc.data_ptr(), ab._f2_ptrs, B, H, W, D, L, 0,
+                                      vol.data_ptr(), nat.stream_of(vol)) == 0
+    N = H * W
+    f1 = ab._f1_nhwc.reshape(B, N, D).double().cpu().numpy()
+    with np.errstate(invalid="ignore", over="ignore"):
+        for lvl in range(L):
+            f2 = ab._f2_nhwc[lvl]
+            h, w = f2.shape[1], f2.shape[2]
+            got = torch.empty((B * N, h, w), device=DEV)
+            assert lib.dxr_pyramid_unpack(vol.data_ptr(), nat.DXR_F32, B, H, W, L, lvl,
+                                          got.data_ptr(), nat.stream_of(got)) == 0
+            got = got.reshape(B, N, h * w).cpu().numpy()
+            g2 = f2.reshape(B, h * w, D).double().cpu().numpy()
+            ref = f1 @ g2.transpose(0, 2, 1)
+            mag = np.abs(f1) @ np.abs(g2).transpose(0, 2, 1)
+            fin = np.isfinite(ref)
+            assert np.array_equal(np.isfinite(got), fin), lvl
+            assert (np.abs(got[fin] - ref[fin]) <= 1e-5 * mag[fin] + 1e-30).all(), lvl
+            if case == "nonfinite":
+                assert not fin.all() and np.isfinite(got[1, 10 * W + 20]).all()
 
 
 @pytest.mark.parametrize("levels", [4, 5])
