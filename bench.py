@@ -415,6 +415,9 @@ def main():
     ap.add_argument("--alt-coarse-min-queries", type=int, default=None,
                     help="--block alt: AlternateCorrBlock.COARSE_MIN_QUERIES (volumes only on maps "
                          "of at least this many query pixels)")
+    ap.add_argument("--alt-volume-planes", type=int, default=None, choices=[0, 1],
+                    help="--block alt: AlternateCorrBlock.COARSE_VOLUME_PLANES (1: the volume "
+                         "GEMM's LDS-DMA form on pre-split f16 pair planes; 0: its register form)")
     ap.add_argument("--layout", default="nchw", choices=["nchw", "nhwc"],
                     help="fmap memory format: nchw (the reference's) or nhwc (channels-last "
                          "encoders, SURVEY §8(f) row 4)")
@@ -468,6 +471,8 @@ def main():
         block_cls.COARSE_LEVEL_MAX_CELLS = args.alt_coarse_cells
     if args.block == "alt" and args.alt_coarse_min_queries is not None:
         block_cls.COARSE_MIN_QUERIES = args.alt_coarse_min_queries
+    if args.block == "alt" and args.alt_volume_planes is not None:
+        block_cls.COARSE_VOLUME_PLANES = bool(args.alt_volume_planes)
 
     def build(i=0):
         # the previous step's block and outputs go first (one pyramid alive at a time)

@@ -77,7 +77,7 @@ extern "C" {
 /* HIP's own definition; repeating an identical typedef is legal in C11/C++. */
 typedef struct ihipStream_t* hipStream_t;
 
-#define DXR_ABI_VERSION 9
+#define DXR_ABI_VERSION 10
 
 enum dxr_status {
   DXR_OK = 0,
@@ -494,12 +494,25 @@ int dxr_alt_corr_lookup_levels_ws(const float* fmap1, const float* const* fmap2_
  * With finite operands inside the f16 pair's range the outputs are
  * dxr_alt_corr_lookup's bit for bit.  Replaces core/corr.py:74-91 (levels
  * >= first_level) with the reference's alt_cuda_corr semantics.  ABI 9.
+ *   dxr_alt_coarse_volumes_ws_bytes / dxr_alt_coarse_volumes_ws (ABI 10): the
+ *                           same volumes, bit for bit, with a caller workspace
+ *                           for the f16 pair planes of fmap1 and of the levels
+ *                           (C % 32 == 0, levels 0-3), which the volume GEMM
+ *                           then stages by LDS-DMA; a null or short workspace
+ *                           falls back to dxr_alt_coarse_volumes.  0 bytes when
+ *                           no level takes the GEMM; -1: bad geometry.
  */
 int64_t dxr_alt_volume_numel(int64_t B, int64_t H, int64_t W, int num_levels, int first_level);
 int dxr_alt_coarse_volumes(const float* fmap1, const float* const* fmap2_levels,
                            int64_t B, int64_t H, int64_t W, int64_t C,
                            int num_levels, int first_level, float* volumes,
                            hipStream_t stream);
+int64_t dxr_alt_coarse_volumes_ws_bytes(int64_t B, int64_t H, int64_t W, int64_t C,
+                                        int num_levels, int first_level);
+int dxr_alt_coarse_volumes_ws(const float* fmap1, const float* const* fmap2_levels,
+                              int64_t B, int64_t H, int64_t W, int64_t C,
+                              int num_levels, int first_level, float* volumes,
+                              void* workspace, int64_t workspace_bytes, hipStream_t stream);
 int dxr_alt_volume_lookup(const float* volumes, const float* coords, float* out,
                           int64_t B, int64_t H, int64_t W, int num_levels, int first_level,
                           int radius, float divisor, hipStream_t stream);

@@ -15,7 +15,7 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_PATH = Path(__file__).resolve().with_name("libdexiraft_corr.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 DXR_OK, DXR_EINVAL, DXR_EUNSUPPORTED, DXR_EHIP = 0, 1, 2, -1
 DXR_F32, DXR_BF16 = 0, 1
@@ -77,6 +77,9 @@ SIGNATURES: dict[str, tuple[object, list[object]]] = {
     "dxr_alt_volume_numel": (_i64, [_i64, _i64, _i64, _int, _int]),
     "dxr_alt_coarse_volumes": (_int, [_vp, ctypes.POINTER(_vp), _i64, _i64, _i64, _i64, _int, _int,
                                       _vp, _vp]),
+    "dxr_alt_coarse_volumes_ws_bytes": (_i64, [_i64, _i64, _i64, _i64, _int, _int]),
+    "dxr_alt_coarse_volumes_ws": (_int, [_vp, ctypes.POINTER(_vp), _i64, _i64, _i64, _i64, _int,
+                                         _int, _vp, _vp, _i64, _vp]),
     "dxr_alt_volume_lookup": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _int, _int, _int, _f32, _vp]),
 }
 

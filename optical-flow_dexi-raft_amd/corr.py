@@ -667,6 +667,10 @@ class AlternateCorrBlock:
     COARSE_LEVEL_MAX_CELLS = 2048          # a level of at most this many cells is precomputed
     COARSE_MIN_QUERIES = 16384             # on maps of at least this many query pixels
     COARSE_VOLUME_MAX_BYTES = 1 << 30      # and all precomputed volumes fit in this
+    # The volume GEMM's LDS-DMA form on pre-split f16 pair planes (dxr_alt_coarse_volumes_ws):
+    # bit-identical, 6 % faster isolated, but 1.2 % slower in the 1080p step (r6u: 563 vs 570
+    # pairs/s, two rounds each on one box), so off.
+    COARSE_VOLUME_PLANES = False
 
     def __init__(self, fmap1, fmap2, num_levels=4, radius=4):
         self.num_levels = num_levels
@@ -718,11 +722,17 @@ class AlternateCorrBlock:
         if first is None or first >= self.num_levels:
             return
         vol = torch.empty((n,), dtype=torch.float32, device=self._device)
+        # with COARSE_VOLUME_PLANES, the f16 pair planes of the operands (the volume GEMM's
+        # LDS-DMA form), from torch's caching allocator: freed once the launches that read
+        # them have run; 0 bytes: the register form
+        nbytes = (lib.dxr_alt_coarse_volumes_ws_bytes(B, H, W, D, self.num_levels, first)
+                  if self.COARSE_VOLUME_PLANES else 0)
+        ws = torch.empty(max(nbytes, 0), dtype=torch.uint8, device=self._device)
         with _Launch(self._device):
-            st = lib.dxr_alt_coarse_volumes(self._f1_nhwc.data_ptr(), self._f2_ptrs, B, H, W, D,
-                                            self.num_levels, first, vol.data_ptr(),
-                                            nat.stream_of(vol))
-        nat.check(st, "AlternateCorrBlock coarse volumes (dxr_alt_coarse_volumes)")
+            st = lib.dxr_alt_coarse_volumes_ws(self._f1_nhwc.data_ptr(), self._f2_ptrs, B, H, W, D,
+                                               self.num_levels, first, vol.data_ptr(), nat.ptr(ws),
+                                               max(nbytes, 0), nat.stream_of(vol))
+        nat.check(st, "AlternateCorrBlock coarse volumes (dxr_alt_coarse_volumes_ws)")
         self.coarse_first_level = first
         self._volumes = vol
 

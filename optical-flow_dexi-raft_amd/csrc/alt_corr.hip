@@ -1539,13 +1539,14 @@ constexpr int VG_STAGE = 8 * VG_BLK;          // [operand][plane][k step] blocks
 // XA (experiments only; 0 in the product): bit 0 stores only sums equal to
 // 12345.0 (none: an ablation of the stores), bit 1 writes the raw f32 bits as the
 // hi / lo planes (no split VALU; results meaningless), bit 2 skips the MFMAs.
-template <int T, int XA = 0>
+template <int T, bool DMA, int XA = 0>
 __global__ __launch_bounds__(256, 2) void alt_volume_gemm_kernel(
     const float* __restrict__ f1, const float* __restrict__ f2, float* __restrict__ out,
-    dxr::LevelLayout vl, int N, int C, int ngroups) {
+    dxr::LevelLayout vl, int N, int C, int ngroups, const _Float16* __restrict__ p1,
+    const _Float16* __restrict__ p2) {
   static_assert(T == 2 || T == 8 || T == 32 || T == 128, "tiled levels 0-3 only");
   constexpr int TPG = 128 / T;                 // level tiles (pages) per workgroup
-  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * VG_STAGE];
+  __shared__ __attribute__((aligned(16))) unsigned char lds[DMA ? 4 * 16384 : 2 * VG_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = lane & 31, kh = lane >> 5;
   const int wc = wave & 1, wq = wave >> 1;     // the wave's 64-cell / 64-query half
@@ -1571,51 +1572,6 @@ __global__ __launch_bounds__(256, 2) void alt_volume_gemm_kernel(
     const int q = qblk * 128 + i;
     return q < N ? q * C : -1;
   };
-  // this thread's 8 load slots: slot i < 4 cells, else queries; piece t + 256 (i % 4)
-  // -> row piece / 8, channels 4 (piece % 8) .. + 4 of the stage
-  int off[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int piece = tid + 256 * (i & 3), row = piece >> 3;
-    off[i] = i < 4 ? cell_off(row) : query_off(row);
-  }
-  const int f4 = tid & 7;
-  const int ch = 4 * f4;
-  // LDS byte offset of this thread's 8-B hi write for slot i (lo: + 2 VG_BLK)
-  auto wr_addr = [&](int i) -> int {
-    const int row = (tid + 256 * (i & 3)) >> 3, o = i >> 2;
-    return ((o * 2 + 0) * 2 + (f4 >> 2)) * VG_BLK + row * 32 + ((f4 >> 1) & 1) * 16 + (f4 & 1) * 8;
-  };
-  float4 pre[8];
-  auto load_stage = [&](int s) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float* base = i < 4 ? f2b : f1b;
-      pre[i] = off[i] >= 0 ? *reinterpret_cast<const float4*>(base + off[i] + 32 * s + ch)
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
-  auto write_stage = [&](int buf) {
-    unsigned char* st = lds + buf * VG_STAGE;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float4 v = pre[i];
-      uint32_t h0, h1, l0, l1;
-      if constexpr ((XA & 2) != 0) {
-        h0 = __float_as_uint(v.x); h1 = __float_as_uint(v.y);
-        l0 = __float_as_uint(v.z); l1 = __float_as_uint(v.w);
-      } else {
-        h0 = alt_cvt_pk_h(v.x, v.y);
-        h1 = alt_cvt_pk_h(v.z, v.w);
-        const ah2 a0 = __builtin_bit_cast(ah2, h0), a1 = __builtin_bit_cast(ah2, h1);
-        l0 = alt_cvt_pk_h((v.x - (float)a0[0]) * 2048.f, (v.y - (float)a0[1]) * 2048.f);
-        l1 = alt_cvt_pk_h((v.z - (float)a1[0]) * 2048.f, (v.w - (float)a1[1]) * 2048.f);
-      }
-      const int a = wr_addr(i);
-      *reinterpret_cast<uint2*>(st + a) = make_uint2(h0, h1);
-      *reinterpret_cast<uint2*>(st + a + 2 * VG_BLK) = make_uint2(l0, l1);
-    }
-  };
   af16 acc[2][2], acc2[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -1623,40 +1579,150 @@ __global__ __launch_bounds__(256, 2) void alt_volume_gemm_kernel(
     for (int q = 0; q < 2; ++q)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][q][r] = acc2[a][q][r] = 0.f;
-  const int nst = C / 32;
-  load_stage(0);
-  write_stage(0);
-  __syncthreads();
-  for (int s = 0; s < nst; ++s) {
-    if (s + 1 < nst) load_stage(s + 1);
-    const unsigned char* st = lds + (s & 1) * VG_STAGE;
+  // one k step of the wave's 2 x 2 tiles: the windowed form's three products
+  auto mfma_step = [&](const ah8 (&th)[2], const ah8 (&tl)[2], const ah8 (&qh)[2],
+                       const ah8 (&ql)[2]) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if constexpr ((XA & 4) != 0) {
+          acc[a][q][0] += (float)th[a][0] * (float)qh[q][1] + (float)tl[a][2] * (float)ql[q][3];
+          continue;
+        }
+        acc2[a][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl[a], qh[q], acc2[a][q], 0, 0, 0);
+        acc2[a][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th[a], ql[q], acc2[a][q], 0, 0, 0);
+        acc[a][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th[a], qh[q], acc[a][q], 0, 0, 0);
+      }
+  };
+  if constexpr (DMA) {
+    // operands pre-split (alt_split_planes_kernel: [pair][hi | lo][k step][row][16]
+    // f16) and staged by LDS-DMA, one k step (16 channels) per ring slot, NS slots: no
+    // staging VGPRs and no split VALU in the loop, NS - 1 k steps of loads in flight.
+    // Slot layout [operand][plane][row block of 32][row][kh] x 16 B: one DMA
+    // instruction (lane l -> row 32 rb + l / 2, kh = l % 2, 16 B) fills one 1 KB row
+    // block — from 32 consecutive 32-B records of one k step, so queries read whole
+    // lines — and every fragment read is a conflict-free ds_read_b128 of 1 KB per
+    // wave.  Wave w moves operand w / 2 (0 cells, 1 queries), plane w % 2; rows past
+    // the level or the query count read out of the buffer's range, i.e. zeros.
+    constexpr int NS = 4, SLOT = 16384;
+    const int o = wave >> 1, pl = wave & 1;
+    const int rows_o = o == 0 ? vl.h * vl.w : N;
+    const _Float16* pbase = (o == 0 ? p2 : p1) + ((long long)b * 2 + pl) * rows_o * C;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<_Float16*>(pbase), (short)0, rows_o * C * 2, 0x00020000);
+    uint32_t voff[4];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) {
+      const int row = rb * 32 + (lane >> 1);
+      const int e = o == 0 ? cell_off(row) : query_off(row);   // row * C, or -1
+      voff[rb] = e >= 0 ? (uint32_t)(e / C) * 32u + (uint32_t)(lane & 1) * 16u : 0x80000000u;
+    }
+    const int kstride = rows_o * 32;               // bytes per k step of a plane
+    const int wslot = __builtin_amdgcn_readfirstlane((o * 2 + pl) * 4096);
+    auto issue = [&](int ks) {
+      unsigned char* dst = lds + (ks % NS) * SLOT + wslot;
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + rb * 1024), 16, voff[rb],
+                                                 ks * kstride, 0, 0);
+    };
+    const int nks = C / 16;
+#pragma unroll
+    for (int u = 0; u < NS - 1; ++u)
+      if (u < nks) issue(u);
+    for (int ks = 0; ks < nks; ++ks) {
+      // this wave's DMAs of step ks done (those of the younger steps may fly), then
+      // everyone's: the barrier also retires the reads of the slot refilled below
+      const int younger = min(NS - 2, nks - 1 - ks);
+      if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (ks + NS - 1 < nks) issue(ks + NS - 1);
+      const unsigned char* st = lds + (ks % NS) * SLOT;
       ah8 th[2], tl[2], qh[2], ql[2];
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
-        const int rc = (wc * 64 + a * 32 + j) * 32 + kh * 16;
-        const int rq = (wq * 64 + a * 32 + j) * 32 + kh * 16;
-        th[a] = __builtin_bit_cast(ah8, *reinterpret_cast<const uint4*>(st + (0 + ks) * VG_BLK + rc));
-        tl[a] = __builtin_bit_cast(ah8, *reinterpret_cast<const uint4*>(st + (2 + ks) * VG_BLK + rc));
-        qh[a] = __builtin_bit_cast(ah8, *reinterpret_cast<const uint4*>(st + (4 + ks) * VG_BLK + rq));
-        ql[a] = __builtin_bit_cast(ah8, *reinterpret_cast<const uint4*>(st + (6 + ks) * VG_BLK + rq));
+        const int rc = (wc * 2 + a) * 1024 + j * 32 + kh * 16;
+        const int rq = (wq * 2 + a) * 1024 + j * 32 + kh * 16;
+        th[a] = __builtin_bit_cast(ah8, *reinterpret_cast<const uint4*>(st + 0 * 4096 + rc));
+        tl[a] = __builtin_bit_cast(ah8, *reinterpret_cast<const uint4*>(st + 1 * 4096 + rc));
+        qh[a] = __builtin_bit_cast(ah8, *reinterpret_cast<const uint4*>(st + 2 * 4096 + rq));
+        ql[a] = __builtin_bit_cast(ah8, *reinterpret_cast<const uint4*>(st + 3 * 4096 + rq));
       }
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          if constexpr ((XA & 4) != 0) {
-            acc[a][q][0] += (float)th[a][0] * (float)qh[q][1] + (float)tl[a][2] * (float)ql[q][3];
-            continue;
-          }
-          acc2[a][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl[a], qh[q], acc2[a][q], 0, 0, 0);
-          acc2[a][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th[a], ql[q], acc2[a][q], 0, 0, 0);
-          acc[a][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(th[a], qh[q], acc[a][q], 0, 0, 0);
-        }
+      mfma_step(th, tl, qh, ql);
     }
-    if (s + 1 < nst) write_stage((s + 1) & 1);
+  } else {
+    // this thread's 8 load slots: slot i < 4 cells, else queries; piece t + 256 (i % 4)
+    // -> row piece / 8, channels 4 (piece % 8) .. + 4 of the stage
+    int off[8];
+  #pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int piece = tid + 256 * (i & 3), row = piece >> 3;
+      off[i] = i < 4 ? cell_off(row) : query_off(row);
+    }
+    const int f4 = tid & 7;
+    const int ch = 4 * f4;
+    // LDS byte offset of this thread's 8-B hi write for slot i (lo: + 2 VG_BLK)
+    auto wr_addr = [&](int i) -> int {
+      const int row = (tid + 256 * (i & 3)) >> 3, o = i >> 2;
+      return ((o * 2 + 0) * 2 + (f4 >> 2)) * VG_BLK + row * 32 + ((f4 >> 1) & 1) * 16 + (f4 & 1) * 8;
+    };
+    float4 pre[8];
+    auto load_stage = [&](int s) {
+  #pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float* base = i < 4 ? f2b : f1b;
+        pre[i] = off[i] >= 0 ? *reinterpret_cast<const float4*>(base + off[i] + 32 * s + ch)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    };
+    auto write_stage = [&](int buf) {
+      unsigned char* st = lds + buf * VG_STAGE;
+  #pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float4 v = pre[i];
+        uint32_t h0, h1, l0, l1;
+        if constexpr ((XA & 2) != 0) {
+          h0 = __float_as_uint(v.x); h1 = __float_as_uint(v.y);
+          l0 = __float_as_uint(v.z); l1 = __float_as_uint(v.w);
+        } else {
+          h0 = alt_cvt_pk_h(v.x, v.y);
+          h1 = alt_cvt_pk_h(v.z, v.w);
+          const ah2 a0 = __builtin_bit_cast(ah2, h0), a1 = __builtin_bit_cast(ah2, h1);
+          l0 = alt_cvt_pk_h((v.x - (float)a0[0]) * 2048.f, (v.y - (float)a0[1]) * 2048.f);
+          l1 = alt_cvt_pk_h((v.z - (float)a1[0]) * 2048.f, (v.w - (float)a1[1]) * 2048.f);
+        }
+        const int a = wr_addr(i);
+        *reinterpret_cast<uint2*>(st + a) = make_uint2(h0, h1);
+        *reinterpret_cast<uint2*>(st + a + 2 * VG_BLK) = make_uint2(l0, l1);
+      }
+    };
+    const int nst = C / 32;
+    load_stage(0);
+    write_stage(0);
     __syncthreads();
+    for (int s = 0; s < nst; ++s) {
+      if (s + 1 < nst) load_stage(s + 1);
+      const unsigned char* st = lds + (s & 1) * VG_STAGE;
+  #pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        ah8 th[2], tl[2], qh[2], ql[2];
+  #pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          const int rc = (wc * 64 + a * 32 + j) * 32 + kh * 16;
+          const int rq = (wq * 64 + a * 32 + j) * 32 + kh * 16;
+          th[a] = __builtin_bit_cast(ah8, *reinterpret_cast<const uint4*>(st + (0 + ks) * VG_BLK + rc));
+          tl[a] = __builtin_bit_cast(ah8, *reinterpret_cast<const uint4*>(st + (2 + ks) * VG_BLK + rc));
+          qh[a] = __builtin_bit_cast(ah8, *reinterpret_cast<const uint4*>(st + (4 + ks) * VG_BLK + rq));
+          ql[a] = __builtin_bit_cast(ah8, *reinterpret_cast<const uint4*>(st + (6 + ks) * VG_BLK + rq));
+        }
+        mfma_step(th, tl, qh, ql);
+      }
+      if (s + 1 < nst) write_stage((s + 1) & 1);
+      __syncthreads();
+    }
   }
   const long long page0 = ((long long)b * vl.qt + qblk) * ntiles + (long long)grp * TPG;
 #pragma unroll
@@ -1723,24 +1789,71 @@ __global__ __launch_bounds__(256, 2) void alt_volume_gemm_kernel(
     }
 }
 
-// one level's volume by alt_volume_gemm_kernel (tiled levels 0-3, C % 32 == 0)
+// f16 pair planes of `rows` f32 rows of C channels per pair, k-step-major so one
+// k step (16 channels) of consecutive rows is contiguous: out[pair][plane][ks][row][16]
+// with plane 0 = RNE_f16(x), plane 1 = RNE_f16((x - hi) * 2^11) — alt_split8h per
+// element, so the DMA form's products are the register form's.  Thread = 4
+// channels of a row, row-major (a wave reads 1 KB contiguous; its 8-B writes form
+// 32-B runs whose neighbours — the next rows' — the next waves write).
+__global__ __launch_bounds__(256) void alt_split_planes_kernel(const float* __restrict__ in,
+                                                               _Float16* __restrict__ out,
+                                                               long long rows, int C,
+                                                               long long n4) {
+  const int c4n = C / 4;
+  for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < n4;
+       t += (long long)gridDim.x * 256) {
+    const long long prow = t / c4n;
+    const int c = (int)(t - prow * c4n) * 4;
+    const long long pair = prow / rows, row = prow - pair * rows;
+    const float4 v = *reinterpret_cast<const float4*>(in + 4 * t);
+    const uint32_t h0 = alt_cvt_pk_h(v.x, v.y), h1 = alt_cvt_pk_h(v.z, v.w);
+    const ah2 a0 = __builtin_bit_cast(ah2, h0), a1 = __builtin_bit_cast(ah2, h1);
+    const uint32_t l0 = alt_cvt_pk_h((v.x - (float)a0[0]) * 2048.f, (v.y - (float)a0[1]) * 2048.f);
+    const uint32_t l1 = alt_cvt_pk_h((v.z - (float)a1[0]) * 2048.f, (v.w - (float)a1[1]) * 2048.f);
+    _Float16* o = out + pair * 2 * rows * C + ((long long)(c >> 4) * rows + row) * 16 + (c & 15);
+    *reinterpret_cast<uint2*>(o) = make_uint2(h0, h1);
+    *reinterpret_cast<uint2*>(o + rows * C) = make_uint2(l0, l1);
+  }
+}
+
+int launch_split_planes(const float* in, _Float16* out, long long B, long long rows, int C,
+                        hipStream_t stream) {
+  const long long n4 = B * rows * C / 4;
+  const long long blocks = std::min<long long>((n4 + 255) / 256, 16384);
+  hipLaunchKernelGGL(alt_split_planes_kernel, dim3((unsigned)std::max<long long>(blocks, 1)),
+                     dim3(256), 0, stream, in, out, rows, C, n4);
+  return dxr::launch_status();
+}
+
+// one level's volume by alt_volume_gemm_kernel (tiled levels 0-3, C % 32 == 0);
+// with f16 pair planes of both operands (p1, p2) the LDS-DMA form
 template <int XA = 0>
 int launch_alt_volume_gemm(const float* f1, const float* f2, float* vol, const dxr::LevelLayout& vl,
-                           int B, int N, int C, hipStream_t stream) {
+                           int B, int N, int C, hipStream_t stream,
+                           const _Float16* p1 = nullptr, const _Float16* p2 = nullptr) {
   const int T = vl.th * vl.tw;
   const int ngroups = (vl.ty * vl.tx + 128 / T - 1) / (128 / T);
   const long long nwg = (long long)vl.qt * ngroups;
-  if (nwg > 0x7fffffffLL || (long long)N * C > 0x7fffffffLL ||
-      (long long)vl.h * vl.w * C > 0x7fffffffLL)
+  if (nwg > 0x7fffffffLL || (long long)N * C > 0x3fffffffLL ||
+      (long long)vl.h * vl.w * C > 0x3fffffffLL)
     return DXR_EUNSUPPORTED;
   const dim3 grid((unsigned)nwg, 1u, (unsigned)B);
+  const bool dma = p1 != nullptr && p2 != nullptr;
+#define DXR_VG(TT)                                                                              \
+  if (dma)                                                                                      \
+    hipLaunchKernelGGL((alt_volume_gemm_kernel<TT, true, XA>), grid, dim3(256), 0, stream, f1, \
+                       f2, vol, vl, N, C, ngroups, p1, p2);                                     \
+  else                                                                                          \
+    hipLaunchKernelGGL((alt_volume_gemm_kernel<TT, false, XA>), grid, dim3(256), 0, stream, f1,\
+                       f2, vol, vl, N, C, ngroups, p1, p2);
   switch (T) {
-    case 2: hipLaunchKernelGGL((alt_volume_gemm_kernel<2, XA>), grid, dim3(256), 0, stream, f1, f2, vol, vl, N, C, ngroups); break;
-    case 8: hipLaunchKernelGGL((alt_volume_gemm_kernel<8, XA>), grid, dim3(256), 0, stream, f1, f2, vol, vl, N, C, ngroups); break;
-    case 32: hipLaunchKernelGGL((alt_volume_gemm_kernel<32, XA>), grid, dim3(256), 0, stream, f1, f2, vol, vl, N, C, ngroups); break;
-    case 128: hipLaunchKernelGGL((alt_volume_gemm_kernel<128, XA>), grid, dim3(256), 0, stream, f1, f2, vol, vl, N, C, ngroups); break;
+    case 2: DXR_VG(2) break;
+    case 8: DXR_VG(8) break;
+    case 32: DXR_VG(32) break;
+    case 128: DXR_VG(128) break;
     default: return DXR_EUNSUPPORTED;
   }
+#undef DXR_VG
   return dxr::launch_status();
 }
 }  // namespace
@@ -1766,10 +1879,27 @@ extern "C" int64_t dxr_alt_volume_numel(int64_t B, int64_t H, int64_t W, int num
 }
 
 namespace {
-// full_form: every level by the FULL box kernel (experiments: the round-6 first form)
+// Bytes of the f16 pair planes the DMA form of the volume GEMM reads (fmap1 and
+// each tiled level >= first_level of fmap2, 2 x 2 B per element, 256-B aligned
+// regions); 0 when no level takes the GEMM.
+long long alt_volume_planes_bytes(const dxr::Levels& L, int64_t B, int64_t H, int64_t W, int64_t C,
+                                  int num_levels, int first_level, long long* level_off) {
+  if (C % 32 != 0 || first_level >= dxr::TILED_LEVELS) return 0;
+  auto up = [](long long x) { return (x + 255) / 256 * 256; };
+  long long off = up(B * H * W * C * 4);
+  for (int l = first_level; l < num_levels && l < dxr::TILED_LEVELS; ++l) {
+    if (level_off) level_off[l] = off;
+    off += up(B * (long long)L.h[l] * L.w[l] * C * 4);
+  }
+  return off;
+}
+
+// full_form: every level by the FULL box kernel (experiments: the round-6 first form);
+// ws (>= alt_volume_planes_bytes): the GEMM's LDS-DMA form on pre-split planes
 int alt_coarse_volumes(const float* fmap1, const float* const* fmap2_levels, int64_t B, int64_t H,
                        int64_t W, int64_t C, int num_levels, int first_level, float* volumes,
-                       hipStream_t stream, bool full_form) {
+                       hipStream_t stream, bool full_form, void* ws = nullptr,
+                       int64_t ws_bytes = 0) {
   dxr::Levels L;
   if (!dxr::make_levels(B, H, W, num_levels, &L) || first_level < 0 || first_level >= num_levels)
     return DXR_EINVAL;
@@ -1788,14 +1918,29 @@ int alt_coarse_volumes(const float* fmap1, const float* const* fmap2_levels, int
   g.coord_qstride = 0;
   const int tiles_x = (int)((W + TQX - 1) / TQX);
   const int ntiles = tiles_x * (int)((H + TQY - 1) / TQY);
+  long long loff[8] = {};
+  const long long pbytes = alt_volume_planes_bytes(L, B, H, W, C, num_levels, first_level, loff);
+  _Float16* planes = nullptr;
+  if (!full_form && pbytes > 0 && ws != nullptr && ws_bytes >= pbytes && aligned16(ws)) {
+    planes = static_cast<_Float16*>(ws);
+    int st = launch_split_planes(fmap1, planes, B, H * W, (int)C, stream);
+    if (st != DXR_OK) return st;
+  }
   for (int l = first_level; l < num_levels; ++l) {
     if (!fmap2_levels[l] || !aligned16(fmap2_levels[l])) return DXR_EINVAL;
     g.lv[0] = AltLevel{fmap2_levels[l], L.h[l], L.w[l], 1.f, 0};
     g.vlay = L.lay[l];
     g.vlay.off -= L.off[first_level];
     if (l < dxr::TILED_LEVELS && C % 32 == 0 && !full_form) {
+      _Float16* p2 = nullptr;
+      if (planes) {
+        p2 = reinterpret_cast<_Float16*>(static_cast<unsigned char*>(ws) + loff[l]);
+        const int st = launch_split_planes(fmap2_levels[l], p2, B, (long long)L.h[l] * L.w[l],
+                                           (int)C, stream);
+        if (st != DXR_OK) return st;
+      }
       const int st = launch_alt_volume_gemm(fmap1, fmap2_levels[l], volumes, g.vlay, (int)B, g.N,
-                                            (int)C, stream);
+                                            (int)C, stream, planes, p2);
       if (st != DXR_OK) return st;
       continue;
     }
@@ -1815,6 +1960,24 @@ extern "C" int dxr_alt_coarse_volumes(const float* fmap1, const float* const* fm
                                       int first_level, float* volumes, hipStream_t stream) {
   return alt_coarse_volumes(fmap1, fmap2_levels, B, H, W, C, num_levels, first_level, volumes,
                             stream, false);
+}
+
+extern "C" int64_t dxr_alt_coarse_volumes_ws_bytes(int64_t B, int64_t H, int64_t W, int64_t C,
+                                                   int num_levels, int first_level) {
+  dxr::Levels L;
+  if (!dxr::make_levels(B, H, W, num_levels, &L) || first_level < 0 ||
+      first_level >= num_levels || C < 1)
+    return -1;
+  return alt_volume_planes_bytes(L, B, H, W, C, num_levels, first_level, nullptr);
+}
+
+extern "C" int dxr_alt_coarse_volumes_ws(const float* fmap1, const float* const* fmap2_levels,
+                                         int64_t B, int64_t H, int64_t W, int64_t C,
+                                         int num_levels, int first_level, float* volumes,
+                                         void* workspace, int64_t workspace_bytes,
+                                         hipStream_t stream) {
+  return alt_coarse_volumes(fmap1, fmap2_levels, B, H, W, C, num_levels, first_level, volumes,
+                            stream, false, workspace, workspace_bytes);
 }
 
 extern "C" int dxr_alt_corr_lookup(const float* fmap1, const float* const* fmap2_levels,

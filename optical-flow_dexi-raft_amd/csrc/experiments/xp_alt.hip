@@ -84,23 +84,37 @@ extern "C" int dxr_xp_alt_coarse_volumes_full(const float* fmap1, const float* c
 }
 
 // One tiled level's volume by alt_volume_gemm_kernel with ablation bits xa (its XA):
-// the volume buffer from `level` on (dxr_alt_volume_numel(B, H, W, level + 1, level)).
+// the volume buffer from `level` on (dxr_alt_volume_numel(B, H, W, level + 1, level));
+// with a workspace (>= dxr_alt_coarse_volumes_ws_bytes(B, H, W, C, level + 1, level))
+// the operands are split into f16 pair planes there first and the LDS-DMA form runs.
 extern "C" int dxr_xp_alt_volume_gemm(const float* fmap1, const float* fmap2_level, float* vol,
                                       int64_t B, int64_t H, int64_t W, int64_t C, int level,
-                                      int xa, hipStream_t stream) {
+                                      int xa, void* ws, hipStream_t stream) {
   dxr::Levels L;
   if (!dxr::make_levels(B, H, W, level + 1, &L) || level >= dxr::TILED_LEVELS || C % 32 != 0)
     return DXR_EINVAL;
   dxr::LevelLayout vl = L.lay[level];
   vl.off = 0;
   const int N = (int)(H * W);
+  _Float16 *p1 = nullptr, *p2 = nullptr;
+  if (ws != nullptr) {
+    long long loff[8] = {};
+    alt_volume_planes_bytes(L, B, H, W, C, level + 1, level, loff);
+    p1 = static_cast<_Float16*>(ws);
+    p2 = reinterpret_cast<_Float16*>(static_cast<unsigned char*>(ws) + loff[level]);
+    int st = launch_split_planes(fmap1, p1, B, H * W, (int)C, stream);
+    if (st == DXR_OK)
+      st = launch_split_planes(fmap2_level, p2, B, (long long)L.h[level] * L.w[level], (int)C, stream);
+    if (st != DXR_OK) return st;
+  }
+  if (xa == 99) return DXR_EINVAL;   // the split passes alone (timing)
   switch (xa) {
-    case 0: return launch_alt_volume_gemm<0>(fmap1, fmap2_level, vol, vl, (int)B, N, (int)C, stream);
-    case 1: return launch_alt_volume_gemm<1>(fmap1, fmap2_level, vol, vl, (int)B, N, (int)C, stream);
-    case 2: return launch_alt_volume_gemm<2>(fmap1, fmap2_level, vol, vl, (int)B, N, (int)C, stream);
-    case 4: return launch_alt_volume_gemm<4>(fmap1, fmap2_level, vol, vl, (int)B, N, (int)C, stream);
-    case 6: return launch_alt_volume_gemm<6>(fmap1, fmap2_level, vol, vl, (int)B, N, (int)C, stream);
-    case 7: return launch_alt_volume_gemm<7>(fmap1, fmap2_level, vol, vl, (int)B, N, (int)C, stream);
+    case 0: return launch_alt_volume_gemm<0>(fmap1, fmap2_level, vol, vl, (int)B, N, (int)C, stream, p1, p2);
+    case 1: return launch_alt_volume_gemm<1>(fmap1, fmap2_level, vol, vl, (int)B, N, (int)C, stream, p1, p2);
+    case 2: return launch_alt_volume_gemm<2>(fmap1, fmap2_level, vol, vl, (int)B, N, (int)C, stream, p1, p2);
+    case 4: return launch_alt_volume_gemm<4>(fmap1, fmap2_level, vol, vl, (int)B, N, (int)C, stream, p1, p2);
+    case 6: return launch_alt_volume_gemm<6>(fmap1, fmap2_level, vol, vl, (int)B, N, (int)C, stream, p1, p2);
+    case 7: return launch_alt_volume_gemm<7>(fmap1, fmap2_level, vol, vl, (int)B, N, (int)C, stream, p1, p2);
     default: return DXR_EINVAL;
   }
 }

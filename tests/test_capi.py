@@ -47,7 +47,8 @@ def test_header_declares_the_documented_entry_points():
         "dxr_corr_lookup_backward_multi", "dxr_lookup_backward_bound_slots",
         "dxr_corr_lookup_backward_multi_bound", "dxr_fmap_grads_bounded",
         "dxr_fmap_grads_bounded_workspace_bytes", "dxr_alt_corr_lookup_levels_ws",
-        "dxr_alt_volume_numel", "dxr_alt_coarse_volumes", "dxr_alt_volume_lookup"}
+        "dxr_alt_volume_numel", "dxr_alt_coarse_volumes", "dxr_alt_volume_lookup",
+        "dxr_alt_coarse_volumes_ws_bytes", "dxr_alt_coarse_volumes_ws"}
 
 
 def test_library_exports_every_declared_symbol(nat):
@@ -71,7 +72,7 @@ def test_library_is_gfx950_code(nat):
 
 def test_abi_version_and_status_strings(nat):
     lib = nat.load()
-    assert lib.dxr_abi_version() == nat.ABI_VERSION == 9
+    assert lib.dxr_abi_version() == nat.ABI_VERSION == 10
     assert lib.dxr_status_string(0) == b"ok"
     assert lib.dxr_status_string(1) == b"invalid argument"
     assert lib.dxr_status_string(2) == b"unsupported by this build"

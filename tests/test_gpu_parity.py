@@ -436,7 +436,8 @@ def test_alt_coarse_volumes_match_on_the_fly(dx, flow, shape, monkeypatch):
 def test_alt_volume_gemm_against_float64(dx, case):
     """Round 6: the coarse-level volumes' tiled GEMM (alt_volume_gemm_kernel,
     levels 0-3: 8x16 .. 1x2 tiles, ragged level edges, a partial last query
-    page, two pairs, D = 96) against float64 dot products of fmap1 with the
+    page, two pairs, D = 96; its register-split and LDS-DMA forms bit for bit
+    alike) against float64 dot products of fmap1 with the
     pooled fmap2 levels: within 1e-5 of sum |a||b| per cell.  "nonfinite": a
     channel of 1e5 (beyond the f16 pair's range: its tiles re-run on the bf16
     split, and stay accurate), a NaN fmap2 pixel and an inf fmap1 pixel — the
@@ -455,6 +456,16 @@ def test_alt_volume_gemm_against_float64(dx, case):
     vol = torch.full((n,), float("nan"), device=DEV)
     assert lib.dxr_alt_coarse_volumes(ab._f1_nhwc.data_ptr(), ab._f2_ptrs, B, H, W, D, L, 0,
                                       vol.data_ptr(), nat.stream_of(vol)) == 0
+    # the LDS-DMA form on pre-split planes (dxr_alt_coarse_volumes_ws): the same bits
+    nb = lib.dxr_alt_coarse_volumes_ws_bytes(B, H, W, D, L, 0)
+    assert nb > 0
+    ws = torch.empty((nb,), dtype=torch.uint8, device=DEV)
+    vol_dma = torch.full((n,), float("nan"), device=DEV)
+    assert lib.dxr_alt_coarse_volumes_ws(ab._f1_nhwc.data_ptr(), ab._f2_ptrs, B, H, W, D, L, 0,
+                                         vol_dma.data_ptr(), ws.data_ptr(), nb,
+                                         nat.stream_of(vol)) == 0
+    assert torch.equal(torch.isnan(vol), torch.isnan(vol_dma))
+    assert torch.equal(torch.nan_to_num(vol, nan=3.0), torch.nan_to_num(vol_dma, nan=3.0))
     N = H * W
     f1 = ab._f1_nhwc.reshape(B, N, D).double().cpu().numpy()
     with np.errstate(invalid="ignore", over="ignore"):
