@@ -30,10 +30,15 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--loss", default="vdot", choices=["vdot", "mulsum"])
     ap.add_argument("--clone-inputs", action="store_true")
+    ap.add_argument("--bw-sets", type=int, default=None,
+                    help="lookup backwards per launch (corr._BW_SETS; the pending output "
+                         "gradients of that many lookups are held until their launch)")
     ap.add_argument("--no-breakdown", action="store_true",
                     help="skip the torch-profiler kernel breakdown (under rocprofv3)")
     a = ap.parse_args()
     import dexiraft_amd
+    if a.bw_sets is not None:
+        sys.modules["dexiraft_amd.corr"]._BW_SETS = a.bw_sets
     dev = torch.device("cuda", 0)
     H, W = {"sintel": (55, 128), "chairs": (46, 62)}[a.workload]
     B, D = 1, 256
@@ -120,6 +125,7 @@ def main():
                     t = getattr(ev, "cuda_time_total", 0.0)
                 kern[key] = round(kern.get(key, 0.0) + t / 1e3, 3)
     print(json.dumps({"workload": a.workload, "fmap": [H, W], "loss": a.loss,
+                      "bw_sets": sys.modules["dexiraft_amd.corr"]._BW_SETS,
                       "inputs": "cloned per step" if a.clone_inputs else "persistent leaves",
                       "forward_ms": round(t_fwd, 3),
                       "train_step_ms": round(t_step, 3), "backward_ms": round(t_step - t_fwd, 3),
