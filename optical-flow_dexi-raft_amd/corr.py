@@ -187,7 +187,11 @@ def _side_stream(device):
 
 # Lookup backwards applied per launch: their window lines stay in L2 across the
 # sets; the pending grad_out tensors ([B, L*(2r+1)^2, H, W] each) live until then.
-_BW_SETS = 4
+# Round 6 (profiles/r06/experiments/r6y_r6z_backward_sets.jsonl, medians of six
+# alternated runs): two per launch 1.299 / 1.335 ms per Sintel training step (cloned
+# inputs + mul-sum loss / persistent leaves + vdot), four 1.353 / 1.340 — the eager
+# step is host-paced, and earlier flushes start the GPU sooner; peak memory alike.
+_BW_SETS = 2
 
 
 class _BuildGrad(torch.autograd.Function):
