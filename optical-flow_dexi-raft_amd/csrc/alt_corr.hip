@@ -1657,7 +1657,7 @@ __global__ __launch_bounds__(256, 2) void alt_volume_gemm_kernel(
     // this thread's 8 load slots: slot i < 4 cells, else queries; piece t + 256 (i % 4)
     // -> row piece / 8, channels 4 (piece % 8) .. + 4 of the stage
     int off[8];
-  #pragma unroll
+#pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int piece = tid + 256 * (i & 3), row = piece >> 3;
       off[i] = i < 4 ? cell_off(row) : query_off(row);
@@ -1671,7 +1671,7 @@ __global__ __launch_bounds__(256, 2) void alt_volume_gemm_kernel(
     };
     float4 pre[8];
     auto load_stage = [&](int s) {
-  #pragma unroll
+#pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float* base = i < 4 ? f2b : f1b;
         pre[i] = off[i] >= 0 ? *reinterpret_cast<const float4*>(base + off[i] + 32 * s + ch)
@@ -1680,7 +1680,7 @@ __global__ __launch_bounds__(256, 2) void alt_volume_gemm_kernel(
     };
     auto write_stage = [&](int buf) {
       unsigned char* st = lds + buf * VG_STAGE;
-  #pragma unroll
+#pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float4 v = pre[i];
         uint32_t h0, h1, l0, l1;
@@ -1706,10 +1706,10 @@ __global__ __launch_bounds__(256, 2) void alt_volume_gemm_kernel(
     for (int s = 0; s < nst; ++s) {
       if (s + 1 < nst) load_stage(s + 1);
       const unsigned char* st = lds + (s & 1) * VG_STAGE;
-  #pragma unroll
+#pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         ah8 th[2], tl[2], qh[2], ql[2];
-  #pragma unroll
+#pragma unroll
         for (int a = 0; a < 2; ++a) {
           const int rc = (wc * 64 + a * 32 + j) * 32 + kh * 16;
           const int rq = (wq * 64 + a * 32 + j) * 32 + kh * 16;
