@@ -245,6 +245,39 @@ def test_alt_workspace_bytes(nat):
     assert aw(None, None, None, None, 0, 16, 16, 64, 4, 4, 16.0, None, 0, None) == nat.DXR_OK
 
 
+def test_alt_coarse_volume_sizes(nat):
+    """The coarse-level volumes: dxr_alt_volume_numel floats = the tail of a
+    num_levels-level paged pyramid from first_level on; the volume GEMM's
+    LDS-DMA workspace (dxr_alt_coarse_volumes_ws_bytes) = fmap1's and each tiled
+    level's f16 pair planes (4 B per element, 256-B aligned regions), 0 when no
+    level takes the GEMM (C % 32 != 0, or only row-major levels), -1 for bad
+    geometry; the entry points validate before any launch."""
+    lib = nat.load()
+    al = lambda x: (x + 255) // 256 * 256   # noqa: E731
+    for B, H, W, L, first in ((1, 136, 240, 4, 2), (2, 55, 128, 4, 1), (1, 48, 70, 5, 3)):
+        assert lib.dxr_alt_volume_numel(B, H, W, L, first) == \
+            lib.dxr_pyramid_numel(B, H, W, L) - lib.dxr_pyramid_numel(B, H, W, first)
+        sizes, h, w = [], H, W
+        for lvl in range(L):
+            sizes.append((h, w))
+            h, w = h // 2, w // 2
+        want = al(B * H * W * 256 * 4) + sum(al(B * sizes[lvl][0] * sizes[lvl][1] * 256 * 4)
+                                               for lvl in range(first, min(L, 4)))
+        assert lib.dxr_alt_coarse_volumes_ws_bytes(B, H, W, 256, L, first) == want
+    assert lib.dxr_alt_coarse_volumes_ws_bytes(1, 48, 70, 48, 4, 2) == 0     # C % 32
+    assert lib.dxr_alt_coarse_volumes_ws_bytes(1, 48, 70, 64, 5, 4) == 0     # row-major only
+    assert lib.dxr_alt_coarse_volumes_ws_bytes(1, 48, 70, 64, 4, 4) == -1    # first >= levels
+    assert lib.dxr_alt_volume_numel(1, 48, 70, 4, 0) == lib.dxr_pyramid_numel(1, 48, 70, 4)
+    assert lib.dxr_alt_volume_numel(1, 0, 70, 4, 1) == -1
+    P = 1 << 12
+    ptrs = (ctypes.c_void_p * 4)(P, P, P, P)
+    cv, cvw = lib.dxr_alt_coarse_volumes, lib.dxr_alt_coarse_volumes_ws
+    assert cv(P, ptrs, 1, 48, 70, 64, 4, 4, P, None) == nat.DXR_EINVAL          # first level
+    assert cv(P, ptrs, 1, 48, 70, 40, 4, 2, P, None) == nat.DXR_EUNSUPPORTED    # C % 16
+    assert cvw(P, ptrs, 1, 48, 70, 64, 4, 0, None, None, 0, None) == nat.DXR_EINVAL  # no volumes
+    assert cv(None, None, 0, 48, 70, 64, 4, 2, None, None) == nat.DXR_OK       # B = 0
+
+
 def _fmap_grads_ws(B, D, H, W):
     """dxr_fmap_grads' workspace: the larger of its two GEMMs' needs, each the
     three-way split fmap operand (3 x 16 bit per element, k padded to whole
